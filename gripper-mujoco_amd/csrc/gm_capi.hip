@@ -1,0 +1,394 @@
+// gm_capi.hip -- C ABI (include/gripper_mi355x.h) over the device kernels.
+//
+// Replaces the pybind11 MjClass boundary (src/bind.cpp:43-205).  A context owns
+// one HIP stream and the device buffers of n_envs envs; every call is
+// asynchronous on that stream except the host-buffer getters, which copy and
+// synchronise.  No C++ exception crosses the ABI: failures return GM_E_* and
+// leave a message for gm_last_error().
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gm_kernels.hip"
+
+struct gm_ctx {
+  int device = 0;
+  int n_envs = 0;
+  long long env_offset = 0;
+  int n_objects = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  gm_model model;
+  gm_config cfg;
+  GmTopo topo;
+  // device buffers
+  GmEnvState* d_state = nullptr;
+  gm_model* d_model = nullptr;
+  gm_config* d_cfg = nullptr;
+  GmTopo* d_topo = nullptr;
+  gm_object* d_objs = nullptr;
+  float* d_eq = nullptr;
+  float* d_obs = nullptr;
+  float* d_rew = nullptr;
+  uint8_t* d_done = nullptr;
+  float* d_act = nullptr;
+  int32_t* d_dact = nullptr;
+  uint8_t* d_mask = nullptr;
+  gm_spawn* d_spawn = nullptr;
+  std::string err;
+};
+
+namespace {
+
+int fail(gm_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+#define HIPCHK(ctx, x)                                                               \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess)                                                            \
+      return fail(ctx, GM_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_));    \
+  } while (0)
+
+int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
+  std::memset(&T, 0, sizeof(T));
+  T.N = m.n_seg;
+  T.CL = m.n_seg + 2;
+  T.nbody = m.nbody; T.nv = m.nv; T.nq = m.nq; T.ngeom = m.ngeom; T.npair = m.npair; T.nlock = m.nlock;
+  T.body_base = m.body_base; T.dof_base = m.dof_base;
+  for (int f = 0; f < 3; f++) {
+    T.dof_f0[f] = m.dof_pris[f];
+    T.body_f0[f] = m.dof_body[m.dof_pris[f]];
+    T.body_finger[f] = m.body_finger[f];
+  }
+  T.body_palm = m.body_palm; T.dof_palm = m.dof_palm;
+  T.body_obj = m.body_obj; T.dof_obj = m.dof_obj; T.geom_obj = m.geom_obj;
+  T.qadr_obj = m.jnt_qposadr[m.body_jnt[m.body_obj]];
+  // verify the canonical tree layout the kernels index arithmetically
+  for (int f = 0; f < 3; f++)
+    for (int p = 1; p <= T.CL; p++) {
+      int d = T.dof_f0[f] + p - 1, b = T.body_f0[f] + p - 1;
+      if (m.dof_body[d] != b || m.body_group[b] != f) { err = "model is not the canonical gripper tree"; return GM_E_ARG; }
+      int par = (p == 1) ? m.dof_base : d - 1;
+      if (m.dof_parent[d] != par) { err = "unexpected dof parent"; return GM_E_ARG; }
+    }
+  if (m.npair > GM_MAX_PAIR || m.nv > GM_MAX_DOF || T.qadr_obj != m.dof_obj) { err = "model exceeds kernel limits"; return GM_E_RANGE; }
+  for (int b = 0; b < GM_MAX_BODY; b++) { T.body_group[b] = -1; T.body_cpos[b] = 0; }
+  for (int b = 0; b < m.nbody; b++) {
+    T.body_group[b] = m.body_group[b];
+    if (m.body_group[b] >= 0 && m.body_group[b] < 3) T.body_cpos[b] = b - T.body_f0[m.body_group[b]] + 1;
+    else if (m.body_group[b] == GM_GRP_PALM) T.body_cpos[b] = 1;
+  }
+  for (int g = 0; g < m.ngeom; g++) {
+    int b = m.geom_body[g];
+    T.geom_group[g] = (b == 0) ? -1 : T.body_group[b];
+    if (T.geom_group[g] == GM_GRP_BASE) T.geom_group[g] = -1;
+    T.geom_cpos[g] = T.body_cpos[b];
+  }
+  return GM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gm_version(void) { return "gripper-mi355x 0.1 (gfx950, one-wave-per-env fused env-step)"; }
+
+int gm_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* objects, int n_objects,
+              int n_envs, int env_offset, int device, uint64_t seed, gm_ctx** out) {
+  if (!model || !cfg || !objects || !out || n_envs <= 0 || n_objects <= 0) return GM_E_ARG;
+  *out = nullptr;
+  gm_ctx* c = new gm_ctx();
+  c->device = device;
+  c->n_envs = n_envs;
+  c->env_offset = env_offset;
+  c->n_objects = n_objects;
+  c->model = *model;
+  c->cfg = *cfg;
+  std::string err;
+  int rc = build_topo(c->model, c->topo, err);
+  if (rc != GM_OK) { fprintf(stderr, "gm_create: %s\n", err.c_str()); delete c; return rc; }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device) {
+    fprintf(stderr, "gm_create: no HIP device %d (found %d)\n", device, ndev);
+    delete c;
+    return GM_E_NOEXT;
+  }
+  *out = c;
+  HIPCHK(c, hipSetDevice(device));
+  HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIPCHK(c, hipEventCreate(&c->ev0));
+  HIPCHK(c, hipEventCreate(&c->ev1));
+  HIPCHK(c, hipMalloc(&c->d_state, sizeof(GmEnvState) * (size_t)n_envs));
+  HIPCHK(c, hipMalloc(&c->d_model, sizeof(gm_model)));
+  HIPCHK(c, hipMalloc(&c->d_cfg, sizeof(gm_config)));
+  HIPCHK(c, hipMalloc(&c->d_topo, sizeof(GmTopo)));
+  HIPCHK(c, hipMalloc(&c->d_objs, sizeof(gm_object) * (size_t)n_objects));
+  HIPCHK(c, hipMalloc(&c->d_eq, sizeof(float) * GM_MAX_QPOS));
+  HIPCHK(c, hipMalloc(&c->d_obs, sizeof(float) * (size_t)n_envs * (cfg->n_obs > 0 ? cfg->n_obs : 1)));
+  HIPCHK(c, hipMalloc(&c->d_rew, sizeof(float) * (size_t)n_envs));
+  HIPCHK(c, hipMalloc(&c->d_done, (size_t)n_envs));
+  HIPCHK(c, hipMalloc(&c->d_act, sizeof(float) * (size_t)n_envs * GM_ACTION_CODE_COUNT));
+  HIPCHK(c, hipMalloc(&c->d_dact, sizeof(int32_t) * (size_t)n_envs));
+  HIPCHK(c, hipMalloc(&c->d_mask, (size_t)n_envs));
+  HIPCHK(c, hipMalloc(&c->d_spawn, sizeof(gm_spawn) * (size_t)n_envs));
+  HIPCHK(c, hipMemsetAsync(c->d_state, 0, sizeof(GmEnvState) * (size_t)n_envs, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_obs, 0, sizeof(float) * (size_t)n_envs * (cfg->n_obs > 0 ? cfg->n_obs : 1), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_rew, 0, sizeof(float) * (size_t)n_envs, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_done, 0, (size_t)n_envs, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_model, &c->model, sizeof(gm_model), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_cfg, &c->cfg, sizeof(gm_config), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_topo, &c->topo, sizeof(GmTopo), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_objs, objects, sizeof(gm_object) * (size_t)n_objects, hipMemcpyHostToDevice, c->stream));
+  // one-time calibrate_reset settle (myfunctions.cpp:1470-1505) on env 0
+  hipLaunchKernelGGL(gm_settle_init_kernel, dim3(1), dim3(1), 0, c->stream, c->d_state, c->d_model, c->d_topo, c->d_objs);
+  DebugOut dbg{nullptr, nullptr, nullptr, nullptr};
+  hipLaunchKernelGGL(gm_step_kernel, dim3(1), dim3(NT), 0, c->stream, c->d_state, c->d_model, c->d_cfg, c->d_topo,
+                     c->d_obs, c->d_rew, c->d_done, 1, 1, dbg);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->d_eq, reinterpret_cast<char*>(c->d_state) + offsetof(GmEnvState, qpos), sizeof(float) * GM_MAX_QPOS, hipMemcpyDeviceToDevice, c->stream));
+  int threads = 256, blocks = (n_envs + threads - 1) / threads;
+  hipLaunchKernelGGL(gm_init_envs_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, cfg->s.random_seed,
+                     (long long)env_offset, n_envs);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+
+void gm_destroy(gm_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(c->d_state); (void)hipFree(c->d_model); (void)hipFree(c->d_cfg); (void)hipFree(c->d_topo); (void)hipFree(c->d_objs);
+  (void)hipFree(c->d_eq); (void)hipFree(c->d_obs); (void)hipFree(c->d_rew); (void)hipFree(c->d_done); (void)hipFree(c->d_act);
+  (void)hipFree(c->d_dact); (void)hipFree(c->d_mask); (void)hipFree(c->d_spawn);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* gm_last_error(const gm_ctx* c) { return c ? c->err.c_str() : "null context"; }
+int gm_n_envs(const gm_ctx* c) { return c ? c->n_envs : 0; }
+int gm_n_obs(const gm_ctx* c) { return c ? c->cfg.n_obs : 0; }
+int gm_n_actions(const gm_ctx* c) { return c ? c->cfg.n_actions : 0; }
+
+int gm_update_config(gm_ctx* c, const gm_config* cfg) {
+  if (!c || !cfg) return GM_E_ARG;
+  if (cfg->n_obs != c->cfg.n_obs) return fail(c, GM_E_STATE, "n_obs changed: recreate the context");
+  c->cfg = *cfg;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpyAsync(c->d_cfg, &c->cfg, sizeof(gm_config), hipMemcpyHostToDevice, c->stream));
+  return GM_OK;
+}
+
+int gm_reset(gm_ctx* c, const uint8_t* mask, const gm_spawn* spawn) {
+  if (!c) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint8_t* dm = nullptr;
+  const gm_spawn* ds = nullptr;
+  if (mask) { HIPCHK(c, hipMemcpyAsync(c->d_mask, mask, (size_t)c->n_envs, hipMemcpyHostToDevice, c->stream)); dm = c->d_mask; }
+  if (spawn) {
+    HIPCHK(c, hipMemcpyAsync(c->d_spawn, spawn, sizeof(gm_spawn) * (size_t)c->n_envs, hipMemcpyHostToDevice, c->stream));
+    ds = c->d_spawn;
+  }
+  int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
+  hipLaunchKernelGGL(gm_reset_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
+                     c->d_topo, c->d_eq, dm, ds, c->d_objs, c->n_objects, c->n_envs);
+  HIPCHK(c, hipGetLastError());
+  if (mask || spawn) HIPCHK(c, hipStreamSynchronize(c->stream));   // host buffers may be reused
+  return GM_OK;
+}
+
+int gm_set_action(gm_ctx* c, const float* actions, int on_device) {
+  if (!c || !actions) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  const float* da = actions;
+  if (!on_device) {
+    HIPCHK(c, hipMemcpyAsync(c->d_act, actions, sizeof(float) * (size_t)c->n_envs * c->cfg.n_actions,
+                             hipMemcpyHostToDevice, c->stream));
+    da = c->d_act;
+  }
+  int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
+  hipLaunchKernelGGL(gm_action_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
+                     da, (const int32_t*)nullptr, c->n_envs);
+  HIPCHK(c, hipGetLastError());
+  if (!on_device) HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+
+int gm_set_discrete_action(gm_ctx* c, const int32_t* actions, int on_device) {
+  if (!c || !actions) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  const int32_t* da = actions;
+  if (!on_device) {
+    HIPCHK(c, hipMemcpyAsync(c->d_dact, actions, sizeof(int32_t) * (size_t)c->n_envs, hipMemcpyHostToDevice, c->stream));
+    da = c->d_dact;
+  }
+  int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
+  hipLaunchKernelGGL(gm_action_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
+                     (const float*)nullptr, da, c->n_envs);
+  HIPCHK(c, hipGetLastError());
+  if (!on_device) HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+
+int gm_step(gm_ctx* c) {
+  if (!c) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  DebugOut dbg{nullptr, nullptr, nullptr, nullptr};
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  hipLaunchKernelGGL(gm_step_kernel, dim3(c->n_envs), dim3(NT), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
+                     c->d_topo, c->d_obs, c->d_rew, c->d_done, c->n_envs, 0, dbg);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  c->timed = true;
+  return GM_OK;
+}
+
+int gm_last_step_ms(gm_ctx* c, float* ms) {
+  if (!c || !ms || !c->timed) return GM_E_STATE;
+  HIPCHK(c, hipEventSynchronize(c->ev1));
+  HIPCHK(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
+  return GM_OK;
+}
+
+int gm_get_obs(gm_ctx* c, float* out, int on_device) {
+  if (!c || !out) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  size_t bytes = sizeof(float) * (size_t)c->n_envs * c->cfg.n_obs;
+  HIPCHK(c, hipMemcpyAsync(out, c->d_obs, bytes, on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+
+int gm_get_reward_done(gm_ctx* c, float* reward, uint8_t* done, int on_device) {
+  if (!c) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipMemcpyKind k = on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  if (reward) HIPCHK(c, hipMemcpyAsync(reward, c->d_rew, sizeof(float) * (size_t)c->n_envs, k, c->stream));
+  if (done) HIPCHK(c, hipMemcpyAsync(done, c->d_done, (size_t)c->n_envs, k, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+
+static int fetch_states(gm_ctx* c, std::vector<GmEnvState>& h) {
+  h.resize(c->n_envs);
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpyAsync(h.data(), c->d_state, sizeof(GmEnvState) * (size_t)c->n_envs, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+
+int gm_get_event_rows(gm_ctx* c, int32_t* rows, int32_t* absc, float* lastv) {
+  if (!c) return GM_E_ARG;
+  std::vector<GmEnvState> h;
+  int rc = fetch_states(c, h);
+  if (rc) return rc;
+  const int W = GM_N_BINARY + GM_N_LINEAR;
+  for (int e = 0; e < c->n_envs; e++) {
+    for (int k = 0; k < GM_N_BINARY; k++) {
+      if (rows) rows[e * W + k] = h[e].bev_row[k];
+      if (absc) absc[e * W + k] = h[e].bev_abs[k];
+      if (lastv) lastv[e * W + k] = (float)h[e].bev_last[k];
+    }
+    for (int k = 0; k < GM_N_LINEAR; k++) {
+      if (rows) rows[e * W + GM_N_BINARY + k] = h[e].lev_row[k];
+      if (absc) absc[e * W + GM_N_BINARY + k] = h[e].lev_abs[k];
+      if (lastv) lastv[e * W + GM_N_BINARY + k] = h[e].lev_last[k];
+    }
+  }
+  return GM_OK;
+}
+
+int gm_get_state(gm_ctx* c, float* qpos, float* qvel, double* time) {
+  if (!c) return GM_E_ARG;
+  std::vector<GmEnvState> h;
+  int rc = fetch_states(c, h);
+  if (rc) return rc;
+  for (int e = 0; e < c->n_envs; e++) {
+    if (qpos) std::memcpy(qpos + (size_t)e * c->model.nq, h[e].qpos, sizeof(float) * c->model.nq);
+    if (qvel) std::memcpy(qvel + (size_t)e * c->model.nv, h[e].qvel, sizeof(float) * c->model.nv);
+    if (time) time[e] = h[e].time;
+  }
+  return GM_OK;
+}
+
+int gm_set_state(gm_ctx* c, const float* qpos, const float* qvel) {
+  if (!c) return GM_E_ARG;
+  std::vector<GmEnvState> h;
+  int rc = fetch_states(c, h);
+  if (rc) return rc;
+  for (int e = 0; e < c->n_envs; e++) {
+    if (qpos) std::memcpy(h[e].qpos, qpos + (size_t)e * c->model.nq, sizeof(float) * c->model.nq);
+    if (qvel) std::memcpy(h[e].qvel, qvel + (size_t)e * c->model.nv, sizeof(float) * c->model.nv);
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_state, h.data(), sizeof(GmEnvState) * (size_t)c->n_envs, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+
+int gm_get_target(gm_ctx* c, double* end_xyzth, int32_t* es, int32_t* ns, double* base_xyz) {
+  if (!c) return GM_E_ARG;
+  std::vector<GmEnvState> h;
+  int rc = fetch_states(c, h);
+  if (rc) return rc;
+  for (int e = 0; e < c->n_envs; e++) {
+    if (end_xyzth) { end_xyzth[4 * e] = h[e].end.x; end_xyzth[4 * e + 1] = h[e].end.y; end_xyzth[4 * e + 2] = h[e].end.z; end_xyzth[4 * e + 3] = h[e].end.th; }
+    if (es) { es[3 * e] = h[e].end.sx; es[3 * e + 1] = h[e].end.sy; es[3 * e + 2] = h[e].end.sz; }
+    if (ns) { ns[3 * e] = h[e].next.sx; ns[3 * e + 1] = h[e].next.sy; ns[3 * e + 2] = h[e].next.sz; }
+    if (base_xyz) { base_xyz[3 * e] = h[e].base[0]; base_xyz[3 * e + 1] = h[e].base[1]; base_xyz[3 * e + 2] = h[e].base[2]; }
+  }
+  return GM_OK;
+}
+
+int gm_get_overflow(gm_ctx* c, int32_t* counts) {
+  if (!c || !counts) return GM_E_ARG;
+  std::vector<GmEnvState> h;
+  int rc = fetch_states(c, h);
+  if (rc) return rc;
+  for (int e = 0; e < c->n_envs; e++) counts[e] = h[e].overflow;
+  return GM_OK;
+}
+
+void* gm_device_obs(gm_ctx* c) { return c ? c->d_obs : nullptr; }
+void* gm_device_reward(gm_ctx* c) { return c ? c->d_rew : nullptr; }
+void* gm_device_done(gm_ctx* c) { return c ? c->d_done : nullptr; }
+void* gm_device_actions(gm_ctx* c) { return c ? c->d_act : nullptr; }
+void* gm_stream(gm_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int gm_debug_substep(gm_ctx* c, int32_t* ncon, float* contact, float* efc_force, float* qacc) {
+  if (!c) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  int32_t* d_ncon; float *d_con, *d_f, *d_q;
+  size_t n = (size_t)c->n_envs;
+  HIPCHK(c, hipMalloc(&d_ncon, sizeof(int32_t) * n));
+  HIPCHK(c, hipMalloc(&d_con, sizeof(float) * n * GM_MAX_CON * 16));
+  HIPCHK(c, hipMalloc(&d_f, sizeof(float) * n * GM_MAX_EFC));
+  HIPCHK(c, hipMalloc(&d_q, sizeof(float) * n * GM_MAX_DOF));
+  DebugOut dbg{d_ncon, d_con, d_f, d_q};
+  hipLaunchKernelGGL(gm_step_kernel, dim3(c->n_envs), dim3(NT), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
+                     c->d_topo, c->d_obs, c->d_rew, c->d_done, c->n_envs, 2, dbg);
+  HIPCHK(c, hipGetLastError());
+  if (ncon) HIPCHK(c, hipMemcpyAsync(ncon, d_ncon, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+  if (contact) HIPCHK(c, hipMemcpyAsync(contact, d_con, sizeof(float) * n * GM_MAX_CON * 16, hipMemcpyDeviceToHost, c->stream));
+  if (efc_force) HIPCHK(c, hipMemcpyAsync(efc_force, d_f, sizeof(float) * n * GM_MAX_EFC, hipMemcpyDeviceToHost, c->stream));
+  if (qacc) HIPCHK(c, hipMemcpyAsync(qacc, d_q, sizeof(float) * n * GM_MAX_DOF, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  (void)hipFree(d_ncon); (void)hipFree(d_con); (void)hipFree(d_f); (void)hipFree(d_q);
+  return GM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,566 @@
+// gm_host_model.cpp -- host-side model compiler, settings defaults and derived
+// configuration for the MI355X gripper env-step path.
+//
+// The reference loads a generated MJCF (mj_loadXML, mjclass.cpp:377-409) whose
+// source lives in the empty `description` submodule.  Here the same gripper is
+// compiled directly from the numerics the reference reads out of that MJCF
+// (read_gripper_dimensions, myfunctions.cpp:836-953) and the constants it
+// hard-codes (JointSettings, myfunctions.cpp:166-296).  Values the MJCF alone
+// holds (masses, damping, collision thickness, solref/solimp) are invented and
+// listed in DESIGN.md section "Model spec".
+#include "gripper_mi355x.h"
+
+#include <cmath>
+#include <cstring>
+#include <cstdint>
+#include <string>
+
+namespace {
+
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kSteelDensity = 7850.0;
+
+void quat_from_mat(const double R[9], double q[4]) {
+  // R row-major; columns are the body axes in the parent frame.
+  double tr = R[0] + R[4] + R[8];
+  if (tr > 0) {
+    double s = std::sqrt(tr + 1.0) * 2;
+    q[0] = 0.25 * s;
+    q[1] = (R[7] - R[5]) / s;
+    q[2] = (R[2] - R[6]) / s;
+    q[3] = (R[3] - R[1]) / s;
+  } else if (R[0] > R[4] && R[0] > R[8]) {
+    double s = std::sqrt(1.0 + R[0] - R[4] - R[8]) * 2;
+    q[0] = (R[7] - R[5]) / s;
+    q[1] = 0.25 * s;
+    q[2] = (R[1] + R[3]) / s;
+    q[3] = (R[2] + R[6]) / s;
+  } else if (R[4] > R[8]) {
+    double s = std::sqrt(1.0 + R[4] - R[0] - R[8]) * 2;
+    q[0] = (R[2] - R[6]) / s;
+    q[1] = (R[1] + R[3]) / s;
+    q[2] = 0.25 * s;
+    q[3] = (R[5] + R[7]) / s;
+  } else {
+    double s = std::sqrt(1.0 + R[8] - R[0] - R[4]) * 2;
+    q[0] = (R[3] - R[1]) / s;
+    q[1] = (R[2] + R[6]) / s;
+    q[2] = (R[5] + R[7]) / s;
+    q[3] = 0.25 * s;
+  }
+  double n = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  for (int i = 0; i < 4; i++) q[i] /= n;
+}
+
+void set3(double* d, double a, double b, double c) { d[0] = a; d[1] = b; d[2] = c; }
+void set4(double* d, double a, double b, double c, double e) { d[0] = a; d[1] = b; d[2] = c; d[3] = e; }
+
+struct Builder {
+  gm_model* m;
+  int add_body(int parent, int group, const double pos[3], const double quat[4],
+               double mass, const double ipos[3], const double inertia[3]) {
+    int b = m->nbody++;
+    m->body_parent[b] = parent;
+    m->body_group[b] = group;
+    m->body_jnt[b] = -1;
+    for (int i = 0; i < 3; i++) m->body_pos[b][i] = pos[i];
+    for (int i = 0; i < 4; i++) m->body_quat[b][i] = quat[i];
+    m->body_mass[b] = mass;
+    for (int i = 0; i < 3; i++) m->body_ipos[b][i] = ipos[i];
+    for (int i = 0; i < 3; i++) m->body_inertia[b][i] = inertia[i];
+    return b;
+  }
+  int add_joint(int body, int type, const double axis[3], double stiffness, double damping,
+                double armature, int parent_dof) {
+    int j = m->njnt++;
+    m->body_jnt[body] = j;
+    m->jnt_type[j] = type;
+    m->jnt_body[j] = body;
+    m->jnt_qposadr[j] = m->nq;
+    m->jnt_dofadr[j] = m->nv;
+    set3(m->jnt_pos[j], 0, 0, 0);
+    for (int i = 0; i < 3; i++) m->jnt_axis[j][i] = axis[i];
+    m->jnt_stiffness[j] = stiffness;
+    m->jnt_damping[j] = damping;
+    m->jnt_armature[j] = armature;
+    int ndof = (type == GM_JNT_FREE) ? 6 : 1;
+    m->nq += (type == GM_JNT_FREE) ? 7 : 1;
+    for (int k = 0; k < ndof; k++) {
+      int d = m->nv++;
+      m->dof_parent[d] = (k == 0) ? parent_dof : d - 1;
+      m->dof_body[d] = body;
+      m->dof_group[d] = m->body_group[body];
+    }
+    return m->jnt_dofadr[j];
+  }
+  int add_geom(int body, int type, int cls, const double pos[3], const double quat[4],
+               const double size[3], double friction) {
+    int g = m->ngeom++;
+    m->geom_type[g] = type;
+    m->geom_body[g] = body;
+    m->geom_class[g] = cls;
+    for (int i = 0; i < 3; i++) m->geom_pos[g][i] = pos[i];
+    for (int i = 0; i < 4; i++) m->geom_quat[g][i] = quat[i];
+    for (int i = 0; i < 3; i++) m->geom_size[g][i] = size[i];
+    m->geom_friction[g] = friction;
+    double rb = 0;
+    if (type == GM_GEOM_BOX) rb = std::sqrt(size[0] * size[0] + size[1] * size[1] + size[2] * size[2]);
+    else if (type == GM_GEOM_SPHERE) rb = size[0];
+    else if (type == GM_GEOM_CYLINDER) rb = std::sqrt(size[0] * size[0] + size[1] * size[1]);
+    else if (type == GM_GEOM_CAPSULE) rb = size[0] + size[1];
+    m->geom_rbound[g] = rb;
+    return g;
+  }
+};
+
+void box_inertia(double mass, double hx, double hy, double hz, double out[3]) {
+  out[0] = mass * (4 * hy * hy + 4 * hz * hz) / 12.0;
+  out[1] = mass * (4 * hx * hx + 4 * hz * hz) / 12.0;
+  out[2] = mass * (4 * hx * hx + 4 * hy * hy) / 12.0;
+}
+
+}  // namespace
+
+extern "C" {
+
+void gm_default_model_params(gm_model_params* p) {
+  p->n_seg = 8;
+  p->finger_length = 235e-3;
+  p->finger_width = 28e-3;
+  p->finger_thickness = 0.86e-3;
+  p->finger_E = 193e9;
+  p->hook_length = 35e-3;
+  p->hook_angle_degrees = 75.0;
+  p->fingertip_clearance = 10e-3;
+  p->segment_inertia_scaling = 50.0;
+  p->timestep = 3.187e-3;
+  p->pgs_iterations = 24;
+  p->collision_half_thickness = 1.5e-3;
+}
+
+int gm_build_model(const gm_model_params* p, gm_model* m) {
+  if (!p || !m) return GM_E_ARG;
+  if (p->n_seg < 1 || p->n_seg > GM_MAX_SEG) return GM_E_RANGE;
+  std::memset(m, 0, sizeof(*m));
+  Builder B{m};
+  const int N = p->n_seg;
+  m->n_seg = N;
+
+  // ---- dimensions (JointSettings::Dim, myfunctions.cpp:207-242) ----
+  m->finger_length = p->finger_length;
+  m->finger_width = p->finger_width;
+  m->finger_thickness = p->finger_thickness;
+  m->finger_E = p->finger_E;
+  double I = p->finger_width * std::pow(p->finger_thickness, 3) / 12.0;
+  m->finger_EI = p->finger_E * I;
+  m->hook_length = p->hook_length;
+  m->hook_angle_degrees = p->hook_angle_degrees;
+  m->fingertip_clearance = p->fingertip_clearance;
+  m->yield_stress = 215e6;
+  m->fixed_first_segment = 1;   // links 2..N+1 carry the N joints (myfunctions.cpp:650-660)
+  const int Ntotal = N + m->fixed_first_segment;
+  const double Ls = p->finger_length / double(Ntotal);   // myfunctions.cpp:535
+  m->segment_length = Ls;
+
+  // ---- gains (myfunctions.cpp:273-296) ----
+  double EI = m->finger_EI;
+  set3(m->kp_gripper, EI * 541.3 + 49.65, EI * 44.92 - 0.846, 1000);
+  set3(m->kd_gripper, 1, 1, 1);
+  set3(m->kp_base, 500, 500, 2000);
+  set3(m->kd_base, 80, 80, 100);
+  m->stepper_num_steps = 10;
+  m->time_per_step = 10 / 2000.0;
+  m->gauge_xpos = 50e-3;
+  m->gauge_order = 3;
+
+  // ---- options ----
+  m->timestep = p->timestep;
+  set3(m->gravity, 0, 0, -9.81);
+  m->solref[0] = 0.02; m->solref[1] = 1.0;
+  m->solimp[0] = 0.9; m->solimp[1] = 0.95; m->solimp[2] = 0.001; m->solimp[3] = 0.5; m->solimp[4] = 2.0;
+  m->pgs_iterations = p->pgs_iterations;
+  m->mpr_tolerance = 1e-6;
+  m->mpr_iterations = 50;
+
+  const double id4[4] = {1, 0, 0, 0};
+  const double zero3[3] = {0, 0, 0};
+
+  // ---- world (body 0) + ground plane ----
+  {
+    double in[3] = {0, 0, 0};
+    B.add_body(-1, GM_GRP_WORLD, zero3, id4, 0, zero3, in);
+  }
+  // ground plane geom id 0 (ObjectHandler::gnd_geom_name "ground_geom")
+  {
+    double sz[3] = {10, 10, 0.1};
+    m->geom_ground = B.add_geom(0, GM_GEOM_PLANE, GM_CLS_GROUND, zero3, id4, sz, 1.0);
+  }
+
+  // ---- gripper base: slide "world_to_base" along -z (target base z +ve = down) ----
+  // the lowest point of the fixed hook sits at fingertip_clearance above the ground
+  const double z_root = p->fingertip_clearance + p->finger_length +
+                        p->hook_length * std::cos(p->hook_angle_degrees * kPi / 180.0) +
+                        std::max(p->collision_half_thickness, 0.5 * p->finger_thickness);
+  {
+    double pos[3] = {0, 0, z_root};
+    double in[3];
+    box_inertia(0.5, 0.05, 0.05, 0.02, in);
+    double ipos[3] = {0, 0, 0.03};
+    m->body_base = B.add_body(0, GM_GRP_BASE, pos, id4, 0.5, ipos, in);
+    double ax[3] = {0, 0, -1};
+    m->dof_base = B.add_joint(m->body_base, GM_JNT_SLIDE, ax, 0, 0, 0, -1);
+  }
+
+  const double ht = std::max(p->collision_half_thickness, 0.5 * p->finger_thickness);
+  const double hw = 0.5 * p->finger_width;
+  const double mseg = kSteelDensity * Ls * p->finger_width * p->finger_thickness;
+  const double mhook = kSteelDensity * p->hook_length * p->finger_width * p->finger_thickness;
+  const double th_h = p->hook_angle_degrees * kPi / 180.0;
+
+  // segment stiffness, set_finger_stiffness_using_model (myfunctions.cpp:1019-1031)
+  auto seg_stiffness = [&](int n) {
+    if (n == 1) return ((2 * EI) / p->finger_length) * ((N * N) / (double)(N - (1.0 / 3.0)));
+    return (N * EI) / p->finger_length;
+  };
+
+  int first_finger_geom = m->ngeom;
+  for (int f = 0; f < 3; f++) {
+    const double a = f * 2.0 * kPi / 3.0;   // angles[] in myfunctions.cpp:3640
+    const double r[3] = {-std::sin(a), -std::cos(a), 0.0};
+    // intermediate carriage: prismatic "finger_f_prismatic_joint" along r (q = radius x)
+    double in_int[3] = {2e-5, 2e-5, 2e-5};
+    int bint = B.add_body(m->body_base, GM_GRP_FINGER0 + f, zero3, id4, 0.05, zero3, in_int);
+    m->dof_pris[f] = B.add_joint(bint, GM_JNT_SLIDE, r, 0, 5.0, 0, m->dof_base);
+    // finger body frame: x down the finger, y radially outward, z = x cross y
+    double xb[3] = {0, 0, -1};
+    double yb[3] = {r[0], r[1], r[2]};
+    double zb[3] = {xb[1] * yb[2] - xb[2] * yb[1], xb[2] * yb[0] - xb[0] * yb[2],
+                    xb[0] * yb[1] - xb[1] * yb[0]};
+    double R[9] = {xb[0], yb[0], zb[0], xb[1], yb[1], zb[1], xb[2], yb[2], zb[2]};
+    double qf[4];
+    quat_from_mat(R, qf);
+    double in_seg[3];
+    box_inertia(mseg, 0.5 * Ls, 0.5 * p->finger_thickness, hw, in_seg);
+    for (int i = 0; i < 3; i++) in_seg[i] *= p->segment_inertia_scaling;
+    double ipos_seg[3] = {0.5 * Ls, 0, 0};
+    // finger_f body (carries fixed segment link 1): revolute "finger_f_revolute_joint",
+    // +q tilts the tip inward (tilt_fing_x = x - L sin th, myfunctions.cpp:3653)
+    int bf = B.add_body(bint, GM_GRP_FINGER0 + f, zero3, qf, mseg, ipos_seg, in_seg);
+    m->body_finger[f] = bf;
+    double axr[3] = {0, 0, -1};
+    m->dof_rev[f] = B.add_joint(bf, GM_JNT_HINGE, axr, 0, 0.0, 0, m->dof_pris[f]);
+    double gpos[3] = {0.5 * Ls, 0, 0};
+    double gsz[3] = {0.5 * Ls, ht, hw};
+    B.add_geom(bf, GM_GEOM_BOX, GM_CLS_FINGER1 + f, gpos, id4, gsz, 1.0);
+    // segment links 2..N+1, hinge about the plate width axis, +q bends outward
+    int parent = bf;
+    int parent_dof = m->dof_rev[f];
+    for (int k = 1; k <= N; k++) {
+      double pos[3] = {Ls, 0, 0};
+      double mass = mseg;
+      double ipos[3] = {0.5 * Ls, 0, 0};
+      double in[3] = {in_seg[0], in_seg[1], in_seg[2]};
+      bool last = (k == N);
+      if (last) {
+        // fixed hook (fixed_hook_segment): lump its mass into the last link
+        double hc[3] = {Ls + 0.5 * p->hook_length * std::cos(th_h),
+                        -0.5 * p->hook_length * std::sin(th_h), 0};
+        double mt = mseg + mhook;
+        double c[3] = {(mseg * 0.5 * Ls + mhook * hc[0]) / mt, (mhook * hc[1]) / mt, 0};
+        // diagonal of the combined tensor (parallel axis), products of inertia dropped
+        double d1[3] = {0.5 * Ls - c[0], 0 - c[1], 0};
+        double d2[3] = {hc[0] - c[0], hc[1] - c[1], 0};
+        double ih[3];
+        box_inertia(mhook, 0.5 * p->hook_length, 0.5 * p->finger_thickness, hw, ih);
+        for (int i = 0; i < 3; i++) ih[i] *= p->segment_inertia_scaling;
+        in[0] = in_seg[0] + ih[0] + mseg * (d1[1] * d1[1]) + mhook * (d2[1] * d2[1]);
+        in[1] = in_seg[1] + ih[1] + mseg * (d1[0] * d1[0]) + mhook * (d2[0] * d2[0]);
+        in[2] = in_seg[2] + ih[2] + mseg * (d1[0] * d1[0] + d1[1] * d1[1]) +
+                mhook * (d2[0] * d2[0] + d2[1] * d2[1]);
+        mass = mt;
+        set3(ipos, c[0], c[1], c[2]);
+      }
+      int bs = B.add_body(parent, GM_GRP_FINGER0 + f, pos, id4, mass, ipos, in);
+      double axs[3] = {0, 0, 1};
+      int d = B.add_joint(bs, GM_JNT_HINGE, axs, seg_stiffness(k), 0.05, 0, parent_dof);
+      if (k == 1) m->dof_seg[f] = d;
+      B.add_geom(bs, GM_GEOM_BOX, GM_CLS_FINGER1 + f, gpos, id4, gsz, 1.0);
+      if (last) {
+        double hpos[3] = {Ls + 0.5 * p->hook_length * std::cos(th_h),
+                          -0.5 * p->hook_length * std::sin(th_h), 0};
+        double hq[4] = {std::cos(-0.5 * th_h), 0, 0, std::sin(-0.5 * th_h)};
+        double hsz[3] = {0.5 * p->hook_length, ht, hw};
+        B.add_geom(bs, GM_GEOM_BOX, GM_CLS_FINGER1 + f, hpos, hq, hsz, 1.0);
+      }
+      parent = bs;
+      parent_dof = d;
+    }
+  }
+  int last_finger_geom = m->ngeom;
+
+  // ---- palm: slide "palm_prismatic_joint" along -z; palm z=0 is 165 mm above the
+  //      finger end (fingerend_to_palm_Z, myfunctions.cpp:3636) ----
+  {
+    double in[3];
+    box_inertia(0.1, 0.03, 0.03, 0.004, in);
+    m->body_palm = B.add_body(m->body_base, GM_GRP_PALM, zero3, id4, 0.1, zero3, in);
+    double ax[3] = {0, 0, -1};
+    m->dof_palm = B.add_joint(m->body_palm, GM_JNT_SLIDE, ax, 0, 10.0, 0, m->dof_base);
+    double gpos[3] = {0, 0, -(p->finger_length - 165e-3)};
+    double gsz[3] = {0.03, 0.03, 0.004};
+    B.add_geom(m->body_palm, GM_GEOM_BOX, GM_CLS_PALM, gpos, id4, gsz, 1.0);
+  }
+  int palm_geom = m->ngeom - 1;
+
+  // ---- object: free joint, one geom; the per-env object set overrides it ----
+  {
+    double in[3];
+    box_inertia(0.2, 0.02, 0.02, 0.03, in);
+    m->body_obj = B.add_body(0, GM_GRP_OBJECT, zero3, id4, 0.2, zero3, in);
+    m->dof_obj = B.add_joint(m->body_obj, GM_JNT_FREE, zero3, 0, 0, 0, -1);
+    double sz[3] = {0.02, 0.02, 0.03};
+    m->geom_obj = B.add_geom(m->body_obj, GM_GEOM_BOX, GM_CLS_OBJECT, zero3, id4, sz, 1.0);
+  }
+
+  // ---- dof compact slots: object dofs 0..5, base, then chain slot ----
+  for (int d = 0; d < m->nv; d++) {
+    int g = m->dof_group[d];
+    if (g == GM_GRP_OBJECT) m->dof_slot[d] = d - m->dof_obj;
+    else if (g == GM_GRP_BASE) m->dof_slot[d] = 0;
+    else if (g == GM_GRP_PALM) m->dof_slot[d] = 0;
+    else m->dof_slot[d] = d - m->dof_pris[g];
+  }
+
+  // ---- collision pairs: object pairs first (kept first under GM_MAX_CON) ----
+  m->npair = 0;
+  auto add_pair = [&](int a, int b) { m->pair_a[m->npair] = a; m->pair_b[m->npair] = b; m->npair++; };
+  add_pair(m->geom_ground, m->geom_obj);
+  for (int g = first_finger_geom; g < last_finger_geom; g++) add_pair(g, m->geom_obj);
+  add_pair(palm_geom, m->geom_obj);
+  for (int g = first_finger_geom; g < last_finger_geom; g++) add_pair(m->geom_ground, g);
+  add_pair(m->geom_ground, palm_geom);
+  if (m->npair > GM_MAX_PAIR) return GM_E_RANGE;
+
+  // ---- motor locks: prismatic x3, palm (revolute locks disabled, myfunctions.cpp:479) ----
+  m->nlock = 4;
+  for (int f = 0; f < 3; f++) { m->lock_dof[f] = m->dof_pris[f]; m->lock_kind[f] = 0; }
+  m->lock_dof[3] = m->dof_palm; m->lock_kind[3] = 2;
+
+  // ---- keyframe "initial pose": gripper at home (gripper.h:51-52) ----
+  const double xy_home = 134e-3 - 1.0 * (4 * 1e-3 / 1.0);
+  const double z_home = 0 + 1.0 * (4.8768 * 1e-3 / 1.0);
+  for (int i = 0; i < GM_MAX_QPOS; i++) m->qpos0[i] = 0;
+  for (int f = 0; f < 3; f++) m->qpos0[m->jnt_qposadr[m->body_jnt[m->body_finger[f]] - 1]] = xy_home;
+  m->qpos0[m->jnt_qposadr[m->body_jnt[m->body_palm]]] = z_home;
+  {
+    int qa = m->jnt_qposadr[m->body_jnt[m->body_obj]];
+    m->qpos0[qa + 0] = 1.0; m->qpos0[qa + 1] = 1.0; m->qpos0[qa + 2] = 0.03;
+    m->qpos0[qa + 3] = 1.0;
+  }
+  if (m->nbody > GM_MAX_BODY || m->nv > GM_MAX_DOF || m->nq > GM_MAX_QPOS || m->ngeom > GM_MAX_GEOM)
+    return GM_E_RANGE;
+  return GM_OK;
+}
+
+int64_t gm_struct_size(int which) {
+  switch (which) {
+    case 0: return (int64_t)sizeof(gm_settings);
+    case 1: return (int64_t)sizeof(gm_model);
+    case 2: return (int64_t)sizeof(gm_config);
+    case 3: return (int64_t)sizeof(gm_object);
+    case 4: return (int64_t)sizeof(gm_spawn);
+    case 5: return (int64_t)sizeof(gm_model_params);
+    default: return -1;
+  }
+}
+
+void gm_model_info(const gm_model* m, int32_t* o) {
+  o[0] = m->nq; o[1] = m->nv; o[2] = m->nbody; o[3] = m->ngeom; o[4] = m->npair; o[5] = m->n_seg;
+  o[6] = m->dof_base; o[7] = m->dof_palm; o[8] = m->dof_obj;
+  for (int f = 0; f < 3; f++) { o[9 + f] = m->dof_pris[f]; o[12 + f] = m->dof_rev[f]; o[15 + f] = m->dof_seg[f]; }
+}
+
+void gm_config_info(const gm_config* c, int32_t* o) {
+  o[0] = c->n_obs; o[1] = c->n_actions; o[2] = c->sim_steps_per_action; o[3] = c->sensor_fcn; o[4] = c->state_fcn;
+}
+
+void gm_default_settings(gm_settings* s) {
+#define GM_XX(n, t, v) s->n = (t)(v);
+#define GM_SS(n, u, nm, r)                                                        \
+  s->n.in_use = u; s->n.normalise = nm; s->n.read_rate = r;                       \
+  s->n.use_normalisation = 1; s->n.use_noise = 1; s->n.raw_value_offset = 0;      \
+  s->n.noise_mag = 0; s->n.noise_mu = 0; s->n.noise_std = -1; s->n.noise_overriden = 0; \
+  s->n.prev_steps = 1; s->n.readings_per_step = 1; s->n.total_readings = 1;
+#define GM_AA(n, u, v, sg) s->n.in_use = u; s->n.continous = 0; s->n.value = v; s->n.sign = sg;
+#define GM_BR(n, r, d, t) s->n.reward = r; s->n.done = d; s->n.trigger = t;
+#define GM_LR(n, r, d, t, a, b, o) s->n.reward = r; s->n.done = d; s->n.trigger = t; \
+  s->n.min = a; s->n.max = b; s->n.overshoot = o;
+#include "gm_settings.def"
+}
+
+static int n_samples(int fcn, const gm_sensor& s) {
+  if (fcn == GM_SAMPLE_RAW) return s.total_readings - 1;
+  return 2 * s.prev_steps + 1;
+}
+
+int gm_configure(const gm_settings* in, const gm_model* m, gm_config* c) {
+  if (!in || !m || !c) return GM_E_ARG;
+  std::memset(c, 0, sizeof(*c));
+  c->s = *in;
+  gm_settings& s = c->s;
+
+  // ---- action options (mjclass.cpp:109-141) ----
+  for (int i = 0; i < GM_ACTION_CODE_COUNT; i++) c->action_options[i] = -1;
+  int i = 0, kind = 0;
+#define GM_AA(n, u, v, sg)                                                        \
+  s.n.continous = s.continous_actions;                                            \
+  if (s.n.in_use) {                                                               \
+    if (s.n.continous) { c->action_options[i++] = 3 * kind + 2; }                 \
+    else { c->action_options[i++] = 3 * kind + 0; c->action_options[i++] = 3 * kind + 1; } \
+  }                                                                               \
+  kind++;
+#include "gm_settings.def"
+  if (s.use_termination_action) c->action_options[i++] = GM_ACTION_TERMINATION;
+  c->n_actions = i;
+
+  // ---- sampling functions (mjclass.cpp:144-211) ----
+  if (s.sensor_sample_mode < 0 || s.sensor_sample_mode > 6) return GM_E_RANGE;
+  if (s.state_sample_mode < 0 || s.state_sample_mode > 6) return GM_E_RANGE;
+  c->sensor_fcn = s.sensor_sample_mode;
+  c->state_fcn = s.state_sample_mode;
+  c->sensor_fcn_state_override = 0;
+  if (s.state_sample_mode == GM_SAMPLE_SCALED_CHANGE_SQ) {
+    // quirk: writes sampleFcnPtr, stateFcnPtr keeps its previous value (mjclass.cpp:204-206)
+    c->sensor_fcn = GM_SAMPLE_SCALED_CHANGE_SQ;
+    c->state_fcn = GM_SAMPLE_SIGN;   // previous default; see DESIGN.md quirks
+    c->sensor_fcn_state_override = 1;
+  }
+
+  // ---- timestep / sim steps (auto timestep search is out of scope: model dt is the
+  //      pinned "found" value; mjclass.cpp:241-308) ----
+  c->timestep = m->timestep;
+  s.mujoco_timestep = m->timestep;
+  if (s.auto_sim_steps) s.sim_steps_per_action = (int32_t)std::ceil(s.time_for_action / c->timestep);
+  if (s.sim_steps_per_action < 1) return GM_E_RANGE;
+  c->sim_steps_per_action = s.sim_steps_per_action;
+
+  // ---- gauge calibration (mjclass.cpp:273-291): analytic Euler-Bernoulli stand-in for
+  //      calibrate_simulated_sensors(); normalise = raw gauge under the saturation load ----
+  double Ifing = m->finger_width * std::pow(m->finger_thickness, 3) / 12.0;
+  double yield = (m->yield_stress * Ifing) / (0.5 * m->finger_thickness) / m->finger_length;
+  if (s.auto_calibrate_gauges) {
+    double P = s.saturation_yield_factor * yield;
+    double x = m->gauge_xpos, L = m->finger_length;
+    double raw = 1000.0 * P * x * x * (3 * L - x) / (6 * m->finger_EI);
+    s.bending_gauge.normalise = (float)raw;
+    c->sim_gauge_raw_to_N_factor = P / (double)s.bending_gauge.normalise;
+    s.wrist_sensor_Z.raw_value_offset = 0.0f;   // userdata[2] is never written
+  } else {
+    c->sim_gauge_raw_to_N_factor = 1.0;
+  }
+
+  // ---- sensor reading counts (mjclass.cpp:5236-5265) ----
+  double time_per_step = c->timestep * s.sim_steps_per_action;
+#define GM_SS(n, u, nm, r) s.n.prev_steps = s.sensor_n_prev_steps;
+#include "gm_settings.def"
+  gm_sensor* state_sensors[5] = {&s.motor_state_sensor, &s.base_state_sensor_XY,
+                                 &s.base_state_sensor_Z, &s.base_state_sensor_yaw,
+                                 &s.cartesian_contacts_XYZ};
+  for (auto* ss : state_sensors) {
+    ss->prev_steps = s.state_n_prev_steps;
+    ss->readings_per_step = 1;
+    ss->total_readings = 1 + ss->readings_per_step * ss->prev_steps;
+  }
+  gm_sensor* other[5] = {&s.bending_gauge, &s.axial_gauge, &s.palm_sensor,
+                         &s.wrist_sensor_XY, &s.wrist_sensor_Z};
+  for (auto* ss : other) {
+    double rs = time_per_step * ss->read_rate;
+    ss->readings_per_step = (int32_t)std::floor(rs);
+    ss->total_readings = 1 + ss->readings_per_step * ss->prev_steps;
+    if (ss->total_readings > GM_RING || ss->total_readings < 1) return GM_E_RANGE;
+  }
+  for (auto* ss : state_sensors)
+    if (ss->total_readings > GM_RING) return GM_E_RANGE;
+
+  // ---- observation size (get_observation order, mjclass.cpp:1721-1936) ----
+  int n = 0;
+  if (s.bending_gauge.in_use) n += 3 * n_samples(c->sensor_fcn, s.bending_gauge);
+  if (s.axial_gauge.in_use) n += 3 * n_samples(c->sensor_fcn, s.axial_gauge);
+  if (s.palm_sensor.in_use) n += n_samples(c->sensor_fcn, s.palm_sensor);
+  if (s.wrist_sensor_XY.in_use) n += 2 * n_samples(c->sensor_fcn, s.wrist_sensor_XY);
+  if (s.wrist_sensor_Z.in_use) n += n_samples(c->sensor_fcn, s.wrist_sensor_XY);  // quirk 1806
+  if (s.motor_state_sensor.in_use) n += 3 * n_samples(c->state_fcn, s.motor_state_sensor);
+  if (s.base_state_sensor_XY.in_use) n += 2 * n_samples(c->state_fcn, s.base_state_sensor_XY);
+  if (s.base_state_sensor_Z.in_use) n += n_samples(c->state_fcn, s.base_state_sensor_Z);
+  if (s.base_state_sensor_yaw.in_use) n += n_samples(c->state_fcn, s.base_state_sensor_yaw);
+  if (s.cartesian_contacts_XYZ.in_use) n += 12 * (2 * s.cartesian_contacts_XYZ.prev_steps + 1);
+  c->n_obs = n;
+
+  // ---- noise parameters that do not need the RNG (apply_noise_params, 5293-5346) ----
+#define GM_SS(nm, u, no, r)                                                        \
+  if (!s.nm.noise_overriden) {                                                    \
+    s.nm.noise_mag = (float)s.sensor_noise_mag;                                   \
+    s.nm.noise_std = (float)s.sensor_noise_std;                                   \
+    s.nm.noise_mu = (float)s.sensor_noise_mu;                                     \
+  }
+#include "gm_settings.def"
+  for (auto* ss : state_sensors) {
+    if (!ss->noise_overriden) {
+      ss->noise_mag = (float)s.state_noise_mag;
+      ss->noise_mu = (float)s.state_noise_mu;
+      ss->noise_std = (float)s.state_noise_std;
+    }
+  }
+
+  // ---- base limits (myfunctions.cpp:245-261, 2286-2307) ----
+  double bmin[6] = {-500e-3, -500e-3, -30e-3, -0.5, -0.5, -kPi / 2};
+  double bmax[6] = {500e-3, 500e-3, 30e-3, 0.5, 0.5, kPi / 2};
+  for (int k = 0; k < 6; k++) { c->base_min[k] = bmin[k]; c->base_max[k] = bmax[k]; }
+  return GM_OK;
+}
+
+// ---- synthetic object sets (the reference's MJCF object sets are unavailable) ----
+static uint64_t splitmix(uint64_t& x) {
+  uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static double unif(uint64_t& x, double a, double b) {
+  return a + (b - a) * ((splitmix(x) >> 11) * (1.0 / 9007199254740992.0));
+}
+
+int gm_make_object_set(const char* name, uint64_t seed, gm_object* out, int max_objects) {
+  if (!name || !out) return GM_E_ARG;
+  std::string nm(name);
+  int n = 0;
+  auto add = [&](int type, double a, double b, double c, double mass) {
+    if (n >= max_objects) return;
+    out[n].type = type;
+    out[n].size[0] = a; out[n].size[1] = b; out[n].size[2] = c;
+    out[n].mass = mass;
+    out[n].friction = 1.0;
+    n++;
+  };
+  if (nm == "cylinder") {                       // configs[1]: one cylinder r=20 mm h=60 mm
+    add(GM_GEOM_CYLINDER, 0.020, 0.030, 0, 0.2);
+  } else if (nm == "set1_synthetic") {          // configs[0] stand-in
+    add(GM_GEOM_BOX, 0.020, 0.020, 0.030, 0.2);
+    add(GM_GEOM_CYLINDER, 0.020, 0.030, 0, 0.2);
+    add(GM_GEOM_SPHERE, 0.025, 0, 0, 0.2);
+  } else if (nm == "set6_synthetic") {          // configs[2]: 20 mixed objects
+    uint64_t x = seed ^ 0x5E76ull;
+    for (int k = 0; k < 20; k++) {
+      int t = k % 3;
+      double mass = unif(x, 0.05, 0.4);
+      if (t == 0) add(GM_GEOM_BOX, unif(x, 0.010, 0.030), unif(x, 0.010, 0.030), unif(x, 0.010, 0.030), mass);
+      else if (t == 1) add(GM_GEOM_CYLINDER, unif(x, 0.010, 0.030), unif(x, 0.010, 0.030), 0, mass);
+      else add(GM_GEOM_SPHERE, unif(x, 0.010, 0.030), 0, 0, mass);
+    }
+  } else {
+    return GM_E_ARG;
+  }
+  return n;
+}
+
+}  // extern "C"

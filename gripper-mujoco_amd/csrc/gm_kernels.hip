@@ -1,0 +1,2162 @@
+// gm_kernels.hip -- the MI355X (gfx950) batched env-step hot path.
+//
+// One 64-lane workgroup (one wavefront) per env.  A launch runs a whole
+// MjClass::action_step() (mjclass.cpp:1483-1508): S = sim_steps_per_action
+// physics substeps, each = MuJoCo-style mj_step1 / control / mj_step2
+// (myfunctions.cpp:1873-1898) + after_step/update_all (1900-1908, 2110-2284)
+// + monitor_sensors (mjclass.cpp:741-898), then sense_gripper_state,
+// update_env, get_observation, is_done and reward -- without leaving the chip.
+// Per-env state is moved HBM -> LDS once at entry and back once at exit; all
+// per-substep working data (kinematics, mass matrix, contacts, constraint
+// rows) stays in LDS / VGPRs.  Lane mapping per stage:
+//   - kinematic chains (3 fingers, palm, object): one lane per chain
+//   - mass-matrix rows, bias/passive/actuator forces: one lane per dof
+//   - collision: one lane per candidate geom pair (63 pairs <= 64 lanes)
+//   - constraint rows (pyramid edges + motor locks): one lane per row; the
+//     row's Delassus column A[:, j] lives in that lane's VGPRs and projected
+//     Gauss-Seidel broadcasts each row's update with v_readlane (no LDS, no
+//     reductions in the inner loop)
+//   - reference scalar logic (stepper in fp64, events, RNG): lane 0
+// The algorithm is the engine spec restated in oracle/oracle.c (fp64); this
+// file is the fp32 device implementation of the same spec.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "gm_state.h"
+
+#define NT 64
+#define CLMAX (GM_MAX_SEG + 2)
+#define TRI(p, q) ((p) * ((p) + 1) / 2 + (q))
+#define TRIF ((CLMAX + 1) * (CLMAX + 2) / 2)
+#define CW 20   // compact row: obj[6], base, chain[CLMAX], group (as float bits)
+#define PI_F 3.14159265358979f
+
+struct DebugOut {
+  int32_t* ncon;      // [n_envs]
+  float* contact;     // [n_envs][GM_MAX_CON][16]
+  float* efc_force;   // [n_envs][GM_MAX_EFC]
+  float* qacc;        // [n_envs][GM_MAX_DOF]
+};
+
+struct __align__(16) Shared {
+  GmEnvState s;
+  float qpos_pre[GM_MAX_QPOS];
+  float qacc_s[GM_MAX_DOF], qacc[GM_MAX_DOF], frc[GM_MAX_DOF], z[GM_MAX_DOF];
+  float xpos[GM_MAX_BODY][3];
+  float xmat[GM_MAX_BODY][9];
+  float cinert[GM_MAX_BODY][10];
+  float Ic[GM_MAX_BODY][10];
+  float cfrc[GM_MAX_BODY][6];
+  float cdof[GM_MAX_DOF][6];
+  float gxpos[GM_MAX_GEOM][3];
+  float gxmat[GM_MAX_GEOM][9];
+  float Hf[3][TRIF], Hp[3], Ho[21], Hbb;
+  float Df[3][CLMAX + 1], Dp[2], Do[6], Dbb;
+  float bdelta[5];
+  float con[GM_MAX_CON][20];   // dist, pos3, frame9, mu, force3, g1, g2, (pad)
+  float Y[GM_MAX_EFC][CW];
+  float efc_f[GM_MAX_EFC];
+  int32_t cnt[NT];
+  int32_t ncon, nefc, nlockrows, overflow;
+  float forces[32];            // extract_forces_faster results (see extract_forces)
+  int32_t have_forces;
+  float gauge_tmp[3];
+};
+
+// ------------------------------------------------------------ small math
+__device__ __forceinline__ float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+__device__ __forceinline__ void cross3(float* r, const float* a, const float* b) {
+  float t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ void mulmv3(float* r, const float* M, const float* v) {
+  float t0 = M[0] * v[0] + M[1] * v[1] + M[2] * v[2];
+  float t1 = M[3] * v[0] + M[4] * v[1] + M[5] * v[2];
+  float t2 = M[6] * v[0] + M[7] * v[1] + M[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ void mulmtv3(float* r, const float* M, const float* v) {
+  float t0 = M[0] * v[0] + M[3] * v[1] + M[6] * v[2];
+  float t1 = M[1] * v[0] + M[4] * v[1] + M[7] * v[2];
+  float t2 = M[2] * v[0] + M[5] * v[1] + M[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ void quat2mat(float* R, const float* q) {
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z);     R[2] = 2 * (x * z + w * y);
+  R[3] = 2 * (x * y + w * z);     R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
+  R[6] = 2 * (x * z - w * y);     R[7] = 2 * (y * z + w * x);     R[8] = 1 - 2 * (x * x + y * y);
+}
+__device__ __forceinline__ void quatmul(float* r, const float* a, const float* b) {
+  float t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  float t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  float t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  float t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
+}
+__device__ __forceinline__ void quatnorm(float* q) {
+  float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < 1e-15f) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  float in = 1.0f / n;
+  for (int i = 0; i < 4; i++) q[i] *= in;
+}
+__device__ __forceinline__ void ld3(float* r, const double* a) { r[0] = (float)a[0]; r[1] = (float)a[1]; r[2] = (float)a[2]; }
+__device__ __forceinline__ void ld4(float* r, const double* a) { r[0] = (float)a[0]; r[1] = (float)a[1]; r[2] = (float)a[2]; r[3] = (float)a[3]; }
+
+// spatial inertia (I_O sym6, h = m c, m) times motion [w; v]
+__device__ __forceinline__ void inert_mul(float* r, const float* ci, const float* v) {
+  const float* w = v; const float* u = v + 3;
+  float Iw0 = ci[0] * w[0] + ci[3] * w[1] + ci[4] * w[2];
+  float Iw1 = ci[3] * w[0] + ci[1] * w[1] + ci[5] * w[2];
+  float Iw2 = ci[4] * w[0] + ci[5] * w[1] + ci[2] * w[2];
+  float hxu[3], hxw[3];
+  cross3(hxu, ci + 6, u);
+  cross3(hxw, ci + 6, w);
+  r[0] = Iw0 + hxu[0]; r[1] = Iw1 + hxu[1]; r[2] = Iw2 + hxu[2];
+  r[3] = ci[9] * u[0] - hxw[0]; r[4] = ci[9] * u[1] - hxw[1]; r[5] = ci[9] * u[2] - hxw[2];
+}
+__device__ __forceinline__ void cross_motion(float* r, const float* v, const float* mv) {
+  float a[3], b[3], c[3];
+  cross3(a, v, mv); cross3(b, v, mv + 3); cross3(c, v + 3, mv);
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
+  r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
+}
+__device__ __forceinline__ void cross_force(float* r, const float* v, const float* f) {
+  float a[3], b[3], c[3];
+  cross3(a, v, f); cross3(b, v + 3, f + 3); cross3(c, v, f + 3);
+  r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
+  r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
+}
+__device__ __forceinline__ float dot6(const float* a, const float* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+
+// ------------------------------------------------------------ topology helpers
+// chain c: 0..2 finger, 3 palm, 4 object.  Chain lengths (positions >= 1).
+__device__ __forceinline__ int chain_len(const GmTopo* T, int c) { return c < 3 ? T->CL : (c == 3 ? 1 : 6); }
+__device__ __forceinline__ int chain_body(const GmTopo* T, int c, int p) {
+  if (c < 3) return T->body_f0[c] + p - 1;
+  if (c == 3) return T->body_palm;
+  return T->body_obj;
+}
+__device__ __forceinline__ int chain_dof(const GmTopo* T, int c, int p) {
+  if (c < 3) return T->dof_f0[c] + p - 1;
+  if (c == 3) return T->dof_palm;
+  return T->dof_obj + p;   // object uses positions 0..5
+}
+// H/L storage accessor: chain c, positions p >= q (object: 0..5, others: 0 = base)
+__device__ __forceinline__ float& Hat(Shared& S, int c, int p, int q) {
+  if (c < 3) return (p == 0) ? S.Hbb : S.Hf[c][TRI(p, q)];
+  if (c == 3) return (p == 0) ? S.Hbb : S.Hp[TRI(p, q)];
+  return S.Ho[TRI(p, q)];
+}
+
+// ============================================================ kinematics
+// mj_kinematics restatement (oracle.c: fk), one lane per chain.
+__device__ void body_fk(Shared& S, const gm_model* __restrict__ m, int b, const float* ppos,
+                        const float* pquat, float* quat_out) {
+  float bp[3], bq[4], t[3], q[4];
+  ld3(bp, m->body_pos[b]);
+  ld4(bq, m->body_quat[b]);
+  float Rp[9];
+  quat2mat(Rp, pquat);
+  mulmv3(t, Rp, bp);
+  float xp[3] = {ppos[0] + t[0], ppos[1] + t[1], ppos[2] + t[2]};
+  quatmul(q, pquat, bq);
+  int j = m->body_jnt[b];
+  if (j >= 0) {
+    int qa = m->jnt_qposadr[j];
+    int type = m->jnt_type[j];
+    if (type == GM_JNT_SLIDE) {
+      float R[9], ax[3], wa[3];
+      quat2mat(R, q);
+      ld3(ax, m->jnt_axis[j]);
+      mulmv3(wa, R, ax);
+      float qv = S.s.qpos[qa];
+      xp[0] += wa[0] * qv; xp[1] += wa[1] * qv; xp[2] += wa[2] * qv;
+    } else if (type == GM_JNT_HINGE) {
+      float ang = S.s.qpos[qa];
+      float sn = sinf(0.5f * ang), cs = cosf(0.5f * ang);
+      float ql[4] = {cs, (float)m->jnt_axis[j][0] * sn, (float)m->jnt_axis[j][1] * sn, (float)m->jnt_axis[j][2] * sn};
+      quatmul(q, q, ql);
+    } else {
+      xp[0] = S.s.qpos[qa]; xp[1] = S.s.qpos[qa + 1]; xp[2] = S.s.qpos[qa + 2];
+      q[0] = S.s.qpos[qa + 3]; q[1] = S.s.qpos[qa + 4]; q[2] = S.s.qpos[qa + 5]; q[3] = S.s.qpos[qa + 6];
+    }
+  }
+  quatnorm(q);
+  S.xpos[b][0] = xp[0]; S.xpos[b][1] = xp[1]; S.xpos[b][2] = xp[2];
+  float R[9];
+  quat2mat(R, q);
+  for (int k = 0; k < 9; k++) S.xmat[b][k] = R[k];
+  for (int k = 0; k < 4; k++) quat_out[k] = q[k];
+  // world-origin spatial inertia
+  float ip[3], c[3];
+  ld3(ip, m->body_ipos[b]);
+  mulmv3(c, R, ip);
+  c[0] += xp[0]; c[1] += xp[1]; c[2] += xp[2];
+  float I[3] = {(float)m->body_inertia[b][0], (float)m->body_inertia[b][1], (float)m->body_inertia[b][2]};
+  float mass = (float)m->body_mass[b];
+  if (b == m->body_obj) {
+    mass = S.s.obj_mass;
+    I[0] = S.s.obj_inertia[0]; I[1] = S.s.obj_inertia[1]; I[2] = S.s.obj_inertia[2];
+  }
+  float Iw[9];
+  for (int i = 0; i < 3; i++)
+    for (int k = 0; k < 3; k++)
+      Iw[3 * i + k] = R[3 * i] * I[0] * R[3 * k] + R[3 * i + 1] * I[1] * R[3 * k + 1] + R[3 * i + 2] * I[2] * R[3 * k + 2];
+  float cc = dot3(c, c);
+  float* ci = S.cinert[b];
+  ci[0] = Iw[0] + mass * (cc - c[0] * c[0]);
+  ci[1] = Iw[4] + mass * (cc - c[1] * c[1]);
+  ci[2] = Iw[8] + mass * (cc - c[2] * c[2]);
+  ci[3] = Iw[1] - mass * c[0] * c[1];
+  ci[4] = Iw[2] - mass * c[0] * c[2];
+  ci[5] = Iw[5] - mass * c[1] * c[2];
+  ci[6] = mass * c[0]; ci[7] = mass * c[1]; ci[8] = mass * c[2];
+  ci[9] = mass;
+  // motion subspaces of this body's dofs
+  if (j >= 0) {
+    int d0 = m->jnt_dofadr[j];
+    int type = m->jnt_type[j];
+    if (type == GM_JNT_FREE) {
+      for (int k = 0; k < 3; k++) {
+        float* cd = S.cdof[d0 + k];
+        cd[0] = cd[1] = cd[2] = 0; cd[3] = cd[4] = cd[5] = 0; cd[3 + k] = 1;
+      }
+      for (int k = 0; k < 3; k++) {
+        float* cd = S.cdof[d0 + 3 + k];
+        float w[3] = {R[k], R[3 + k], R[6 + k]};
+        cd[0] = w[0]; cd[1] = w[1]; cd[2] = w[2];
+        cross3(cd + 3, xp, w);
+      }
+    } else {
+      float ax[3], wa[3];
+      ld3(ax, m->jnt_axis[j]);
+      mulmv3(wa, R, ax);
+      float* cd = S.cdof[d0];
+      if (type == GM_JNT_SLIDE) {
+        cd[0] = cd[1] = cd[2] = 0; cd[3] = wa[0]; cd[4] = wa[1]; cd[5] = wa[2];
+      } else {
+        cd[0] = wa[0]; cd[1] = wa[1]; cd[2] = wa[2];
+        cross3(cd + 3, xp, wa);   // anchor at the body origin in this model
+      }
+    }
+  }
+}
+
+__device__ void kinematics(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+  // base body (world child) first, then one lane per chain (fingers 0..2, palm 3, object 4)
+  __shared__ float base_quat[4];
+  if (lane == 0) {
+    float q0[4] = {1, 0, 0, 0}, p0[3] = {0, 0, 0};
+    body_fk(S, m, T->body_base, p0, q0, base_quat);
+  }
+  __syncthreads();
+  if (lane < 5) {
+    float q[4];
+    if (lane == 4) {
+      float q0[4] = {1, 0, 0, 0}, p0[3] = {0, 0, 0};
+      body_fk(S, m, T->body_obj, p0, q0, q);
+    } else {
+      float pq[4] = {base_quat[0], base_quat[1], base_quat[2], base_quat[3]};
+      float pp[3] = {S.xpos[T->body_base][0], S.xpos[T->body_base][1], S.xpos[T->body_base][2]};
+      int L = chain_len(T, lane);
+      for (int p = 1; p <= L; p++) {
+        int b = chain_body(T, lane, p);
+        body_fk(S, m, b, pp, pq, q);
+        pp[0] = S.xpos[b][0]; pp[1] = S.xpos[b][1]; pp[2] = S.xpos[b][2];
+        pq[0] = q[0]; pq[1] = q[1]; pq[2] = q[2]; pq[3] = q[3];
+      }
+    }
+  }
+  __syncthreads();
+  // geoms: one lane per geom
+  if (lane < T->ngeom) {
+    int g = lane;
+    int b = m->geom_body[g];
+    float R[9];
+    if (b == 0) {
+      R[0] = 1; R[1] = 0; R[2] = 0; R[3] = 0; R[4] = 1; R[5] = 0; R[6] = 0; R[7] = 0; R[8] = 1;
+    } else {
+      for (int k = 0; k < 9; k++) R[k] = S.xmat[b][k];
+    }
+    float gp[3], t[3], gq[4], Rg[9];
+    ld3(gp, m->geom_pos[g]);
+    mulmv3(t, R, gp);
+    float bp0 = b == 0 ? 0.f : S.xpos[b][0], bp1 = b == 0 ? 0.f : S.xpos[b][1], bp2 = b == 0 ? 0.f : S.xpos[b][2];
+    S.gxpos[g][0] = bp0 + t[0]; S.gxpos[g][1] = bp1 + t[1]; S.gxpos[g][2] = bp2 + t[2];
+    ld4(gq, m->geom_quat[g]);
+    quat2mat(Rg, gq);
+    for (int i = 0; i < 3; i++)
+      for (int k = 0; k < 3; k++)
+        S.gxmat[g][3 * i + k] = R[3 * i] * Rg[k] + R[3 * i + 1] * Rg[3 + k] + R[3 * i + 2] * Rg[6 + k];
+  }
+}
+
+// ============================================================ CRB + RNE
+__device__ void crb_rne(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+  // ---- composite inertia and RNE forward/backward along each chain (lanes 0..4) ----
+  if (lane < 5) {
+    int c = lane;
+    int L = chain_len(T, c);
+    // forward: velocities and bias accelerations
+    float cvel[6], cacc[6];
+    for (int k = 0; k < 6; k++) { cvel[k] = 0; cacc[k] = 0; }
+    cacc[3] = -(float)m->gravity[0]; cacc[4] = -(float)m->gravity[1]; cacc[5] = -(float)m->gravity[2];
+    if (c < 4) {
+      // base body
+      int db = T->dof_base;
+      float cdd[6];
+      cross_motion(cdd, cvel, S.cdof[db]);
+      float qd = S.s.qvel[db];
+      for (int k = 0; k < 6; k++) { cvel[k] += S.cdof[db][k] * qd; cacc[k] += cdd[k] * qd; }
+      if (c == 0) {
+        float t1[6], t2[6], f[6];
+        inert_mul(f, S.cinert[T->body_base], cacc);
+        inert_mul(t1, S.cinert[T->body_base], cvel);
+        cross_force(t2, cvel, t1);
+        for (int k = 0; k < 6; k++) S.cfrc[T->body_base][k] = f[k] + t2[k];
+      }
+      for (int p = 1; p <= L; p++) {
+        int b = chain_body(T, c, p), d = chain_dof(T, c, p);
+        float cdd2[6];
+        cross_motion(cdd2, cvel, S.cdof[d]);
+        float qv = S.s.qvel[d];
+        for (int k = 0; k < 6; k++) { cvel[k] += S.cdof[d][k] * qv; cacc[k] += cdd2[k] * qv; }
+        float t1[6], t2[6], f[6];
+        inert_mul(f, S.cinert[b], cacc);
+        inert_mul(t1, S.cinert[b], cvel);
+        cross_force(t2, cvel, t1);
+        for (int k = 0; k < 6; k++) S.cfrc[b][k] = f[k] + t2[k];
+      }
+      // backward within the chain
+      for (int p = L; p >= 2; p--) {
+        int b = chain_body(T, c, p), pb = chain_body(T, c, p - 1);
+        for (int k = 0; k < 6; k++) S.cfrc[pb][k] += S.cfrc[b][k];
+      }
+      // composite inertia backward
+      for (int p = L; p >= 1; p--) {
+        int b = chain_body(T, c, p);
+        for (int k = 0; k < 10; k++) S.Ic[b][k] = S.cinert[b][k] + (p < L ? S.Ic[chain_body(T, c, p + 1)][k] : 0.0f);
+      }
+    } else {
+      // object: free joint on one body
+      int b = T->body_obj, d0 = T->dof_obj;
+      for (int k = 0; k < 3; k++) {
+        float qv = S.s.qvel[d0 + k];
+        for (int t = 0; t < 6; t++) cvel[t] += S.cdof[d0 + k][t] * qv;
+      }
+      float cdd[3][6];
+      for (int k = 0; k < 3; k++) cross_motion(cdd[k], cvel, S.cdof[d0 + 3 + k]);
+      for (int k = 0; k < 3; k++) {
+        float qv = S.s.qvel[d0 + 3 + k];
+        for (int t = 0; t < 6; t++) cvel[t] += S.cdof[d0 + 3 + k][t] * qv;
+      }
+      for (int k = 0; k < 3; k++) {
+        float qv = S.s.qvel[d0 + 3 + k];
+        for (int t = 0; t < 6; t++) cacc[t] += cdd[k][t] * qv;
+      }
+      float t1[6], t2[6], f[6];
+      inert_mul(f, S.cinert[b], cacc);
+      inert_mul(t1, S.cinert[b], cvel);
+      cross_force(t2, cvel, t1);
+      for (int k = 0; k < 6; k++) S.cfrc[b][k] = f[k] + t2[k];
+      for (int k = 0; k < 10; k++) S.Ic[b][k] = S.cinert[b][k];
+    }
+  }
+  __syncthreads();
+  // base body: add chain roots (fingers' intermediates and palm)
+  if (lane == 0) {
+    int bb = T->body_base;
+    float ic[10], f[6];
+    for (int k = 0; k < 10; k++) ic[k] = S.cinert[bb][k];
+    for (int k = 0; k < 6; k++) f[k] = S.cfrc[bb][k];
+    for (int c = 0; c < 4; c++) {
+      int r = chain_body(T, c, 1);
+      for (int k = 0; k < 10; k++) ic[k] += S.Ic[r][k];
+      for (int k = 0; k < 6; k++) f[k] += S.cfrc[r][k];
+    }
+    for (int k = 0; k < 10; k++) S.Ic[bb][k] = ic[k];
+    for (int k = 0; k < 6; k++) S.cfrc[bb][k] = f[k];
+  }
+  __syncthreads();
+}
+
+// ============================================================ mass matrix rows + forces
+__device__ __forceinline__ void ctrl_gains(const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int d,
+                                           float* kp, float* kd) {
+  *kp = 0; *kd = 0;
+  for (int f = 0; f < 3; f++) {
+    if (d == m->dof_pris[f]) { *kp = (float)m->kp_gripper[0]; *kd = (float)m->kd_gripper[0]; }
+    if (d == m->dof_rev[f]) { *kp = (float)m->kp_gripper[1]; *kd = (float)m->kd_gripper[1]; }
+  }
+  if (d == m->dof_palm) { *kp = (float)m->kp_gripper[2]; *kd = (float)m->kd_gripper[2]; }
+  if (d == m->dof_base) { *kp = (float)m->kp_base[2]; *kd = (float)m->kd_base[2]; }
+}
+
+// lane per dof: H row entries (compact), bias/passive/actuator force
+__device__ void mass_and_forces(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+  if (lane < T->nv) {
+    int d = lane;
+    int b = m->dof_body[d];
+    float F[6];
+    inert_mul(F, S.Ic[b], S.cdof[d]);
+    float h = (float)m->timestep;
+    int j = m->body_jnt[b];
+    float kp, kd;
+    ctrl_gains(m, T, d, &kp, &kd);
+    float add = (float)m->jnt_armature[j] + h * ((float)m->jnt_damping[j] + kd);
+    if (m->jnt_type[j] != GM_JNT_FREE) add += h * h * ((float)m->jnt_stiffness[j] + kp);
+    int c = T->body_group[b];          // 0..2 finger, 3 palm, 5 object, 4 base
+    if (c == GM_GRP_BASE) {
+      S.Hbb = dot6(S.cdof[d], F) + add;
+    } else if (c == GM_GRP_OBJECT) {
+      int p = d - T->dof_obj;
+      for (int q = 0; q <= p; q++) {
+        float v = dot6(S.cdof[T->dof_obj + q], F);
+        if (q == p) v += add;
+        S.Ho[TRI(p, q)] = v;
+      }
+    } else {
+      int p = T->body_cpos[b];
+      for (int q = 0; q <= p; q++) {
+        int dq = (q == 0) ? T->dof_base : chain_dof(T, c, q);
+        float v = dot6(S.cdof[dq], F);
+        if (q == p) v += add;
+        if (c < 3) S.Hf[c][TRI(p, q)] = v; else S.Hp[TRI(p, q)] = v;
+      }
+    }
+    // forces: passive springs/damping, PD control (target_.next, base target), RNE bias
+    float bias = dot6(S.cdof[d], S.cfrc[b]);
+    float pas = 0;
+    if (m->jnt_type[j] != GM_JNT_FREE) pas -= (float)m->jnt_stiffness[j] * S.s.qpos[d];
+    pas -= (float)m->jnt_damping[j] * S.s.qvel[d];
+    float act = 0;
+    float q = S.s.qpos[d], v = S.s.qvel[d];
+    for (int f = 0; f < 3; f++) {
+      if (d == m->dof_pris[f]) act = -((q - (float)S.s.next.x) * kp + v * kd);
+      if (d == m->dof_rev[f]) act = -((q - (float)S.s.next.th) * kp + v * kd);
+    }
+    if (d == m->dof_palm) act = -((q - (float)S.s.next.z) * kp + v * kd);
+    if (d == m->dof_base) act = -((q - (float)S.s.base[2]) * kp + v * kd);
+    S.frc[d] = pas + act - bias;
+  }
+  __syncthreads();
+}
+
+// ============================================================ LTDL factor + solves
+__device__ void factor(Shared& S, const GmTopo* __restrict__ T, int lane) {
+  if (lane < 5) {
+    int c = lane;
+    int L = chain_len(T, c);
+    float delta = 0;
+    if (c < 4) {
+      for (int k = L; k >= 1; k--) {
+        float hk = Hat(S, c, k, k);
+        for (int i = k - 1; i >= 0; i--) {
+          float a = Hat(S, c, k, i) / hk;
+          for (int jj = i; jj >= 0; jj--) {
+            float v = Hat(S, c, k, jj) * a;
+            if (i == 0 && jj == 0) delta += v; else Hat(S, c, i, jj) -= v;
+          }
+          Hat(S, c, k, i) = a;
+        }
+      }
+      S.bdelta[c] = delta;
+      for (int p = 1; p <= L; p++) { float dv = Hat(S, c, p, p); if (c < 3) S.Df[c][p] = dv; else S.Dp[p] = dv; }
+    } else {
+      for (int k = 5; k >= 1; k--) {
+        float hk = S.Ho[TRI(k, k)];
+        for (int i = k - 1; i >= 0; i--) {
+          float a = S.Ho[TRI(k, i)] / hk;
+          for (int jj = i; jj >= 0; jj--) S.Ho[TRI(i, jj)] -= S.Ho[TRI(k, jj)] * a;
+          S.Ho[TRI(k, i)] = a;
+        }
+      }
+      for (int p = 0; p < 6; p++) S.Do[p] = S.Ho[TRI(p, p)];
+    }
+  }
+  __syncthreads();
+  if (lane == 0) S.Dbb = S.Hbb - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3]);
+  __syncthreads();
+}
+
+__device__ __forceinline__ float Dof(Shared& S, int c, int p) {
+  if (c < 3) return p == 0 ? S.Dbb : S.Df[c][p];
+  if (c == 3) return p == 0 ? S.Dbb : S.Dp[p];
+  return S.Do[p];
+}
+
+// x = H^-1 b over full dof vectors (b, x in LDS, may alias)
+__device__ void solve_full(Shared& S, const GmTopo* __restrict__ T, const float* b, float* x, int lane) {
+  // L^T y = b  (leaves -> root); chain lanes, base accumulated
+  float ych[CLMAX + 1];
+  float ybase_part = 0;
+  int c = lane;
+  if (lane < 5) {
+    int L = chain_len(T, c);
+    if (c < 4) {
+      for (int p = 1; p <= L; p++) ych[p] = b[chain_dof(T, c, p)];
+      for (int k = L; k >= 1; k--) {
+        for (int i = k - 1; i >= 1; i--) ych[i] -= Hat(S, c, k, i) * ych[k];
+        ybase_part += Hat(S, c, k, 0) * ych[k];
+      }
+      for (int p = 1; p <= L; p++) ych[p] /= Dof(S, c, p);
+    } else {
+      for (int p = 0; p < 6; p++) ych[p] = b[T->dof_obj + p];
+      for (int k = 5; k >= 1; k--)
+        for (int i = k - 1; i >= 0; i--) ych[i] -= S.Ho[TRI(k, i)] * ych[k];
+      for (int p = 0; p < 6; p++) ych[p] /= S.Do[p];
+    }
+    if (c < 4) S.bdelta[c] = ybase_part;
+  }
+  __syncthreads();
+  float xbase = (b[T->dof_base] - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3])) / S.Dbb;
+  __syncthreads();
+  if (lane < 5) {
+    int L = chain_len(T, c);
+    if (c < 4) {
+      float xs[CLMAX + 1];
+      xs[0] = xbase;
+      for (int k = 1; k <= L; k++) {
+        float v = ych[k];
+        for (int i = k - 1; i >= 0; i--) v -= Hat(S, c, k, i) * xs[i];
+        xs[k] = v;
+        x[chain_dof(T, c, k)] = v;
+      }
+      if (c == 0) x[T->dof_base] = xbase;
+    } else {
+      float xs[6];
+      for (int k = 0; k < 6; k++) {
+        float v = ych[k];
+        for (int i = k - 1; i >= 0; i--) v -= S.Ho[TRI(k, i)] * xs[i];
+        xs[k] = v;
+        x[T->dof_obj + k] = v;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// ============================================================ collision
+struct Hit { float dist, pos[3], n[3]; };
+
+__device__ void make_frame(float* F, const float* n) {
+  float a[3] = {0, 0, 0};
+  if (fabsf(n[0]) < 0.5f) a[0] = 1; else a[1] = 1;
+  float d = dot3(a, n);
+  float t1[3] = {a[0] - d * n[0], a[1] - d * n[1], a[2] - d * n[2]};
+  float l = sqrtf(dot3(t1, t1));
+  t1[0] /= l; t1[1] /= l; t1[2] /= l;
+  float t2[3];
+  cross3(t2, n, t1);
+  F[0] = n[0]; F[1] = n[1]; F[2] = n[2];
+  F[3] = t1[0]; F[4] = t1[1]; F[5] = t1[2];
+  F[6] = t2[0]; F[7] = t2[1]; F[8] = t2[2];
+}
+
+struct GeomV { int type; float size[3]; float c[3]; float R[9]; float rbound; float friction; };
+
+__device__ __forceinline__ void load_geom(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int g, GeomV& G) {
+  if (g == T->geom_obj) {
+    G.type = S.s.obj_type;
+    G.size[0] = S.s.obj_size[0]; G.size[1] = S.s.obj_size[1]; G.size[2] = S.s.obj_size[2];
+    G.rbound = S.s.obj_rbound; G.friction = S.s.obj_friction;
+  } else {
+    G.type = m->geom_type[g];
+    ld3(G.size, m->geom_size[g]);
+    G.rbound = (float)m->geom_rbound[g];
+    G.friction = (float)m->geom_friction[g];
+  }
+  for (int k = 0; k < 3; k++) G.c[k] = S.gxpos[g][k];
+  for (int k = 0; k < 9; k++) G.R[k] = S.gxmat[g][k];
+}
+
+// plane-X multi-contact generators: k-th candidate point (returns 0 if none)
+__device__ __forceinline__ int plane_box_point(const GeomV& P, const GeomV& B, int i, Hit& h) {
+  float nz[3] = {P.R[2], P.R[5], P.R[8]};
+  float s[3] = {(i & 1) ? B.size[0] : -B.size[0], (i & 2) ? B.size[1] : -B.size[1], (i & 4) ? B.size[2] : -B.size[2]};
+  float v[3];
+  mulmv3(v, B.R, s);
+  v[0] += B.c[0]; v[1] += B.c[1]; v[2] += B.c[2];
+  float dv[3] = {v[0] - P.c[0], v[1] - P.c[1], v[2] - P.c[2]};
+  float d = dot3(dv, nz);
+  if (!(d < 0)) return 0;
+  h.dist = d;
+  for (int k = 0; k < 3; k++) { h.pos[k] = v[k] - 0.5f * d * nz[k]; h.n[k] = nz[k]; }
+  return 1;
+}
+__device__ __forceinline__ int plane_cyl_point(const GeomV& P, const GeomV& Cy, int i, Hit& h) {
+  float nz[3] = {P.R[2], P.R[5], P.R[8]};
+  float a[3] = {Cy.R[2], Cy.R[5], Cy.R[8]};
+  float r = Cy.size[0], hh = Cy.size[1];
+  float na = dot3(nz, a);
+  float w[3] = {-nz[0] + na * a[0], -nz[1] + na * a[1], -nz[2] + na * a[2]};
+  float lw = sqrtf(dot3(w, w));
+  if (lw < 1e-6f) { w[0] = Cy.R[0]; w[1] = Cy.R[3]; w[2] = Cy.R[6]; }
+  else { w[0] /= lw; w[1] /= lw; w[2] /= lw; }
+  float axw[3];
+  cross3(axw, a, w);
+  int s = i >> 2, k = i & 3;
+  float sg = s == 0 ? 1.0f : -1.0f;
+  float dir[3];
+  if (k == 0) { dir[0] = w[0]; dir[1] = w[1]; dir[2] = w[2]; }
+  else if (k == 1) { dir[0] = axw[0]; dir[1] = axw[1]; dir[2] = axw[2]; }
+  else if (k == 2) { dir[0] = -w[0]; dir[1] = -w[1]; dir[2] = -w[2]; }
+  else { dir[0] = -axw[0]; dir[1] = -axw[1]; dir[2] = -axw[2]; }
+  float v[3];
+  for (int t = 0; t < 3; t++) v[t] = Cy.c[t] + sg * hh * a[t] + r * dir[t];
+  float dv[3] = {v[0] - P.c[0], v[1] - P.c[1], v[2] - P.c[2]};
+  float d = dot3(dv, nz);
+  if (!(d < 0)) return 0;
+  h.dist = d;
+  for (int t = 0; t < 3; t++) { h.pos[t] = v[t] - 0.5f * d * nz[t]; h.n[t] = nz[t]; }
+  return 1;
+}
+__device__ int plane_sphere(const GeomV& P, const GeomV& Sp, Hit& h) {
+  float nz[3] = {P.R[2], P.R[5], P.R[8]};
+  float r = Sp.size[0];
+  float dv[3] = {Sp.c[0] - P.c[0], Sp.c[1] - P.c[1], Sp.c[2] - P.c[2]};
+  float dist = dot3(dv, nz) - r;
+  if (!(dist < 0)) return 0;
+  h.dist = dist;
+  for (int k = 0; k < 3; k++) { h.pos[k] = Sp.c[k] - nz[k] * (r + 0.5f * dist); h.n[k] = nz[k]; }
+  return 1;
+}
+__device__ int sphere_box(const GeomV& Sp, const GeomV& B, Hit& h) {
+  const float* R = B.R;
+  const float* hs = B.size;
+  float r = Sp.size[0];
+  float dv[3] = {Sp.c[0] - B.c[0], Sp.c[1] - B.c[1], Sp.c[2] - B.c[2]};
+  float cl[3];
+  mulmtv3(cl, R, dv);
+  float q[3];
+  int inside = 1;
+  for (int k = 0; k < 3; k++) {
+    q[k] = cl[k];
+    if (q[k] > hs[k]) { q[k] = hs[k]; inside = 0; }
+    if (q[k] < -hs[k]) { q[k] = -hs[k]; inside = 0; }
+  }
+  float nl[3], dist, ql[3];
+  if (!inside) {
+    float df[3] = {cl[0] - q[0], cl[1] - q[1], cl[2] - q[2]};
+    float l = sqrtf(dot3(df, df));
+    if (l < 1e-12f) return 0;
+    dist = l - r;
+    if (!(dist < 0)) return 0;
+    nl[0] = -df[0] / l; nl[1] = -df[1] / l; nl[2] = -df[2] / l;
+    ql[0] = q[0]; ql[1] = q[1]; ql[2] = q[2];
+  } else {
+    int kmin = 0;
+    float best = hs[0] - fabsf(cl[0]);
+    for (int k = 1; k < 3; k++) { float v = hs[k] - fabsf(cl[k]); if (v < best) { best = v; kmin = k; } }
+    float sg = cl[kmin] >= 0 ? 1.0f : -1.0f;
+    nl[0] = nl[1] = nl[2] = 0; nl[kmin] = -sg;
+    dist = -(best + r);
+    ql[0] = cl[0]; ql[1] = cl[1]; ql[2] = cl[2]; ql[kmin] = sg * hs[kmin];
+  }
+  float n[3], qw[3];
+  mulmv3(n, R, nl);
+  mulmv3(qw, R, ql);
+  h.dist = dist;
+  for (int k = 0; k < 3; k++) {
+    qw[k] += B.c[k];
+    float sp = Sp.c[k] + n[k] * r;
+    h.pos[k] = 0.5f * (qw[k] + sp);
+    h.n[k] = n[k];
+  }
+  return 1;
+}
+
+// ---- MPR ----
+struct SV { float v[3], p1[3], p2[3]; };
+__device__ __forceinline__ void support_geom(const GeomV& G, const float* d, float* out) {
+  float dl[3];
+  mulmtv3(dl, G.R, d);
+  float pl[3] = {0, 0, 0};
+  if (G.type == GM_GEOM_BOX) {
+    for (int k = 0; k < 3; k++) pl[k] = dl[k] >= 0 ? G.size[k] : -G.size[k];
+  } else if (G.type == GM_GEOM_CYLINDER) {
+    float rr = sqrtf(dl[0] * dl[0] + dl[1] * dl[1]);
+    if (rr > 1e-12f) { pl[0] = G.size[0] * dl[0] / rr; pl[1] = G.size[0] * dl[1] / rr; }
+    pl[2] = dl[2] >= 0 ? G.size[1] : -G.size[1];
+  } else if (G.type == GM_GEOM_SPHERE) {
+    float l = sqrtf(dot3(dl, dl));
+    if (l > 1e-12f) { pl[0] = dl[0] * G.size[0] / l; pl[1] = dl[1] * G.size[0] / l; pl[2] = dl[2] * G.size[0] / l; }
+  }
+  mulmv3(out, G.R, pl);
+  out[0] += G.c[0]; out[1] += G.c[1]; out[2] += G.c[2];
+}
+__device__ __forceinline__ void mpr_support(const GeomV& A, const GeomV& B, const float* d, SV& sv) {
+  float nd[3] = {-d[0], -d[1], -d[2]};
+  support_geom(A, d, sv.p1);
+  support_geom(B, nd, sv.p2);
+  sv.v[0] = sv.p1[0] - sv.p2[0]; sv.v[1] = sv.p1[1] - sv.p2[1]; sv.v[2] = sv.p1[2] - sv.p2[2];
+}
+__device__ __forceinline__ int fzero(float x) { return fabsf(x) < 1e-12f; }
+__device__ __forceinline__ void normalize3(float* d) {
+  float l = sqrtf(dot3(d, d));
+  if (l > 0) { d[0] /= l; d[1] /= l; d[2] /= l; }
+}
+__device__ void portal_dir(const SV* P, float* dir) {
+  float a[3] = {P[2].v[0] - P[1].v[0], P[2].v[1] - P[1].v[1], P[2].v[2] - P[1].v[2]};
+  float b[3] = {P[3].v[0] - P[1].v[0], P[3].v[1] - P[1].v[1], P[3].v[2] - P[1].v[2]};
+  cross3(dir, a, b);
+  normalize3(dir);
+}
+__device__ void expand_portal(SV* P, const SV& v4) {
+  float v4v0[3];
+  cross3(v4v0, v4.v, P[0].v);
+  float d = dot3(P[1].v, v4v0);
+  if (d > 0) {
+    d = dot3(P[2].v, v4v0);
+    if (d > 0) P[1] = v4; else P[3] = v4;
+  } else {
+    d = dot3(P[3].v, v4v0);
+    if (d > 0) P[2] = v4; else P[1] = v4;
+  }
+}
+__device__ int reach_tol(const SV* P, const SV& v4, const float* dir, float tol) {
+  float dv1 = dot3(P[1].v, dir), dv2 = dot3(P[2].v, dir), dv3 = dot3(P[3].v, dir), dv4 = dot3(v4.v, dir);
+  float d1 = dv4 - dv1, d2 = dv4 - dv2, d3 = dv4 - dv3;
+  float dd = fminf(fminf(d1, d2), d3);
+  return dd < tol || fabsf(dd - tol) < 1e-12f;
+}
+__device__ void tri_closest_origin(const float* a, const float* b, const float* c, float* out) {
+  float ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+  float ac[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+  float ap[3] = {-a[0], -a[1], -a[2]};
+  float d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+  if (d1 <= 0 && d2 <= 0) { out[0] = a[0]; out[1] = a[1]; out[2] = a[2]; return; }
+  float bp[3] = {-b[0], -b[1], -b[2]};
+  float d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  if (d3 >= 0 && d4 <= d3) { out[0] = b[0]; out[1] = b[1]; out[2] = b[2]; return; }
+  float vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) { float v = d1 / (d1 - d3); for (int k = 0; k < 3; k++) out[k] = a[k] + v * ab[k]; return; }
+  float cp[3] = {-c[0], -c[1], -c[2]};
+  float d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+  if (d6 >= 0 && d5 <= d6) { out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; return; }
+  float vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) { float w = d2 / (d2 - d6); for (int k = 0; k < 3; k++) out[k] = a[k] + w * ac[k]; return; }
+  float va = d3 * d6 - d5 * d4;
+  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+    float w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    for (int k = 0; k < 3; k++) out[k] = b[k] + w * (c[k] - b[k]);
+    return;
+  }
+  float den = 1.0f / (va + vb + vc);
+  float v = vb * den, w = vc * den;
+  for (int k = 0; k < 3; k++) out[k] = a[k] + ab[k] * v + ac[k] * w;
+}
+__device__ void mpr_pos(const SV* P, float* pos) {
+  float dir[3];
+  portal_dir(P, dir);
+  float t[3];
+  cross3(t, P[1].v, P[2].v); float b0 = dot3(t, P[3].v);
+  cross3(t, P[3].v, P[2].v); float b1 = dot3(t, P[0].v);
+  cross3(t, P[0].v, P[1].v); float b2 = dot3(t, P[3].v);
+  cross3(t, P[2].v, P[1].v); float b3 = dot3(t, P[0].v);
+  float sum = b0 + b1 + b2 + b3;
+  if (sum <= 0) {
+    b0 = 0;
+    cross3(t, P[2].v, P[3].v); b1 = dot3(t, dir);
+    cross3(t, P[3].v, P[1].v); b2 = dot3(t, dir);
+    cross3(t, P[1].v, P[2].v); b3 = dot3(t, dir);
+    sum = b1 + b2 + b3;
+  }
+  float inv = 1.0f / sum;
+  float bb[4] = {b0, b1, b2, b3};
+  float p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
+  for (int i = 0; i < 4; i++)
+    for (int k = 0; k < 3; k++) { p1[k] += bb[i] * P[i].p1[k]; p2[k] += bb[i] * P[i].p2[k]; }
+  for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p1[k] + p2[k]) * inv;
+}
+__device__ int mpr(const GeomV& A, const GeomV& B, float tol, int maxit, Hit& h) {
+  SV P[4];
+  for (int k = 0; k < 3; k++) { P[0].v[k] = A.c[k] - B.c[k]; P[0].p1[k] = A.c[k]; P[0].p2[k] = B.c[k]; }
+  if (fzero(P[0].v[0]) && fzero(P[0].v[1]) && fzero(P[0].v[2])) P[0].v[0] += 1e-5f;
+  float d[3] = {-P[0].v[0], -P[0].v[1], -P[0].v[2]};
+  normalize3(d);
+  mpr_support(A, B, d, P[1]);
+  if (dot3(P[1].v, d) <= 0) return 0;
+  cross3(d, P[0].v, P[1].v);
+  if (fzero(sqrtf(dot3(d, d)))) {
+    float l1 = sqrtf(dot3(P[1].v, P[1].v));
+    if (fzero(l1)) return 0;
+    h.dist = -l1;
+    for (int k = 0; k < 3; k++) { h.n[k] = P[1].v[k] / l1; h.pos[k] = 0.5f * (P[1].p1[k] + P[1].p2[k]); }
+    return 1;
+  }
+  normalize3(d);
+  mpr_support(A, B, d, P[2]);
+  if (dot3(P[2].v, d) <= 0) return 0;
+  float va[3], vb[3];
+  for (int k = 0; k < 3; k++) { va[k] = P[1].v[k] - P[0].v[k]; vb[k] = P[2].v[k] - P[0].v[k]; }
+  cross3(d, va, vb);
+  normalize3(d);
+  if (dot3(d, P[0].v) > 0) { SV t = P[1]; P[1] = P[2]; P[2] = t; d[0] = -d[0]; d[1] = -d[1]; d[2] = -d[2]; }
+  int it = 0;
+  for (;;) {
+    mpr_support(A, B, d, P[3]);
+    if (dot3(P[3].v, d) <= 0) return 0;
+    int cont = 0;
+    cross3(va, P[1].v, P[3].v);
+    if (dot3(va, P[0].v) < -1e-12f) { P[2] = P[3]; cont = 1; }
+    if (!cont) {
+      cross3(va, P[3].v, P[2].v);
+      if (dot3(va, P[0].v) < -1e-12f) { P[1] = P[3]; cont = 1; }
+    }
+    if (!cont) break;
+    for (int k = 0; k < 3; k++) { va[k] = P[1].v[k] - P[0].v[k]; vb[k] = P[2].v[k] - P[0].v[k]; }
+    cross3(d, va, vb);
+    normalize3(d);
+    if (++it > maxit) return 0;
+  }
+  it = 0;
+  for (;;) {
+    portal_dir(P, d);
+    if (dot3(d, P[1].v) >= -1e-12f) break;
+    SV v4;
+    mpr_support(A, B, d, v4);
+    float dv4 = dot3(v4.v, d);
+    if (!(fzero(dv4) || dv4 > 0)) return 0;
+    if (reach_tol(P, v4, d, tol)) return 0;
+    expand_portal(P, v4);
+    if (++it > maxit) return 0;
+  }
+  it = 0;
+  for (;;) {
+    portal_dir(P, d);
+    SV v4;
+    mpr_support(A, B, d, v4);
+    if (reach_tol(P, v4, d, tol) || it > maxit) {
+      float cp[3];
+      tri_closest_origin(P[1].v, P[2].v, P[3].v, cp);
+      float depth = sqrtf(dot3(cp, cp));
+      if (fzero(depth)) return 0;
+      h.dist = -depth;
+      h.n[0] = cp[0] / depth; h.n[1] = cp[1] / depth; h.n[2] = cp[2] / depth;
+      mpr_pos(P, h.pos);
+      return depth > 0;
+    }
+    expand_portal(P, v4);
+    it++;
+  }
+}
+
+// canonical (geom1, geom2): lower type first, then lower id
+__device__ __forceinline__ void canon_pair(int a, int b, int ta, int tb, int& g1, int& g2) {
+  if (ta > tb || (ta == tb && a > b)) { g1 = b; g2 = a; } else { g1 = a; g2 = b; }
+}
+
+__device__ void write_contact(Shared& S, int slot, int g1, int g2, const Hit& h, float mu) {
+  float* C = S.con[slot];
+  C[0] = h.dist;
+  C[1] = h.pos[0]; C[2] = h.pos[1]; C[3] = h.pos[2];
+  make_frame(C + 4, h.n);
+  C[13] = mu;
+  C[14] = 0; C[15] = 0; C[16] = 0;
+  C[17] = (float)g1; C[18] = (float)g2;
+}
+
+__device__ void collision(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+  int cnt = 0, kind = 0, g1 = 0, g2 = 0;
+  Hit single;
+  GeomV A, B;
+  if (lane < T->npair) {
+    int a = m->pair_a[lane], b = m->pair_b[lane];
+    int ta = (a == T->geom_obj) ? S.s.obj_type : m->geom_type[a];
+    int tb = (b == T->geom_obj) ? S.s.obj_type : m->geom_type[b];
+    canon_pair(a, b, ta, tb, g1, g2);
+    load_geom(S, m, T, g1, A);
+    load_geom(S, m, T, g2, B);
+    bool pass;
+    if (A.type == GM_GEOM_PLANE) {
+      float nz[3] = {A.R[2], A.R[5], A.R[8]};
+      float dv[3] = {B.c[0] - A.c[0], B.c[1] - A.c[1], B.c[2] - A.c[2]};
+      pass = !(dot3(dv, nz) > B.rbound);
+    } else {
+      float dv[3] = {B.c[0] - A.c[0], B.c[1] - A.c[1], B.c[2] - A.c[2]};
+      float rr = A.rbound + B.rbound;
+      pass = !(dot3(dv, dv) > rr * rr);
+    }
+    if (pass) {
+      if (A.type == GM_GEOM_PLANE) {
+        if (B.type == GM_GEOM_SPHERE) { kind = 1; cnt = plane_sphere(A, B, single); }
+        else if (B.type == GM_GEOM_BOX) {
+          kind = 2;
+          Hit t;
+          for (int i = 0; i < 8 && cnt < 4; i++) cnt += plane_box_point(A, B, i, t);
+        } else if (B.type == GM_GEOM_CYLINDER) {
+          kind = 3;
+          Hit t;
+          for (int i = 0; i < 8 && cnt < 4; i++) cnt += plane_cyl_point(A, B, i, t);
+        }
+      } else if (A.type == GM_GEOM_SPHERE && B.type == GM_GEOM_BOX) {
+        kind = 1; cnt = sphere_box(A, B, single);
+      } else {
+        kind = 1; cnt = mpr(A, B, (float)m->mpr_tolerance, m->mpr_iterations, single);
+        if (cnt && !(single.dist < 0)) cnt = 0;
+      }
+    }
+  }
+  S.cnt[lane] = cnt;
+  __syncthreads();
+  int off = 0, total = 0;
+  for (int i = 0; i < NT; i++) { int c = S.cnt[i]; if (i < lane) off += c; total += c; }
+  if (cnt > 0) {
+    float mu = fmaxf(A.friction, B.friction);
+    if (kind == 1) {
+      if (off < GM_MAX_CON) write_contact(S, off, g1, g2, single, mu);
+    } else {
+      Hit t;
+      int w = 0;
+      for (int i = 0; i < 8 && w < cnt; i++) {
+        int ok = (kind == 2) ? plane_box_point(A, B, i, t) : plane_cyl_point(A, B, i, t);
+        if (ok) { if (off + w < GM_MAX_CON) write_contact(S, off + w, g1, g2, t, mu); w++; }
+      }
+    }
+  }
+  if (lane == 0) {
+    S.ncon = total < GM_MAX_CON ? total : GM_MAX_CON;
+    S.overflow = total > GM_MAX_CON;
+  }
+  __syncthreads();
+}
+
+// ============================================================ constraints + PGS
+__device__ __forceinline__ int geom_chain(const GmTopo* T, int g) { return T->geom_group[g]; }
+
+// compact Jacobian row of contact c along unit direction `dir` (rows of the frame)
+__device__ void contact_jac(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int c,
+                            const float* dir, float* J, int& grp) {
+  for (int k = 0; k < CW; k++) J[k] = 0;
+  const float* C = S.con[c];
+  const float* pos = C + 1;
+  int gs[2] = {(int)C[17], (int)C[18]};
+  float sg[2] = {-1.0f, 1.0f};
+  grp = -1;
+  for (int side = 0; side < 2; side++) {
+    int g = gs[side];
+    int grpg = T->geom_group[g];
+    if (grpg < 0) continue;
+    float s = sg[side];
+    if (grpg == GM_GRP_OBJECT) {
+      for (int k = 0; k < 6; k++) {
+        const float* cd = S.cdof[T->dof_obj + k];
+        float wxp[3];
+        cross3(wxp, cd, pos);
+        float col[3] = {cd[3] + wxp[0], cd[4] + wxp[1], cd[5] + wxp[2]};
+        J[k] += s * dot3(dir, col);
+      }
+    } else {
+      grp = grpg;
+      int P = T->geom_cpos[g];
+      for (int q = 0; q <= P; q++) {
+        int d = (q == 0) ? T->dof_base : chain_dof(T, grpg, q);
+        const float* cd = S.cdof[d];
+        float wxp[3];
+        cross3(wxp, cd, pos);
+        float col[3] = {cd[3] + wxp[0], cd[4] + wxp[1], cd[5] + wxp[2]};
+        float v = s * dot3(dir, col);
+        if (q == 0) J[6] += v; else J[6 + q] += v;
+      }
+    }
+  }
+}
+
+// Y = J L^-1 on a compact row (in place)
+__device__ void row_LTsolve(Shared& S, const GmTopo* __restrict__ T, float* J, int grp) {
+  for (int k = 5; k >= 1; k--)
+    for (int i = k - 1; i >= 0; i--) J[i] -= S.Ho[TRI(k, i)] * J[k];
+  if (grp >= 0 && grp <= 3) {
+    int L = chain_len(T, grp);
+    for (int k = L; k >= 1; k--) {
+      for (int i = k - 1; i >= 1; i--) J[6 + i] -= Hat(S, grp, k, i) * J[6 + k];
+      J[6] -= Hat(S, grp, k, 0) * J[6 + k];
+    }
+  }
+}
+__device__ __forceinline__ float row_dot_dofs(Shared& S, const GmTopo* __restrict__ T, const float* J, int grp, const float* v) {
+  float acc = 0;
+  for (int k = 0; k < 6; k++) acc += J[k] * v[T->dof_obj + k];
+  if (grp >= 0 && grp <= 3) {
+    acc += J[6] * v[T->dof_base];
+    int L = chain_len(T, grp);
+    for (int q = 1; q <= L; q++) acc += J[6 + q] * v[chain_dof(T, grp, q)];
+  }
+  return acc;
+}
+
+__device__ float impedance(const gm_model* __restrict__ m, float r) {
+  float dmin = (float)m->solimp[0], dmax = (float)m->solimp[1], width = (float)m->solimp[2];
+  float mid = (float)m->solimp[3], pw = (float)m->solimp[4];
+  if (dmin == dmax || width <= 1e-15f) return dmin;
+  float x = fabsf(r) / width;
+  if (x >= 1) return dmax;
+  if (x <= 0) return dmin;
+  float y;
+  if (pw == 1) y = x;
+  else if (x <= mid) y = powf(x, pw) / powf(mid, pw - 1);
+  else y = 1 - powf(1 - x, pw) / powf(1 - mid, pw - 1);
+  return dmin + y * (dmax - dmin);
+}
+
+__device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+  // row layout: active locks (lock order) then 4 pyramid edges per contact
+  int nl = 0;
+  for (int k = 0; k < T->nlock; k++) nl += S.s.lock_active[k] ? 1 : 0;
+  int nefc = nl + 4 * S.ncon;
+  float J[CW];
+  int grp = -1;
+  float pos = 0;
+  int is_contact = 0;
+  if (lane < nefc) {
+    if (lane < nl) {
+      int k = 0, cntl = -1;
+      for (k = 0; k < T->nlock; k++) { if (S.s.lock_active[k]) cntl++; if (cntl == lane) break; }
+      int d = m->lock_dof[k];
+      for (int t = 0; t < CW; t++) J[t] = 0;
+      int b = m->dof_body[d];
+      grp = T->body_group[b];
+      J[6 + T->body_cpos[b]] = 1.0f;
+      pos = S.s.qpos[d] - S.s.lock_q[k];
+    } else {
+      int r = lane - nl;
+      int c = r >> 2, e = r & 3;
+      const float* C = S.con[c];
+      float Jn[CW], Jt[CW];
+      int g2;
+      contact_jac(S, m, T, c, C + 4, Jn, grp);
+      contact_jac(S, m, T, c, C + 4 + 3 * (1 + (e >> 1)), Jt, g2);
+      float sgn = (e & 1) ? -1.0f : 1.0f;
+      float mu = C[13];
+      for (int t = 0; t < CW; t++) J[t] = Jn[t] + sgn * mu * Jt[t];
+      pos = C[0];
+      is_contact = 1;
+    }
+  }
+  // a0 = J qacc_smooth, vel = J qvel (uses J before the in-place solve)
+  float a0 = 0, vel = 0;
+  if (lane < nefc) {
+    a0 = row_dot_dofs(S, T, J, grp, S.qacc_s);
+    vel = row_dot_dofs(S, T, J, grp, S.s.qvel);
+    row_LTsolve(S, T, J, grp);
+    for (int t = 0; t < CW - 1; t++) S.Y[lane][t] = J[t];
+    S.Y[lane][CW - 1] = __int_as_float(grp);
+  }
+  if (lane == 0) { S.nefc = nefc; S.nlockrows = nl; }
+  __syncthreads();
+  // Y D^-1 for this lane's row
+  float Yd[CW - 1];
+  if (lane < nefc) {
+    for (int k = 0; k < 6; k++) Yd[k] = J[k] / S.Do[k];
+    Yd[6] = J[6] / S.Dbb;
+    for (int q = 1; q <= CLMAX; q++) {
+      float dv = 1.0f;
+      if (grp >= 0 && grp < 3 && q <= T->CL) dv = S.Df[grp][q];
+      else if (grp == 3 && q == 1) dv = S.Dp[1];
+      Yd[6 + q] = J[6 + q] / dv;
+    }
+  } else {
+    for (int k = 0; k < CW - 1; k++) Yd[k] = 0;
+  }
+  // Delassus column A[:, lane] in VGPRs
+  float A[GM_MAX_EFC];
+#pragma unroll
+  for (int i = 0; i < GM_MAX_EFC; i++) {
+    float acc = 0;
+    if (i < nefc) {
+      const float* Yi = S.Y[i];
+      int gi = __float_as_int(Yi[CW - 1]);
+      for (int k = 0; k < 6; k++) acc += Yd[k] * Yi[k];
+      float ch = Yd[6] * Yi[6];
+      float chn = 0;
+      for (int q = 1; q <= CLMAX; q++) chn += Yd[6 + q] * Yi[6 + q];
+      if (gi == grp && grp >= 0 && grp <= 3) ch += chn;
+      else if (!(gi >= 0 && gi <= 3 && grp >= 0 && grp <= 3)) ch = 0;
+      acc += ch;
+    }
+    A[i] = acc;
+  }
+  // impedance / reference acceleration (mj_makeImpedance)
+  float h = (float)m->timestep;
+  float tc = (float)m->solref[0];
+  if (tc < 2 * h) tc = 2 * h;
+  float dr = (float)m->solref[1], dmax = (float)m->solimp[1];
+  float K = 1.0f / (dmax * dmax * tc * tc * dr * dr);
+  float Bd = 2.0f / (dmax * tc);
+  float Ajj = 0;
+#pragma unroll
+  for (int i = 0; i < GM_MAX_EFC; i++) if (i == lane) Ajj = A[i];
+  float imp = impedance(m, pos);
+  float aref = -Bd * vel - K * imp * pos;
+  float R = (1 - imp) / imp * Ajj;
+  if (R < 1e-15f) R = 1e-15f;
+  float invd = (lane < nefc) ? 1.0f / (Ajj + R) : 0.0f;
+  float res = (lane < nefc) ? (a0 - aref) : 0.0f;   // (A f + b) with f = 0
+  float f = 0;
+  // projected Gauss-Seidel, residual broadcast through v_readlane
+  for (int it = 0; it < m->pgs_iterations; it++) {
+#pragma unroll
+    for (int r = 0; r < GM_MAX_EFC; r++) {
+      if (r < nefc) {
+        float g = res + R * f;
+        float fn = f - g * invd;
+        if (is_contact && fn < 0) fn = 0;
+        float dl = fn - f;
+        float delta = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dl), r));
+        res += A[r] * delta;
+        if (lane == r) f += delta;
+      }
+    }
+  }
+  S.efc_f[lane] = (lane < nefc) ? f : 0.0f;
+  __syncthreads();
+}
+
+// qacc = qacc_smooth + H^-1 J^T f  via  z = D^-1 Y^T f,  x = L^-1 z
+__device__ void constraint_accel(Shared& S, const GmTopo* __restrict__ T, int lane) {
+  int nefc = S.nefc;
+  if (lane < T->nv) {
+    int d = lane;
+    int b = -1;
+    // classify the dof into (group, compact slot)
+    int grp_d, slot;
+    if (d >= T->dof_obj) { grp_d = GM_GRP_OBJECT; slot = d - T->dof_obj; }
+    else if (d == T->dof_base) { grp_d = GM_GRP_BASE; slot = 6; }
+    else if (d == T->dof_palm) { grp_d = 3; slot = 7; }
+    else { grp_d = (d - T->dof_f0[0]) / T->CL; slot = 6 + 1 + (d - T->dof_f0[grp_d]); }
+    (void)b;
+    float acc = 0;
+    for (int r = 0; r < nefc; r++) {
+      int g = __float_as_int(S.Y[r][CW - 1]);
+      bool use = (grp_d == GM_GRP_OBJECT) || (grp_d == GM_GRP_BASE && g >= 0 && g <= 3) || (grp_d == g);
+      if (use) acc += S.Y[r][slot] * S.efc_f[r];
+    }
+    float Dd;
+    if (grp_d == GM_GRP_OBJECT) Dd = S.Do[slot];
+    else if (grp_d == GM_GRP_BASE) Dd = S.Dbb;
+    else if (grp_d == 3) Dd = S.Dp[1];
+    else Dd = S.Df[grp_d][slot - 6];
+    S.z[d] = acc / Dd;
+  }
+  __syncthreads();
+  // x = L^-1 z : root -> leaves
+  if (lane < 5) {
+    int c = lane;
+    int L = chain_len(T, c);
+    if (c < 4) {
+      float xs[CLMAX + 1];
+      xs[0] = S.z[T->dof_base];
+      for (int k = 1; k <= L; k++) {
+        float v = S.z[chain_dof(T, c, k)];
+        for (int i = k - 1; i >= 0; i--) v -= Hat(S, c, k, i) * xs[i];
+        xs[k] = v;
+        int d = chain_dof(T, c, k);
+        S.qacc[d] = S.qacc_s[d] + v;
+      }
+      if (c == 0) S.qacc[T->dof_base] = S.qacc_s[T->dof_base] + xs[0];
+    } else {
+      float xs[6];
+      for (int k = 0; k < 6; k++) {
+        float v = S.z[T->dof_obj + k];
+        for (int i = k - 1; i >= 0; i--) v -= S.Ho[TRI(k, i)] * xs[i];
+        xs[k] = v;
+        S.qacc[T->dof_obj + k] = S.qacc_s[T->dof_obj + k] + v;
+      }
+    }
+  }
+  // contact forces in the contact frame (mj_contactForce, pyramidal decode)
+  if (lane < S.ncon) {
+    const float* fe = &S.efc_f[S.nlockrows + 4 * lane];
+    float mu = S.con[lane][13];
+    S.con[lane][14] = fe[0] + fe[1] + fe[2] + fe[3];
+    S.con[lane][15] = mu * (fe[0] - fe[1]);
+    S.con[lane][16] = mu * (fe[2] - fe[3]);
+  }
+  __syncthreads();
+}
+
+// ============================================================ integrate
+__device__ void integrate(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+  float h = (float)m->timestep;
+  if (lane < T->nv) S.s.qvel[lane] += h * S.qacc[lane];
+  __syncthreads();
+  if (lane < T->nv && lane < T->dof_obj) {
+    S.s.qpos[lane] += h * S.s.qvel[lane];   // slides/hinges: qposadr == dofadr before the object
+  }
+  if (lane == 0) {
+    int qa = T->qadr_obj, da = T->dof_obj;
+    for (int k = 0; k < 3; k++) S.s.qpos[qa + k] += h * S.s.qvel[da + k];
+    float* q = &S.s.qpos[qa + 3];
+    float w[3] = {S.s.qvel[da + 3], S.s.qvel[da + 4], S.s.qvel[da + 5]};
+    float wn = sqrtf(dot3(w, w));
+    if (wn > 1e-15f) {
+      float ang = wn * h;
+      float sn = sinf(0.5f * ang) / wn, cs = cosf(0.5f * ang);
+      float dq[4] = {cs, w[0] * sn, w[1] * sn, w[2] * sn};
+      quatmul(q, q, dq);
+    }
+    quatnorm(q);
+    S.s.time += m->timestep;
+  }
+  __syncthreads();
+}
+
+// ============================================================ reference scalar logic (lane 0)
+// luke::Gripper in fp64 (gripper.cpp), bit-for-bit the same operations as the reference
+#define G_XY_MIN 49e-3
+#define G_XY_MAX 134e-3
+#define G_Z_MIN 0e-3
+#define G_Z_MAX 165e-3
+#define G_TOL 1e-4
+#define G_LEAD 35e-3
+__device__ __forceinline__ double g_xy_step_m() { return 4.0 / (1.0 * 400 * 1e3); }
+__device__ __forceinline__ double g_z_step_m() { return 4.8768 / (1 * 400 * 1e3); }
+__device__ __forceinline__ double g_calc_th(double x, double y) { return asin((y - x) / G_LEAD) * 1; }
+__device__ __forceinline__ double g_calc_y(const GmGrip& g, double th) { return g.x + 1 * G_LEAD * sin(th); }
+__device__ __forceinline__ int g_xs(const GmGrip& g) { return (int)round((G_XY_MAX - g.x) / g_xy_step_m()); }
+__device__ __forceinline__ int g_ys(const GmGrip& g) { return (int)round((G_XY_MAX - g.y) / g_xy_step_m()); }
+__device__ __forceinline__ int g_zs(const GmGrip& g) { return (int)round(g.z / g_z_step_m()); }
+__device__ __forceinline__ double g_th_deg(const GmGrip& g) { return (180.0 / 3.14159265358979323846) * g_calc_th(g.x, g.y); }
+__device__ int g_update_xy(GmGrip& g) {
+  const double to_rad = 3.14159265358979323846 / 180.0;
+  const double th_min = -40 * to_rad, th_max = 40 * to_rad;
+  const double hyp = sqrt(pow(235e-3, 2) + pow(35.0e-3, 2));
+  const double rest = atan(35.0e-3 / 235e-3);
+  int wl = 1;
+  if (g.x > G_XY_MAX + G_TOL) { g.x = G_XY_MAX; wl = 0; }
+  if (g.x < G_XY_MIN - G_TOL) { g.x = G_XY_MIN; wl = 0; }
+  if (g.y > G_XY_MAX + G_TOL) { g.y = G_XY_MAX; wl = 0; }
+  if (g.y < G_XY_MIN - G_TOL) { g.y = G_XY_MIN; wl = 0; }
+  double nth = g_calc_th(g.x, g.y);
+  if (nth > th_max) { nth = th_max; g.y = g_calc_y(g, th_max); wl = 0; }
+  if (nth < th_min) { nth = th_min; g.y = g_calc_y(g, th_min); wl = 0; }
+  g.th = nth;
+  double th_lim = (asin((-1.0 - g.x) / hyp) + rest) * 1;
+  if (g.th < th_lim) { g.y = g_calc_y(g, th_lim); g.th = th_lim; wl = 0; }
+  g.sx = g_xs(g);
+  g.sy = g_ys(g);
+  return wl;
+}
+__device__ int g_update_z(GmGrip& g) {
+  int wl = 1;
+  if (g.z > G_Z_MAX + G_TOL) { g.z = G_Z_MAX; wl = 0; }
+  if (g.z < G_Z_MIN - G_TOL) { g.z = G_Z_MIN; wl = 0; }
+  g.sz = g_zs(g);
+  return wl;
+}
+__device__ void g_reset(GmGrip& g) {
+  g.x = G_XY_MAX - 1.0 * (4 * 1e-3 / 1.0);
+  g.y = g.x;
+  g.z = G_Z_MIN + 1.0 * (4.8768 * 1e-3 / 1);
+  int a = g_update_xy(g); int b = g_update_z(g); (void)a; (void)b;
+}
+__device__ int g_set_xyz_m_rad(GmGrip& g, double x, double th, double z) {
+  g.x = x; g.y = g_calc_y(g, th);
+  int in_lim = g_update_xy(g);
+  g.z = z;
+  return g_update_z(g) ? in_lim : 0;
+}
+__device__ int g_set_xyz_m(GmGrip& g, double x, double y, double z) {
+  g.x = x; g.y = y; g.z = z;
+  int a = g_update_xy(g); int b = g_update_z(g);
+  return a * b;
+}
+__device__ int g_set_xyz_step(GmGrip& g, int xs, int ys, int zs) {
+  g.x = G_XY_MAX - g_xy_step_m() * xs; g.y = G_XY_MAX - g_xy_step_m() * ys;
+  int in_lim = g_update_xy(g);
+  g.z = g_z_step_m() * zs;
+  return g_update_z(g) ? in_lim : 0;
+}
+__device__ int g_step_to(GmGrip& g, const GmGrip& t, int num) {
+  int fin = 1;
+  int xg = t.sx - g.sx, yg = t.sy - g.sy, zg = t.sz - g.sz;
+  if (xg < 0) { if (-xg > num) { xg = -num; fin = 0; } } else if (xg > num) { xg = num; fin = 0; }
+  if (yg < 0) { if (-yg > num) { yg = -num; fin = 0; } } else if (yg > num) { yg = num; fin = 0; }
+  if (zg < 0) { if (-zg > num) { zg = -num; fin = 0; } } else if (zg > num) { zg = num; fin = 0; }
+  g_set_xyz_step(g, g.sx + xg, g.sy + yg, g.sz + zg);
+  return fin;
+}
+
+// update_all: update_stepper / update_constraints (myfunctions.cpp:2129-2284), antiroll
+__device__ void update_all(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+  if (lane == 0) {
+    GmEnvState& s = S.s;
+    if (s.time > s.last_step_time + m->time_per_step) {
+      int nx = g_xs(s.end) != g_xs(s.next);
+      int ny = !(fabs(g_th_deg(s.end) - g_th_deg(s.next)) < 5e-1);
+      int nz = g_zs(s.end) != g_zs(s.next);
+      if (nx != s.old_x) {
+        for (int k = 0; k < T->nlock; k++)
+          if (m->lock_kind[k] == 0) { s.lock_active[k] = !nx; if (!nx) s.lock_q[k] = S.qpos_pre[m->lock_dof[k]]; }
+        s.old_x = nx;
+      }
+      if (ny != s.old_y) s.old_y = ny;   // revolute locks disabled (myfunctions.cpp:479)
+      if (nz != s.old_z) {
+        for (int k = 0; k < T->nlock; k++)
+          if (m->lock_kind[k] == 2) { s.lock_active[k] = !nz; if (!nz) s.lock_q[k] = S.qpos_pre[m->lock_dof[k]]; }
+        s.old_z = nz;
+      }
+      s.last_step_time = s.time;
+      g_step_to(s.next, s.end, m->stepper_num_steps);
+    }
+    const float* v = &s.qvel[T->dof_obj];
+    float mag = sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    if (mag < 1e-6f) for (int k = 0; k < 6; k++) s.qvel[T->dof_obj + k] = 0;
+  }
+  __syncthreads();
+}
+
+// ---- RNG: minstd_rand0 + generate_canonical (libstdc++), per-env stream ----
+__device__ __forceinline__ uint32_t lcg_next(uint32_t& s) {
+  s = (uint32_t)(((uint64_t)s * 16807ull) % 2147483647ull);
+  return s;
+}
+__device__ float unif01(uint32_t& s) {
+#pragma clang fp contract(off)
+  const float r = 2147483646.0f;
+  float sum = (float)(lcg_next(s) - 1u) * 1.0f;
+  float ret = sum / r;
+  if (ret >= 1.0f) ret = __int_as_float(0x3F7FFFFF);  // nextafterf(1, 0)
+  return ret * (1.0f - 0.0f) + 0.0f;
+}
+__device__ double canon_d(uint32_t& s) {
+#pragma clang fp contract(off)
+  const double r = 2147483646.0;
+  double sum = 0.0, tmp = 1.0;
+  for (int k = 0; k < 2; k++) { sum += (double)(lcg_next(s) - 1u) * tmp; tmp *= r; }
+  double ret = sum / tmp;
+  if (ret >= 1.0) ret = __longlong_as_double(0x3FEFFFFFFFFFFFFFLL);  // nextafter(1, 0)
+  return ret;
+}
+
+// ---- sensors (mjclass.h:155-241) ----
+__device__ __forceinline__ void ring_add(GmEnvState& s, int st, float x) {
+  int i = s.ring_i[st] + 1;
+  if (i > GM_RING - 1) i = 0;
+  s.ring_i[st] = i;
+  s.ring[st][i] = x;
+}
+__device__ __forceinline__ float ring_read(const GmEnvState& s, int st, int n) {
+  int idx = s.ring_i[st] - n;
+  while (idx < 0) idx += GM_RING;
+  return s.ring[st][idx];
+}
+__device__ __forceinline__ float ring_latest(const GmEnvState& s, int st) {
+  return s.ring_i[st] == -1 ? s.ring[st][0] : s.ring[st][s.ring_i[st]];
+}
+__device__ float s_normalise(const gm_sensor& ss, float v) {
+#pragma clang fp contract(off)
+  if (!ss.use_normalisation) return v;
+  if (ss.normalise <= 0) return v < 0 ? -1.0f : 1.0f;
+  else if (v > ss.normalise) return 1.0f;
+  if (v < -ss.normalise) return -1.0f;
+  return v / ss.normalise;
+}
+__device__ float s_noise(GmEnvState& s, const gm_sensor& ss, int slot, float value, int i) {
+#pragma clang fp contract(off)
+  if (!ss.use_noise) return value;
+  const float two_pi = (float)(2.0 * 3.14159265358979323846);
+  const float eps = 1.1920928955078125e-07f;
+  float mu = s.rand_mu[slot][i - 1];
+  if (ss.noise_std < eps) {
+    float noise = mu + ss.noise_mag * (2 * unif01(s.rng) - 1);
+    value += noise;
+  } else {
+    float u1, u2;
+    do { u1 = unif01(s.rng); } while (u1 <= eps);
+    u2 = unif01(s.rng);
+    float mag = (float)(ss.noise_std * sqrt(-2.0 * (double)logf(u1)));
+    float z0 = mag * cosf(two_pi * u2) + mu;
+    value += z0;
+  }
+  if (value > 1) value = 1;
+  else if (value < -1) value = -1;
+  return value;
+}
+__device__ int s_ready(GmEnvState& s, const gm_sensor& ss, int slot) {
+  double tbr = (double)(1 / ss.read_rate);
+  if (s.time > s.last_read[slot] + tbr) { s.last_read[slot] = s.time; return 1; }
+  return 0;
+}
+
+// bending gauge: cubic least squares through the N+1 joint points, evaluated at
+// gauge.xpos (read_armadillo_gauge, myfunctions.cpp:2699-2795).  fp32 Householder
+// QR on a centred/scaled abscissa (same least-squares solution as the reference's
+// arma::polyfit on the raw Vandermonde, better conditioned in fp32).
+__device__ float gauge_reading(const gm_model* __restrict__ m, const float* q) {
+  int N = m->n_seg, P = N + 1;
+  float Ls = (float)m->segment_length;
+  float X[GM_MAX_SEG + 1], Yv[GM_MAX_SEG + 1];
+  X[0] = m->fixed_first_segment ? Ls : 0.0f;
+  Yv[0] = 0;
+  float cum = 0;
+  for (int i = 0; i < N; i++) {
+    cum = (i == 0) ? q[0] : cum + q[i];
+    X[i + 1] = X[i] + Ls * cosf(cum);
+    Yv[i + 1] = Yv[i] + Ls * sinf(cum);
+  }
+  float half = 0.5f * (float)m->finger_length;
+  float A[GM_MAX_SEG + 1][4], b[GM_MAX_SEG + 1];
+  for (int i = 0; i < P; i++) {
+    float t = (X[i] - half) / half;
+    A[i][0] = t * t * t; A[i][1] = t * t; A[i][2] = t; A[i][3] = 1.0f;
+    b[i] = Yv[i];
+  }
+  for (int k = 0; k < 4; k++) {
+    float nrm = 0;
+    for (int i = k; i < P; i++) nrm += A[i][k] * A[i][k];
+    nrm = sqrtf(nrm);
+    float alpha = A[k][k] > 0 ? -nrm : nrm;
+    float v[GM_MAX_SEG + 1];
+    for (int i = 0; i < P; i++) v[i] = (i >= k) ? A[i][k] : 0.0f;
+    v[k] -= alpha;
+    float vv = 0;
+    for (int i = k; i < P; i++) vv += v[i] * v[i];
+    if (vv < 1e-30f) continue;
+    for (int j = k; j < 4; j++) {
+      float s = 0;
+      for (int i = k; i < P; i++) s += v[i] * A[i][j];
+      s = 2 * s / vv;
+      for (int i = k; i < P; i++) A[i][j] -= s * v[i];
+    }
+    float s = 0;
+    for (int i = k; i < P; i++) s += v[i] * b[i];
+    s = 2 * s / vv;
+    for (int i = k; i < P; i++) b[i] -= s * v[i];
+  }
+  float coeff[4];
+  for (int k = 3; k >= 0; k--) {
+    float s = b[k];
+    for (int j = k + 1; j < 4; j++) s -= A[k][j] * coeff[j];
+    coeff[k] = s / A[k][k];
+  }
+  float tg = ((float)m->gauge_xpos - half) / half;
+  float y = ((coeff[0] * tg + coeff[1]) * tg + coeff[2]) * tg + coeff[3];
+  return y * 1000.0f;
+}
+
+// extract_forces_faster (objecthandler.cpp:737-992) over the last substep's contacts.
+// forces[]: obj_loc f1,f2,f3,palm (12) | obj ground global (3) | all_loc f1,f2,f3 x (3),
+//           all_loc palm x (1) | gnd_loc f1,f2,f3 x (3)
+__device__ void extract_forces(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T) {
+  float og[5][3], ag[4][3], gg[3][3];
+  for (int a = 0; a < 5; a++) for (int k = 0; k < 3; k++) og[a][k] = 0;
+  for (int a = 0; a < 4; a++) for (int k = 0; k < 3; k++) ag[a][k] = 0;
+  for (int a = 0; a < 3; a++) for (int k = 0; k < 3; k++) gg[a][k] = 0;
+  for (int i = 0; i < S.ncon; i++) {
+    const float* C = S.con[i];
+    int c1 = m->geom_class[(int)C[17]], c2 = m->geom_class[(int)C[18]];
+    int w_obj = (c1 == GM_CLS_OBJECT || c2 == GM_CLS_OBJECT);
+    int w_f0 = (c1 == GM_CLS_FINGER1 || c2 == GM_CLS_FINGER1);
+    int w_f1 = (c1 == GM_CLS_FINGER2 || c2 == GM_CLS_FINGER2);
+    int w_f2 = (c1 == GM_CLS_FINGER3 || c2 == GM_CLS_FINGER3);
+    int w_palm = (c1 == GM_CLS_PALM || c2 == GM_CLS_PALM);
+    int w_gnd = (c1 == GM_CLS_GROUND || c2 == GM_CLS_GROUND);
+    float g[3];
+    for (int k = 0; k < 3; k++) g[k] = C[4 + k] * C[14] + C[7 + k] * C[15] + C[10 + k] * C[16];
+    int wf[3] = {w_f0, w_f1, w_f2};
+    if (w_obj) {
+      for (int f = 0; f < 3; f++) if (wf[f]) for (int k = 0; k < 3; k++) og[f][k] += g[k];
+      if (w_palm) for (int k = 0; k < 3; k++) og[3][k] += g[k];
+      if (w_gnd) for (int k = 0; k < 3; k++) og[4][k] += g[k];
+    }
+    for (int f = 0; f < 3; f++)
+      if (wf[f]) {
+        for (int k = 0; k < 3; k++) ag[f][k] += g[k];
+        if (w_gnd) for (int k = 0; k < 3; k++) gg[f][k] += g[k];
+      }
+    if (w_palm) for (int k = 0; k < 3; k++) ag[3][k] += g[k];
+  }
+  float* F = S.forces;
+  for (int f = 0; f < 4; f++) {
+    int b = f < 3 ? T->body_finger[f] : T->body_palm;
+    float loc[3];
+    mulmtv3(loc, S.xmat[b], og[f]);
+    F[3 * f] = loc[0]; F[3 * f + 1] = loc[1]; F[3 * f + 2] = loc[2];
+    float al[3];
+    mulmtv3(al, S.xmat[b], ag[f]);
+    if (f < 3) F[15 + f] = al[0]; else F[18] = al[0];
+    if (f < 3) { float gl[3]; mulmtv3(gl, S.xmat[b], gg[f]); F[19 + f] = gl[0]; }
+  }
+  F[12] = og[4][0]; F[13] = og[4][1]; F[14] = og[4][2];
+}
+
+// MjClass::monitor_sensors (mjclass.cpp:741-898)
+__device__ void monitor_sensors(Shared& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
+                                const GmTopo* __restrict__ T, int lane) {
+  __shared__ int bend_ready;
+  if (lane == 0) bend_ready = s_ready(S.s, C->s.bending_gauge, SL_BEND);
+  __syncthreads();
+  if (bend_ready && lane < 3) S.gauge_tmp[lane] = gauge_reading(m, &S.s.qpos[chain_dof(T, lane, 3)]);
+  __syncthreads();
+  if (lane == 0) {
+#pragma clang fp contract(off)
+    GmEnvState& s = S.s;
+    const gm_settings& st = C->s;
+    int have = 0;
+    if (bend_ready) {
+      float g[3] = {S.gauge_tmp[0], S.gauge_tmp[1], S.gauge_tmp[2]};
+      for (int f = 0; f < 3; f++) ring_add(s, ST_SI_GAUGE + f, (float)(g[f] * C->sim_gauge_raw_to_N_factor));
+      for (int f = 0; f < 3; f++) g[f] = s_normalise(st.bending_gauge, g[f]);
+      for (int f = 0; f < 3; f++) g[f] = s_noise(s, st.bending_gauge, SL_BEND, g[f], f + 1);
+      for (int f = 0; f < 3; f++) ring_add(s, ST_GAUGE + f, g[f]);
+    }
+    if (s_ready(s, st.axial_gauge, SL_AXIAL)) {
+      if (!have) { extract_forces(S, m, T); have = 1; }
+      float a[3] = {S.forces[15], S.forces[16], S.forces[17]};
+      for (int f = 0; f < 3; f++) ring_add(s, ST_SI_AXIAL + f, a[f]);
+      for (int f = 0; f < 3; f++) a[f] = s_normalise(st.axial_gauge, a[f]);
+      for (int f = 0; f < 3; f++) a[f] = s_noise(s, st.axial_gauge, SL_AXIAL, a[f], f + 1);
+      for (int f = 0; f < 3; f++) ring_add(s, ST_AXIAL + f, a[f]);
+    }
+    if (s_ready(s, st.palm_sensor, SL_PALM)) {
+      if (!have) { extract_forces(S, m, T); have = 1; }
+      float p = S.forces[18];
+      p *= st.palm_scale_factor;
+      ring_add(s, ST_SI_PALM, p);
+      p = s_normalise(st.palm_sensor, p);
+      p = s_noise(s, st.palm_sensor, SL_PALM, p, 1);
+      ring_add(s, ST_PALM, p);
+    }
+    if (s_ready(s, st.wrist_sensor_Z, SL_WRISTZ)) {
+      float z = 0.0f;
+      z -= st.wrist_sensor_Z.raw_value_offset;
+      ring_add(s, ST_SI_WZ, z);
+      z = s_normalise(st.wrist_sensor_Z, z);
+      z = s_noise(s, st.wrist_sensor_Z, SL_WRISTZ, z, 1);
+      ring_add(s, ST_WZ, z);
+    }
+  }
+  __syncthreads();
+}
+
+// ============================================================ one full substep
+__device__ void physics_substep(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+  if (lane < T->nq) S.qpos_pre[lane] = S.s.qpos[lane];
+  kinematics(S, m, T, lane);
+  crb_rne(S, m, T, lane);
+  mass_and_forces(S, m, T, lane);
+  factor(S, T, lane);
+  solve_full(S, T, S.frc, S.qacc_s, lane);
+  collision(S, m, T, lane);
+  constraints(S, m, T, lane);
+  constraint_accel(S, T, lane);
+  integrate(S, m, T, lane);
+}
+
+// ============================================================ env-step epilogue (lane 0)
+__device__ __forceinline__ float normalise_between(float val, float mn, float mx) {
+#pragma clang fp contract(off)
+  if (val > mx) return 1.0f;
+  else if (val < mn) return -1.0f;
+  return 2 * (val - mn) / (mx - mn) - 1;
+}
+
+__device__ void sense_gripper_state(Shared& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C) {
+#pragma clang fp contract(off)
+  GmEnvState& s = S.s;
+  const gm_settings& st = C->s;
+  const double* bmn = C->base_min;
+  const double* bmx = C->base_max;
+  double gx = normalise_between((float)s.end.x, (float)G_XY_MIN, (float)G_XY_MAX);
+  double gy = normalise_between((float)s.end.y, (float)G_XY_MIN, (float)G_XY_MAX);
+  double gz = normalise_between((float)s.end.z, (float)G_Z_MIN, (float)G_Z_MAX);
+  double bx = normalise_between((float)s.base[0], (float)bmn[0], (float)bmx[0]);
+  double by = normalise_between((float)s.base[1], (float)bmn[1], (float)bmx[1]);
+  double bz = normalise_between((float)s.base[2], (float)bmn[2], (float)bmx[2]);
+  double byaw = normalise_between((float)s.base[5], (float)bmn[5], (float)bmx[5]);
+  gx = s_noise(s, st.motor_state_sensor, SL_MOTOR, (float)gx, 1);
+  gy = s_noise(s, st.motor_state_sensor, SL_MOTOR, (float)gy, 2);
+  gz = s_noise(s, st.motor_state_sensor, SL_MOTOR, (float)gz, 3);
+  bx = s_noise(s, st.base_state_sensor_XY, SL_BASEXY, (float)bx, 1);
+  by = s_noise(s, st.base_state_sensor_XY, SL_BASEXY, (float)by, 2);
+  bz = s_noise(s, st.base_state_sensor_Z, SL_BASEZ, (float)bz, 1);
+  byaw = s_noise(s, st.base_state_sensor_yaw, SL_YAW, (float)byaw, 1);
+  ring_add(s, ST_MOTOR + 0, (float)gx);
+  ring_add(s, ST_MOTOR + 1, (float)gy);
+  ring_add(s, ST_MOTOR + 2, (float)gz);
+  ring_add(s, ST_BASE + 0, (float)bx);
+  ring_add(s, ST_BASE + 1, (float)by);
+  ring_add(s, ST_BASE + 2, (float)bz);
+  ring_add(s, ST_YAW, (float)byaw);
+  // MAT cartesian contact points (get_fingerend_and_palm_xyz, myfunctions.cpp:3622-3688)
+  double fsi[3] = {ring_latest(s, ST_SI_GAUGE), ring_latest(s, ST_SI_GAUGE + 1), ring_latest(s, ST_SI_GAUGE + 2)};
+  double psi = ring_latest(s, ST_SI_PALM);
+  double fx = s.end.x, fth = g_calc_th(s.end.x, s.end.y), pz = s.end.z;
+  const double PI23 = 3.14159265358979323846 * (2.0 / 3.0);
+  double ang[3] = {0.0, PI23, 2 * PI23};
+  double unt = m->fingertip_clearance - s.base[2];
+  double lift = m->finger_length * (1 - cos(fth));
+  double tilted = unt + lift;
+  const double ft = 0.2;
+  for (int i = 0; i < 3; i++) {
+    double tilt_x = fx - m->finger_length * sin(fth);
+    double defl = fsi[i] * pow(m->finger_length, 3) / (3 * m->finger_EI);
+    double fin_x = tilt_x + defl * cos(fth);
+    double px = -fin_x * sin(ang[i] + s.base[5]) + s.base[0];
+    double py = -fin_x * cos(ang[i] + s.base[5]) + s.base[1];
+    double pzz = tilted - defl * sin(fth);
+    bool on = fabs(fsi[i]) > ft;
+    ring_add(s, ST_CART + 3 * i + 0, (float)(on ? px : 0.0));
+    ring_add(s, ST_CART + 3 * i + 1, (float)(on ? py : 0.0));
+    ring_add(s, ST_CART + 3 * i + 2, (float)(on ? pzz : 0.0));
+  }
+  bool pon = psi > ft;
+  ring_add(s, ST_CART + 9, (float)(pon ? s.base[0] : 0.0));
+  ring_add(s, ST_CART + 10, (float)(pon ? s.base[1] : 0.0));
+  ring_add(s, ST_CART + 11, (float)(pon ? unt + 165e-3 - pz : 0.0));
+}
+
+__device__ float mag3f(const float* v) { return (float)sqrt((double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2]); }
+
+// MjClass::update_env (mjclass.cpp:966-1346) + update_events (5437-5469)
+__device__ void update_env(Shared& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
+                           const GmTopo* __restrict__ T) {
+#pragma clang fp contract(off)
+  GmEnvState& s = S.s;
+  const gm_settings& st = C->s;
+  const double ftol = 1e-5;
+  extract_forces(S, m, T);
+  const float* F = S.forces;
+  int qa = T->qadr_obj;
+  double ox = s.qpos[qa], oy = s.qpos[qa + 1], oz = s.qpos[qa + 2];
+  double relx = s.base[0] - ox, rely = s.base[1] - oy;
+  float dist_from_gripper = (float)sqrt(pow(relx, 2) + pow(rely, 2));
+  float f1m = mag3f(F + 0), f2m = mag3f(F + 3), f3m = mag3f(F + 6), pm = mag3f(F + 9), gm = mag3f(F + 12);
+  float palm_axial = F[9];
+  float lift_height = (float)(oz - (double)s.start_qpos[2]);
+  float avg_finger = (float)(0.33333 * (f1m + f2m + f3m));
+  float mn = F[1];
+  if (F[4] < mn) mn = F[4];
+  if (F[7] < mn) mn = F[7];
+  float peak_lat = -1 * mn;
+  float ov_avg = 0, ov_palm = 0, ov_lift = 0;
+  if (avg_finger > ov_avg) ov_avg = avg_finger;
+  if (palm_axial > ov_palm) ov_palm = palm_axial;
+  if (peak_lat > s.grp_peak_lateral) s.grp_peak_lateral = peak_lat;
+  if (lift_height > ov_lift) ov_lift = lift_height;
+  float gripper_z_height = (float)(-1 * s.base[2]);
+  float ga = F[19];
+  if (F[20] < ga) ga = F[20];
+  if (F[21] < ga) ga = F[21];
+  float grp_peak_axial = -1 * ga;
+  float g1 = ring_latest(s, ST_SI_GAUGE), g2 = ring_latest(s, ST_SI_GAUGE + 1), g3 = ring_latest(s, ST_SI_GAUGE + 2);
+  float last_palm = ring_latest(s, ST_SI_PALM), last_wrist = ring_latest(s, ST_SI_WZ);
+  float max_gauge = g1 > g2 ? g1 : g2;
+  max_gauge = max_gauge > g3 ? max_gauge : g3;
+  float avg_gauge = (float)((1.0 / 3.0) * (g1 + g2 + g3));
+  int* B = s.bev_value;
+  B[GM_EV_step_num] = 1;
+  double closest = dist_from_gripper;
+  int o_lifted = 0, o_oob = 0, o_l2h = 0, o_th = 0, o_stable = 0;
+  if (gm < ftol && 0.0f < ftol) { B[GM_EV_lifted] = 1; o_lifted = 1; }
+  if (ox > st.oob_distance || ox < -st.oob_distance || oy > st.oob_distance || oy < -st.oob_distance) { B[GM_EV_oob] = 1; o_oob = 1; }
+  if (ov_lift > st.lift_height - ftol && o_lifted && !o_oob) { B[GM_EV_lifted_to_height] = 1; o_l2h = 1; }
+  if (o_l2h && gripper_z_height > st.gripper_target_height - ftol) { B[GM_EV_target_height] = 1; o_th = 1; }
+  if (f1m > ftol || f2m > ftol || f3m > ftol || pm > ftol) B[GM_EV_object_contact] = 1;
+  if (f1m > st.stable_finger_force && f2m > st.stable_finger_force && f3m > st.stable_finger_force &&
+      f1m < st.stable_finger_force_lim && f2m < st.stable_finger_force_lim && f3m < st.stable_finger_force_lim &&
+      pm > st.stable_palm_force && pm < st.stable_palm_force_lim && B[GM_EV_lifted]) {
+    B[GM_EV_object_stable] = 1; o_stable = 1;
+  }
+  if (o_stable && o_th) B[GM_EV_stable_height] = 1;
+  if (s.termination_signal_sent) {
+    if (st.lifted_termination.done) {
+      if (o_l2h) B[GM_EV_lifted_termination] = 1; else B[GM_EV_failed_termination] = 1;
+    } else {
+      if (B[GM_EV_stable_height]) B[GM_EV_stable_termination] = 1; else B[GM_EV_failed_termination] = 1;
+    }
+  }
+  if (dist_from_gripper < st.XY_distance_threshold) B[GM_EV_within_XY_distance] = 1;
+  if (dist_from_gripper < closest) closest = dist_from_gripper;
+  {
+    int* R = s.bev_row;
+    int v = (!R[GM_EV_dropped] * !B[GM_EV_lifted] * R[GM_EV_lifted]) ? 1
+            : (B[GM_EV_lifted] ? 0 : (R[GM_EV_dropped] ? R[GM_EV_dropped] + 1 : 0));
+    B[GM_EV_dropped] = v != 0;
+  }
+  float* Lv = s.lev_value;
+  Lv[GM_LEV_exceed_axial] = grp_peak_axial;
+  Lv[GM_LEV_exceed_lateral] = s.grp_peak_lateral;
+  Lv[GM_LEV_palm_force] = ov_palm * B[GM_EV_lifted];
+  Lv[GM_LEV_exceed_palm] = ov_palm;
+  Lv[GM_LEV_finger_force] = ov_avg;
+  Lv[GM_LEV_finger1_force] = f1m;
+  Lv[GM_LEV_finger2_force] = f2m;
+  Lv[GM_LEV_finger3_force] = f3m;
+  Lv[GM_LEV_ground_force] = gm;
+  Lv[GM_LEV_good_bend_sensor] = avg_gauge;
+  Lv[GM_LEV_exceed_bend_sensor] = max_gauge;
+  Lv[GM_LEV_dangerous_bend_sensor] = max_gauge;
+  Lv[GM_LEV_good_palm_sensor] = last_palm;
+  Lv[GM_LEV_exceed_palm_sensor] = last_palm;
+  Lv[GM_LEV_dangerous_palm_sensor] = last_palm;
+  Lv[GM_LEV_exceed_wrist_sensor] = last_wrist;
+  Lv[GM_LEV_dangerous_wrist_sensor] = last_wrist;
+  Lv[GM_LEV_action_penalty_lin] /= (float)(C->n_actions - st.use_termination_action);
+  Lv[GM_LEV_action_penalty_sq] /= (float)(C->n_actions - st.use_termination_action);
+  Lv[GM_LEV_object_XY_distance] = (float)(-closest);
+  {
+    int k = 0;
+#define GM_BR(n, r, d, t)                                                                         \
+    if (B[k] && st.n.reward >= (1.0 - 1e-5) && st.n.done && s.bev_row[k] + 1 >= st.n.trigger)    \
+      B[GM_EV_successful_grasp] = 1;                                                              \
+    k++;
+#include "gm_settings.def"
+  }
+  // update_events
+  for (int k = 0; k < GM_N_BINARY; k++) {
+    s.bev_row[k] = s.bev_row[k] * s.bev_value[k] + s.bev_value[k];
+    s.bev_abs[k] += s.bev_value[k];
+    s.bev_last[k] = s.bev_value[k];
+    s.bev_value[k] = 0;
+  }
+  {
+    int k = 0;
+#define GM_LR(n, r, d, t, a, b, o)                                                         \
+    {                                                                                      \
+      int active = (Lv[k] > st.n.min && (Lv[k] < st.n.overshoot || st.n.overshoot < 0));   \
+      s.lev_row[k] = s.lev_row[k] * active + active;                                       \
+      s.lev_abs[k] += active;                                                              \
+      s.lev_last[k] = Lv[k];                                                               \
+      Lv[k] = 0.0f;                                                                        \
+    }                                                                                      \
+    k++;
+#include "gm_settings.def"
+  }
+}
+
+__device__ int sample_stream(const GmEnvState& s, int mode, int st, const gm_sensor& ss, float* out) {
+#pragma clang fp contract(off)
+  int prev = ss.prev_steps, rps = ss.readings_per_step, total = ss.total_readings;
+  if (mode == GM_SAMPLE_RAW) {
+    int n = total - 1;
+    for (int j = n - 1, k = 0; j >= 0; j--, k++) out[k] = ring_read(s, st, j);
+    return n;
+  }
+  out[0] = ring_read(s, st, total - 1);
+  for (int i = 0; i < prev; i++) {
+    int first = total - 1 - i * rps;
+    out[2 * i + 2] = ring_read(s, st, first - rps);
+    float a = out[2 * i], b = out[2 * i + 2];
+    float r;
+    if (mode == GM_SAMPLE_CHANGE) r = b - a;
+    else if (mode == GM_SAMPLE_AVERAGE) {
+      float acc = 0;
+      for (int j = 0; j < rps + 1; j++) acc += ring_read(s, st, first - j);
+      r = acc / (rps + 1);
+    } else if (mode == GM_SAMPLE_MEDIAN) {
+      float v[GM_RING + 1];
+      int nv = rps + 1;
+      for (int j = 0; j < nv; j++) v[j] = ring_read(s, st, first - j);
+      for (int x = 1; x < nv; x++) { float t = v[x]; int y = x - 1; while (y >= 0 && v[y] > t) { v[y + 1] = v[y]; y--; } v[y + 1] = t; }
+      int hn = nv / 2;
+      float med = v[hn];
+      if (!(nv & 1)) med = (v[hn - 1] + med) / 2.0f;
+      r = med;
+    } else if (mode == GM_SAMPLE_SIGN) {
+      float ch = b - a;
+      r = ch > 1e-6f ? 1.0f : (ch < -1e-6f ? -1.0f : 0.0f);
+    } else if (mode == GM_SAMPLE_SCALED_CHANGE) {
+      float sc = (b - a) / 0.07f;
+      r = sc > 1.0f ? 1.0f : (sc < -1.0f ? -1.0f : sc);
+    } else {
+      float ch = fabsf(b - a);
+      float sc = (b - a) * ch * (1.0f / (0.10f * 0.10f));
+      r = sc > 1.0f ? 1.0f : (sc < -1.0f ? -1.0f : sc);
+    }
+    out[2 * i + 1] = r;
+  }
+  return 2 * prev + 1;
+}
+
+// MjClass::get_observation (mjclass.cpp:1707-1959)
+__device__ int get_obs(const GmEnvState& s, const gm_config* __restrict__ C, float* out) {
+  const gm_settings& st = C->s;
+  int sf = C->sensor_fcn, tf = C->state_fcn, n = 0;
+  if (st.bending_gauge.in_use) for (int f = 0; f < 3; f++) n += sample_stream(s, sf, ST_GAUGE + f, st.bending_gauge, out + n);
+  if (st.axial_gauge.in_use) for (int f = 0; f < 3; f++) n += sample_stream(s, sf, ST_AXIAL + f, st.axial_gauge, out + n);
+  if (st.palm_sensor.in_use) n += sample_stream(s, sf, ST_PALM, st.palm_sensor, out + n);
+  if (st.wrist_sensor_XY.in_use) {
+    n += sample_stream(s, sf, ST_WX, st.wrist_sensor_XY, out + n);
+    n += sample_stream(s, sf, ST_WY, st.wrist_sensor_XY, out + n);
+  }
+  if (st.wrist_sensor_Z.in_use) n += sample_stream(s, sf, ST_WZ, st.wrist_sensor_XY, out + n);
+  if (st.motor_state_sensor.in_use) for (int k = 0; k < 3; k++) n += sample_stream(s, tf, ST_MOTOR + k, st.motor_state_sensor, out + n);
+  if (st.base_state_sensor_XY.in_use) for (int k = 0; k < 2; k++) n += sample_stream(s, tf, ST_BASE + k, st.base_state_sensor_XY, out + n);
+  if (st.base_state_sensor_Z.in_use) n += sample_stream(s, tf, ST_BASE + 2, st.base_state_sensor_Z, out + n);
+  if (st.base_state_sensor_yaw.in_use) n += sample_stream(s, tf, ST_YAW, st.base_state_sensor_yaw, out + n);
+  if (st.cartesian_contacts_XYZ.in_use)
+    for (int k = 0; k < 12; k++) n += sample_stream(s, GM_SAMPLE_CHANGE, ST_CART + k, st.cartesian_contacts_XYZ, out + n);
+  return n;
+}
+
+__device__ int is_done(const GmEnvState& s, const gm_config* __restrict__ C) {
+  const gm_settings& st = C->s;
+  int k = 0;
+  int done = 0;
+#define GM_BR(n, r, d, t) if (st.n.done && s.bev_row[k] >= st.n.done) done = 1; k++;
+#include "gm_settings.def"
+  k = 0;
+#define GM_LR(n, r, d, t, a, b, o) if (st.n.done && s.lev_row[k] >= st.n.done) done = 1; k++;
+#include "gm_settings.def"
+  if (st.cap_reward && st.quit_if_cap_exceeded) {
+    if (s.cumulative_reward - 1e-5 < st.reward_cap_lower_bound) done = 1;
+    if (s.cumulative_reward + 1e-5 > st.reward_cap_upper_bound) done = 1;
+  }
+  return done;
+}
+
+__device__ float linear_reward(float val, float mn, float mx, float overshoot) {
+#pragma clang fp contract(off)
+  if (val < mn) return 0.0f;
+  if (val > mx) {
+    if (overshoot < mx) return 1.0f;
+    if (val > overshoot) return 0.0f;
+    mn = 0; mx = overshoot - mx; val = overshoot - val;
+  }
+  return (val - mn) / (mx - mn);
+}
+__device__ float reward(GmEnvState& s, const gm_config* __restrict__ C) {
+#pragma clang fp contract(off)
+  const gm_settings& st = C->s;
+  float r = 0;
+  int k = 0;
+#define GM_BR(n, rr, d, t) if (s.bev_row[k] >= st.n.trigger) r += st.n.reward; k++;
+#include "gm_settings.def"
+  k = 0;
+#define GM_LR(n, rr, d, t, a, b, o)                                                        \
+  if (s.lev_row[k] >= st.n.trigger) {                                                      \
+    float fr = linear_reward(s.lev_last[k], st.n.min, st.n.max, st.n.overshoot);           \
+    r += st.n.reward * fr;                                                                 \
+  }                                                                                        \
+  k++;
+#include "gm_settings.def"
+  s.cumulative_reward += r;
+  if (s.cumulative_reward < st.reward_cap_lower_bound && st.cap_reward) {
+    r += st.reward_cap_lower_bound - s.cumulative_reward;
+    s.cumulative_reward = st.reward_cap_lower_bound;
+  }
+  if (s.cumulative_reward > st.reward_cap_upper_bound && st.cap_reward) {
+    r += st.reward_cap_upper_bound - s.cumulative_reward;
+    s.cumulative_reward = st.reward_cap_upper_bound;
+  }
+  return r;
+}
+
+// ============================================================ kernels
+__device__ __forceinline__ void load_state(Shared& S, const GmEnvState* __restrict__ g, int lane) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&S.s);
+  for (int i = lane; i < GM_STATE_WORDS; i += NT) dst[i] = src[i];
+  __syncthreads();
+}
+__device__ __forceinline__ void store_state(const Shared& S, GmEnvState* __restrict__ g, int lane) {
+  __syncthreads();
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&S.s);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(g);
+  for (int i = lane; i < GM_STATE_WORDS; i += NT) dst[i] = src[i];
+}
+
+// mode 0: action_step + obs/done/reward; mode 1: calibrate_reset settle (400 substeps,
+// no sensors); mode 2: one full substep with diagnostics
+extern "C" __global__ __launch_bounds__(NT) void gm_step_kernel(
+    GmEnvState* __restrict__ states, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
+    const GmTopo* __restrict__ T, float* __restrict__ obs, float* __restrict__ rew,
+    uint8_t* __restrict__ done, int n_envs, int mode, DebugOut dbg) {
+  __shared__ Shared S;
+  const int lane = threadIdx.x;
+  const int env = blockIdx.x;
+  if (env >= n_envs) return;
+  load_state(S, states + env, lane);
+  if (mode == 1) {
+    for (int i = 0; i < 400; i++) {
+      physics_substep(S, m, T, lane);
+      update_all(S, m, T, lane);
+    }
+    store_state(S, states + env, lane);
+    return;
+  }
+  int nsub = (mode == 2) ? 1 : C->sim_steps_per_action + S.s.extra_substeps;
+  for (int i = 0; i < nsub; i++) {
+    physics_substep(S, m, T, lane);
+    update_all(S, m, T, lane);
+    monitor_sensors(S, m, C, T, lane);
+  }
+  if (mode == 2) {
+    if (lane == 0) dbg.ncon[env] = S.ncon;
+    if (lane < GM_MAX_CON) {
+      float* o = dbg.contact + ((size_t)env * GM_MAX_CON + lane) * 16;
+      for (int k = 0; k < 16; k++) o[k] = 0;
+      if (lane < S.ncon) {
+        const float* Cc = S.con[lane];
+        o[0] = Cc[0];
+        for (int k = 0; k < 3; k++) o[1 + k] = Cc[1 + k];
+        for (int k = 0; k < 9; k++) o[4 + k] = Cc[4 + k];
+        o[13] = Cc[17]; o[14] = Cc[18]; o[15] = Cc[13];
+      }
+    }
+    dbg.efc_force[(size_t)env * GM_MAX_EFC + lane] = lane < S.nefc ? S.efc_f[lane] : 0.0f;
+    if (lane < GM_MAX_DOF) dbg.qacc[(size_t)env * GM_MAX_DOF + lane] = lane < T->nv ? S.qacc[lane] : 0.0f;
+    store_state(S, states + env, lane);
+    return;
+  }
+  if (lane == 0) {
+    S.s.extra_substeps = 0;
+    S.s.overflow = S.overflow;
+    sense_gripper_state(S, m, C);
+    update_env(S, m, C, T);
+    S.s.num_action_steps += 1;
+    float* o = obs + (size_t)env * C->n_obs;
+    get_obs(S.s, C, o);
+    int d = is_done(S.s, C);
+    float r = reward(S.s, C);
+    S.s.done = d;
+    S.s.reward = r;
+    rew[env] = r;
+    done[env] = (uint8_t)d;
+  }
+  store_state(S, states + env, lane);
+}
+
+// ---------------------------------------------------------------- actions
+// MjClass::set_action for every action index (mjclass.cpp:1528-1630); one thread per env.
+__device__ int move_base_target_m(GmEnvState& s, const gm_config* __restrict__ C, double x, double y, double z) {
+  double* b = s.base;
+  b[0] += x; b[1] += y; b[2] += z;
+  int wl = 1;
+  for (int k = 0; k < 3; k++) {
+    if (b[k] > C->base_max[k]) { b[k] = C->base_max[k]; wl = 0; }
+    if (b[k] < C->base_min[k]) { b[k] = C->base_min[k]; wl = 0; }
+  }
+  return wl;
+}
+__device__ int call_action(GmEnvState& s, const gm_config* __restrict__ C, int kind, double v) {
+  const gm_action* acts[GM_N_ACTION_KINDS] = {
+#define GM_AA(n, u, vv, sg) &C->s.n,
+#include "gm_settings.def"
+  };
+  v *= acts[kind]->sign;
+  switch (kind) {
+    case GM_ACT_gripper_X: return g_set_xyz_m(s.end, s.end.x + v, s.end.y, s.end.z);
+    case GM_ACT_gripper_Y: return g_set_xyz_m(s.end, s.end.x, s.end.y + v, s.end.z);
+    case GM_ACT_gripper_prismatic_X: return g_set_xyz_m_rad(s.end, s.end.x + v, s.end.th, s.end.z);
+    case GM_ACT_gripper_revolute_Y: return g_set_xyz_m_rad(s.end, s.end.x, s.end.th + v, s.end.z);
+    case GM_ACT_gripper_Z: return g_set_xyz_m(s.end, s.end.x, s.end.y, s.end.z + v);
+    case GM_ACT_base_X: return move_base_target_m(s, C, v, 0, 0);
+    case GM_ACT_base_Y: return move_base_target_m(s, C, 0, v, 0);
+    case GM_ACT_base_Z: return move_base_target_m(s, C, 0, 0, v);
+    case GM_ACT_base_roll:
+    case GM_ACT_base_pitch: return 1;
+    default: {
+      s.base[5] += v;
+      int wl = 1;
+      if (s.base[5] > C->base_max[5]) { s.base[5] = C->base_max[5]; wl = 0; }
+      if (s.base[5] < C->base_min[5]) { s.base[5] = C->base_min[5]; wl = 0; }
+      return wl;
+    }
+  }
+}
+__device__ void set_action_one(GmEnvState& s, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
+                               int action, float frac) {
+#pragma clang fp contract(off)
+  const gm_settings& st = C->s;
+  int wl = 1;
+  s.termination_signal_sent = 0;
+  if (action < 0 || action >= C->n_actions) return;
+  int code = C->action_options[action];
+  if (code == GM_ACTION_TERMINATION) {
+    float value = st.continous_actions ? frac : 1.0f;
+    if (value > st.termination_threshold) {
+      s.termination_signal_sent = 1;
+      if (st.lift_on_termination) {
+        s.base[2] = -C->base_max[2];
+        if (s.base[2] > C->base_max[2]) s.base[2] = C->base_max[2];
+        if (s.base[2] < C->base_min[2]) s.base[2] = C->base_min[2];
+        s.extra_substeps += C->sim_steps_per_action * 2;
+      }
+    }
+    wl = 1;
+  } else {
+    const gm_action* acts[GM_N_ACTION_KINDS] = {
+#define GM_AA(n, u, vv, sg) &st.n,
+#include "gm_settings.def"
+    };
+    int kind = code / 3, sub = code % 3;
+    if (sub == 0) wl = call_action(s, C, kind, acts[kind]->value);
+    else if (sub == 1) wl = call_action(s, C, kind, -1 * acts[kind]->value);
+    else {
+      wl = call_action(s, C, kind, acts[kind]->value * frac);
+      s.lev_value[GM_LEV_action_penalty_lin] += fabsf(frac);
+      s.lev_value[GM_LEV_action_penalty_sq] += (frac * frac);
+    }
+  }
+  // get_fingertip_z_height (myfunctions.cpp:3608-3620)
+  float straight = (float)(-C->base_min[2] - s.base[2]);
+  float tip_lift = (float)(m->finger_length * (1 - cos(g_calc_th(s.end.x, s.end.y))));
+  float hgt = straight + tip_lift;
+  float fz = (float)(hgt + C->base_min[2]);
+  if (fz < st.fingertip_min_mm * 1e-3) wl = 0;
+  s.bev_value[GM_EV_exceed_limits] = s.bev_value[GM_EV_exceed_limits] || !wl;
+}
+
+extern "C" __global__ void gm_action_kernel(GmEnvState* __restrict__ states, const gm_model* __restrict__ m,
+                                            const gm_config* __restrict__ C, const float* __restrict__ cont,
+                                            const int32_t* __restrict__ disc, int n_envs) {
+  int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n_envs) return;
+  GmEnvState& s = states[env];
+  if (cont) {
+    for (int i = 0; i < C->n_actions; i++) {
+      float f = cont[(size_t)env * C->n_actions + i];
+      if (f < -1.0f) f = -1.0f; else if (f > 1.0f) f = 1.0f;
+      set_action_one(s, m, C, i, f);
+    }
+  } else {
+    set_action_one(s, m, C, disc[env], 0.0f);
+  }
+}
+
+// ---------------------------------------------------------------- reset + spawn
+// MjClass::reset (mjclass.cpp:434-486) -> luke::reset / calibrate_reset (non-first call),
+// configure_settings RNG draws, random_base_Z_movement, then spawn_object.
+extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, const gm_model* __restrict__ m,
+                                           const gm_config* __restrict__ C, const GmTopo* __restrict__ T,
+                                           const float* __restrict__ eq_qpos, const uint8_t* __restrict__ mask,
+                                           const gm_spawn* __restrict__ spawn, const gm_object* __restrict__ objs,
+                                           int n_objects, int n_envs) {
+  int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n_envs) return;
+  if (mask && !mask[env]) return;
+  GmEnvState& s = states[env];
+  // keep the per-env RNG stream and the function-static stepper flags (quirk)
+  uint32_t rng = s.rng;
+  int ox = s.old_x, oy = s.old_y, oz = s.old_z;
+  uint32_t* w = reinterpret_cast<uint32_t*>(&s);
+  for (int i = 0; i < GM_STATE_WORDS; i++) w[i] = 0;
+  s.rng = rng; s.old_x = ox; s.old_y = oy; s.old_z = oz;
+  g_reset(s.end); g_reset(s.next);
+  for (int k = 0; k < GM_MAX_QPOS; k++) s.qpos[k] = (float)m->qpos0[k];
+  s.time = 0; s.last_step_time = 0;
+  for (int d = 0; d < T->nv; d++) {
+    bool motor = (d == m->dof_base || d == m->dof_palm);
+    for (int f = 0; f < 3; f++) motor = motor || d == m->dof_pris[f] || d == m->dof_rev[f];
+    if (motor) s.qpos[d] = eq_qpos[d];
+  }
+  for (int k = 0; k < T->nlock; k++) { s.lock_active[k] = 1; s.lock_q[k] = (float)m->qpos0[m->lock_dof[k]]; }
+  for (int st = 0; st < GM_NSTREAM; st++) s.ring_i[st] = -1;
+  // apply_noise_params: mean draws, SS order then the state sensors again
+  {
+    const gm_settings& st = C->s;
+    const gm_sensor* ss[SL_N] = {&st.motor_state_sensor, &st.base_state_sensor_Z, &st.base_state_sensor_XY,
+                                 &st.base_state_sensor_yaw, &st.bending_gauge, &st.axial_gauge, &st.palm_sensor,
+                                 &st.wrist_sensor_XY, &st.wrist_sensor_Z, &st.cartesian_contacts_XYZ};
+    for (int k = 0; k < SL_N; k++)
+      for (int i = 0; i < 3; i++) {
+#pragma clang fp contract(off)
+        s.rand_mu[k][i] = ss[k]->noise_mu * (2 * unif01(s.rng) - 1);
+      }
+    int order[5] = {SL_MOTOR, SL_BASEXY, SL_BASEZ, SL_YAW, SL_CART};
+    for (int k = 0; k < 5; k++)
+      for (int i = 0; i < 3; i++) {
+#pragma clang fp contract(off)
+        s.rand_mu[order[k]][i] = ss[order[k]]->noise_mu * (2 * unif01(s.rng) - 1);
+      }
+  }
+  {
+#pragma clang fp contract(off)
+    double size = C->s.base_position_noise;
+    double u = canon_d(s.rng);
+    double z = u * (size - (-size)) + (-size);
+    s.base[2] = z;
+    if (s.base[2] > C->base_max[2]) s.base[2] = C->base_max[2];
+    if (s.base[2] < C->base_min[2]) s.base[2] = C->base_min[2];
+    s.qpos[m->dof_base] = (float)(s.base[2] + (double)eq_qpos[m->dof_base]);
+  }
+  // spawn_object
+  gm_spawn sp = spawn ? spawn[env] : gm_spawn{0, 0.0, 0.0, 0.0};
+  int oi = sp.object_index;
+  if (oi < 0 || oi >= n_objects) oi = 0;
+  const gm_object& o = objs[oi];
+  s.obj_index = oi;
+  s.obj_type = o.type;
+  s.obj_size[0] = (float)o.size[0]; s.obj_size[1] = (float)o.size[1]; s.obj_size[2] = (float)o.size[2];
+  s.obj_mass = (float)o.mass;
+  s.obj_friction = (float)o.friction;
+  double I0, I1, I2, rb, restz;
+  if (o.type == GM_GEOM_BOX) {
+    double a = 2 * o.size[0], bb = 2 * o.size[1], c = 2 * o.size[2];
+    I0 = o.mass * (bb * bb + c * c) / 12; I1 = o.mass * (a * a + c * c) / 12; I2 = o.mass * (a * a + bb * bb) / 12;
+    rb = sqrt(o.size[0] * o.size[0] + o.size[1] * o.size[1] + o.size[2] * o.size[2]);
+    restz = o.size[2];
+  } else if (o.type == GM_GEOM_CYLINDER) {
+    double r = o.size[0], hh = 2 * o.size[1];
+    I0 = I1 = o.mass * (3 * r * r + hh * hh) / 12; I2 = o.mass * r * r / 2;
+    rb = sqrt(o.size[0] * o.size[0] + o.size[1] * o.size[1]);
+    restz = o.size[1];
+  } else {
+    double r = o.size[0];
+    I0 = I1 = I2 = 2 * o.mass * r * r / 5;
+    rb = r;
+    restz = r;
+  }
+  s.obj_inertia[0] = (float)I0; s.obj_inertia[1] = (float)I1; s.obj_inertia[2] = (float)I2;
+  s.obj_rbound = (float)rb;
+  s.obj_rest_z = (float)restz;
+  int qa = T->qadr_obj;
+  double x2 = sin(-sp.zrot / 2.0), w2 = cos(-sp.zrot / 2.0);
+  double q4[4] = {x2, 0, 0, w2};   // reference QPos quirk: qx lands in MuJoCo's w slot
+  double nq = sqrt(q4[0] * q4[0] + q4[1] * q4[1] + q4[2] * q4[2] + q4[3] * q4[3]);
+  s.qpos[qa + 0] = (float)sp.x;
+  s.qpos[qa + 1] = (float)sp.y;
+  s.qpos[qa + 2] = (float)(restz + 1e-6);
+  for (int k = 0; k < 4; k++) s.qpos[qa + 3 + k] = (float)(q4[k] / nq);
+  for (int k = 0; k < 7; k++) s.start_qpos[k] = s.qpos[qa + k];
+}
+
+// settle initialisation (keyframe, targets home, locks off, flags true) for env 0
+extern "C" __global__ void gm_settle_init_kernel(GmEnvState* __restrict__ states, const gm_model* __restrict__ m,
+                                                 const GmTopo* __restrict__ T, const gm_object* __restrict__ objs) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  GmEnvState& s = states[0];
+  uint32_t* w = reinterpret_cast<uint32_t*>(&s);
+  for (int i = 0; i < GM_STATE_WORDS; i++) w[i] = 0;
+  g_reset(s.end); g_reset(s.next);
+  for (int k = 0; k < GM_MAX_QPOS; k++) s.qpos[k] = (float)m->qpos0[k];
+  s.old_x = s.old_y = s.old_z = 1;
+  for (int st = 0; st < GM_NSTREAM; st++) s.ring_i[st] = -1;
+  const gm_object& o = objs[0];
+  s.obj_type = o.type;
+  s.obj_size[0] = (float)o.size[0]; s.obj_size[1] = (float)o.size[1]; s.obj_size[2] = (float)o.size[2];
+  s.obj_mass = (float)o.mass;
+  s.obj_friction = (float)o.friction;
+  if (o.type == GM_GEOM_BOX) {
+    double a = 2 * o.size[0], bb = 2 * o.size[1], c = 2 * o.size[2];
+    s.obj_inertia[0] = (float)(o.mass * (bb * bb + c * c) / 12); s.obj_inertia[1] = (float)(o.mass * (a * a + c * c) / 12);
+    s.obj_inertia[2] = (float)(o.mass * (a * a + bb * bb) / 12);
+    s.obj_rbound = (float)sqrt(o.size[0] * o.size[0] + o.size[1] * o.size[1] + o.size[2] * o.size[2]);
+  } else if (o.type == GM_GEOM_CYLINDER) {
+    double r = o.size[0], hh = 2 * o.size[1];
+    s.obj_inertia[0] = s.obj_inertia[1] = (float)(o.mass * (3 * r * r + hh * hh) / 12);
+    s.obj_inertia[2] = (float)(o.mass * r * r / 2);
+    s.obj_rbound = (float)sqrt(o.size[0] * o.size[0] + o.size[1] * o.size[1]);
+  } else {
+    double r = o.size[0];
+    s.obj_inertia[0] = s.obj_inertia[1] = s.obj_inertia[2] = (float)(2 * o.mass * r * r / 5);
+    s.obj_rbound = (float)r;
+  }
+}
+
+// per-env initialisation after the settle: RNG seeds and settled stepper flags
+extern "C" __global__ void gm_init_envs_kernel(GmEnvState* __restrict__ states, uint32_t base_seed, long long env_offset,
+                                               int n_envs) {
+  int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n_envs) return;
+  GmEnvState& s = states[env];
+  uint64_t seed = ((uint64_t)base_seed + (uint64_t)(env_offset + env) * 1000003ull) % 2147483647ull;
+  s.rng = seed == 0 ? 1u : (uint32_t)seed;
+  s.old_x = s.old_y = s.old_z = 0;
+}

@@ -1,0 +1,98 @@
+// gm_state.h -- per-env persistent state in HBM and the device model view.
+//
+// One EnvState per env, array-of-structs: the fused step kernel runs one
+// 64-lane workgroup per env and moves the whole struct HBM<->LDS with fully
+// coalesced 4-byte-per-lane sweeps at launch entry/exit.  Everything an
+// MjClass instance carries between action_step() calls (mjclass.h:1554-1833,
+// myfunctions.cpp:464-473 globals, the function-static flags the reference
+// keeps across resets) lives here.
+#pragma once
+#include <stdint.h>
+#include "gripper_mi355x.h"
+
+#define GM_NSTREAM 37          // sensor ring streams, see stream ids below
+// stream ids (observation windows, then SI windows)
+enum {
+  ST_GAUGE = 0,      // 3
+  ST_AXIAL = 3,      // 3
+  ST_PALM = 6,
+  ST_WX = 7,
+  ST_WY = 8,
+  ST_WZ = 9,
+  ST_MOTOR = 10,     // 3
+  ST_BASE = 13,      // 3 (x, y, z)
+  ST_YAW = 16,
+  ST_CART = 17,      // 12
+  ST_SI_GAUGE = 29,  // 3
+  ST_SI_AXIAL = 32,  // 3
+  ST_SI_PALM = 35,
+  ST_SI_WZ = 36
+};
+// sensor slots in settings (SS) order, used for last_read_time / rand_mu
+enum { SL_MOTOR = 0, SL_BASEZ, SL_BASEXY, SL_YAW, SL_BEND, SL_AXIAL, SL_PALM, SL_WRISTXY, SL_WRISTZ, SL_CART, SL_N };
+
+struct GmGrip {            // luke::Gripper (gripper.h:11-198)
+  double x, y, z, th;
+  int32_t sx, sy, sz, pad;
+};
+
+struct GmEnvState {
+  // ---- doubles first (8-byte aligned) ----
+  double time;
+  double last_step_time;
+  GmGrip end, next;
+  double base[6];
+  double last_read[SL_N];
+  // ---- floats ----
+  float qpos[GM_MAX_QPOS];
+  float qvel[GM_MAX_DOF];
+  float lock_q[GM_MAX_LOCK];
+  float rand_mu[SL_N][3];
+  float ring[GM_NSTREAM][GM_RING];
+  float lev_value[GM_N_LINEAR];
+  float lev_last[GM_N_LINEAR];
+  float cumulative_reward;
+  float grp_peak_lateral;
+  float start_qpos[7];
+  float obj_size[3];
+  float obj_mass, obj_inertia[3], obj_friction, obj_rbound, obj_rest_z;
+  float reward;
+  // ---- ints ----
+  int32_t ring_i[GM_NSTREAM];
+  int32_t bev_value[GM_N_BINARY];
+  int32_t bev_last[GM_N_BINARY];
+  int32_t bev_row[GM_N_BINARY];
+  int32_t bev_abs[GM_N_BINARY];
+  int32_t lev_row[GM_N_LINEAR];
+  int32_t lev_abs[GM_N_LINEAR];
+  int32_t lock_active[GM_MAX_LOCK];
+  int32_t old_x, old_y, old_z;
+  int32_t num_action_steps;
+  int32_t termination_signal_sent;
+  int32_t extra_substeps;        // termination lift substeps pending (2 * S)
+  int32_t obj_type;
+  int32_t obj_index;
+  int32_t done;
+  int32_t overflow;
+  uint32_t rng;
+  int32_t pad_end;
+};
+
+// word count for HBM<->LDS sweeps
+#define GM_STATE_WORDS ((int)(sizeof(GmEnvState) / 4))
+static_assert(sizeof(GmEnvState) % 8 == 0, "GmEnvState must be 8-byte padded");
+
+// Topology derived from gm_model on the host (the canonical gripper tree):
+// dof/body of chain position p in finger chain f is first + p - 1 (p >= 1),
+// position 0 of every finger / palm chain is the base dof.
+struct GmTopo {
+  int32_t N, CL, nbody, nv, nq, ngeom, npair, nlock;
+  int32_t body_base, dof_base;
+  int32_t body_f0[3], dof_f0[3];       // first chain body / dof (intermediate / prismatic)
+  int32_t body_palm, dof_palm, body_obj, dof_obj, qadr_obj, geom_obj;
+  int32_t body_finger[3];              // "finger_f" bodies (local force frames)
+  int32_t geom_group[GM_MAX_GEOM];     // 0..2 finger, 3 palm, 5 object, -1 world
+  int32_t geom_cpos[GM_MAX_GEOM];      // chain position of the geom's body (fingers / palm)
+  int32_t body_group[GM_MAX_BODY];
+  int32_t body_cpos[GM_MAX_BODY];
+};

@@ -1,0 +1,16 @@
+"""gmx -- MI355X-native batched gripper env-step (the reference's MjClass hot path).
+
+Host-side mirror of the reference's MjClass / MjEnv step contract over the C ABI
+in include/gripper_mi355x.h.  Every env-step runs on the GPU; there is no CPU
+fallback (the library raises ImportError when the HIP extension is missing).
+"""
+from ._lib import (load_library, Settings, ModelParams, Object, Spawn, ModelBlob, ConfigBlob,
+                   default_settings, make_object_set, BINARY_EVENTS, LINEAR_EVENTS, ACTION_KINDS,
+                   SENSORS, LIB_PATH)
+from .settings import canonical_settings, disable_noise, MAX_EPISODE_STEPS
+from .env import BatchedGripperEnv, spawn_positions
+
+__all__ = ["load_library", "Settings", "ModelParams", "Object", "Spawn", "ModelBlob", "ConfigBlob",
+           "default_settings", "make_object_set", "canonical_settings", "disable_noise",
+           "BatchedGripperEnv", "spawn_positions", "MAX_EPISODE_STEPS", "BINARY_EVENTS",
+           "LINEAR_EVENTS", "ACTION_KINDS", "SENSORS", "LIB_PATH"]

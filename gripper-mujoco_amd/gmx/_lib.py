@@ -1,0 +1,251 @@
+"""ctypes binding of the C ABI in include/gripper_mi355x.h.
+
+The struct layouts are generated from the same X-macro list the C side uses
+(include/gm_settings.def) and verified against gm_struct_size() at load time,
+so a layout drift fails loudly instead of corrupting settings.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_DIR = os.path.dirname(PKG_DIR)
+INCLUDE_DIR = os.path.join(REPO_DIR, "include")
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libgm.so")
+
+GM_MAX_SEG = 10
+GM_MAX_BODY = 40
+GM_MAX_DOF = 40
+GM_MAX_QPOS = 48
+GM_MAX_GEOM = 40
+GM_MAX_PAIR = 64
+GM_MAX_CON = 15
+GM_MAX_EFC = 64
+GM_MAX_LOCK = 4
+GM_MAX_OBJSET = 64
+
+GEOM_SPHERE, GEOM_CYLINDER, GEOM_BOX = 2, 5, 6
+
+_CTYPE = {"int32_t": C.c_int32, "uint32_t": C.c_uint32, "double": C.c_double, "float": C.c_float}
+
+
+class Sensor(C.Structure):
+    _fields_ = [("in_use", C.c_int32), ("normalise", C.c_float), ("read_rate", C.c_float),
+                ("use_normalisation", C.c_int32), ("use_noise", C.c_int32),
+                ("raw_value_offset", C.c_float), ("noise_mag", C.c_float), ("noise_mu", C.c_float),
+                ("noise_std", C.c_float), ("noise_overriden", C.c_int32), ("prev_steps", C.c_int32),
+                ("readings_per_step", C.c_int32), ("total_readings", C.c_int32)]
+
+
+class Action(C.Structure):
+    _fields_ = [("in_use", C.c_int32), ("continous", C.c_int32), ("value", C.c_double),
+                ("sign", C.c_int32)]
+
+
+class BinaryReward(C.Structure):
+    _fields_ = [("reward", C.c_float), ("done", C.c_int32), ("trigger", C.c_int32)]
+
+
+class LinearReward(C.Structure):
+    _fields_ = [("reward", C.c_float), ("done", C.c_int32), ("trigger", C.c_int32),
+                ("min", C.c_float), ("max", C.c_float), ("overshoot", C.c_float)]
+
+
+def parse_settings_def(path=None):
+    """Return [(kind, name, args...)] in declaration order from gm_settings.def."""
+    path = path or os.path.join(INCLUDE_DIR, "gm_settings.def")
+    out = []
+    pat = re.compile(r"^\s*GM_(XX|SS|AA|BR|LR)\(\s*([A-Za-z0-9_]+)\s*,(.*)\)\s*$")
+    with open(path) as f:
+        for line in f:
+            m = pat.match(line)
+            if not m:
+                continue
+            args = [a.strip() for a in m.group(3).split(",")]
+            out.append((m.group(1), m.group(2), args))
+    return out
+
+
+SETTINGS_DEF = parse_settings_def()
+BINARY_EVENTS = [n for k, n, _ in SETTINGS_DEF if k == "BR"]
+LINEAR_EVENTS = [n for k, n, _ in SETTINGS_DEF if k == "LR"]
+ACTION_KINDS = [n for k, n, _ in SETTINGS_DEF if k == "AA"]
+SENSORS = [n for k, n, _ in SETTINGS_DEF if k == "SS"]
+
+
+def _settings_fields():
+    fields = []
+    for kind, name, args in SETTINGS_DEF:
+        if kind == "XX":
+            fields.append((name, _CTYPE[args[0]]))
+        elif kind == "SS":
+            fields.append((name, Sensor))
+        elif kind == "AA":
+            fields.append((name, Action))
+        elif kind == "BR":
+            fields.append((name, BinaryReward))
+        else:
+            fields.append((name, LinearReward))
+    return fields
+
+
+class Settings(C.Structure):
+    _fields_ = _settings_fields()
+
+
+class ModelParams(C.Structure):
+    _fields_ = [("n_seg", C.c_int32), ("finger_length", C.c_double), ("finger_width", C.c_double),
+                ("finger_thickness", C.c_double), ("finger_E", C.c_double),
+                ("hook_length", C.c_double), ("hook_angle_degrees", C.c_double),
+                ("fingertip_clearance", C.c_double), ("segment_inertia_scaling", C.c_double),
+                ("timestep", C.c_double), ("pgs_iterations", C.c_int32),
+                ("collision_half_thickness", C.c_double)]
+
+
+class Object(C.Structure):
+    _fields_ = [("type", C.c_int32), ("size", C.c_double * 3), ("mass", C.c_double),
+                ("friction", C.c_double)]
+
+
+class Spawn(C.Structure):
+    _fields_ = [("object_index", C.c_int32), ("x", C.c_double), ("y", C.c_double),
+                ("zrot", C.c_double)]
+
+
+_lib = None
+
+
+def load_library(path: str | None = None):
+    """Load libgm.so.  Raises ImportError (loudly) when the HIP extension is missing:
+    there is no CPU fallback for the product path."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError(
+            f"gripper-mi355x HIP extension not built: {p} is missing "
+            "(run `python -c 'import __graft_entry__ as g; g.build()'` from the repo root)")
+    lib = C.CDLL(p)
+    _declare(lib)
+    sizes = {0: Settings, 3: Object, 4: Spawn, 5: ModelParams}
+    for which, cls in sizes.items():
+        n = lib.gm_struct_size(which)
+        if n != C.sizeof(cls):
+            raise ImportError(f"struct layout mismatch for {cls.__name__}: C {n} vs ctypes {C.sizeof(cls)}")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _declare(lib):
+    vp, i32, f32p, i32p, u8p, f64p = C.c_void_p, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int32), \
+        C.POINTER(C.c_uint8), C.POINTER(C.c_double)
+    sig = {
+        "gm_version": (C.c_char_p, []),
+        "gm_device_count": (i32, []),
+        "gm_struct_size": (C.c_int64, [i32]),
+        "gm_model_info": (None, [vp, i32p]),
+        "gm_config_info": (None, [vp, i32p]),
+        "gm_default_model_params": (None, [vp]),
+        "gm_build_model": (i32, [vp, vp]),
+        "gm_default_settings": (None, [vp]),
+        "gm_configure": (i32, [vp, vp, vp]),
+        "gm_make_object_set": (i32, [C.c_char_p, C.c_uint64, vp, i32]),
+        "gm_create": (i32, [vp, vp, vp, i32, i32, i32, i32, C.c_uint64, C.POINTER(vp)]),
+        "gm_destroy": (None, [vp]),
+        "gm_last_error": (C.c_char_p, [vp]),
+        "gm_n_envs": (i32, [vp]),
+        "gm_n_obs": (i32, [vp]),
+        "gm_n_actions": (i32, [vp]),
+        "gm_update_config": (i32, [vp, vp]),
+        "gm_reset": (i32, [vp, u8p, vp]),
+        "gm_set_action": (i32, [vp, vp, i32]),
+        "gm_set_discrete_action": (i32, [vp, vp, i32]),
+        "gm_step": (i32, [vp]),
+        "gm_get_obs": (i32, [vp, vp, i32]),
+        "gm_get_reward_done": (i32, [vp, vp, vp, i32]),
+        "gm_get_event_rows": (i32, [vp, i32p, i32p, f32p]),
+        "gm_get_state": (i32, [vp, f32p, f32p, f64p]),
+        "gm_set_state": (i32, [vp, f32p, f32p]),
+        "gm_get_target": (i32, [vp, f64p, i32p, i32p, f64p]),
+        "gm_get_overflow": (i32, [vp, i32p]),
+        "gm_device_obs": (vp, [vp]),
+        "gm_device_reward": (vp, [vp]),
+        "gm_device_done": (vp, [vp]),
+        "gm_device_actions": (vp, [vp]),
+        "gm_stream": (vp, [vp]),
+        "gm_last_step_ms": (i32, [vp, f32p]),
+        "gm_debug_substep": (i32, [vp, i32p, f32p, f32p, f32p]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def struct_size(which: int) -> int:
+    return int(load_library().gm_struct_size(which))
+
+
+class ModelBlob:
+    """An opaque gm_model (the compiled gripper, what mj_loadXML would return)."""
+
+    def __init__(self, params: ModelParams | None = None):
+        lib = load_library()
+        if params is None:
+            params = ModelParams()
+            lib.gm_default_model_params(C.byref(params))
+        self.params = params
+        self.buf = C.create_string_buffer(struct_size(1))
+        rc = lib.gm_build_model(C.byref(params), self.buf)
+        if rc != 0:
+            raise RuntimeError(f"gm_build_model failed ({rc})")
+        info = (C.c_int32 * 18)()
+        lib.gm_model_info(self.buf, info)
+        (self.nq, self.nv, self.nbody, self.ngeom, self.npair, self.n_seg, self.dof_base,
+         self.dof_palm, self.dof_obj) = info[:9]
+        self.dof_pris = list(info[9:12])
+        self.dof_rev = list(info[12:15])
+        self.dof_seg = list(info[15:18])
+
+    @property
+    def ptr(self):
+        return C.cast(self.buf, C.c_void_p)
+
+
+class ConfigBlob:
+    """An opaque gm_config: settings + what configure_settings() derives from them."""
+
+    def __init__(self, settings: Settings, model: ModelBlob):
+        lib = load_library()
+        self.buf = C.create_string_buffer(struct_size(2))
+        rc = lib.gm_configure(C.byref(settings), model.buf, self.buf)
+        if rc != 0:
+            raise RuntimeError(f"gm_configure rejected the settings ({rc})")
+        info = (C.c_int32 * 5)()
+        lib.gm_config_info(self.buf, info)
+        self.n_obs, self.n_actions, self.sim_steps_per_action, self.sensor_fcn, self.state_fcn = info[:5]
+
+    @property
+    def ptr(self):
+        return C.cast(self.buf, C.c_void_p)
+
+
+def default_settings() -> Settings:
+    s = Settings()
+    load_library().gm_default_settings(C.byref(s))
+    return s
+
+
+def make_object_set(name: str, seed: int = 1234):
+    arr = (Object * GM_MAX_OBJSET)()
+    n = load_library().gm_make_object_set(name.encode(), seed, arr, GM_MAX_OBJSET)
+    if n <= 0:
+        raise ValueError(f"unknown object set {name!r}")
+    out = (Object * n)()
+    for i in range(n):
+        out[i] = arr[i]
+    return out

@@ -1,0 +1,30 @@
+"""Build the in-tree HIP extension (gfx950) and the C-ABI shared library."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+from ._lib import PKG_DIR, REPO_DIR, LIB_PATH
+
+SOURCES = ["csrc/gm_capi.hip", "csrc/gm_host_model.cpp"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+         "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics"]
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    srcs = [os.path.join(PKG_DIR, s) for s in SOURCES]
+    deps = srcs + [os.path.join(PKG_DIR, "csrc", f) for f in ("gm_kernels.hip", "gm_state.h")] + \
+        [os.path.join(REPO_DIR, "include", f) for f in ("gripper_mi355x.h", "gm_settings.def")]
+    if not force and os.path.exists(LIB_PATH):
+        t = os.path.getmtime(LIB_PATH)
+        if all(os.path.getmtime(d) <= t for d in deps):
+            return LIB_PATH
+    os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
+    cmd = [HIPCC, *FLAGS, "-I" + os.path.join(REPO_DIR, "include"), "-I" + os.path.join(PKG_DIR, "csrc"),
+           *srcs, "-o", LIB_PATH + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH

@@ -1,0 +1,205 @@
+"""Batched env: the reference's MjEnv.step / reset contract (rl/env/MjEnv.py:2170-2263)
+for n_envs envs at once, every env-step executed by the fused device kernel.
+
+Step order matches MjEnv.step: actions -> action_step -> observation -> (terminated,
+truncated) -> reward.  Truncation at max_episode_steps is tracked on the host exactly
+as MjEnv._is_done does (MjEnv.py:616-637).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import (load_library, ModelBlob, ConfigBlob, ModelParams, Spawn, make_object_set,
+                   BINARY_EVENTS, LINEAR_EVENTS)
+from .settings import canonical_settings, MAX_EPISODE_STEPS
+
+
+def spawn_positions(rng: np.random.Generator, n: int, n_objects: int, pos_noise_m: float = 10e-3,
+                    rot_noise_rad: float = np.deg2rad(5.0)):
+    """Object index and pose per env, MjEnv._spawn_object defaults
+    (object_position_noise_mm=10, object_rotation_noise_deg=5; MjEnv.py:1177-1267)."""
+    idx = rng.integers(0, n_objects, size=n)
+    x = rng.uniform(-pos_noise_m, pos_noise_m, size=n)
+    y = rng.uniform(-pos_noise_m, pos_noise_m, size=n)
+    rot = rng.uniform(-rot_noise_rad, rot_noise_rad, size=n)
+    return idx, x, y, rot
+
+
+class BatchedGripperEnv:
+    def __init__(self, n_envs: int, object_set: str = "set6_synthetic", settings=None,
+                 model_params: ModelParams | None = None, device: int = 0, seed: int = 1234,
+                 env_offset: int = 0, max_episode_steps: int = MAX_EPISODE_STEPS):
+        self.lib = load_library()
+        self.n_envs = int(n_envs)
+        self.model = ModelBlob(model_params)
+        self.settings = settings if settings is not None else canonical_settings(seed=seed)
+        self.cfg = ConfigBlob(self.settings, self.model)
+        self.objects = make_object_set(object_set, seed)
+        self.max_episode_steps = max_episode_steps
+        self.device = device
+        self.rng = np.random.default_rng(seed + 7919 * env_offset)
+        self._ctx = C.c_void_p()
+        rc = self.lib.gm_create(self.model.ptr, self.cfg.ptr, self.objects, len(self.objects), self.n_envs,
+                                int(env_offset), int(device), int(seed), C.byref(self._ctx))
+        if rc != 0:
+            msg = self.lib.gm_last_error(self._ctx).decode() if self._ctx else ""
+            raise RuntimeError(f"gm_create failed ({rc}) {msg}")
+        self.n_obs = self.lib.gm_n_obs(self._ctx)
+        self.n_actions = self.lib.gm_n_actions(self._ctx)
+        self.current_step = np.zeros(self.n_envs, dtype=np.int64)
+        self._obs = np.zeros((self.n_envs, self.n_obs), dtype=np.float32)
+        self._rew = np.zeros(self.n_envs, dtype=np.float32)
+        self._done = np.zeros(self.n_envs, dtype=np.uint8)
+
+    # ------------------------------------------------------------ plumbing
+    def _check(self, rc):
+        if rc != 0:
+            raise RuntimeError(self.lib.gm_last_error(self._ctx).decode() or f"gm error {rc}")
+
+    def close(self):
+        if self._ctx:
+            self.lib.gm_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ctx(self):
+        return self._ctx
+
+    @property
+    def stream(self) -> int:
+        return self.lib.gm_stream(self._ctx)
+
+    # ------------------------------------------------------------ env API
+    def make_spawn(self, mask=None, idx=None, x=None, y=None, rot=None):
+        n = self.n_envs
+        si, sx, sy, sr = spawn_positions(self.rng, n, len(self.objects))
+        if idx is not None: si = np.broadcast_to(np.asarray(idx), (n,))
+        if x is not None: sx = np.broadcast_to(np.asarray(x, dtype=np.float64), (n,))
+        if y is not None: sy = np.broadcast_to(np.asarray(y, dtype=np.float64), (n,))
+        if rot is not None: sr = np.broadcast_to(np.asarray(rot, dtype=np.float64), (n,))
+        arr = (Spawn * n)()
+        for e in range(n):
+            arr[e].object_index = int(si[e]); arr[e].x = float(sx[e]); arr[e].y = float(sy[e]); arr[e].zrot = float(sr[e])
+        return arr
+
+    def reset(self, mask=None, spawn=None):
+        """MjClass::reset + spawn for masked envs; returns the observation (MjEnv.reset)."""
+        if spawn is None:
+            spawn = self.make_spawn()
+        if mask is not None:
+            m = np.ascontiguousarray(np.asarray(mask, dtype=np.uint8))
+            self._check(self.lib.gm_reset(self._ctx, m.ctypes.data_as(C.POINTER(C.c_uint8)), spawn))
+            self.current_step[m.astype(bool)] = 0
+        else:
+            self._check(self.lib.gm_reset(self._ctx, None, spawn))
+            self.current_step[:] = 0
+        return self.observation()
+
+    def set_action(self, actions):
+        a = np.ascontiguousarray(np.asarray(actions, dtype=np.float32).reshape(self.n_envs, self.n_actions))
+        self._check(self.lib.gm_set_action(self._ctx, a.ctypes.data, 0))
+
+    def set_discrete_action(self, actions):
+        a = np.ascontiguousarray(np.asarray(actions, dtype=np.int32).reshape(self.n_envs))
+        self._check(self.lib.gm_set_discrete_action(self._ctx, a.ctypes.data, 0))
+
+    def action_step(self):
+        self._check(self.lib.gm_step(self._ctx))
+
+    def observation(self):
+        self._check(self.lib.gm_get_obs(self._ctx, self._obs.ctypes.data, 0))
+        return self._obs.copy()
+
+    def reward_done(self):
+        self._check(self.lib.gm_get_reward_done(self._ctx, self._rew.ctypes.data, self._done.ctypes.data, 0))
+        return self._rew.copy(), self._done.astype(bool)
+
+    def step(self, actions, discrete: bool = False):
+        """Returns (obs, reward, terminated, truncated) like MjEnv.step."""
+        self.current_step += 1
+        if discrete:
+            self.set_discrete_action(actions)
+        else:
+            self.set_action(actions)
+        self.action_step()
+        obs = self.observation()
+        rew, term = self.reward_done()
+        trunc = self.current_step >= self.max_episode_steps
+        term = np.where(trunc, False, term)
+        return obs, rew, term, trunc
+
+    # ------------------------------------------------------------ device (zero-copy) path
+    def step_device(self, actions_dev_ptr: int):
+        """actions already on the device (e.g. a torch tensor's data_ptr() written on
+        this context's stream); obs/reward/done stay on the device."""
+        self._check(self.lib.gm_set_action(self._ctx, C.c_void_p(actions_dev_ptr), 1))
+        self._check(self.lib.gm_step(self._ctx))
+
+    def device_buffers(self):
+        return (self.lib.gm_device_obs(self._ctx), self.lib.gm_device_reward(self._ctx),
+                self.lib.gm_device_done(self._ctx))
+
+    def last_step_ms(self) -> float:
+        v = C.c_float()
+        self._check(self.lib.gm_last_step_ms(self._ctx, C.byref(v)))
+        return float(v.value)
+
+    # ------------------------------------------------------------ inspection
+    def state(self):
+        q = np.zeros((self.n_envs, self.model.nq), dtype=np.float32)
+        v = np.zeros((self.n_envs, self.model.nv), dtype=np.float32)
+        t = np.zeros(self.n_envs, dtype=np.float64)
+        self._check(self.lib.gm_get_state(self._ctx, q.ctypes.data_as(C.POINTER(C.c_float)),
+                                          v.ctypes.data_as(C.POINTER(C.c_float)),
+                                          t.ctypes.data_as(C.POINTER(C.c_double))))
+        return q, v, t
+
+    def set_state(self, qpos, qvel):
+        q = np.ascontiguousarray(np.asarray(qpos, dtype=np.float32))
+        v = np.ascontiguousarray(np.asarray(qvel, dtype=np.float32))
+        self._check(self.lib.gm_set_state(self._ctx, q.ctypes.data_as(C.POINTER(C.c_float)),
+                                          v.ctypes.data_as(C.POINTER(C.c_float))))
+
+    def target(self):
+        e = np.zeros((self.n_envs, 4)); es = np.zeros((self.n_envs, 3), dtype=np.int32)
+        ns = np.zeros((self.n_envs, 3), dtype=np.int32); b = np.zeros((self.n_envs, 3))
+        self._check(self.lib.gm_get_target(self._ctx, e.ctypes.data_as(C.POINTER(C.c_double)),
+                                           es.ctypes.data_as(C.POINTER(C.c_int32)),
+                                           ns.ctypes.data_as(C.POINTER(C.c_int32)),
+                                           b.ctypes.data_as(C.POINTER(C.c_double))))
+        return e, es, ns, b
+
+    def event_rows(self):
+        W = len(BINARY_EVENTS) + len(LINEAR_EVENTS)
+        rows = np.zeros((self.n_envs, W), dtype=np.int32)
+        absc = np.zeros((self.n_envs, W), dtype=np.int32)
+        lastv = np.zeros((self.n_envs, W), dtype=np.float32)
+        self._check(self.lib.gm_get_event_rows(self._ctx, rows.ctypes.data_as(C.POINTER(C.c_int32)),
+                                               absc.ctypes.data_as(C.POINTER(C.c_int32)),
+                                               lastv.ctypes.data_as(C.POINTER(C.c_float))))
+        return rows, absc, lastv
+
+    def overflow(self):
+        o = np.zeros(self.n_envs, dtype=np.int32)
+        self._check(self.lib.gm_get_overflow(self._ctx, o.ctypes.data_as(C.POINTER(C.c_int32))))
+        return o
+
+    def debug_substep(self):
+        n = self.n_envs
+        ncon = np.zeros(n, dtype=np.int32)
+        con = np.zeros((n, 15, 16), dtype=np.float32)
+        f = np.zeros((n, 64), dtype=np.float32)
+        qacc = np.zeros((n, 40), dtype=np.float32)
+        self._check(self.lib.gm_debug_substep(self._ctx, ncon.ctypes.data_as(C.POINTER(C.c_int32)),
+                                              con.ctypes.data_as(C.POINTER(C.c_float)),
+                                              f.ctypes.data_as(C.POINTER(C.c_float)),
+                                              qacc.ctypes.data_as(C.POINTER(C.c_float))))
+        return ncon, con, f, qacc

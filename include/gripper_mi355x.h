@@ -1,0 +1,367 @@
+/* gripper_mi355x.h -- C ABI of the MI355X-native batched gripper env-step path.
+ *
+ * This is the drop-in boundary that replaces the per-env MjClass hot path which
+ * the reference exposes through pybind11 (src/bind.cpp:32-205, compiled to
+ * rl/env/mjpy/bind.so by Makefile:22,31,155-156).  Every entry point below names
+ * the reference interface it replaces.  Conventions:
+ *   - plain C types and pointers only; no C++ exceptions cross the ABI;
+ *   - every call returns GM_OK (0) or a negative GM_E* code, and the per-context
+ *     message is available from gm_last_error(ctx) (the Python facade raises
+ *     RuntimeError with it, as pybind11's default translator does for
+ *     std::runtime_error in the reference);
+ *   - host buffers are owned by the caller; `on_device != 0` means the pointer is
+ *     a HIP device pointer on the context's device (zero-copy torch tensors);
+ *   - one context per HIP stream; calls on one context are not reentrant.
+ *
+ * The interface data types (settings, model, object descriptors) are plain POD
+ * structs; tests/ hand the same structs to the CPU oracle in oracle/.
+ */
+#ifndef GRIPPER_MI355X_H_
+#define GRIPPER_MI355X_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ limits */
+#define GM_MAX_SEG    10      /* finger segment joints N (reference: 5..10)   */
+#define GM_MAX_BODY   40
+#define GM_MAX_DOF    40
+#define GM_MAX_QPOS   48
+#define GM_MAX_GEOM   40
+#define GM_MAX_PAIR   64      /* one wave lane per collision pair              */
+#define GM_MAX_CON    15      /* contacts kept per env per substep             */
+#define GM_MAX_EFC    64      /* constraint rows: 4 per contact + motor locks  */
+#define GM_MAX_LOCK   4       /* prismatic x3 + palm (revolute locks disabled) */
+#define GM_MAX_OBJSET 64      /* objects in one synthetic object set          */
+#define GM_RING       8       /* sensor ring length (needs 1 + 2*3 = 7)       */
+#define GM_CHAIN      (GM_MAX_SEG + 2)  /* dofs per finger chain below base   */
+
+/* ------------------------------------------------------------------ errors */
+#define GM_OK            0
+#define GM_E_ARG        -1
+#define GM_E_HIP        -2
+#define GM_E_STATE      -3
+#define GM_E_NOEXT      -4
+#define GM_E_RANGE      -5
+
+/* ------------------------------------------------------------- geom types */
+/* numbering follows MuJoCo's mjtGeom so the (geom1, geom2) canonical order
+ * "lower type first, then lower id" is the one the reference's contact signs
+ * depend on (hard part 3). */
+#define GM_GEOM_PLANE    0
+#define GM_GEOM_SPHERE   2
+#define GM_GEOM_CAPSULE  3
+#define GM_GEOM_CYLINDER 5
+#define GM_GEOM_BOX      6
+
+/* contact classes: Contact::check_involves() prefixes (objecthandler.h:117-129) */
+#define GM_CLS_NONE    0
+#define GM_CLS_FINGER1 1
+#define GM_CLS_FINGER2 2
+#define GM_CLS_FINGER3 3
+#define GM_CLS_PALM    4
+#define GM_CLS_GROUND  5
+#define GM_CLS_OBJECT  6
+
+/* joint types (MuJoCo mjtJoint numbering) */
+#define GM_JNT_FREE   0
+#define GM_JNT_SLIDE  2
+#define GM_JNT_HINGE  3
+
+/* body chain groups: which compact Jacobian block a body's dofs live in */
+#define GM_GRP_WORLD  -1
+#define GM_GRP_FINGER0 0
+#define GM_GRP_PALM    3
+#define GM_GRP_BASE    4
+#define GM_GRP_OBJECT  5
+
+/* ------------------------------------------------------------ settings */
+typedef struct gm_sensor {            /* MjType::Sensor, mjclass.h:79-241 */
+  int32_t in_use;
+  float   normalise;
+  float   read_rate;
+  int32_t use_normalisation;
+  int32_t use_noise;
+  float   raw_value_offset;
+  float   noise_mag;
+  float   noise_mu;
+  float   noise_std;
+  int32_t noise_overriden;
+  int32_t prev_steps;
+  int32_t readings_per_step;
+  int32_t total_readings;
+} gm_sensor;
+
+typedef struct gm_action {            /* MjType::ActionSetting, mjclass.h:458-572 */
+  int32_t in_use;
+  int32_t continous;
+  double  value;
+  int32_t sign;
+} gm_action;
+
+typedef struct gm_binary_reward {     /* MjType::BinaryReward, mjclass.h:649-663 */
+  float   reward;
+  int32_t done;
+  int32_t trigger;
+} gm_binary_reward;
+
+typedef struct gm_linear_reward {     /* MjType::LinearReward, mjclass.h:665-684 */
+  float   reward;
+  int32_t done;
+  int32_t trigger;
+  float   min;
+  float   max;
+  float   overshoot;
+} gm_linear_reward;
+
+typedef struct gm_settings {          /* MjType::Settings, mjclass.h:736-779 */
+#define GM_XX(n, t, v) t n;
+#define GM_SS(n, u, nm, r) gm_sensor n;
+#define GM_AA(n, u, v, s) gm_action n;
+#define GM_BR(n, r, d, t) gm_binary_reward n;
+#define GM_LR(n, r, d, t, a, b, o) gm_linear_reward n;
+#include "gm_settings.def"
+} gm_settings;
+
+/* event indices, in settings order (binary first, then linear) */
+enum {
+#define GM_BR(n, r, d, t) GM_EV_##n,
+#include "gm_settings.def"
+  GM_N_BINARY
+};
+enum {
+#define GM_LR(n, r, d, t, a, b, o) GM_LEV_##n,
+#include "gm_settings.def"
+  GM_N_LINEAR
+};
+enum {
+#define GM_AA(n, u, v, s) GM_ACT_##n,
+#include "gm_settings.def"
+  GM_N_ACTION_KINDS
+};
+/* action codes, MjType::Action (mjclass.h:40-63): 3 per action kind + termination */
+#define GM_ACTION_CODE_COUNT (3 * GM_N_ACTION_KINDS + 1)
+#define GM_ACTION_TERMINATION (3 * GM_N_ACTION_KINDS)
+
+/* sample modes, MjType::Sample (mjclass.h:66-76) */
+#define GM_SAMPLE_RAW 0
+#define GM_SAMPLE_CHANGE 1
+#define GM_SAMPLE_AVERAGE 2
+#define GM_SAMPLE_MEDIAN 3
+#define GM_SAMPLE_SIGN 4
+#define GM_SAMPLE_SCALED_CHANGE 5
+#define GM_SAMPLE_SCALED_CHANGE_SQ 6
+
+/* Derived configuration: what MjClass::configure_settings() (mjclass.cpp:97-314)
+ * and Settings::update_sensor_settings() (mjclass.cpp:5236-5265) compute from
+ * gm_settings.  Built on the host by gm_configure(); shared by all envs. */
+typedef struct gm_config {
+  gm_settings s;
+  int32_t n_actions;
+  int32_t action_options[GM_ACTION_CODE_COUNT];
+  int32_t sensor_fcn;                 /* sample mode for sensors            */
+  int32_t state_fcn;                  /* sample mode for state sensors      */
+  int32_t sensor_fcn_state_override;  /* reference quirk mjclass.cpp:204-206 */
+  int32_t sim_steps_per_action;
+  int32_t n_obs;
+  double  timestep;
+  double  sim_gauge_raw_to_N_factor;  /* mjclass.cpp:281                    */
+  double  base_min[6];                /* x,y,z,roll,pitch,yaw (myfunctions.cpp:245-261) */
+  double  base_max[6];
+} gm_config;
+
+/* ------------------------------------------------------------ model */
+typedef struct gm_model_params {      /* numerics the MJCF would carry (myfunctions.cpp:836-953) */
+  int32_t n_seg;                      /* N finger segment joints              */
+  double  finger_length;              /* 235e-3                               */
+  double  finger_width;               /* 28e-3                                */
+  double  finger_thickness;           /* 0.86e-3 (baseline yaml)              */
+  double  finger_E;                   /* 193e9                                */
+  double  hook_length;                /* 35e-3                                */
+  double  hook_angle_degrees;         /* 75                                   */
+  double  fingertip_clearance;        /* 10e-3                                */
+  double  segment_inertia_scaling;    /* 50                                   */
+  double  timestep;                   /* 3.187e-3 (test.cpp:207)              */
+  int32_t pgs_iterations;             /* fixed sweep count (deterministic)    */
+  double  collision_half_thickness;   /* finger plate collision half-thickness */
+} gm_model_params;
+
+typedef struct gm_model {
+  int32_t nbody, njnt, nq, nv, ngeom, npair, nlock, n_seg;
+  /* bodies (parent always has a lower index) */
+  int32_t body_parent[GM_MAX_BODY];
+  int32_t body_jnt[GM_MAX_BODY];      /* -1 = welded to parent             */
+  int32_t body_group[GM_MAX_BODY];    /* GM_GRP_*                          */
+  double  body_pos[GM_MAX_BODY][3];   /* in parent frame                   */
+  double  body_quat[GM_MAX_BODY][4];  /* w,x,y,z in parent frame           */
+  double  body_mass[GM_MAX_BODY];
+  double  body_ipos[GM_MAX_BODY][3];  /* centre of mass, body frame        */
+  double  body_inertia[GM_MAX_BODY][3]; /* principal, body-frame aligned   */
+  /* joints: at most one per body */
+  int32_t jnt_type[GM_MAX_BODY];
+  int32_t jnt_body[GM_MAX_BODY];
+  int32_t jnt_qposadr[GM_MAX_BODY];
+  int32_t jnt_dofadr[GM_MAX_BODY];
+  double  jnt_pos[GM_MAX_BODY][3];    /* anchor, body frame                */
+  double  jnt_axis[GM_MAX_BODY][3];   /* body frame, unit                  */
+  double  jnt_stiffness[GM_MAX_BODY];
+  double  jnt_damping[GM_MAX_BODY];
+  double  jnt_armature[GM_MAX_BODY];
+  /* dofs */
+  int32_t dof_parent[GM_MAX_DOF];
+  int32_t dof_body[GM_MAX_DOF];
+  int32_t dof_group[GM_MAX_DOF];      /* GM_GRP_* of the owning chain       */
+  int32_t dof_slot[GM_MAX_DOF];       /* index inside the compact group block */
+  /* geoms */
+  int32_t geom_type[GM_MAX_GEOM];
+  int32_t geom_body[GM_MAX_GEOM];
+  int32_t geom_class[GM_MAX_GEOM];
+  double  geom_pos[GM_MAX_GEOM][3];
+  double  geom_quat[GM_MAX_GEOM][4];
+  double  geom_size[GM_MAX_GEOM][3];
+  double  geom_friction[GM_MAX_GEOM];
+  double  geom_rbound[GM_MAX_GEOM];
+  /* candidate pairs (object pairs first; unordered: canonical order per env) */
+  int32_t pair_a[GM_MAX_PAIR];
+  int32_t pair_b[GM_MAX_PAIR];
+  /* motor locks (reference weld constraints on 1-DoF motors) */
+  int32_t lock_dof[GM_MAX_LOCK];
+  int32_t lock_kind[GM_MAX_LOCK];     /* 0 prismatic, 2 palm               */
+  /* keyframe "initial pose" (myfunctions.cpp:171) */
+  double  qpos0[GM_MAX_QPOS];
+  /* named indices */
+  int32_t dof_base, dof_palm, dof_obj;
+  int32_t dof_pris[3], dof_rev[3], dof_seg[3];   /* first segment dof per finger */
+  int32_t body_base, body_finger[3], body_palm, body_obj, geom_obj, geom_ground;
+  /* physics options */
+  double  timestep;
+  double  gravity[3];
+  double  solref[2];                  /* timeconst, dampratio              */
+  double  solimp[5];                  /* dmin, dmax, width, midpoint, power */
+  int32_t pgs_iterations;
+  double  mpr_tolerance;
+  int32_t mpr_iterations;
+  /* gripper dimensions used by the env logic (JointSettings::Dim) */
+  double  finger_length, finger_width, finger_thickness, finger_E, finger_EI;
+  double  segment_length, hook_length, hook_angle_degrees, fingertip_clearance;
+  double  yield_stress;
+  int32_t fixed_first_segment;
+  /* PD gains (JointSettings::ctrl, myfunctions.cpp:273-296) */
+  double  kp_gripper[3], kd_gripper[3], kp_base[3], kd_base[3];
+  double  time_per_step;              /* stepper chunk: num_steps / pulses_per_s */
+  int32_t stepper_num_steps;
+  /* gauge (JointSettings::gauge, myfunctions.cpp:264-270) */
+  double  gauge_xpos;
+  int32_t gauge_order;
+} gm_model;
+
+/* one graspable object (a synthetic object-set entry) */
+typedef struct gm_object {
+  int32_t type;                       /* GM_GEOM_BOX / _CYLINDER / _SPHERE  */
+  double  size[3];                    /* MuJoCo geom size semantics (half sizes) */
+  double  mass;
+  double  friction;
+} gm_object;
+
+/* per-env spawn request: MjClass::spawn_object(index, x, y, zrot) (mjclass.cpp:2352-2420) */
+typedef struct gm_spawn {
+  int32_t object_index;
+  double  x, y, zrot;
+} gm_spawn;
+
+/* ------------------------------------------------------------ C ABI */
+typedef struct gm_ctx gm_ctx;
+
+/* library / build information */
+const char* gm_version(void);
+int  gm_device_count(void);
+/* sizes of the interface structs (0 settings, 1 model, 2 config, 3 object, 4 spawn,
+ * 5 model params) so bindings can verify their layouts */
+int64_t gm_struct_size(int which);
+/* model summary: nq, nv, nbody, ngeom, npair, n_seg, dof_base, dof_palm, dof_obj,
+ * dof_pris[3], dof_rev[3], dof_seg[3]  (18 int32) */
+void gm_model_info(const gm_model* m, int32_t* out);
+/* derived config summary: n_obs, n_actions, sim_steps_per_action, sensor_fcn, state_fcn */
+void gm_config_info(const gm_config* c, int32_t* out);
+
+/* Model builder: the MJCF the reference loads with mj_loadXML
+ * (mjclass.cpp:377-409) is unavailable (empty `description` submodule), so the
+ * gripper is compiled from its numeric parameters instead. */
+void gm_default_model_params(gm_model_params* p);
+int  gm_build_model(const gm_model_params* p, gm_model* out);
+
+/* Settings defaults (simsettings.h) and derived configuration
+ * (MjClass::configure_settings, mjclass.cpp:97-314). */
+void gm_default_settings(gm_settings* s);
+int  gm_configure(const gm_settings* s, const gm_model* m, gm_config* out);
+
+/* Synthetic object sets (the reference's set6/set9 MJCF sets are unavailable). */
+int  gm_make_object_set(const char* name, uint64_t seed, gm_object* out, int max_objects);
+
+/* Context lifetime: MjClass() + load() + init() (bind.cpp:46-52, mjclass.cpp:8-95) */
+int  gm_create(const gm_model* model, const gm_config* cfg, const gm_object* objects,
+               int n_objects, int n_envs, int env_offset, int device, uint64_t seed,
+               gm_ctx** out);
+void gm_destroy(gm_ctx* ctx);
+const char* gm_last_error(const gm_ctx* ctx);
+int  gm_n_envs(const gm_ctx* ctx);
+int  gm_n_obs(const gm_ctx* ctx);        /* MjClass::get_n_obs     (bind.cpp:157) */
+int  gm_n_actions(const gm_ctx* ctx);    /* MjClass::get_n_actions (bind.cpp:156) */
+int  gm_update_config(gm_ctx* ctx, const gm_config* cfg);  /* mj.set.* writes */
+
+/* MjClass::reset() (mjclass.cpp:434-486) for envs with mask[e] != 0 (NULL = all),
+ * followed by spawn_object(spawn[e]) (mjclass.cpp:2352-2420).  Host arrays. */
+int  gm_reset(gm_ctx* ctx, const uint8_t* mask, const gm_spawn* spawn);
+
+/* MjClass::set_continous_action for every action index i in order
+ * (mjclass.cpp:1517-1630; called per index by MjEnv._set_action, MjEnv.py:591-594).
+ * actions: [n_envs x n_actions] float32. */
+int  gm_set_action(gm_ctx* ctx, const float* actions, int on_device);
+/* MjClass::set_discrete_action (mjclass.cpp:1510-1515). actions: [n_envs] int32. */
+int  gm_set_discrete_action(gm_ctx* ctx, const int32_t* actions, int on_device);
+
+/* MjClass::action_step() (mjclass.cpp:1483-1508) + get_observation (1700-1959)
+ * + is_done (1632-1698) + reward (3000-3049), fused in one device launch,
+ * evaluated in the order MjEnv.step uses them (obs, done, reward). */
+int  gm_step(gm_ctx* ctx);
+
+int  gm_get_obs(gm_ctx* ctx, float* out, int on_device);                 /* [n_envs x n_obs] */
+int  gm_get_reward_done(gm_ctx* ctx, float* reward, uint8_t* done, int on_device);
+/* EventTrack rows: [n_envs x (GM_N_BINARY + GM_N_LINEAR)] int32 `row`, and
+ * `abs` counters; MjClass::get_event_state / EventTrack (bind.cpp:525-590). */
+int  gm_get_event_rows(gm_ctx* ctx, int32_t* rows, int32_t* abs_counts, float* last_values);
+/* raw state readback (testing / checkpoint): qpos [n_envs x nq], qvel [n_envs x nv] */
+int  gm_get_state(gm_ctx* ctx, float* qpos, float* qvel, double* time);
+int  gm_set_state(gm_ctx* ctx, const float* qpos, const float* qvel);
+/* target (stepper) state: [n_envs x 8] = end x,y,z,th (m/rad) then step x,y,z and base z */
+int  gm_get_target(gm_ctx* ctx, double* end_xyzth, int32_t* end_steps, int32_t* next_steps,
+                   double* base_xyz);
+/* number of envs whose contact list overflowed GM_MAX_CON in the last gm_step */
+int  gm_get_overflow(gm_ctx* ctx, int32_t* counts);
+
+/* device pointers for zero-copy (torch.from_blob-style) access */
+void* gm_device_obs(gm_ctx* ctx);
+void* gm_device_reward(gm_ctx* ctx);
+void* gm_device_done(gm_ctx* ctx);
+void* gm_device_actions(gm_ctx* ctx);
+void* gm_stream(gm_ctx* ctx);            /* hipStream_t the context launches on */
+
+/* Timing of the fused env-step kernel (HIP events on the context's stream). */
+int  gm_last_step_ms(gm_ctx* ctx, float* ms);
+
+/* ---- single-substep stage hooks for parity testing (GPU vs oracle) ---- */
+/* Runs exactly one physics substep (mj_step1 + control + mj_step2 equivalent)
+ * on every env, from the current state, and copies out diagnostics:
+ * ncon[n_envs], contact [n_envs x GM_MAX_CON x 16] (dist, pos3, frame9, g1, g2, mu),
+ * efc_force [n_envs x GM_MAX_EFC], qacc [n_envs x nv]. */
+int  gm_debug_substep(gm_ctx* ctx, int32_t* ncon, float* contact, float* efc_force,
+                      float* qacc);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GRIPPER_MI355X_H_ */

@@ -1,0 +1,2020 @@
+/* oracle.c -- fp64 CPU restatement of the reference MjClass env-step hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).  Serial, one env per or_env, written
+ * for readability against the reference sources it restates.  The physics is a
+ * restatement of MuJoCo 2.1.5's published pipeline (mj_step1 / mj_step2, an
+ * un-vendored dependency pinned by reference buildsettings.mk:32) with the
+ * deliberate, documented deviations listed in DESIGN.md ("Engine spec"):
+ * implicit joint spring+damper in the Euler step, PGS on a pyramidal cone with
+ * a fixed sweep count, MPR single-contact for box-box and box-cylinder.
+ */
+#define _POSIX_C_SOURCE 200809L
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <float.h>
+#include <time.h>
+#include <stdio.h>
+
+#define NB GM_MAX_BODY
+#define NV GM_MAX_DOF
+#define NQ GM_MAX_QPOS
+#define NG GM_MAX_GEOM
+#define NC GM_MAX_CON
+#define NE GM_MAX_EFC
+#define PI_D 3.14159265358979323846
+
+/* =====================================================================
+ * RNG: std::default_random_engine == minstd_rand0 in libstdc++
+ * (mjclass.cpp:4, 219-224); generate_canonical as libstdc++ implements it.
+ * ===================================================================== */
+static uint32_t lcg_next(uint32_t* s) {
+  uint64_t x = (uint64_t)(*s) * 16807ull % 2147483647ull;
+  *s = (uint32_t)x;
+  return *s;
+}
+static uint32_t lcg_seed(uint64_t seed) {
+  uint32_t s = (uint32_t)(seed % 2147483647ull);
+  return s == 0 ? 1u : s;
+}
+/* generate_canonical<float, 24>: one draw, computed in float */
+static float canon_f(uint32_t* s) {
+  const float r = 2147483646.0f;   /* max - min + 1, rounded to float */
+  float sum = (float)(lcg_next(s) - 1u) * 1.0f;
+  float ret = sum / r;
+  if (ret >= 1.0f) ret = nextafterf(1.0f, 0.0f);
+  return ret;
+}
+/* generate_canonical<double, 53>: two draws */
+static double canon_d(uint32_t* s) {
+  const double r = 2147483646.0;
+  double sum = 0.0, tmp = 1.0;
+  for (int k = 0; k < 2; k++) { sum += (double)(lcg_next(s) - 1u) * tmp; tmp *= r; }
+  double ret = sum / tmp;
+  if (ret >= 1.0) ret = nextafter(1.0, 0.0);
+  return ret;
+}
+double or_minstd_next_canonical_float(uint32_t* s) { return canon_f(s); }
+double or_minstd_next_canonical_double(uint32_t* s) { return canon_d(s); }
+/* uniform_real_distribution<float>(0,1) used by MjClass::uniform_dist (mjclass.h:1567) */
+static float unif01(uint32_t* s) { return canon_f(s) * (1.0f - 0.0f) + 0.0f; }
+
+/* =====================================================================
+ * luke::Gripper (gripper.h / gripper.cpp), restated in fp64
+ * ===================================================================== */
+typedef struct { double x, y, z, th; int32_t sx, sy, sz; } grip_t;
+static const double G_leadscrew = 35e-3, G_finger_length = 235e-3, G_hook_length = 35.0e-3;
+static const double G_xy_min = 49e-3, G_xy_max = 134e-3, G_z_min = 0e-3, G_z_max = 165e-3;
+static const double G_limit_tol = 1e-4;
+#define G_TO_RAD (PI_D / 180.0)
+#define G_TO_DEG (180.0 / PI_D)
+static double g_xy_step_m(void) { return 4.0 / (1.0 * 400 * 1e3); }
+static double g_z_step_m(void) { return 4.8768 / (1 * 400 * 1e3); }
+static double g_xy_home(void) { return G_xy_max - 1.0 * (4 * 1e-3 / 1.0); }
+static double g_z_home(void) { return G_z_min + 1.0 * (4.8768 * 1e-3 / 1); }
+static double g_hyp(void) { return sqrt(pow(G_finger_length, 2) + pow(G_hook_length, 2)); }
+static double g_rest(void) { return atan(G_hook_length / G_finger_length); }
+static double g_th_min(void) { return -40 * G_TO_RAD; }
+static double g_th_max(void) { return 40 * G_TO_RAD; }
+static const double G_fingertip_radius_min = -1;
+
+static double g_calc_y(const grip_t* g, double th) { return g->x + 1 * G_leadscrew * sin(th); }
+static double g_calc_th(double x, double y) { return asin((y - x) / G_leadscrew) * 1; }
+static int32_t g_x_step(const grip_t* g) { return (int32_t)round((G_xy_max - g->x) / g_xy_step_m()); }
+static int32_t g_y_step(const grip_t* g) { return (int32_t)round((G_xy_max - g->y) / g_xy_step_m()); }
+static int32_t g_z_step(const grip_t* g) { return (int32_t)round(g->z / g_z_step_m()); }
+static double g_th_rad(const grip_t* g) { return g_calc_th(g->x, g->y); }
+static double g_th_deg(const grip_t* g) { return G_TO_DEG * g_th_rad(g); }
+
+/* Gripper::update_xy, gripper.cpp:6-90 */
+static int g_update_xy(grip_t* g) {
+  int wl = 1;
+  if (g->x > G_xy_max + G_limit_tol) { g->x = G_xy_max; wl = 0; }
+  if (g->x < G_xy_min - G_limit_tol) { g->x = G_xy_min; wl = 0; }
+  if (g->y > G_xy_max + G_limit_tol) { g->y = G_xy_max; wl = 0; }
+  if (g->y < G_xy_min - G_limit_tol) { g->y = G_xy_min; wl = 0; }
+  double new_th = g_calc_th(g->x, g->y);
+  if (new_th > g_th_max()) { new_th = g_th_max(); g->y = g_calc_y(g, g_th_max()); wl = 0; }
+  if (new_th < g_th_min()) { new_th = g_th_min(); g->y = g_calc_y(g, g_th_min()); wl = 0; }
+  g->th = new_th;
+  double th_lim = (asin((G_fingertip_radius_min - g->x) / g_hyp()) + g_rest()) * 1;
+  if (g->th < th_lim) { g->y = g_calc_y(g, th_lim); g->th = th_lim; wl = 0; }
+  g->sx = g_x_step(g);
+  g->sy = g_y_step(g);
+  return wl;
+}
+/* Gripper::update_z, gripper.cpp:92-118 */
+static int g_update_z(grip_t* g) {
+  int wl = 1;
+  if (g->z > G_z_max + G_limit_tol) { g->z = G_z_max; wl = 0; }
+  if (g->z < G_z_min - G_limit_tol) { g->z = G_z_min; wl = 0; }
+  g->sz = g_z_step(g);
+  return wl;
+}
+static int g_update(grip_t* g) { int a = g_update_xy(g); int b = g_update_z(g); return a * b; }
+static void g_reset(grip_t* g) { g->x = g_xy_home(); g->y = g_xy_home(); g->z = g_z_home(); g_update(g); }
+/* set_th_rad / set_xyz_m_rad / set_xyz_m / set_xyz_step (gripper.h:113-166) */
+static int g_set_th_rad(grip_t* g, double th) { g->y = g_calc_y(g, th); return g_update_xy(g); }
+static int g_set_xyz_m_rad(grip_t* g, double x, double th, double z) {
+  g->x = x; int in_lim = g_set_th_rad(g, th); g->z = z;
+  return g_update_z(g) ? in_lim : 0;
+}
+static int g_set_xyz_m(grip_t* g, double x, double y, double z) {
+  g->x = x; g->y = y; g->z = z; return g_update(g);
+}
+static int g_set_xyz_step(grip_t* g, int xs, int ys, int zs) {
+  g->x = G_xy_max - g_xy_step_m() * xs; g->y = G_xy_max - g_xy_step_m() * ys;
+  int in_lim = g_update_xy(g);
+  g->z = g_z_step_m() * zs;
+  return g_update_z(g) ? in_lim : 0;
+}
+/* Gripper::step_to, gripper.cpp:158-213 */
+static int g_step_to(grip_t* g, const grip_t* t, int num) {
+  int fin = 1;
+  int xg = t->sx - g->sx, yg = t->sy - g->sy, zg = t->sz - g->sz;
+  if (xg < 0) { if (-xg > num) { xg = -num; fin = 0; } } else if (xg > num) { xg = num; fin = 0; }
+  if (yg < 0) { if (-yg > num) { yg = -num; fin = 0; } } else if (yg > num) { yg = num; fin = 0; }
+  if (zg < 0) { if (-zg > num) { zg = -num; fin = 0; } } else if (zg > num) { zg = num; fin = 0; }
+  g_set_xyz_step(g, g->sx + xg, g->sy + yg, g->sz + zg);
+  return fin;
+}
+
+/* golden driver, op codes documented in tests/golden/make_gripper_golden.sh */
+int or_grip_step_sequence(const double* cmds, int n, double* out) {
+  grip_t end, next;
+  g_reset(&end); g_reset(&next);
+  for (int i = 0; i < n; i++) {
+    int op = (int)cmds[4 * i];
+    double a = cmds[4 * i + 1], b = cmds[4 * i + 2], c = cmds[4 * i + 3];
+    int ret = 0;
+    if (op == 0) ret = g_set_xyz_m_rad(&end, end.x + a, end.th + b, end.z + c);
+    else if (op == 1) ret = g_set_xyz_m(&end, end.x + a, end.y + b, end.z + c);
+    else if (op == 2) ret = g_step_to(&next, &end, (int)a);
+    else if (op == 3) { g_reset(&end); g_reset(&next); ret = 1; }
+    double* o = out + 15 * i;
+    o[0] = ret;
+    o[1] = end.x; o[2] = end.y; o[3] = end.z; o[4] = end.th; o[5] = end.sx; o[6] = end.sy; o[7] = end.sz;
+    o[8] = next.x; o[9] = next.y; o[10] = next.z; o[11] = next.th; o[12] = next.sx; o[13] = next.sy; o[14] = next.sz;
+  }
+  return n;
+}
+
+/* =====================================================================
+ * small vector helpers
+ * ===================================================================== */
+static double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void cross3(double* r, const double* a, const double* b) {
+  double t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+static double norm3(const double* a) { return sqrt(dot3(a, a)); }
+static void sub3(double* r, const double* a, const double* b) { r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2]; }
+static void add3(double* r, const double* a, const double* b) { r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2]; }
+static void scl3(double* r, const double* a, double s) { r[0] = a[0] * s; r[1] = a[1] * s; r[2] = a[2] * s; }
+static void copy3(double* r, const double* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
+static void mulmv3(double* r, const double* M, const double* v) {   /* r = M v, M row-major */
+  double t0 = M[0] * v[0] + M[1] * v[1] + M[2] * v[2];
+  double t1 = M[3] * v[0] + M[4] * v[1] + M[5] * v[2];
+  double t2 = M[6] * v[0] + M[7] * v[1] + M[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+static void mulmtv3(double* r, const double* M, const double* v) {  /* r = M^T v */
+  double t0 = M[0] * v[0] + M[3] * v[1] + M[6] * v[2];
+  double t1 = M[1] * v[0] + M[4] * v[1] + M[7] * v[2];
+  double t2 = M[2] * v[0] + M[5] * v[1] + M[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+static void mulmm3(double* r, const double* A, const double* B) {
+  double t[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) t[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+  memcpy(r, t, sizeof(t));
+}
+static void quat2mat(double* R, const double* q) {
+  double w = q[0], x = q[1], y = q[2], z = q[3];
+  R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z);     R[2] = 2 * (x * z + w * y);
+  R[3] = 2 * (x * y + w * z);     R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
+  R[6] = 2 * (x * z - w * y);     R[7] = 2 * (y * z + w * x);     R[8] = 1 - 2 * (x * x + y * y);
+}
+static void quatmul(double* r, const double* a, const double* b) {
+  double t[4];
+  t[0] = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  t[1] = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  t[2] = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  t[3] = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  memcpy(r, t, sizeof(t));
+}
+static void quatnorm(double* q) {
+  double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < 1e-15) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  for (int i = 0; i < 4; i++) q[i] /= n;
+}
+/* mju_makeFrame-style tangent basis from a unit normal (engine spec) */
+static void make_frame(double* F, const double* n) {
+  double a[3] = {0, 0, 0};
+  if (fabs(n[0]) < 0.5) a[0] = 1; else a[1] = 1;
+  double d = dot3(a, n);
+  double t1[3] = {a[0] - d * n[0], a[1] - d * n[1], a[2] - d * n[2]};
+  double l = norm3(t1);
+  scl3(t1, t1, 1.0 / l);
+  double t2[3];
+  cross3(t2, n, t1);
+  copy3(F, n); copy3(F + 3, t1); copy3(F + 6, t2);
+}
+
+/* =====================================================================
+ * env state
+ * ===================================================================== */
+typedef struct { float v[GM_RING]; int i; } ring_t;
+static void ring_reset(ring_t* r) { for (int k = 0; k < GM_RING; k++) r->v[k] = 0; r->i = -1; }
+/* SlidingWindow::add / read_element (slidingwindow.h:36-55) on a ring of GM_RING */
+static void ring_add(ring_t* r, float x) { r->i += 1; if (r->i > GM_RING - 1) r->i = 0; r->v[r->i] = x; }
+static float ring_read(const ring_t* r, int n) {
+  int idx = r->i - n;
+  while (idx < 0) idx += GM_RING;
+  return r->v[idx];
+}
+static float ring_latest(const ring_t* r) { return r->i == -1 ? r->v[0] : r->v[r->i]; }
+
+typedef struct { int value; int last_value; int active_sum; int row; int abs; } bev_t;
+typedef struct { float value; float last_value; int active_sum; int row; int abs; } lev_t;
+
+typedef struct {
+  double dist, pos[3], frame[9], mu;
+  double force[3];            /* contact-frame force (normal, t1, t2) after the solve */
+  int g1, g2;
+} con_t;
+
+/* sensor slots in settings order (SS macro order) */
+enum { S_MOTOR = 0, S_BASEZ, S_BASEXY, S_YAW, S_BEND, S_AXIAL, S_PALM, S_WRISTXY, S_WRISTZ, S_CART, S_N };
+
+struct or_env {
+  gm_model m;
+  gm_config c;
+  gm_object objs[GM_MAX_OBJSET];
+  int nobj;
+  int64_t env_id;
+  /* physics state */
+  double qpos[NQ], qvel[NV], time;
+  /* kinematics / dynamics scratch (mjData) */
+  double xpos[NB][3], xmat[NB][9], xquat[NB][4], xipos[NB][3];
+  double cinert[NB][10], cdof[NV][6], cdof_dot[NV][6], cvel[NB][6];
+  double xaxis[NB][3], xanchor[NB][3];
+  double gxpos[NG][3], gxmat[NG][9];
+  double M[NV][NV], L[NV][NV], D[NV];
+  double qfrc_bias[NV], qfrc_passive[NV], qfrc_act[NV], qacc_smooth[NV], qacc[NV];
+  int ncon, overflow;
+  con_t con[NC];
+  int nefc;
+  double J[NE][NV], efc_f[NE], efc_R[NE], efc_b[NE];
+  int efc_type[NE];  /* 0 equality, 1 pyramid edge */
+  double qpos_pre[NQ];
+  /* target (myfunctions.cpp:470, customtypes.h:574-694) */
+  grip_t end, next;
+  double base[6];
+  double last_step_time;
+  int lock_active[GM_MAX_LOCK];
+  double lock_q[GM_MAX_LOCK];
+  int old_x, old_y, old_z;         /* function-static in update_constraints (2221-2223) */
+  double eq_q[NQ];                 /* calibrate_reset equilibrium (gripper + base) */
+  /* sensors */
+  double last_read[S_N];
+  float rand_mu[S_N][3];
+  ring_t w_gauge[3], w_axial[3], w_palm, w_wx, w_wy, w_wz, w_motor[3], w_base[3], w_yaw, w_cart[12];
+  ring_t si_gauge[3], si_palm, si_wz, si_axial[3];
+  uint32_t rng;
+  /* env tracking (MjType::Env, mjclass.h:782-913) */
+  bev_t bev[GM_N_BINARY];
+  lev_t lev[GM_N_LINEAR];
+  float cumulative_reward;
+  int num_action_steps;
+  int termination_signal_sent;
+  int term_pending_steps;
+  float grp_peak_lateral;
+  int obj_index;
+  double start_qpos[7];
+};
+
+size_t or_sizeof(void) { return sizeof(or_env); }
+
+/* =====================================================================
+ * model helpers: per-env object slot (objects are culled to one live slot)
+ * ===================================================================== */
+static double object_rest_z(const gm_object* o) {
+  if (o->type == GM_GEOM_BOX) return o->size[2];
+  if (o->type == GM_GEOM_CYLINDER) return o->size[1];
+  return o->size[0];
+}
+static void apply_object(gm_model* m, const gm_object* o) {
+  int g = m->geom_obj, b = m->body_obj;
+  m->geom_type[g] = o->type;
+  for (int i = 0; i < 3; i++) m->geom_size[g][i] = o->size[i];
+  m->geom_friction[g] = o->friction;
+  double mass = o->mass, I0, I1, I2;
+  if (o->type == GM_GEOM_BOX) {
+    double a = 2 * o->size[0], bb = 2 * o->size[1], c = 2 * o->size[2];
+    I0 = mass * (bb * bb + c * c) / 12; I1 = mass * (a * a + c * c) / 12; I2 = mass * (a * a + bb * bb) / 12;
+    m->geom_rbound[g] = sqrt(o->size[0] * o->size[0] + o->size[1] * o->size[1] + o->size[2] * o->size[2]);
+  } else if (o->type == GM_GEOM_CYLINDER) {
+    double r = o->size[0], h = 2 * o->size[1];
+    I0 = I1 = mass * (3 * r * r + h * h) / 12; I2 = mass * r * r / 2;
+    m->geom_rbound[g] = sqrt(o->size[0] * o->size[0] + o->size[1] * o->size[1]);
+  } else {
+    double r = o->size[0];
+    I0 = I1 = I2 = 2 * mass * r * r / 5;
+    m->geom_rbound[g] = r;
+  }
+  m->body_mass[b] = mass;
+  m->body_inertia[b][0] = I0; m->body_inertia[b][1] = I1; m->body_inertia[b][2] = I2;
+}
+
+/* =====================================================================
+ * kinematics (mj_kinematics + mj_comPos restatement)
+ * ===================================================================== */
+static void fk(or_env* e) {
+  const gm_model* m = &e->m;
+  for (int i = 0; i < 3; i++) e->xpos[0][i] = 0;
+  e->xquat[0][0] = 1; e->xquat[0][1] = e->xquat[0][2] = e->xquat[0][3] = 0;
+  quat2mat(e->xmat[0], e->xquat[0]);
+  for (int b = 1; b < m->nbody; b++) {
+    int p = m->body_parent[b];
+    double tmp[3];
+    mulmv3(tmp, e->xmat[p], m->body_pos[b]);
+    add3(e->xpos[b], e->xpos[p], tmp);
+    quatmul(e->xquat[b], e->xquat[p], m->body_quat[b]);
+    int j = m->body_jnt[b];
+    if (j >= 0) {
+      double R[9];
+      quat2mat(R, e->xquat[b]);
+      mulmv3(e->xaxis[b], R, m->jnt_axis[j]);
+      double an[3];
+      mulmv3(an, R, m->jnt_pos[j]);
+      add3(e->xanchor[b], e->xpos[b], an);
+      int qa = m->jnt_qposadr[j];
+      if (m->jnt_type[j] == GM_JNT_SLIDE) {
+        double d[3];
+        scl3(d, e->xaxis[b], e->qpos[qa]);
+        add3(e->xpos[b], e->xpos[b], d);
+        add3(e->xanchor[b], e->xanchor[b], d);
+      } else if (m->jnt_type[j] == GM_JNT_HINGE) {
+        double ang = e->qpos[qa], s = sin(0.5 * ang), c = cos(0.5 * ang);
+        const double* ax = m->jnt_axis[j];
+        double ql[4] = {c, ax[0] * s, ax[1] * s, ax[2] * s};
+        quatmul(e->xquat[b], e->xquat[b], ql);
+        /* anchor at body origin in this model: xpos unchanged */
+      } else if (m->jnt_type[j] == GM_JNT_FREE) {
+        copy3(e->xpos[b], &e->qpos[qa]);
+        for (int k = 0; k < 4; k++) e->xquat[b][k] = e->qpos[qa + 3 + k];
+        copy3(e->xanchor[b], e->xpos[b]);
+      }
+    }
+    quatnorm(e->xquat[b]);
+    quat2mat(e->xmat[b], e->xquat[b]);
+    double c[3];
+    mulmv3(c, e->xmat[b], m->body_ipos[b]);
+    add3(e->xipos[b], e->xpos[b], c);
+  }
+  for (int g = 0; g < m->ngeom; g++) {
+    int b = m->geom_body[g];
+    double t[3], Rg[9];
+    mulmv3(t, e->xmat[b], m->geom_pos[g]);
+    add3(e->gxpos[g], e->xpos[b], t);
+    quat2mat(Rg, m->geom_quat[g]);
+    mulmm3(e->gxmat[g], e->xmat[b], Rg);
+  }
+  /* spatial inertia about the world origin: I_O(6: xx,yy,zz,xy,xz,yz), h = m c, m */
+  for (int b = 0; b < m->nbody; b++) {
+    double* ci = e->cinert[b];
+    for (int k = 0; k < 10; k++) ci[k] = 0;
+    if (b == 0) continue;
+    const double* R = e->xmat[b];
+    const double* I = m->body_inertia[b];
+    double mass = m->body_mass[b];
+    const double* c = e->xipos[b];
+    double Iw[9];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++)
+        Iw[3 * i + j] = R[3 * i] * I[0] * R[3 * j] + R[3 * i + 1] * I[1] * R[3 * j + 1] + R[3 * i + 2] * I[2] * R[3 * j + 2];
+    double cc = dot3(c, c);
+    ci[0] = Iw[0] + mass * (cc - c[0] * c[0]);
+    ci[1] = Iw[4] + mass * (cc - c[1] * c[1]);
+    ci[2] = Iw[8] + mass * (cc - c[2] * c[2]);
+    ci[3] = Iw[1] - mass * c[0] * c[1];
+    ci[4] = Iw[2] - mass * c[0] * c[2];
+    ci[5] = Iw[5] - mass * c[1] * c[2];
+    ci[6] = mass * c[0]; ci[7] = mass * c[1]; ci[8] = mass * c[2];
+    ci[9] = mass;
+  }
+  /* motion subspaces cdof = [angular; linear velocity of the world origin] */
+  for (int d = 0; d < m->nv; d++) {
+    int b = m->dof_body[d];
+    int j = m->body_jnt[b];
+    double* cd = e->cdof[d];
+    if (m->jnt_type[j] == GM_JNT_SLIDE) {
+      cd[0] = cd[1] = cd[2] = 0;
+      copy3(cd + 3, e->xaxis[b]);
+    } else if (m->jnt_type[j] == GM_JNT_HINGE) {
+      copy3(cd, e->xaxis[b]);
+      cross3(cd + 3, e->xanchor[b], e->xaxis[b]);
+    } else {
+      int k = d - m->jnt_dofadr[j];
+      if (k < 3) {
+        cd[0] = cd[1] = cd[2] = 0;
+        cd[3] = cd[4] = cd[5] = 0; cd[3 + k] = 1;
+      } else {
+        double w[3] = {e->xmat[b][k - 3], e->xmat[b][3 + k - 3], e->xmat[b][6 + k - 3]};
+        copy3(cd, w);
+        cross3(cd + 3, e->xpos[b], w);
+      }
+    }
+  }
+}
+
+/* spatial algebra (Plucker [angular; linear] about the world origin) */
+static void inert_mul(double* r, const double* ci, const double* v) {
+  const double* w = v; const double* u = v + 3;
+  double Iw[3] = {ci[0] * w[0] + ci[3] * w[1] + ci[4] * w[2],
+                  ci[3] * w[0] + ci[1] * w[1] + ci[5] * w[2],
+                  ci[4] * w[0] + ci[5] * w[1] + ci[2] * w[2]};
+  double hxu[3], hxw[3];
+  cross3(hxu, ci + 6, u);
+  cross3(hxw, ci + 6, w);
+  r[0] = Iw[0] + hxu[0]; r[1] = Iw[1] + hxu[1]; r[2] = Iw[2] + hxu[2];
+  r[3] = ci[9] * u[0] - hxw[0]; r[4] = ci[9] * u[1] - hxw[1]; r[5] = ci[9] * u[2] - hxw[2];
+}
+static void cross_motion(double* r, const double* v, const double* mv) {
+  double a[3], b[3], c[3];
+  cross3(a, v, mv);
+  cross3(b, v, mv + 3);
+  cross3(c, v + 3, mv);
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
+  r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
+}
+static void cross_force(double* r, const double* v, const double* f) {
+  double a[3], b[3], c[3];
+  cross3(a, v, f);
+  cross3(b, v + 3, f + 3);
+  cross3(c, v, f + 3);
+  r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
+  r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
+}
+static double dot6(const double* a, const double* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+
+/* composite rigid body mass matrix (mj_crb) */
+static void crb(or_env* e) {
+  const gm_model* m = &e->m;
+  double Ic[NB][10];
+  memcpy(Ic, e->cinert, sizeof(Ic));
+  for (int b = m->nbody - 1; b > 0; b--) {
+    int p = m->body_parent[b];
+    if (p > 0) for (int k = 0; k < 10; k++) Ic[p][k] += Ic[b][k];
+  }
+  for (int i = 0; i < m->nv; i++) for (int j = 0; j < m->nv; j++) e->M[i][j] = 0;
+  for (int j = 0; j < m->nv; j++) {
+    double F[6];
+    inert_mul(F, Ic[m->dof_body[j]], e->cdof[j]);
+    for (int i = j; i >= 0; i = m->dof_parent[i]) {
+      double v = dot6(e->cdof[i], F);
+      e->M[j][i] = v; e->M[i][j] = v;
+    }
+  }
+}
+
+/* RNE bias with zero acceleration (mj_comVel + mj_rne(flg_acc=0)) */
+static void rne_bias(or_env* e) {
+  const gm_model* m = &e->m;
+  double cacc[NB][6], cfrc[NB][6];
+  for (int k = 0; k < 6; k++) { e->cvel[0][k] = 0; cacc[0][k] = 0; }
+  cacc[0][3] = -m->gravity[0]; cacc[0][4] = -m->gravity[1]; cacc[0][5] = -m->gravity[2];
+  for (int b = 1; b < m->nbody; b++) {
+    int p = m->body_parent[b];
+    double v[6];
+    memcpy(v, e->cvel[p], sizeof(v));
+    memcpy(cacc[b], cacc[p], sizeof(cacc[b]));
+    int j = m->body_jnt[b];
+    if (j >= 0) {
+      int d0 = m->jnt_dofadr[j];
+      if (m->jnt_type[j] == GM_JNT_FREE) {
+        for (int k = 0; k < 3; k++) for (int t = 0; t < 6; t++) e->cdof_dot[d0 + k][t] = 0;
+        for (int k = 0; k < 3; k++) for (int t = 0; t < 6; t++) v[t] += e->cdof[d0 + k][t] * e->qvel[d0 + k];
+        for (int k = 3; k < 6; k++) cross_motion(e->cdof_dot[d0 + k], v, e->cdof[d0 + k]);
+        for (int k = 3; k < 6; k++) for (int t = 0; t < 6; t++) v[t] += e->cdof[d0 + k][t] * e->qvel[d0 + k];
+        for (int k = 0; k < 6; k++) for (int t = 0; t < 6; t++) cacc[b][t] += e->cdof_dot[d0 + k][t] * e->qvel[d0 + k];
+      } else {
+        cross_motion(e->cdof_dot[d0], v, e->cdof[d0]);
+        for (int t = 0; t < 6; t++) v[t] += e->cdof[d0][t] * e->qvel[d0];
+        for (int t = 0; t < 6; t++) cacc[b][t] += e->cdof_dot[d0][t] * e->qvel[d0];
+      }
+    }
+    memcpy(e->cvel[b], v, sizeof(v));
+    double t1[6], t2[6];
+    inert_mul(cfrc[b], e->cinert[b], cacc[b]);
+    inert_mul(t1, e->cinert[b], v);
+    cross_force(t2, v, t1);
+    for (int t = 0; t < 6; t++) cfrc[b][t] += t2[t];
+  }
+  for (int b = m->nbody - 1; b > 0; b--) {
+    int p = m->body_parent[b];
+    if (p > 0) for (int t = 0; t < 6; t++) cfrc[p][t] += cfrc[b][t];
+  }
+  for (int d = 0; d < m->nv; d++) e->qfrc_bias[d] = dot6(e->cdof[d], cfrc[m->dof_body[d]]);
+}
+
+/* sparse LTDL of the tree mass matrix (mj_factorM): H = L^T D L, in place on L */
+static void factor(or_env* e, double H[NV][NV]) {
+  const gm_model* m = &e->m;
+  int nv = m->nv;
+  for (int k = nv - 1; k >= 0; k--) {
+    for (int i = m->dof_parent[k]; i >= 0; i = m->dof_parent[i]) {
+      double a = H[k][i] / H[k][k];
+      for (int j = i; j >= 0; j = m->dof_parent[j]) H[i][j] -= H[k][j] * a;
+      H[k][i] = a;
+    }
+  }
+  for (int k = 0; k < nv; k++) {
+    e->D[k] = H[k][k];
+    for (int i = 0; i < nv; i++) e->L[k][i] = 0;
+    e->L[k][k] = 1;
+    for (int i = m->dof_parent[k]; i >= 0; i = m->dof_parent[i]) e->L[k][i] = H[k][i];
+  }
+}
+/* solve H x = b with H = L^T D L (mj_solveLD) */
+static void solve(const or_env* e, double* x, const double* b) {
+  const gm_model* m = &e->m;
+  int nv = m->nv;
+  for (int i = 0; i < nv; i++) x[i] = b[i];
+  for (int k = nv - 1; k >= 0; k--)            /* L^T y = b : leaves to root */
+    for (int i = m->dof_parent[k]; i >= 0; i = m->dof_parent[i]) x[i] -= e->L[k][i] * x[k];
+  for (int k = 0; k < nv; k++) x[k] /= e->D[k];
+  for (int k = 0; k < nv; k++)                 /* L x = y : root to leaves */
+    for (int i = m->dof_parent[k]; i >= 0; i = m->dof_parent[i]) x[k] -= e->L[k][i] * x[i];
+}
+
+/* =====================================================================
+ * collision (mj_collision restatement; engine spec)
+ * ===================================================================== */
+static int add_contact(or_env* e, int g1, int g2, double dist, const double* pos, const double* n) {
+  if (e->ncon >= NC) { e->overflow = 1; return 0; }
+  con_t* c = &e->con[e->ncon++];
+  c->dist = dist;
+  copy3(c->pos, pos);
+  make_frame(c->frame, n);
+  c->g1 = g1; c->g2 = g2;
+  double f1 = e->m.geom_friction[g1], f2 = e->m.geom_friction[g2];
+  c->mu = f1 > f2 ? f1 : f2;
+  return 1;
+}
+
+static void plane_sphere(or_env* e, int gp, int gs) {
+  const double* n = &e->gxmat[gp][0];
+  double nz[3] = {e->gxmat[gp][2], e->gxmat[gp][5], e->gxmat[gp][8]};
+  (void)n;
+  double r = e->m.geom_size[gs][0];
+  double dv[3];
+  sub3(dv, e->gxpos[gs], e->gxpos[gp]);
+  double dist = dot3(dv, nz) - r;
+  if (dist < 0) {
+    double pos[3];
+    for (int i = 0; i < 3; i++) pos[i] = e->gxpos[gs][i] - nz[i] * (r + 0.5 * dist);
+    add_contact(e, gp, gs, dist, pos, nz);
+  }
+}
+static void plane_box(or_env* e, int gp, int gb) {
+  double nz[3] = {e->gxmat[gp][2], e->gxmat[gp][5], e->gxmat[gp][8]};
+  const double* h = e->m.geom_size[gb];
+  int cnt = 0;
+  for (int i = 0; i < 8 && cnt < 4; i++) {
+    double s[3] = {(i & 1) ? h[0] : -h[0], (i & 2) ? h[1] : -h[1], (i & 4) ? h[2] : -h[2]};
+    double v[3], dv[3];
+    mulmv3(v, e->gxmat[gb], s);
+    add3(v, v, e->gxpos[gb]);
+    sub3(dv, v, e->gxpos[gp]);
+    double d = dot3(dv, nz);
+    if (d < 0) {
+      double pos[3];
+      for (int k = 0; k < 3; k++) pos[k] = v[k] - 0.5 * d * nz[k];
+      add_contact(e, gp, gb, d, pos, nz);
+      cnt++;
+    }
+  }
+}
+static void plane_cylinder(or_env* e, int gp, int gc) {
+  double nz[3] = {e->gxmat[gp][2], e->gxmat[gp][5], e->gxmat[gp][8]};
+  const double* R = e->gxmat[gc];
+  double a[3] = {R[2], R[5], R[8]};
+  double r = e->m.geom_size[gc][0], hh = e->m.geom_size[gc][1];
+  double na = dot3(nz, a);
+  double w[3] = {-nz[0] + na * a[0], -nz[1] + na * a[1], -nz[2] + na * a[2]};
+  double lw = norm3(w);
+  if (lw < 1e-6) { w[0] = R[0]; w[1] = R[3]; w[2] = R[6]; }
+  else scl3(w, w, 1.0 / lw);
+  double axw[3];
+  cross3(axw, a, w);
+  int cnt = 0;
+  for (int s = 0; s < 2 && cnt < 4; s++) {
+    double sg = s == 0 ? 1.0 : -1.0;
+    double cc[3] = {e->gxpos[gc][0] + sg * hh * a[0], e->gxpos[gc][1] + sg * hh * a[1],
+                    e->gxpos[gc][2] + sg * hh * a[2]};
+    for (int k = 0; k < 4 && cnt < 4; k++) {
+      double dir[3];
+      if (k == 0) copy3(dir, w);
+      else if (k == 1) copy3(dir, axw);
+      else if (k == 2) scl3(dir, w, -1.0);
+      else scl3(dir, axw, -1.0);
+      double v[3] = {cc[0] + r * dir[0], cc[1] + r * dir[1], cc[2] + r * dir[2]};
+      double dv[3];
+      sub3(dv, v, e->gxpos[gp]);
+      double d = dot3(dv, nz);
+      if (d < 0) {
+        double pos[3];
+        for (int t = 0; t < 3; t++) pos[t] = v[t] - 0.5 * d * nz[t];
+        add_contact(e, gp, gc, d, pos, nz);
+        cnt++;
+      }
+    }
+  }
+}
+static void sphere_box(or_env* e, int gs, int gb) {
+  const double* R = e->gxmat[gb];
+  const double* h = e->m.geom_size[gb];
+  double r = e->m.geom_size[gs][0];
+  double dv[3], cl[3];
+  sub3(dv, e->gxpos[gs], e->gxpos[gb]);
+  mulmtv3(cl, R, dv);
+  double q[3];
+  int inside = 1;
+  for (int k = 0; k < 3; k++) {
+    q[k] = cl[k];
+    if (q[k] > h[k]) { q[k] = h[k]; inside = 0; }
+    if (q[k] < -h[k]) { q[k] = -h[k]; inside = 0; }
+  }
+  double nl[3], dist, ql[3];
+  if (!inside) {
+    double df[3];
+    sub3(df, cl, q);
+    double l = norm3(df);
+    if (l < 1e-12) return;
+    dist = l - r;
+    if (dist >= 0) return;
+    scl3(nl, df, -1.0 / l);
+    copy3(ql, q);
+  } else {
+    int kmin = 0;
+    double best = h[0] - fabs(cl[0]);
+    for (int k = 1; k < 3; k++) { double v = h[k] - fabs(cl[k]); if (v < best) { best = v; kmin = k; } }
+    double sg = cl[kmin] >= 0 ? 1.0 : -1.0;
+    nl[0] = nl[1] = nl[2] = 0; nl[kmin] = -sg;
+    dist = -(best + r);
+    copy3(ql, cl); ql[kmin] = sg * h[kmin];
+  }
+  double n[3], qw[3], sp[3], pos[3];
+  mulmv3(n, R, nl);
+  mulmv3(qw, R, ql);
+  add3(qw, qw, e->gxpos[gb]);
+  for (int k = 0; k < 3; k++) sp[k] = e->gxpos[gs][k] + n[k] * r;
+  for (int k = 0; k < 3; k++) pos[k] = 0.5 * (qw[k] + sp[k]);
+  add_contact(e, gs, gb, dist, pos, n);
+}
+
+/* ---- MPR (Minkowski portal refinement, libccd algorithm as used by MuJoCo's
+ *      mjc_Convex for pairs without a dedicated collider) ---- */
+typedef struct { double v[3], p1[3], p2[3]; } sv_t;
+static void support_geom(const or_env* e, int g, const double* d, double* out) {
+  const double* R = e->gxmat[g];
+  const double* c = e->gxpos[g];
+  const double* s = e->m.geom_size[g];
+  double dl[3];
+  mulmtv3(dl, R, d);
+  double pl[3] = {0, 0, 0};
+  int t = e->m.geom_type[g];
+  if (t == GM_GEOM_BOX) {
+    for (int k = 0; k < 3; k++) pl[k] = dl[k] >= 0 ? s[k] : -s[k];
+  } else if (t == GM_GEOM_CYLINDER) {
+    double rr = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
+    if (rr > 1e-12) { pl[0] = s[0] * dl[0] / rr; pl[1] = s[0] * dl[1] / rr; }
+    pl[2] = dl[2] >= 0 ? s[1] : -s[1];
+  } else if (t == GM_GEOM_SPHERE) {
+    double l = norm3(dl);
+    if (l > 1e-12) scl3(pl, dl, s[0] / l);
+  }
+  mulmv3(out, R, pl);
+  add3(out, out, c);
+}
+static void mpr_support(const or_env* e, int g1, int g2, const double* d, sv_t* sv) {
+  double nd[3] = {-d[0], -d[1], -d[2]};
+  support_geom(e, g1, d, sv->p1);
+  support_geom(e, g2, nd, sv->p2);
+  sub3(sv->v, sv->p1, sv->p2);
+}
+static int is_zero(double x) { return fabs(x) < 1e-12; }
+static void portal_dir(const sv_t* P, double* dir) {
+  double a[3], b[3];
+  sub3(a, P[2].v, P[1].v);
+  sub3(b, P[3].v, P[1].v);
+  cross3(dir, a, b);
+  double l = norm3(dir);
+  if (l > 0) scl3(dir, dir, 1.0 / l);
+}
+static void expand_portal(sv_t* P, const sv_t* v4) {
+  double v4v0[3];
+  cross3(v4v0, v4->v, P[0].v);
+  double d = dot3(P[1].v, v4v0);
+  if (d > 0) {
+    d = dot3(P[2].v, v4v0);
+    if (d > 0) P[1] = *v4; else P[3] = *v4;
+  } else {
+    d = dot3(P[3].v, v4v0);
+    if (d > 0) P[2] = *v4; else P[1] = *v4;
+  }
+}
+static int reach_tol(const sv_t* P, const sv_t* v4, const double* dir, double tol) {
+  double dv1 = dot3(P[1].v, dir), dv2 = dot3(P[2].v, dir), dv3 = dot3(P[3].v, dir), dv4 = dot3(v4->v, dir);
+  double d1 = dv4 - dv1, d2 = dv4 - dv2, d3 = dv4 - dv3;
+  double dd = d1 < d2 ? d1 : d2;
+  dd = dd < d3 ? dd : d3;
+  return dd < tol || fabs(dd - tol) < 1e-12;
+}
+/* closest point on triangle (a,b,c) to the origin */
+static void tri_closest_origin(const double* a, const double* b, const double* c, double* out) {
+  double ab[3], ac[3], ap[3];
+  sub3(ab, b, a); sub3(ac, c, a); scl3(ap, a, -1.0);
+  double d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+  if (d1 <= 0 && d2 <= 0) { copy3(out, a); return; }
+  double bp[3]; scl3(bp, b, -1.0);
+  double d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  if (d3 >= 0 && d4 <= d3) { copy3(out, b); return; }
+  double vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) { double v = d1 / (d1 - d3); for (int k = 0; k < 3; k++) out[k] = a[k] + v * ab[k]; return; }
+  double cp[3]; scl3(cp, c, -1.0);
+  double d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+  if (d6 >= 0 && d5 <= d6) { copy3(out, c); return; }
+  double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) { double w = d2 / (d2 - d6); for (int k = 0; k < 3; k++) out[k] = a[k] + w * ac[k]; return; }
+  double va = d3 * d6 - d5 * d4;
+  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+    double w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    for (int k = 0; k < 3; k++) out[k] = b[k] + w * (c[k] - b[k]);
+    return;
+  }
+  double den = 1.0 / (va + vb + vc);
+  double v = vb * den, w = vc * den;
+  for (int k = 0; k < 3; k++) out[k] = a[k] + ab[k] * v + ac[k] * w;
+}
+static void mpr_pos(const sv_t* P, double* pos) {
+  double dir[3];
+  portal_dir(P, dir);
+  double t[3];
+  cross3(t, P[1].v, P[2].v); double b0 = dot3(t, P[3].v);
+  cross3(t, P[3].v, P[2].v); double b1 = dot3(t, P[0].v);
+  cross3(t, P[0].v, P[1].v); double b2 = dot3(t, P[3].v);
+  cross3(t, P[2].v, P[1].v); double b3 = dot3(t, P[0].v);
+  double sum = b0 + b1 + b2 + b3;
+  if (sum <= 0) {
+    b0 = 0;
+    cross3(t, P[2].v, P[3].v); b1 = dot3(t, dir);
+    cross3(t, P[3].v, P[1].v); b2 = dot3(t, dir);
+    cross3(t, P[1].v, P[2].v); b3 = dot3(t, dir);
+    sum = b1 + b2 + b3;
+  }
+  double inv = 1.0 / sum;
+  double p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
+  double bb[4] = {b0, b1, b2, b3};
+  for (int i = 0; i < 4; i++)
+    for (int k = 0; k < 3; k++) { p1[k] += bb[i] * P[i].p1[k]; p2[k] += bb[i] * P[i].p2[k]; }
+  for (int k = 0; k < 3; k++) pos[k] = 0.5 * (p1[k] + p2[k]) * inv;
+}
+/* returns 1 and fills depth/dir/pos on penetration; 0 otherwise */
+static int mpr_penetration(const or_env* e, int g1, int g2, double* depth, double* dir, double* pos) {
+  const double tol = e->m.mpr_tolerance;
+  const int maxit = e->m.mpr_iterations;
+  sv_t P[4];
+  /* discover portal */
+  sub3(P[0].v, e->gxpos[g1], e->gxpos[g2]);
+  copy3(P[0].p1, e->gxpos[g1]);
+  copy3(P[0].p2, e->gxpos[g2]);
+  if (is_zero(P[0].v[0]) && is_zero(P[0].v[1]) && is_zero(P[0].v[2])) P[0].v[0] += 1e-5;
+  double d[3];
+  scl3(d, P[0].v, -1.0);
+  double l = norm3(d); scl3(d, d, 1.0 / l);
+  mpr_support(e, g1, g2, d, &P[1]);
+  if (dot3(P[1].v, d) <= 0) return 0;
+  cross3(d, P[0].v, P[1].v);
+  if (is_zero(norm3(d))) {
+    if (is_zero(norm3(P[1].v))) return 0;   /* touching: depth 0 */
+    /* origin on segment v0-v1 */
+    *depth = norm3(P[1].v);
+    scl3(dir, P[1].v, 1.0 / *depth);
+    for (int k = 0; k < 3; k++) pos[k] = 0.5 * (P[1].p1[k] + P[1].p2[k]);
+    return *depth > 0;
+  }
+  l = norm3(d); scl3(d, d, 1.0 / l);
+  mpr_support(e, g1, g2, d, &P[2]);
+  if (dot3(P[2].v, d) <= 0) return 0;
+  double va[3], vb[3];
+  sub3(va, P[1].v, P[0].v); sub3(vb, P[2].v, P[0].v);
+  cross3(d, va, vb);
+  l = norm3(d); scl3(d, d, 1.0 / l);
+  if (dot3(d, P[0].v) > 0) { sv_t t = P[1]; P[1] = P[2]; P[2] = t; scl3(d, d, -1.0); }
+  int it = 0;
+  for (;;) {
+    mpr_support(e, g1, g2, d, &P[3]);
+    if (dot3(P[3].v, d) <= 0) return 0;
+    int cont = 0;
+    cross3(va, P[1].v, P[3].v);
+    if (dot3(va, P[0].v) < -1e-12) { P[2] = P[3]; cont = 1; }
+    if (!cont) {
+      cross3(va, P[3].v, P[2].v);
+      if (dot3(va, P[0].v) < -1e-12) { P[1] = P[3]; cont = 1; }
+    }
+    if (!cont) break;
+    sub3(va, P[1].v, P[0].v); sub3(vb, P[2].v, P[0].v);
+    cross3(d, va, vb);
+    l = norm3(d); scl3(d, d, 1.0 / l);
+    if (++it > maxit) return 0;
+  }
+  /* refine portal */
+  it = 0;
+  for (;;) {
+    portal_dir(P, d);
+    if (dot3(d, P[1].v) >= -1e-12) break;   /* portal encapsulates the origin */
+    sv_t v4;
+    mpr_support(e, g1, g2, d, &v4);
+    double dv4 = dot3(v4.v, d);
+    if (!(is_zero(dv4) || dv4 > 0)) return 0;
+    if (reach_tol(P, &v4, d, tol)) return 0;
+    expand_portal(P, &v4);
+    if (++it > maxit) return 0;
+  }
+  /* find penetration */
+  it = 0;
+  for (;;) {
+    portal_dir(P, d);
+    sv_t v4;
+    mpr_support(e, g1, g2, d, &v4);
+    if (reach_tol(P, &v4, d, tol) || it > maxit) {
+      double cp[3];
+      tri_closest_origin(P[1].v, P[2].v, P[3].v, cp);
+      *depth = norm3(cp);
+      if (is_zero(*depth)) return 0;
+      scl3(dir, cp, 1.0 / *depth);
+      mpr_pos(P, pos);
+      return 1;
+    }
+    expand_portal(P, &v4);
+    it++;
+  }
+}
+static void convex_pair(or_env* e, int g1, int g2) {
+  double depth, dir[3], pos[3];
+  if (mpr_penetration(e, g1, g2, &depth, dir, pos) && depth > 0) add_contact(e, g1, g2, -depth, pos, dir);
+}
+
+static void collision(or_env* e) {
+  const gm_model* m = &e->m;
+  e->ncon = 0;
+  e->overflow = 0;
+  for (int p = 0; p < m->npair; p++) {
+    int a = m->pair_a[p], b = m->pair_b[p];
+    int ta = m->geom_type[a], tb = m->geom_type[b];
+    int g1 = a, g2 = b;
+    if (ta > tb || (ta == tb && a > b)) { g1 = b; g2 = a; }
+    int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+    /* bounding-sphere broadphase */
+    if (t1 == GM_GEOM_PLANE) {
+      double nz[3] = {e->gxmat[g1][2], e->gxmat[g1][5], e->gxmat[g1][8]}, dv[3];
+      sub3(dv, e->gxpos[g2], e->gxpos[g1]);
+      if (dot3(dv, nz) > m->geom_rbound[g2]) continue;
+    } else {
+      double dv[3];
+      sub3(dv, e->gxpos[g2], e->gxpos[g1]);
+      double rr = m->geom_rbound[g1] + m->geom_rbound[g2];
+      if (dot3(dv, dv) > rr * rr) continue;
+    }
+    if (t1 == GM_GEOM_PLANE) {
+      if (t2 == GM_GEOM_SPHERE) plane_sphere(e, g1, g2);
+      else if (t2 == GM_GEOM_BOX) plane_box(e, g1, g2);
+      else if (t2 == GM_GEOM_CYLINDER) plane_cylinder(e, g1, g2);
+    } else if (t1 == GM_GEOM_SPHERE && t2 == GM_GEOM_BOX) {
+      sphere_box(e, g1, g2);
+    } else {
+      convex_pair(e, g1, g2);
+    }
+  }
+}
+
+/* translational Jacobian column of dof d at world point p */
+static void jac_point_col(const or_env* e, int d, const double* p, double* out) {
+  const double* cd = e->cdof[d];
+  double wxp[3];
+  cross3(wxp, cd, p);
+  out[0] = cd[3] + wxp[0]; out[1] = cd[4] + wxp[1]; out[2] = cd[5] + wxp[2];
+}
+static int is_ancestor_body(const gm_model* m, int anc, int b) {
+  for (; b > 0; b = m->body_parent[b]) if (b == anc) return 1;
+  return anc == 0;
+}
+
+/* =====================================================================
+ * constraint assembly + PGS (mj_makeConstraint / mj_makeImpedance / PGS)
+ * ===================================================================== */
+static double impedance(const gm_model* m, double r) {
+  double dmin = m->solimp[0], dmax = m->solimp[1], width = m->solimp[2], mid = m->solimp[3], pw = m->solimp[4];
+  if (dmin == dmax || width <= 1e-15) return dmin;
+  double x = fabs(r) / width;
+  if (x >= 1) return dmax;
+  if (x <= 0) return dmin;
+  double y;
+  if (pw == 1) y = x;
+  else if (x <= mid) y = pow(x, pw) / pow(mid, pw - 1);
+  else y = 1 - pow(1 - x, pw) / pow(1 - mid, pw - 1);
+  return dmin + y * (dmax - dmin);
+}
+
+static void constraint_solve(or_env* e) {
+  const gm_model* m = &e->m;
+  int nv = m->nv;
+  int n = 0;
+  double pos[NE], vel[NE];
+  /* motor locks (equality rows first) */
+  for (int k = 0; k < m->nlock; k++) {
+    if (!e->lock_active[k]) continue;
+    int d = m->lock_dof[k];
+    for (int i = 0; i < nv; i++) e->J[n][i] = 0;
+    e->J[n][d] = 1;
+    pos[n] = e->qpos[d] - e->lock_q[k];
+    e->efc_type[n] = 0;
+    n++;
+  }
+  /* contacts: 4 pyramid edges each */
+  for (int c = 0; c < e->ncon; c++) {
+    const con_t* C = &e->con[c];
+    double Jc[3][NV];
+    for (int r = 0; r < 3; r++) for (int i = 0; i < nv; i++) Jc[r][i] = 0;
+    int b1 = m->geom_body[C->g1], b2 = m->geom_body[C->g2];
+    for (int d = 0; d < nv; d++) {
+      int bd = m->dof_body[d];
+      double s = 0;
+      if (b2 > 0 && is_ancestor_body(m, bd, b2)) s += 1;
+      if (b1 > 0 && is_ancestor_body(m, bd, b1)) s -= 1;
+      if (s == 0) continue;
+      double col[3];
+      jac_point_col(e, d, C->pos, col);
+      for (int r = 0; r < 3; r++) Jc[r][d] = s * dot3(C->frame + 3 * r, col);
+    }
+    for (int k = 0; k < 2; k++) {
+      for (int sg = 0; sg < 2; sg++) {
+        double sgn = sg == 0 ? 1.0 : -1.0;
+        for (int i = 0; i < nv; i++) e->J[n][i] = Jc[0][i] + sgn * C->mu * Jc[1 + k][i];
+        pos[n] = C->dist;
+        e->efc_type[n] = 1;
+        n++;
+      }
+    }
+  }
+  e->nefc = n;
+  if (n == 0) return;
+  /* A = J H^-1 J^T */
+  static double W[NE][NV];
+  double A[NE][NE];
+  for (int r = 0; r < n; r++) solve(e, W[r], e->J[r]);
+  for (int r = 0; r < n; r++)
+    for (int s = 0; s < n; s++) {
+      double v = 0;
+      for (int i = 0; i < nv; i++) v += e->J[r][i] * W[s][i];
+      A[r][s] = v;
+    }
+  double h = m->timestep;
+  double tc = m->solref[0] < 2 * h ? 2 * h : m->solref[0];
+  double dr = m->solref[1], dmax = m->solimp[1];
+  double K = 1.0 / (dmax * dmax * tc * tc * dr * dr);
+  double Bd = 2.0 / (dmax * tc);
+  for (int r = 0; r < n; r++) {
+    double jv = 0, ja = 0;
+    for (int i = 0; i < nv; i++) { jv += e->J[r][i] * e->qvel[i]; ja += e->J[r][i] * e->qacc_smooth[i]; }
+    vel[r] = jv;
+    double imp = impedance(m, pos[r]);
+    double aref = -Bd * jv - K * imp * pos[r];
+    double R = (1 - imp) / imp * A[r][r];
+    if (R < 1e-15) R = 1e-15;
+    e->efc_R[r] = R;
+    e->efc_b[r] = ja - aref;
+    e->efc_f[r] = 0;
+  }
+  /* projected Gauss-Seidel, fixed sweep count */
+  for (int it = 0; it < m->pgs_iterations; it++) {
+    for (int r = 0; r < n; r++) {
+      double g = e->efc_b[r] + e->efc_R[r] * e->efc_f[r];
+      for (int s = 0; s < n; s++) g += A[r][s] * e->efc_f[s];
+      double f = e->efc_f[r] - g / (A[r][r] + e->efc_R[r]);
+      if (e->efc_type[r] == 1 && f < 0) f = 0;
+      e->efc_f[r] = f;
+    }
+  }
+  (void)vel;
+  /* mj_contactForce for pyramidal cones: normal = sum of edges, t_k = mu (f+ - f-) */
+  int r0 = n - 4 * e->ncon;
+  for (int c = 0; c < e->ncon; c++) {
+    const double* fe = &e->efc_f[r0 + 4 * c];
+    e->con[c].force[0] = fe[0] + fe[1] + fe[2] + fe[3];
+    e->con[c].force[1] = e->con[c].mu * (fe[0] - fe[1]);
+    e->con[c].force[2] = e->con[c].mu * (fe[2] - fe[3]);
+  }
+}
+
+/* =====================================================================
+ * one physics substep: before_step + step + after_step (physics part)
+ * myfunctions.cpp:1864-1908
+ * ===================================================================== */
+static void control(or_env* e, double* act) {
+  /* luke::control -> control_gripper(target_.next) + control_base (1912-2057) */
+  const gm_model* m = &e->m;
+  for (int d = 0; d < m->nv; d++) act[d] = 0;
+  for (int f = 0; f < 3; f++) {
+    int d = m->dof_pris[f];
+    double u = (e->qpos[d] - e->next.x) * m->kp_gripper[0] + e->qvel[d] * m->kd_gripper[0];
+    act[d] = -u;
+    d = m->dof_rev[f];
+    u = (e->qpos[d] - e->next.th) * m->kp_gripper[1] + e->qvel[d] * m->kd_gripper[1];
+    act[d] = -u;
+  }
+  int d = m->dof_palm;
+  double u = (e->qpos[d] - e->next.z) * m->kp_gripper[2] + e->qvel[d] * m->kd_gripper[2];
+  act[d] = -u;
+  d = m->dof_base;
+  u = (e->qpos[d] - e->base[2]) * m->kp_base[2] + e->qvel[d] * m->kd_base[2];
+  act[d] = -u;
+}
+
+/* PD gains acting on dof d (control_gripper / control_base) */
+static void ctrl_gains(const gm_model* m, int d, double* kp, double* kd) {
+  *kp = 0; *kd = 0;
+  for (int f = 0; f < 3; f++) {
+    if (d == m->dof_pris[f]) { *kp = m->kp_gripper[0]; *kd = m->kd_gripper[0]; }
+    if (d == m->dof_rev[f]) { *kp = m->kp_gripper[1]; *kd = m->kd_gripper[1]; }
+  }
+  if (d == m->dof_palm) { *kp = m->kp_gripper[2]; *kd = m->kd_gripper[2]; }
+  if (d == m->dof_base) { *kp = m->kp_base[2]; *kd = m->kd_base[2]; }
+}
+
+static void physics_substep(or_env* e) {
+  const gm_model* m = &e->m;
+  int nv = m->nv;
+  double h = m->timestep;
+  memcpy(e->qpos_pre, e->qpos, sizeof(e->qpos));
+  /* mj_step1 */
+  fk(e);
+  crb(e);
+  collision(e);
+  rne_bias(e);
+  for (int d = 0; d < nv; d++) {
+    int j = m->body_jnt[m->dof_body[d]];
+    e->qfrc_passive[d] = 0;
+    if (m->jnt_type[j] != GM_JNT_FREE) e->qfrc_passive[d] -= m->jnt_stiffness[j] * e->qpos[d];
+    e->qfrc_passive[d] -= m->jnt_damping[j] * e->qvel[d];
+  }
+  /* control between step1 and step2 */
+  control(e, e->qfrc_act);
+  /* mj_step2: implicit spring/damper mass matrix, smooth accel, constraints */
+  double H[NV][NV];
+  memcpy(H, e->M, sizeof(H));
+  for (int d = 0; d < nv; d++) {
+    /* implicit joint spring/damper and implicit PD motor gains (engine spec) */
+    int j = m->body_jnt[m->dof_body[d]];
+    double kp, kd;
+    ctrl_gains(m, d, &kp, &kd);
+    double add = m->jnt_armature[j] + h * (m->jnt_damping[j] + kd);
+    if (m->jnt_type[j] != GM_JNT_FREE) add += h * h * (m->jnt_stiffness[j] + kp);
+    H[d][d] += add;
+  }
+  factor(e, H);
+  double f[NV];
+  for (int d = 0; d < nv; d++) f[d] = e->qfrc_passive[d] + e->qfrc_act[d] - e->qfrc_bias[d];
+  solve(e, e->qacc_smooth, f);
+  constraint_solve(e);
+  double jtf[NV];
+  for (int d = 0; d < nv; d++) jtf[d] = 0;
+  for (int r = 0; r < e->nefc; r++)
+    for (int d = 0; d < nv; d++) jtf[d] += e->J[r][d] * e->efc_f[r];
+  double dq[NV];
+  solve(e, dq, jtf);
+  for (int d = 0; d < nv; d++) e->qacc[d] = e->qacc_smooth[d] + dq[d];
+  if (getenv("ORACLE_DEBUG")) {
+    static int once = 0;
+    if (once++ < 1) {
+      for (int d = 0; d < nv; d++) printf("d=%d M=%.4g D=%.4g bias=%.4g pas=%.4g act=%.4g qacc_s=%.4g qacc=%.4g\n", d, e->M[d][d], e->D[d], e->qfrc_bias[d], e->qfrc_passive[d], e->qfrc_act[d], e->qacc_smooth[d], e->qacc[d]);
+      printf("ncon=%d nefc=%d\n", e->ncon, e->nefc);
+    }
+  }
+  /* semi-implicit Euler */
+  for (int d = 0; d < nv; d++) e->qvel[d] += h * e->qacc[d];
+  for (int b = 1; b < m->nbody; b++) {
+    int j = m->body_jnt[b];
+    if (j < 0) continue;
+    int qa = m->jnt_qposadr[j], da = m->jnt_dofadr[j];
+    if (m->jnt_type[j] == GM_JNT_FREE) {
+      for (int k = 0; k < 3; k++) e->qpos[qa + k] += h * e->qvel[da + k];
+      double* q = &e->qpos[qa + 3];
+      const double* w = &e->qvel[da + 3];
+      double wn = norm3(w);
+      if (wn > 1e-15) {
+        double ang = wn * h;
+        double s = sin(0.5 * ang) / wn, c = cos(0.5 * ang);
+        double dq4[4] = {c, w[0] * s, w[1] * s, w[2] * s};
+        quatmul(q, q, dq4);
+      }
+      quatnorm(q);
+    } else {
+      e->qpos[qa] += h * e->qvel[da];
+    }
+  }
+  e->time += h;
+  if (getenv("ORACLE_DEBUG")) {
+    static int reported = 0;
+    int bad = 0;
+    for (int d = 0; d < nv; d++) if (!isfinite(e->qvel[d])) bad = 1;
+    static int cnt = 0;
+    if (cnt++ < 12) {
+      double vm = 0; int dm = 0;
+      for (int d = 0; d < nv; d++) if (fabs(e->qvel[d]) > vm) { vm = fabs(e->qvel[d]); dm = d; }
+      printf("sub %d t=%.4f ncon=%d nefc=%d vmax=%g at d%d q=%g\n", cnt, e->time, e->ncon, e->nefc, vm, dm, e->qpos[dm]);
+      for (int c = 0; c < e->ncon; c++) printf("   con g1=%d g2=%d dist=%g f=(%g %g %g)\n", e->con[c].g1, e->con[c].g2, e->con[c].dist, e->con[c].force[0], e->con[c].force[1], e->con[c].force[2]);
+    }
+    if (bad && !reported) {
+      reported = 1;
+      printf("NaN at time %.5f ncon=%d nefc=%d\n", e->time, e->ncon, e->nefc);
+      for (int c = 0; c < e->ncon; c++) printf(" con %d g1=%d g2=%d dist=%g n=(%g %g %g) f=(%g %g %g)\n", c, e->con[c].g1, e->con[c].g2, e->con[c].dist, e->con[c].frame[0], e->con[c].frame[1], e->con[c].frame[2], e->con[c].force[0], e->con[c].force[1], e->con[c].force[2]);
+      for (int r = 0; r < e->nefc; r++) printf(" efc %d f=%g R=%g b=%g\n", r, e->efc_f[r], e->efc_R[r], e->efc_b[r]);
+      for (int d = 0; d < nv; d++) printf(" d%d qacc_s=%g qacc=%g D=%g\n", d, e->qacc_smooth[d], e->qacc[d], e->D[d]);
+    }
+  }
+}
+
+/* =====================================================================
+ * after_step: update_all -> update_stepper / update_constraints, antiroll
+ * myfunctions.cpp:2110-2284, objecthandler.cpp:1034-1059
+ * ===================================================================== */
+static int prismatic_moving(const or_env* e) { return g_x_step(&e->end) != g_x_step(&e->next); }
+static int revolute_moving(const or_env* e) { return !(fabs(g_th_deg(&e->end) - g_th_deg(&e->next)) < 5e-1); }
+static int z_moving(const or_env* e) { return g_z_step(&e->end) != g_z_step(&e->next); }
+
+static void set_lock(or_env* e, int kind, int active) {
+  for (int k = 0; k < e->m.nlock; k++) {
+    if (e->m.lock_kind[k] != kind) continue;
+    e->lock_active[k] = active;
+    /* set_constraint reads xpos/xmat of mj_step1 (pre-integration) */
+    if (active) e->lock_q[k] = e->qpos_pre[e->m.lock_dof[k]];
+  }
+}
+static void update_constraints(or_env* e) {
+  int nx = prismatic_moving(e), ny = revolute_moving(e), nz = z_moving(e);
+  if (nx != e->old_x) { set_lock(e, 0, !nx); e->old_x = nx; }
+  if (ny != e->old_y) { /* revolute locks disabled (myfunctions.cpp:479, 2261) */ e->old_y = ny; }
+  if (nz != e->old_z) { set_lock(e, 2, !nz); e->old_z = nz; }
+}
+static void update_all(or_env* e) {
+  if (e->time > e->last_step_time + e->m.time_per_step) {
+    update_constraints(e);
+    e->last_step_time = e->time;
+    g_step_to(&e->next, &e->end, e->m.stepper_num_steps);
+  }
+  /* apply_antiroll on the live object */
+  const double* v = &e->qvel[e->m.dof_obj];
+  double mag = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+  if (mag < 1e-6) for (int k = 0; k < 6; k++) e->qvel[e->m.dof_obj + k] = 0;
+}
+
+/* =====================================================================
+ * sensors
+ * ===================================================================== */
+/* read_armadillo_gauge (myfunctions.cpp:2699-2795): cubic least squares through the
+ * N+1 joint points, evaluated at gauge.xpos, in mm.  Least squares by Householder
+ * QR on the Vandermonde matrix, as arma::polyfit -> LAPACK does. */
+float or_gauge_reading(const gm_model* m, const double* q) {
+  int N = m->n_seg, P = N + 1;
+  double X[GM_MAX_SEG + 1], Y[GM_MAX_SEG + 1];
+  X[0] = m->fixed_first_segment ? m->segment_length : 0;
+  Y[0] = 0;
+  double cum = 0;
+  for (int i = 0; i < N; i++) {
+    cum = (i == 0) ? q[0] : cum + q[i];
+    X[i + 1] = X[i] + m->segment_length * cos(cum);
+    Y[i + 1] = Y[i] + m->segment_length * sin(cum);
+  }
+  int order = m->gauge_order, nc = order + 1;
+  double A[GM_MAX_SEG + 1][4], b[GM_MAX_SEG + 1];
+  for (int i = 0; i < P; i++) {
+    for (int k = 0; k < nc; k++) A[i][k] = pow(X[i], order - k);
+    b[i] = Y[i];
+  }
+  for (int k = 0; k < nc; k++) {
+    double nrm = 0;
+    for (int i = k; i < P; i++) nrm += A[i][k] * A[i][k];
+    nrm = sqrt(nrm);
+    double alpha = A[k][k] > 0 ? -nrm : nrm;
+    double v[GM_MAX_SEG + 1];
+    for (int i = 0; i < P; i++) v[i] = 0;
+    for (int i = k; i < P; i++) v[i] = A[i][k];
+    v[k] -= alpha;
+    double vv = 0;
+    for (int i = k; i < P; i++) vv += v[i] * v[i];
+    if (vv < 1e-300) continue;
+    for (int j = k; j < nc; j++) {
+      double s = 0;
+      for (int i = k; i < P; i++) s += v[i] * A[i][j];
+      s = 2 * s / vv;
+      for (int i = k; i < P; i++) A[i][j] -= s * v[i];
+    }
+    double s = 0;
+    for (int i = k; i < P; i++) s += v[i] * b[i];
+    s = 2 * s / vv;
+    for (int i = k; i < P; i++) b[i] -= s * v[i];
+  }
+  double coeff[4];
+  for (int k = nc - 1; k >= 0; k--) {
+    double s = b[k];
+    for (int j = k + 1; j < nc; j++) s -= A[k][j] * coeff[j];
+    coeff[k] = s / A[k][k];
+  }
+  float y = 0.0f;
+  for (int i = 0; i <= order; i++) y += (float)(coeff[i] * pow(m->gauge_xpos, order - i));
+  return y * 1000;
+}
+
+/* Sensor::apply_normalisation (mjclass.h:155-174) */
+static float s_normalise(const gm_sensor* s, float v) {
+  if (!s->use_normalisation) return v;
+  if (s->normalise <= 0) return v < 0 ? -1.0f : 1.0f;
+  else if (v > s->normalise) return 1.0f;
+  if (v < -s->normalise) return -1.0f;
+  return v / s->normalise;
+}
+/* Sensor::apply_noise (mjclass.h:176-223) */
+static float s_noise(or_env* e, const gm_sensor* s, int slot, float value, int i) {
+  if (!s->use_noise) return value;
+  const float two_pi = (float)(2.0 * PI_D);
+  const float eps = FLT_EPSILON;
+  float mu = e->rand_mu[slot][i - 1];
+  if (s->noise_std < eps) {
+    float noise = mu + s->noise_mag * (2 * unif01(&e->rng) - 1);
+    value += noise;
+  } else {
+    float u1, u2;
+    do { u1 = unif01(&e->rng); } while (u1 <= eps);
+    u2 = unif01(&e->rng);
+    float mag = (float)(s->noise_std * sqrt(-2.0 * (double)logf(u1)));
+    float z0 = mag * cosf(two_pi * u2) + mu;
+    value += z0;
+  }
+  if (value > 1) value = 1;
+  else if (value < -1) value = -1;
+  return value;
+}
+/* Sensor::ready_to_read (mjclass.h:225-241) */
+static int s_ready(or_env* e, const gm_sensor* s, int slot) {
+  double tbr = (double)(1 / s->read_rate);
+  if (e->time > e->last_read[slot] + tbr) { e->last_read[slot] = e->time; return 1; }
+  return 0;
+}
+
+/* ObjectHandler::extract_forces_faster (objecthandler.cpp:737-992) over the contacts
+ * and forces of the last substep; body frames from that substep's mj_step1 kinematics */
+typedef struct {
+  double obj_glob[6][6];     /* sum, f1, f2, f3, palm, gnd (global, [f; t]) */
+  double obj_loc[4][3];      /* f1, f2, f3, palm (local) */
+  double all_glob[4][6];
+  double all_loc[4][3];
+  double gnd_glob[3][6];
+  double gnd_loc[3][3];
+} forces_t;
+static void extract_forces(const or_env* e, forces_t* F) {
+  const gm_model* m = &e->m;
+  memset(F, 0, sizeof(*F));
+  for (int i = 0; i < e->ncon; i++) {
+    const con_t* C = &e->con[i];
+    int c1 = m->geom_class[C->g1], c2 = m->geom_class[C->g2];
+    int w_obj = (c1 == GM_CLS_OBJECT || c2 == GM_CLS_OBJECT);
+    int w_f[3];
+    for (int f = 0; f < 3; f++) w_f[f] = (c1 == GM_CLS_FINGER1 + f || c2 == GM_CLS_FINGER1 + f);
+    int w_palm = (c1 == GM_CLS_PALM || c2 == GM_CLS_PALM);
+    int w_gnd = (c1 == GM_CLS_GROUND || c2 == GM_CLS_GROUND);
+    if (!(w_obj || w_f[0] || w_f[1] || w_f[2] || w_palm || w_gnd)) continue;
+    /* global = frame^T * local; torques are zero for condim 3 */
+    double g[6] = {0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < 3; k++)
+      for (int r = 0; r < 3; r++) g[k] += C->frame[3 * r + k] * C->force[r];
+    if (w_obj) {
+      for (int k = 0; k < 6; k++) F->obj_glob[0][k] += g[k];
+      for (int f = 0; f < 3; f++) if (w_f[f]) for (int k = 0; k < 6; k++) F->obj_glob[1 + f][k] += g[k];
+      if (w_palm) for (int k = 0; k < 6; k++) F->obj_glob[4][k] += g[k];
+      if (w_gnd) for (int k = 0; k < 6; k++) F->obj_glob[5][k] += g[k];
+    }
+    for (int f = 0; f < 3; f++) {
+      if (w_f[f]) {
+        for (int k = 0; k < 6; k++) F->all_glob[f][k] += g[k];
+        if (w_gnd) for (int k = 0; k < 6; k++) F->gnd_glob[f][k] += g[k];
+      }
+    }
+    if (w_palm) for (int k = 0; k < 6; k++) F->all_glob[3][k] += g[k];
+  }
+  for (int f = 0; f < 4; f++) {
+    const double* R = e->xmat[f < 3 ? m->body_finger[f] : m->body_palm];
+    mulmtv3(F->obj_loc[f], R, F->obj_glob[1 + f]);
+    mulmtv3(F->all_loc[f], R, F->all_glob[f]);
+    if (f < 3) mulmtv3(F->gnd_loc[f], R, F->gnd_glob[f]);
+  }
+}
+
+/* MjClass::monitor_sensors (mjclass.cpp:741-898) */
+static void monitor_sensors(or_env* e) {
+  gm_settings* s = &e->c.s;
+  int have_forces = 0;
+  forces_t F;
+  if (s_ready(e, &s->bending_gauge, S_BEND)) {
+    float g[3];
+    for (int f = 0; f < 3; f++) g[f] = or_gauge_reading(&e->m, &e->qpos[e->m.dof_seg[f]]);
+    for (int f = 0; f < 3; f++) ring_add(&e->si_gauge[f], (float)(g[f] * e->c.sim_gauge_raw_to_N_factor));
+    for (int f = 0; f < 3; f++) g[f] = s_normalise(&s->bending_gauge, g[f]);
+    for (int f = 0; f < 3; f++) g[f] = s_noise(e, &s->bending_gauge, S_BEND, g[f], f + 1);
+    for (int f = 0; f < 3; f++) ring_add(&e->w_gauge[f], g[f]);
+  }
+  if (s_ready(e, &s->axial_gauge, S_AXIAL)) {
+    if (!have_forces) { extract_forces(e, &F); have_forces = 1; }
+    float a[3];
+    for (int f = 0; f < 3; f++) a[f] = (float)F.all_loc[f][0];
+    for (int f = 0; f < 3; f++) ring_add(&e->si_axial[f], a[f]);
+    for (int f = 0; f < 3; f++) a[f] = s_normalise(&s->axial_gauge, a[f]);
+    for (int f = 0; f < 3; f++) a[f] = s_noise(e, &s->axial_gauge, S_AXIAL, a[f], f + 1);
+    for (int f = 0; f < 3; f++) ring_add(&e->w_axial[f], a[f]);
+  }
+  if (s_ready(e, &s->palm_sensor, S_PALM)) {
+    if (!have_forces) { extract_forces(e, &F); have_forces = 1; }
+    float p = (float)F.all_loc[3][0];
+    p *= s->palm_scale_factor;
+    ring_add(&e->si_palm, p);
+    p = s_normalise(&s->palm_sensor, p);
+    p = s_noise(e, &s->palm_sensor, S_PALM, p, 1);
+    ring_add(&e->w_palm, p);
+  }
+  if (s_ready(e, &s->wrist_sensor_Z, S_WRISTZ)) {
+    float z = 0.0f;   /* data->userdata[2] is never written */
+    z -= s->wrist_sensor_Z.raw_value_offset;
+    ring_add(&e->si_wz, z);
+    z = s_normalise(&s->wrist_sensor_Z, z);
+    z = s_noise(e, &s->wrist_sensor_Z, S_WRISTZ, z, 1);
+    ring_add(&e->w_wz, z);
+  }
+}
+
+/* normalise_between (mjclass.cpp:4896-4904) */
+static float normalise_between(float val, float mn, float mx) {
+  if (val > mx) return 1.0f;
+  else if (val < mn) return -1.0f;
+  return 2 * (val - mn) / (mx - mn) - 1;
+}
+
+/* luke::get_fingerend_and_palm_xyz (myfunctions.cpp:3622-3688) */
+static void fingerend_palm_xyz(const or_env* e, const double* fsi, double out[4][3]) {
+  const gm_model* m = &e->m;
+  double bx = e->base[0], by = e->base[1], bz = e->base[2], yaw = e->base[5];
+  double fx = e->end.x, fth = g_th_rad(&e->end), pz = e->end.z;
+  const double PI23 = PI_D * (2.0 / 3.0);
+  double ang[3] = {0.0, PI23, 2 * PI23};
+  double unt = m->fingertip_clearance - bz;
+  double lift = m->finger_length * (1 - cos(fth));
+  double tilted = unt + lift;
+  for (int i = 0; i < 3; i++) {
+    double tilt_x = fx - m->finger_length * sin(fth);
+    double defl = fsi[i] * pow(m->finger_length, 3) / (3 * m->finger_EI);
+    double fin_x = tilt_x + defl * cos(fth);
+    out[i][0] = -fin_x * sin(ang[i] + yaw) + bx;
+    out[i][1] = -fin_x * cos(ang[i] + yaw) + by;
+    out[i][2] = tilted - defl * sin(fth);
+  }
+  out[3][0] = bx; out[3][1] = by; out[3][2] = unt + 165e-3 - pz;
+}
+
+/* MjClass::sense_gripper_state (mjclass.cpp:900-964) */
+static void sense_gripper_state(or_env* e) {
+  gm_settings* s = &e->c.s;
+  const double* bmn = e->c.base_min;
+  const double* bmx = e->c.base_max;
+  double gx = normalise_between((float)e->end.x, (float)G_xy_min, (float)G_xy_max);
+  double gy = normalise_between((float)e->end.y, (float)G_xy_min, (float)G_xy_max);
+  double gz = normalise_between((float)e->end.z, (float)G_z_min, (float)G_z_max);
+  double bx = normalise_between((float)e->base[0], (float)bmn[0], (float)bmx[0]);
+  double by = normalise_between((float)e->base[1], (float)bmn[1], (float)bmx[1]);
+  double bz = normalise_between((float)e->base[2], (float)bmn[2], (float)bmx[2]);
+  double byaw = normalise_between((float)e->base[5], (float)bmn[5], (float)bmx[5]);
+  gx = s_noise(e, &s->motor_state_sensor, S_MOTOR, (float)gx, 1);
+  gy = s_noise(e, &s->motor_state_sensor, S_MOTOR, (float)gy, 2);
+  gz = s_noise(e, &s->motor_state_sensor, S_MOTOR, (float)gz, 3);
+  bx = s_noise(e, &s->base_state_sensor_XY, S_BASEXY, (float)bx, 1);
+  by = s_noise(e, &s->base_state_sensor_XY, S_BASEXY, (float)by, 2);
+  bz = s_noise(e, &s->base_state_sensor_Z, S_BASEZ, (float)bz, 1);
+  byaw = s_noise(e, &s->base_state_sensor_yaw, S_YAW, (float)byaw, 1);
+  ring_add(&e->w_motor[0], (float)gx);
+  ring_add(&e->w_motor[1], (float)gy);
+  ring_add(&e->w_motor[2], (float)gz);
+  ring_add(&e->w_base[0], (float)bx);
+  ring_add(&e->w_base[1], (float)by);
+  ring_add(&e->w_base[2], (float)bz);
+  ring_add(&e->w_yaw, (float)byaw);
+  /* MAT cartesian contact points */
+  double fsi[3] = {ring_latest(&e->si_gauge[0]), ring_latest(&e->si_gauge[1]), ring_latest(&e->si_gauge[2])};
+  double psi = ring_latest(&e->si_palm);
+  double xyz[4][3];
+  fingerend_palm_xyz(e, fsi, xyz);
+  const double ft = 0.2;
+  for (int f = 0; f < 3; f++)
+    for (int k = 0; k < 3; k++) ring_add(&e->w_cart[3 * f + k], (float)((fabs(fsi[f]) > ft) ? xyz[f][k] : 0.0));
+  for (int k = 0; k < 3; k++) ring_add(&e->w_cart[9 + k], (float)((psi > ft) ? xyz[3][k] : 0.0));
+}
+
+static double mag3(const double* v) { return sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+
+/* update_events (mjclass.cpp:5437-5469) */
+static void update_events(or_env* e) {
+  const gm_settings* s = &e->c.s;
+  for (int k = 0; k < GM_N_BINARY; k++) {
+    bev_t* b = &e->bev[k];
+    b->row = b->row * b->value + b->value;
+    b->abs += b->value;
+    b->last_value = b->value;
+    b->active_sum = b->row != 0;
+    b->value = 0;
+  }
+  const gm_linear_reward* lr[GM_N_LINEAR] = {
+#define GM_LR(n, r, d, t, a, b, o) &s->n,
+#include "../include/gm_settings.def"
+  };
+  for (int k = 0; k < GM_N_LINEAR; k++) {
+    lev_t* l = &e->lev[k];
+    int active = 0;
+    if (l->value > lr[k]->min && (l->value < lr[k]->overshoot || lr[k]->overshoot < 0)) active = 1;
+    l->row = l->row * active + active;
+    l->abs += active;
+    l->last_value = l->value;
+    l->active_sum = active;
+    l->value = 0.0f;
+  }
+}
+
+/* MjClass::update_env (mjclass.cpp:966-1346) for the single live object */
+static void update_env(or_env* e) {
+  const gm_settings* s = &e->c.s;
+  const gm_model* m = &e->m;
+  const double ftol = 1e-5;
+  forces_t F;
+  extract_forces(e, &F);
+  int qa = m->jnt_qposadr[m->body_jnt[m->body_obj]];
+  double ox = e->qpos[qa], oy = e->qpos[qa + 1], oz = e->qpos[qa + 2];
+  double relx = e->base[0] - ox, rely = e->base[1] - oy;
+  float dist_from_gripper = (float)sqrt(pow(relx, 2) + pow(rely, 2));
+  float f1m = (float)mag3(F.obj_loc[0]), f2m = (float)mag3(F.obj_loc[1]), f3m = (float)mag3(F.obj_loc[2]);
+  float pm = (float)mag3(F.obj_loc[3]);
+  float gm = (float)mag3(F.obj_glob[5]);
+  float palm_axial = (float)F.obj_loc[3][0];
+  float lift_height = (float)(oz - e->start_qpos[2]);
+  float avg_finger = (float)(0.33333 * (f1m + f2m + f3m));
+  double mn = F.obj_loc[0][1];
+  if (F.obj_loc[1][1] < mn) mn = F.obj_loc[1][1];
+  if (F.obj_loc[2][1] < mn) mn = F.obj_loc[2][1];
+  float peak_lat = (float)(-1 * mn);
+  float ov_avg = 0, ov_palm = 0, ov_lift = 0;
+  if (avg_finger > ov_avg) ov_avg = avg_finger;
+  if (palm_axial > ov_palm) ov_palm = palm_axial;
+  if (peak_lat > e->grp_peak_lateral) e->grp_peak_lateral = peak_lat;
+  if (lift_height > ov_lift) ov_lift = lift_height;
+  float gripper_z_height = (float)(-1 * e->base[2]);
+  double ga = F.gnd_loc[0][0];
+  if (F.gnd_loc[1][0] < ga) ga = F.gnd_loc[1][0];
+  if (F.gnd_loc[2][0] < ga) ga = F.gnd_loc[2][0];
+  float grp_peak_axial = (float)(-1 * ga);
+  float g1 = ring_latest(&e->si_gauge[0]), g2 = ring_latest(&e->si_gauge[1]), g3 = ring_latest(&e->si_gauge[2]);
+  float last_palm = ring_latest(&e->si_palm), last_wrist = ring_latest(&e->si_wz);
+  float max_gauge = g1 > g2 ? g1 : g2;
+  max_gauge = max_gauge > g3 ? max_gauge : g3;
+  float avg_gauge = (float)((1.0 / 3.0) * (g1 + g2 + g3));
+
+  bev_t* B = e->bev;
+  B[GM_EV_step_num].value = 1;
+  double closest = dist_from_gripper;
+  /* quirk: Obj::peak_finger_axial_force is never assigned (stays 0) (mjclass.cpp:1156) */
+  int o_lifted = 0, o_oob = 0, o_l2h = 0, o_th = 0, o_stable = 0, o_sh = 0;
+  if (gm < ftol && 0.0f < ftol) { B[GM_EV_lifted].value = 1; o_lifted = 1; }
+  if (ox > s->oob_distance || ox < -s->oob_distance || oy > s->oob_distance || oy < -s->oob_distance) {
+    B[GM_EV_oob].value = 1; o_oob = 1;
+  }
+  if (ov_lift > s->lift_height - ftol && o_lifted && !o_oob) { B[GM_EV_lifted_to_height].value = 1; o_l2h = 1; }
+  if (o_l2h && gripper_z_height > s->gripper_target_height - ftol) { B[GM_EV_target_height].value = 1; o_th = 1; }
+  if (f1m > ftol || f2m > ftol || f3m > ftol || pm > ftol) B[GM_EV_object_contact].value = 1;
+  if (f1m > s->stable_finger_force && f2m > s->stable_finger_force && f3m > s->stable_finger_force &&
+      f1m < s->stable_finger_force_lim && f2m < s->stable_finger_force_lim && f3m < s->stable_finger_force_lim &&
+      pm > s->stable_palm_force && pm < s->stable_palm_force_lim && B[GM_EV_lifted].value) {
+    B[GM_EV_object_stable].value = 1; o_stable = 1;
+  }
+  if (o_stable && o_th) { B[GM_EV_stable_height].value = 1; o_sh = 1; }
+  (void)o_sh;
+  if (e->termination_signal_sent) {
+    if (s->lifted_termination.done) {
+      if (o_l2h) B[GM_EV_lifted_termination].value = 1;
+      else B[GM_EV_failed_termination].value = 1;
+    } else {
+      if (B[GM_EV_stable_height].value) B[GM_EV_stable_termination].value = 1;
+      else B[GM_EV_failed_termination].value = 1;
+    }
+  }
+  if (dist_from_gripper < s->XY_distance_threshold) B[GM_EV_within_XY_distance].value = 1;
+  if (dist_from_gripper < closest) closest = dist_from_gripper;
+  {
+    int v = (!B[GM_EV_dropped].row * !B[GM_EV_lifted].value * B[GM_EV_lifted].row) ? 1
+            : (B[GM_EV_lifted].value ? 0 : (B[GM_EV_dropped].row ? B[GM_EV_dropped].row + 1 : 0));
+    B[GM_EV_dropped].value = v != 0;
+  }
+  lev_t* Lv = e->lev;
+  Lv[GM_LEV_exceed_axial].value = grp_peak_axial;
+  Lv[GM_LEV_exceed_lateral].value = e->grp_peak_lateral;
+  Lv[GM_LEV_palm_force].value = ov_palm * B[GM_EV_lifted].value;
+  Lv[GM_LEV_exceed_palm].value = ov_palm;
+  Lv[GM_LEV_finger_force].value = ov_avg;
+  Lv[GM_LEV_finger1_force].value = f1m;
+  Lv[GM_LEV_finger2_force].value = f2m;
+  Lv[GM_LEV_finger3_force].value = f3m;
+  Lv[GM_LEV_ground_force].value = gm;
+  Lv[GM_LEV_good_bend_sensor].value = avg_gauge;
+  Lv[GM_LEV_exceed_bend_sensor].value = max_gauge;
+  Lv[GM_LEV_dangerous_bend_sensor].value = max_gauge;
+  Lv[GM_LEV_good_palm_sensor].value = last_palm;
+  Lv[GM_LEV_exceed_palm_sensor].value = last_palm;
+  Lv[GM_LEV_dangerous_palm_sensor].value = last_palm;
+  Lv[GM_LEV_exceed_wrist_sensor].value = last_wrist;
+  Lv[GM_LEV_dangerous_wrist_sensor].value = last_wrist;
+  Lv[GM_LEV_action_penalty_lin].value /= (float)(e->c.n_actions - s->use_termination_action);
+  Lv[GM_LEV_action_penalty_sq].value /= (float)(e->c.n_actions - s->use_termination_action);
+  Lv[GM_LEV_object_XY_distance].value = (float)(-closest);
+  /* successful_grasp metric (mjclass.cpp:1305-1322) */
+  const gm_binary_reward* br[GM_N_BINARY] = {
+#define GM_BR(n, r, d, t) &s->n,
+#include "../include/gm_settings.def"
+  };
+  for (int k = 0; k < GM_N_BINARY; k++)
+    if (B[k].value && br[k]->reward >= (1.0 - 1e-5) && br[k]->done && B[k].row + 1 >= br[k]->trigger)
+      B[GM_EV_successful_grasp].value = 1;
+  update_events(e);
+}
+
+/* sample functions (mjclass.h:278-453) on a ring */
+static int sample_ring(int mode, const ring_t* w, int prev_steps, int rps, int total, float* out) {
+  if (mode == GM_SAMPLE_RAW) {
+    int n = total - 1;
+    for (int j = n - 1, k = 0; j >= 0; j--, k++) out[k] = ring_read(w, j);
+    return n;
+  }
+  out[0] = ring_read(w, total - 1);
+  for (int i = 0; i < prev_steps; i++) {
+    int first = total - 1 - i * rps;
+    out[2 * i + 2] = ring_read(w, first - rps);
+    float a = out[2 * i], b = out[2 * i + 2];
+    if (mode == GM_SAMPLE_CHANGE) out[2 * i + 1] = b - a;
+    else if (mode == GM_SAMPLE_AVERAGE) {
+      float acc = 0;
+      for (int j = 0; j < rps + 1; j++) acc += ring_read(w, first - j);
+      out[2 * i + 1] = acc / (rps + 1);
+    } else if (mode == GM_SAMPLE_MEDIAN) {
+      float v[GM_RING + 1];
+      int nv = rps + 1;
+      for (int j = 0; j < nv; j++) v[j] = ring_read(w, first - j);
+      for (int x = 1; x < nv; x++) { float t = v[x]; int y = x - 1; while (y >= 0 && v[y] > t) { v[y + 1] = v[y]; y--; } v[y + 1] = t; }
+      int hn = nv / 2;
+      float med = v[hn];
+      if (!(nv & 1)) med = (v[hn - 1] + med) / 2.0f;
+      out[2 * i + 1] = med;
+    } else if (mode == GM_SAMPLE_SIGN) {
+      float ch = b - a;
+      out[2 * i + 1] = ch > 1e-6f ? 1.0f : (ch < -1e-6f ? -1.0f : 0.0f);
+    } else if (mode == GM_SAMPLE_SCALED_CHANGE) {
+      float sc = (b - a) / 0.07f;
+      if (sc > 1.0f) sc = 1.0f; else if (sc < -1.0f) sc = -1.0f;
+      out[2 * i + 1] = sc;
+    } else {
+      float ch = fabsf(b - a);
+      float f = 1.0f / (0.10f * 0.10f);
+      float sc = (b - a) * ch * f;
+      if (sc > 1.0f) sc = 1.0f; else if (sc < -1.0f) sc = -1.0f;
+      out[2 * i + 1] = sc;
+    }
+  }
+  return 2 * prev_steps + 1;
+}
+int or_sample(int mode, const float* recent_first, int n_avail, int prev_steps, int rps, float* out) {
+  ring_t w;
+  ring_reset(&w);
+  for (int k = n_avail - 1; k >= 0; k--) ring_add(&w, recent_first[k]);
+  return sample_ring(mode, &w, prev_steps, rps, 1 + rps * prev_steps, out);
+}
+static int sample_sensor(int mode, const ring_t* w, const gm_sensor* s, float* out) {
+  return sample_ring(mode, w, s->prev_steps, s->readings_per_step, s->total_readings, out);
+}
+
+/* MjClass::get_observation (mjclass.cpp:1707-1959) */
+int or_get_obs(or_env* e, float* out) {
+  const gm_settings* s = &e->c.s;
+  int sf = e->c.sensor_fcn, tf = e->c.state_fcn, n = 0;
+  if (s->bending_gauge.in_use) for (int f = 0; f < 3; f++) n += sample_sensor(sf, &e->w_gauge[f], &s->bending_gauge, out + n);
+  if (s->axial_gauge.in_use) for (int f = 0; f < 3; f++) n += sample_sensor(sf, &e->w_axial[f], &s->axial_gauge, out + n);
+  if (s->palm_sensor.in_use) n += sample_sensor(sf, &e->w_palm, &s->palm_sensor, out + n);
+  if (s->wrist_sensor_XY.in_use) {
+    n += sample_sensor(sf, &e->w_wx, &s->wrist_sensor_XY, out + n);
+    n += sample_sensor(sf, &e->w_wy, &s->wrist_sensor_XY, out + n);
+  }
+  if (s->wrist_sensor_Z.in_use) n += sample_sensor(sf, &e->w_wz, &s->wrist_sensor_XY, out + n);  /* quirk 1806 */
+  if (s->motor_state_sensor.in_use) for (int k = 0; k < 3; k++) n += sample_sensor(tf, &e->w_motor[k], &s->motor_state_sensor, out + n);
+  if (s->base_state_sensor_XY.in_use) for (int k = 0; k < 2; k++) n += sample_sensor(tf, &e->w_base[k], &s->base_state_sensor_XY, out + n);
+  if (s->base_state_sensor_Z.in_use) n += sample_sensor(tf, &e->w_base[2], &s->base_state_sensor_Z, out + n);
+  if (s->base_state_sensor_yaw.in_use) n += sample_sensor(tf, &e->w_yaw, &s->base_state_sensor_yaw, out + n);
+  if (s->cartesian_contacts_XYZ.in_use)
+    for (int k = 0; k < 12; k++) n += sample_sensor(GM_SAMPLE_CHANGE, &e->w_cart[k], &s->cartesian_contacts_XYZ, out + n);
+  return n;
+}
+
+/* MjClass::is_done (mjclass.cpp:1632-1698) */
+int or_is_done(or_env* e) {
+  const gm_settings* s = &e->c.s;
+  int k = 0;
+#define GM_BR(n, r, d, t) if (s->n.done && e->bev[k].row >= s->n.done) return 1; k++;
+#include "../include/gm_settings.def"
+  k = 0;
+#define GM_LR(n, r, d, t, a, b, o) if (s->n.done && e->lev[k].row >= s->n.done) return 1; k++;
+#include "../include/gm_settings.def"
+  if (s->cap_reward && s->quit_if_cap_exceeded) {
+    if (e->cumulative_reward - 1e-5 < s->reward_cap_lower_bound) return 1;
+    if (e->cumulative_reward + 1e-5 > s->reward_cap_upper_bound) return 1;
+  }
+  return 0;
+}
+
+/* linear_reward (mjclass.cpp:4866-4894) */
+static float linear_reward(float val, float mn, float mx, float overshoot) {
+  if (val < mn) return 0.0f;
+  if (val > mx) {
+    if (overshoot < mx) return 1.0f;
+    if (val > overshoot) return 0.0f;
+    mn = 0; mx = overshoot - mx; val = overshoot - val;
+  }
+  return (val - mn) / (mx - mn);
+}
+/* MjClass::reward + calc_rewards (mjclass.cpp:3000-3049, 5471-5528) */
+float or_reward(or_env* e) {
+  const gm_settings* s = &e->c.s;
+  float r = 0;
+  int k = 0;
+#define GM_BR(n, rr, d, t) if (e->bev[k].row >= s->n.trigger) r += s->n.reward; k++;
+#include "../include/gm_settings.def"
+  k = 0;
+#define GM_LR(n, rr, d, t, a, b, o)                                                   \
+  if (e->lev[k].row >= s->n.trigger) {                                               \
+    float fr = linear_reward(e->lev[k].last_value, s->n.min, s->n.max, s->n.overshoot); \
+    r += s->n.reward * fr;                                                           \
+  }                                                                                  \
+  k++;
+#include "../include/gm_settings.def"
+  e->cumulative_reward += r;
+  if (e->cumulative_reward < s->reward_cap_lower_bound && s->cap_reward) {
+    r += s->reward_cap_lower_bound - e->cumulative_reward;
+    e->cumulative_reward = s->reward_cap_lower_bound;
+  }
+  if (e->cumulative_reward > s->reward_cap_upper_bound && s->cap_reward) {
+    r += s->reward_cap_upper_bound - e->cumulative_reward;
+    e->cumulative_reward = s->reward_cap_upper_bound;
+  }
+  return r;
+}
+
+/* =====================================================================
+ * actions: MjClass::set_action (mjclass.cpp:1528-1630) + luke::move_* (2422-2536)
+ * ===================================================================== */
+static int move_base_target_m(or_env* e, double x, double y, double z) {
+  double* b = e->base;
+  const double* mn = e->c.base_min;
+  const double* mx = e->c.base_max;
+  b[0] += x; b[1] += y; b[2] += z;
+  int wl = 1;
+  for (int k = 0; k < 3; k++) {
+    if (b[k] > mx[k]) { b[k] = mx[k]; wl = 0; }
+    if (b[k] < mn[k]) { b[k] = mn[k]; wl = 0; }
+  }
+  return wl;
+}
+static int move_base_target_rad(or_env* e, double r, double p, double y) {
+  (void)r; (void)p;
+  e->base[5] += y;
+  int wl = 1;
+  if (e->base[5] > e->c.base_max[5]) { e->base[5] = e->c.base_max[5]; wl = 0; }
+  if (e->base[5] < e->c.base_min[5]) { e->base[5] = e->c.base_min[5]; wl = 0; }
+  return wl;
+}
+/* ActionSetting::call_action_function (mjclass.h:546-571) with the name-derived
+ * function and argument (update_action_function, mjclass.h:488-544) */
+static int call_action(or_env* e, int kind, double v) {
+  const gm_action* acts[GM_N_ACTION_KINDS] = {
+#define GM_AA(n, u, vv, sg) &e->c.s.n,
+#include "../include/gm_settings.def"
+  };
+  v *= acts[kind]->sign;
+  double a[3] = {0, 0, 0};
+  switch (kind) {
+    case GM_ACT_gripper_X: a[0] = v; return g_set_xyz_m(&e->end, e->end.x + a[0], e->end.y, e->end.z);
+    case GM_ACT_gripper_Y: a[1] = v; return g_set_xyz_m(&e->end, e->end.x, e->end.y + a[1], e->end.z);
+    case GM_ACT_gripper_prismatic_X: return g_set_xyz_m_rad(&e->end, e->end.x + v, e->end.th, e->end.z);
+    case GM_ACT_gripper_revolute_Y: return g_set_xyz_m_rad(&e->end, e->end.x, e->end.th + v, e->end.z);
+    case GM_ACT_gripper_Z: return g_set_xyz_m(&e->end, e->end.x, e->end.y, e->end.z + v);
+    case GM_ACT_base_X: return move_base_target_m(e, v, 0, 0);
+    case GM_ACT_base_Y: return move_base_target_m(e, 0, v, 0);
+    case GM_ACT_base_Z: return move_base_target_m(e, 0, 0, v);
+    case GM_ACT_base_roll: return move_base_target_rad(e, v, 0, 0);
+    case GM_ACT_base_pitch: return move_base_target_rad(e, 0, v, 0);
+    default: return move_base_target_rad(e, 0, 0, v);
+  }
+}
+/* luke::get_fingertip_z_height (myfunctions.cpp:3608-3620) */
+static float fingertip_z_height(const or_env* e) {
+  float straight = (float)(-e->c.base_min[2] - e->base[2]);
+  float tip_lift = (float)(e->m.finger_length * (1 - cos(g_th_rad(&e->end))));
+  float h = straight + tip_lift;
+  return (float)(h + e->c.base_min[2]);
+}
+static void lift_base_to_height(or_env* e, double z) {
+  e->base[2] = -z;
+  if (e->base[2] > e->c.base_max[2]) e->base[2] = e->c.base_max[2];
+  if (e->base[2] < e->c.base_min[2]) e->base[2] = e->c.base_min[2];
+}
+static void full_substep(or_env* e);
+static void set_action(or_env* e, int action, float frac) {
+  const gm_settings* s = &e->c.s;
+  int wl = 1;
+  e->termination_signal_sent = 0;
+  if (action < 0 || action >= e->c.n_actions) return;
+  int code = e->c.action_options[action];
+  if (code == GM_ACTION_TERMINATION) {
+    float value = s->continous_actions ? frac : 1.0f;
+    if (value > s->termination_threshold) {
+      e->termination_signal_sent = 1;
+      if (s->lift_on_termination) {
+        lift_base_to_height(e, e->c.base_max[2]);
+        for (int i = 0; i < e->c.sim_steps_per_action * 2; i++) full_substep(e);
+      }
+    }
+    wl = 1;
+  } else {
+    int kind = code / 3, sub = code % 3;
+    const gm_action* acts[GM_N_ACTION_KINDS] = {
+#define GM_AA(n, u, vv, sg) &s->n,
+#include "../include/gm_settings.def"
+    };
+    if (sub == 0) wl = call_action(e, kind, acts[kind]->value);
+    else if (sub == 1) wl = call_action(e, kind, -1 * acts[kind]->value);
+    else {
+      wl = call_action(e, kind, acts[kind]->value * frac);
+      e->lev[GM_LEV_action_penalty_lin].value += fabsf(frac);
+      e->lev[GM_LEV_action_penalty_sq].value += (frac * frac);
+    }
+  }
+  if (fingertip_z_height(e) < s->fingertip_min_mm * 1e-3) wl = 0;
+  e->bev[GM_EV_exceed_limits].value = e->bev[GM_EV_exceed_limits].value || !wl;
+}
+void or_set_action(or_env* e, const float* a) {
+  for (int i = 0; i < e->c.n_actions; i++) {
+    float f = a[i];
+    if (f < -1.0f) f = -1.0f; else if (f > 1.0f) f = 1.0f;
+    set_action(e, i, f);
+  }
+}
+void or_set_discrete_action(or_env* e, int32_t a) { set_action(e, a, 0); }
+
+/* MjClass::step (mjclass.cpp:504-530): physics + update_all + monitor_sensors */
+static void full_substep(or_env* e) {
+  physics_substep(e);
+  update_all(e);
+  monitor_sensors(e);
+}
+/* MjClass::action_step (mjclass.cpp:1483-1508) */
+void or_step(or_env* e) {
+  for (int i = 0; i < e->c.sim_steps_per_action; i++) full_substep(e);
+  sense_gripper_state(e);
+  update_env(e);
+  e->num_action_steps += 1;
+}
+
+/* =====================================================================
+ * reset (mjclass.cpp:434-486, myfunctions.cpp:544-570, 1441-1519) and spawn
+ * ===================================================================== */
+static void keyframe_state(or_env* e) {
+  for (int i = 0; i < NQ; i++) e->qpos[i] = e->m.qpos0[i];
+  for (int i = 0; i < NV; i++) e->qvel[i] = 0;
+  e->time = 0;
+  e->last_step_time = 0;
+}
+static int is_motor_or_base_dof(const gm_model* m, int d) {
+  if (d == m->dof_base || d == m->dof_palm) return 1;
+  for (int f = 0; f < 3; f++) if (d == m->dof_pris[f] || d == m->dof_rev[f]) return 1;
+  return 0;
+}
+/* first-call settle of calibrate_reset (400 substeps, no sensors) */
+static void settle(or_env* e) {
+  g_reset(&e->end); g_reset(&e->next);
+  for (int k = 0; k < 6; k++) e->base[k] = 0;
+  for (int k = 0; k < GM_MAX_LOCK; k++) { e->lock_active[k] = 0; e->lock_q[k] = 0; }
+  e->old_x = e->old_y = e->old_z = 1;
+  keyframe_state(e);
+  for (int i = 0; i < 400; i++) { physics_substep(e); update_all(e); }
+  for (int i = 0; i < NQ; i++) e->eq_q[i] = e->qpos[i];
+}
+
+static void sensors_reset(or_env* e) {
+  for (int f = 0; f < 3; f++) {
+    ring_reset(&e->w_gauge[f]); ring_reset(&e->w_axial[f]); ring_reset(&e->w_motor[f]);
+    ring_reset(&e->w_base[f]); ring_reset(&e->si_gauge[f]); ring_reset(&e->si_axial[f]);
+  }
+  ring_reset(&e->w_palm); ring_reset(&e->w_wx); ring_reset(&e->w_wy); ring_reset(&e->w_wz);
+  ring_reset(&e->w_yaw); ring_reset(&e->si_palm); ring_reset(&e->si_wz);
+  for (int k = 0; k < 12; k++) ring_reset(&e->w_cart[k]);
+  for (int k = 0; k < S_N; k++) e->last_read[k] = 0;
+}
+
+/* Settings::apply_noise_params RNG draws (mjclass.cpp:5293-5346) */
+static void randomise_mu(or_env* e) {
+  gm_settings* s = &e->c.s;
+  gm_sensor* ss[S_N] = {&s->motor_state_sensor, &s->base_state_sensor_Z, &s->base_state_sensor_XY,
+                        &s->base_state_sensor_yaw, &s->bending_gauge, &s->axial_gauge, &s->palm_sensor,
+                        &s->wrist_sensor_XY, &s->wrist_sensor_Z, &s->cartesian_contacts_XYZ};
+  for (int k = 0; k < S_N; k++)
+    for (int i = 0; i < 3; i++) e->rand_mu[k][i] = ss[k]->noise_mu * (2 * unif01(&e->rng) - 1);
+  int order[5] = {S_MOTOR, S_BASEXY, S_BASEZ, S_YAW, S_CART};
+  for (int k = 0; k < 5; k++)
+    for (int i = 0; i < 3; i++) e->rand_mu[order[k]][i] = ss[order[k]]->noise_mu * (2 * unif01(&e->rng) - 1);
+}
+
+void or_reset(or_env* e, const gm_spawn* sp) {
+  const gm_model* m0 = &e->m;
+  /* luke::reset: targets home, locks off, keyframe, object parked */
+  g_reset(&e->end); g_reset(&e->next);
+  for (int k = 0; k < 6; k++) e->base[k] = 0;
+  keyframe_state(e);
+  /* calibrate_reset: equilibrium gripper + base joints */
+  for (int d = 0; d < m0->nv; d++) if (is_motor_or_base_dof(m0, d)) e->qpos[d] = e->eq_q[d];
+  /* set_all_constraints(true): locks read the stale keyframe kinematics */
+  for (int k = 0; k < m0->nlock; k++) { e->lock_active[k] = 1; e->lock_q[k] = m0->qpos0[m0->lock_dof[k]]; }
+  sensors_reset(e);
+  memset(e->bev, 0, sizeof(e->bev));
+  memset(e->lev, 0, sizeof(e->lev));
+  e->cumulative_reward = 0;
+  e->num_action_steps = 0;
+  e->termination_signal_sent = 0;
+  e->grp_peak_lateral = 0;
+  /* configure_settings: noise mean draws */
+  randomise_mu(e);
+  /* random_base_Z_movement (mjclass.cpp:1423-1434) */
+  {
+    double size = e->c.s.base_position_noise;
+    double u = canon_d(&e->rng);
+    double z = u * (size - (-size)) + (-size);
+    e->base[2] = z;
+    if (e->base[2] > e->c.base_max[2]) e->base[2] = e->c.base_max[2];
+    if (e->base[2] < e->c.base_min[2]) e->base[2] = e->c.base_min[2];
+    e->qpos[m0->dof_base] = e->base[2] + e->eq_q[m0->dof_base];
+  }
+  /* spawn_object (mjclass.cpp:2352-2420, objecthandler.cpp:403-428) */
+  int oi = sp ? sp->object_index : 0;
+  if (oi < 0 || oi >= e->nobj) oi = 0;
+  e->obj_index = oi;
+  apply_object(&e->m, &e->objs[oi]);
+  int qa = e->m.jnt_qposadr[e->m.body_jnt[e->m.body_obj]];
+  double zr = sp ? sp->zrot : 0.0;
+  /* quaternion exactly as the reference composes it: QPos (x,y,z,qx,qy,qz,qw) with
+   * qx written to qpos[3] (MuJoCo's w slot) -- net effect: rotation pi+zrot about z */
+  double x2 = sin(-zr / 2.0), w2 = cos(-zr / 2.0);
+  double qw = w2, qx = x2, qy = 0, qz = 0;
+  e->qpos[qa + 0] = sp ? sp->x : 0.0;
+  e->qpos[qa + 1] = sp ? sp->y : 0.0;
+  e->qpos[qa + 2] = object_rest_z(&e->objs[oi]) + 1e-6;
+  e->qpos[qa + 3] = qx; e->qpos[qa + 4] = qy; e->qpos[qa + 5] = qz; e->qpos[qa + 6] = qw;
+  quatnorm(&e->qpos[qa + 3]);
+  for (int k = 0; k < 6; k++) e->qvel[e->m.dof_obj + k] = 0;
+  for (int k = 0; k < 7; k++) e->start_qpos[k] = e->qpos[qa + k];
+}
+
+or_env* or_create(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects,
+                  int64_t env_id) {
+  or_env* e = (or_env*)calloc(1, sizeof(or_env));
+  if (!e) return NULL;
+  e->m = *m;
+  e->c = *c;
+  e->nobj = n_objects > GM_MAX_OBJSET ? GM_MAX_OBJSET : n_objects;
+  for (int i = 0; i < e->nobj; i++) e->objs[i] = objects[i];
+  e->env_id = env_id;
+  e->rng = lcg_seed((uint64_t)c->s.random_seed + (uint64_t)env_id * 1000003ull);
+  /* settle with the first object parked at the keyframe pose */
+  if (e->nobj > 0) apply_object(&e->m, &e->objs[0]);
+  settle(e);
+  e->old_x = e->old_y = e->old_z = 0;
+  /* state after settle (function-static flags keep their settled values) */
+  {
+    or_env tmp = *e;
+    (void)tmp;
+  }
+  return e;
+}
+void or_destroy(or_env* e) { free(e); }
+
+void or_get_state(const or_env* e, double* qpos, double* qvel, double* time) {
+  if (qpos) for (int i = 0; i < e->m.nq; i++) qpos[i] = e->qpos[i];
+  if (qvel) for (int i = 0; i < e->m.nv; i++) qvel[i] = e->qvel[i];
+  if (time) *time = e->time;
+}
+void or_set_state(or_env* e, const double* qpos, const double* qvel) {
+  if (qpos) for (int i = 0; i < e->m.nq; i++) e->qpos[i] = qpos[i];
+  if (qvel) for (int i = 0; i < e->m.nv; i++) e->qvel[i] = qvel[i];
+}
+void or_get_target(const or_env* e, double* end_xyzth, int32_t* es, int32_t* ns, double* base_xyz) {
+  if (end_xyzth) { end_xyzth[0] = e->end.x; end_xyzth[1] = e->end.y; end_xyzth[2] = e->end.z; end_xyzth[3] = e->end.th; }
+  if (es) { es[0] = e->end.sx; es[1] = e->end.sy; es[2] = e->end.sz; }
+  if (ns) { ns[0] = e->next.sx; ns[1] = e->next.sy; ns[2] = e->next.sz; }
+  if (base_xyz) { base_xyz[0] = e->base[0]; base_xyz[1] = e->base[1]; base_xyz[2] = e->base[2]; }
+}
+void or_get_event_rows(const or_env* e, int32_t* rows, int32_t* absc, float* lastv) {
+  for (int k = 0; k < GM_N_BINARY; k++) {
+    if (rows) rows[k] = e->bev[k].row;
+    if (absc) absc[k] = e->bev[k].abs;
+    if (lastv) lastv[k] = (float)e->bev[k].last_value;
+  }
+  for (int k = 0; k < GM_N_LINEAR; k++) {
+    if (rows) rows[GM_N_BINARY + k] = e->lev[k].row;
+    if (absc) absc[GM_N_BINARY + k] = e->lev[k].abs;
+    if (lastv) lastv[GM_N_BINARY + k] = e->lev[k].last_value;
+  }
+}
+int or_overflow(const or_env* e) { return e->overflow; }
+void or_get_eq(const or_env* e, double* eq) { for (int i = 0; i < e->m.nq; i++) eq[i] = e->eq_q[i]; }
+
+void or_debug_substep(or_env* e, int32_t* ncon, float* contact, float* efc_force, double* qacc) {
+  full_substep(e);
+  if (ncon) *ncon = e->ncon;
+  if (contact) {
+    for (int c = 0; c < NC; c++) {
+      float* o = contact + 16 * c;
+      for (int k = 0; k < 16; k++) o[k] = 0;
+      if (c >= e->ncon) continue;
+      const con_t* C = &e->con[c];
+      o[0] = (float)C->dist;
+      for (int k = 0; k < 3; k++) o[1 + k] = (float)C->pos[k];
+      for (int k = 0; k < 9; k++) o[4 + k] = (float)C->frame[k];
+      o[13] = (float)C->g1; o[14] = (float)C->g2; o[15] = (float)C->mu;
+    }
+  }
+  if (efc_force) for (int r = 0; r < NE; r++) efc_force[r] = r < e->nefc ? (float)e->efc_f[r] : 0.0f;
+  if (qacc) for (int d = 0; d < e->m.nv; d++) qacc[d] = e->qacc[d];
+}
+
+/* bounded CPU baseline: n_envs independent envs, random continuous actions */
+double or_bench(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects,
+                int n_envs, int n_steps, uint64_t seed, int n_threads) {
+  (void)n_threads;
+  or_env* proto = or_create(m, c, objects, n_objects, 0);
+  if (!proto) return -1;
+  uint64_t x = seed;
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  long done_steps = 0;
+  for (int k = 0; k < n_envs; k++) {
+    or_env* e = (or_env*)malloc(sizeof(or_env));
+    *e = *proto;
+    e->env_id = k;
+    e->rng = lcg_seed((uint64_t)c->s.random_seed + (uint64_t)k * 1000003ull);
+    gm_spawn sp = {k % (n_objects > 0 ? n_objects : 1), 0.0, 0.0, 0.0};
+    or_reset(e, &sp);
+    for (int t = 0; t < n_steps; t++) {
+      float a[8];
+      for (int i = 0; i < e->c.n_actions && i < 8; i++) {
+        x = x * 6364136223846793005ull + 1442695040888963407ull;
+        a[i] = (float)((double)(x >> 11) / 9007199254740992.0 * 2 - 1);
+      }
+      or_set_action(e, a);
+      or_step(e);
+      float obs[256];
+      or_get_obs(e, obs);
+      int d = or_is_done(e);
+      or_reward(e);
+      done_steps++;
+      if (d) or_reset(e, &sp);
+    }
+    free(e);
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  or_destroy(proto);
+  double dt = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+  return dt > 0 ? done_steps / dt : 0;
+}

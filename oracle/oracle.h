@@ -1,0 +1,68 @@
+/* oracle.h -- CPU fp64 restatement of the reference env-step hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker /
+ * CPU baseline -- never as the thing measured or shipped.  The product path
+ * (gripper-mujoco_amd/) never links or calls it.
+ *
+ * One or_env is one reference MjClass: single env, single thread, fp64.
+ * Each function cites the reference code it restates (paths relative to the
+ * reference checkout).  Parity status is recorded in DESIGN.md section "Oracle":
+ * pinned by the reference's own compilable code (src/gripper.cpp,
+ * src/slidingwindow.h via oracle/_ref), the test.cpp:293-311 known answer and
+ * numpy.polyfit; the MuJoCo physics restatement is "parity unpinned" against
+ * MuJoCo 2.1.5 itself (not present), and pinned only to this oracle.
+ */
+#ifndef GM_ORACLE_H_
+#define GM_ORACLE_H_
+
+#include <stdint.h>
+#include <stddef.h>
+#include "../include/gripper_mi355x.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct or_env or_env;
+
+/* create one env; runs the one-time 400-substep settle of calibrate_reset()
+ * (myfunctions.cpp:1470-1505) once, shared semantics with the product */
+or_env* or_create(const gm_model* m, const gm_config* c, const gm_object* objects,
+                  int n_objects, int64_t env_id);
+void    or_destroy(or_env* e);
+size_t  or_sizeof(void);
+
+void  or_reset(or_env* e, const gm_spawn* spawn);                  /* MjClass::reset + spawn_object */
+void  or_set_action(or_env* e, const float* actions);              /* set_continous_action x n_actions */
+void  or_set_discrete_action(or_env* e, int32_t action);           /* set_discrete_action */
+void  or_step(or_env* e);                                          /* action_step */
+int   or_get_obs(or_env* e, float* out);                           /* get_observation */
+int   or_is_done(or_env* e);                                       /* is_done */
+float or_reward(or_env* e);                                        /* reward */
+void  or_get_state(const or_env* e, double* qpos, double* qvel, double* time);
+void  or_set_state(or_env* e, const double* qpos, const double* qvel);
+void  or_get_target(const or_env* e, double* end_xyzth, int32_t* end_steps, int32_t* next_steps,
+                    double* base_xyz);
+void  or_get_event_rows(const or_env* e, int32_t* rows, int32_t* abs_counts, float* last_values);
+int   or_overflow(const or_env* e);
+void  or_get_eq(const or_env* e, double* eq_qpos);                 /* settled equilibrium */
+
+/* one physics substep, with diagnostics (same layout as gm_debug_substep) */
+void  or_debug_substep(or_env* e, int32_t* ncon, float* contact, float* efc_force, double* qacc);
+
+/* standalone pieces used by the golden-vector tests */
+float  or_gauge_reading(const gm_model* m, const double* finger_q);   /* read_armadillo_gauge */
+double or_minstd_next_canonical_float(uint32_t* state);               /* generate_canonical<float> */
+double or_minstd_next_canonical_double(uint32_t* state);              /* generate_canonical<double> */
+int    or_grip_step_sequence(const double* cmds, int n, double* out);  /* Gripper golden driver */
+int    or_sample(int mode, const float* window_recent_first, int n_avail, int prev_steps,
+                 int readings_per_step, float* out);                  /* Sensor::*_sample */
+/* time one bounded CPU sample: n_envs envs x n_steps env-steps, random actions */
+double or_bench(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects,
+                int n_envs, int n_steps, uint64_t seed, int n_threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

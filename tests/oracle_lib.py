@@ -1,0 +1,195 @@
+"""ctypes wrapper of oracle/liboracle.so (the fp64 CPU restatement).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, as the checker / CPU baseline.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+
+
+def build_oracle():
+    if not os.path.exists(ORACLE_LIB) or os.path.getmtime(ORACLE_LIB) < os.path.getmtime(os.path.join(ORACLE_DIR, "oracle.c")):
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR, os.path.join(ORACLE_DIR, "liboracle.so")], check=True)
+    return ORACLE_LIB
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build_oracle()
+        L = C.CDLL(ORACLE_LIB)
+        vp, i32, f32p, f64p, i32p = C.c_void_p, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_double), C.POINTER(C.c_int32)
+        sig = {
+            "or_create": (vp, [vp, vp, vp, i32, C.c_int64]),
+            "or_destroy": (None, [vp]),
+            "or_sizeof": (C.c_size_t, []),
+            "or_reset": (None, [vp, vp]),
+            "or_set_action": (None, [vp, f32p]),
+            "or_set_discrete_action": (None, [vp, C.c_int32]),
+            "or_step": (None, [vp]),
+            "or_get_obs": (i32, [vp, f32p]),
+            "or_is_done": (i32, [vp]),
+            "or_reward": (C.c_float, [vp]),
+            "or_get_state": (None, [vp, f64p, f64p, f64p]),
+            "or_set_state": (None, [vp, f64p, f64p]),
+            "or_get_target": (None, [vp, f64p, i32p, i32p, f64p]),
+            "or_get_event_rows": (None, [vp, i32p, i32p, f32p]),
+            "or_overflow": (i32, [vp]),
+            "or_get_eq": (None, [vp, f64p]),
+            "or_debug_substep": (None, [vp, i32p, f32p, f32p, f64p]),
+            "or_gauge_reading": (C.c_float, [vp, f64p]),
+            "or_minstd_next_canonical_float": (C.c_double, [C.POINTER(C.c_uint32)]),
+            "or_minstd_next_canonical_double": (C.c_double, [C.POINTER(C.c_uint32)]),
+            "or_grip_step_sequence": (i32, [f64p, i32, f64p]),
+            "or_sample": (i32, [i32, f32p, i32, i32, i32, f32p]),
+            "or_bench": (C.c_double, [vp, vp, vp, i32, i32, i32, C.c_uint64, i32]),
+        }
+        for n, (r, a) in sig.items():
+            f = getattr(L, n)
+            f.restype = r
+            f.argtypes = a
+        _lib = L
+    return _lib
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+class OracleEnv:
+    """One reference MjClass, fp64 CPU restatement."""
+
+    def __init__(self, model, cfg, objects, env_id: int = 0):
+        L = lib()
+        self.L = L
+        self.model = model
+        self.cfg = cfg
+        self.objects = objects
+        self.h = L.or_create(model.ptr, cfg.ptr, C.cast(objects, C.c_void_p), len(objects), env_id)
+        if not self.h:
+            raise RuntimeError("or_create failed")
+        self.n_obs = cfg.n_obs
+        self.n_actions = cfg.n_actions
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.L.or_destroy(self.h)
+        except Exception:
+            pass
+
+    def reset(self, spawn):
+        self.L.or_reset(self.h, C.byref(spawn))
+
+    def set_action(self, a):
+        a = _f32(a)
+        self.L.or_set_action(self.h, a.ctypes.data_as(C.POINTER(C.c_float)))
+
+    def set_discrete_action(self, a: int):
+        self.L.or_set_discrete_action(self.h, int(a))
+
+    def action_step(self):
+        self.L.or_step(self.h)
+
+    def observation(self):
+        out = np.zeros(max(self.n_obs, 1), dtype=np.float32)
+        n = self.L.or_get_obs(self.h, out.ctypes.data_as(C.POINTER(C.c_float)))
+        return out[:n]
+
+    def is_done(self):
+        return bool(self.L.or_is_done(self.h))
+
+    def reward(self):
+        return float(self.L.or_reward(self.h))
+
+    def step(self, a):
+        self.set_action(a)
+        self.action_step()
+        obs = self.observation()
+        d = self.is_done()
+        r = self.reward()
+        return obs, r, d
+
+    def state(self):
+        q = np.zeros(self.model.nq); v = np.zeros(self.model.nv); t = np.zeros(1)
+        self.L.or_get_state(self.h, q.ctypes.data_as(C.POINTER(C.c_double)), v.ctypes.data_as(C.POINTER(C.c_double)),
+                            t.ctypes.data_as(C.POINTER(C.c_double)))
+        return q, v, float(t[0])
+
+    def set_state(self, q, v):
+        q = np.ascontiguousarray(q, dtype=np.float64); v = np.ascontiguousarray(v, dtype=np.float64)
+        self.L.or_set_state(self.h, q.ctypes.data_as(C.POINTER(C.c_double)), v.ctypes.data_as(C.POINTER(C.c_double)))
+
+    def target(self):
+        e = np.zeros(4); es = np.zeros(3, dtype=np.int32); ns = np.zeros(3, dtype=np.int32); b = np.zeros(3)
+        self.L.or_get_target(self.h, e.ctypes.data_as(C.POINTER(C.c_double)), es.ctypes.data_as(C.POINTER(C.c_int32)),
+                             ns.ctypes.data_as(C.POINTER(C.c_int32)), b.ctypes.data_as(C.POINTER(C.c_double)))
+        return e, es, ns, b
+
+    def event_rows(self):
+        from gmx import BINARY_EVENTS, LINEAR_EVENTS
+        W = len(BINARY_EVENTS) + len(LINEAR_EVENTS)
+        rows = np.zeros(W, dtype=np.int32); absc = np.zeros(W, dtype=np.int32); lv = np.zeros(W, dtype=np.float32)
+        self.L.or_get_event_rows(self.h, rows.ctypes.data_as(C.POINTER(C.c_int32)),
+                                 absc.ctypes.data_as(C.POINTER(C.c_int32)), lv.ctypes.data_as(C.POINTER(C.c_float)))
+        return rows, absc, lv
+
+    def eq(self):
+        q = np.zeros(self.model.nq)
+        self.L.or_get_eq(self.h, q.ctypes.data_as(C.POINTER(C.c_double)))
+        return q
+
+    def overflow(self):
+        return int(self.L.or_overflow(self.h))
+
+    def debug_substep(self):
+        n = C.c_int32()
+        con = np.zeros((15, 16), dtype=np.float32)
+        f = np.zeros(64, dtype=np.float32)
+        qacc = np.zeros(self.model.nv)
+        self.L.or_debug_substep(self.h, C.byref(n), con.ctypes.data_as(C.POINTER(C.c_float)),
+                                f.ctypes.data_as(C.POINTER(C.c_float)), qacc.ctypes.data_as(C.POINTER(C.c_double)))
+        return n.value, con, f, qacc
+
+
+def gauge_reading(model, finger_q):
+    q = np.ascontiguousarray(finger_q, dtype=np.float64)
+    return float(lib().or_gauge_reading(model.ptr, q.ctypes.data_as(C.POINTER(C.c_double))))
+
+
+def grip_step_sequence(cmds):
+    cmds = np.ascontiguousarray(cmds, dtype=np.float64).reshape(-1, 4)
+    out = np.zeros((len(cmds), 15))
+    lib().or_grip_step_sequence(cmds.ctypes.data_as(C.POINTER(C.c_double)), len(cmds),
+                                out.ctypes.data_as(C.POINTER(C.c_double)))
+    return out
+
+
+def sample(mode, recent_first, prev_steps, rps):
+    w = _f32(recent_first)
+    out = np.zeros(64, dtype=np.float32)
+    n = lib().or_sample(mode, w.ctypes.data_as(C.POINTER(C.c_float)), len(w), prev_steps, rps,
+                        out.ctypes.data_as(C.POINTER(C.c_float)))
+    return out[:n]
+
+
+def canonical_floats(seed, n):
+    s = C.c_uint32(seed)
+    return np.array([lib().or_minstd_next_canonical_float(C.byref(s)) for _ in range(n)])
+
+
+def bench(model, cfg, objects, n_envs, n_steps, seed=1234, n_threads=1):
+    return float(lib().or_bench(model.ptr, cfg.ptr, C.cast(objects, C.c_void_p), len(objects), n_envs, n_steps,
+                                seed, n_threads))

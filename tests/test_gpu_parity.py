@@ -1,0 +1,129 @@
+"""GPU parity: the HIP env-step path (through the C ABI) against the fp64 oracle.
+
+Tolerances: observations max rel-err <= 1e-4 over entries with
+|ref| >= 1e-3 and abs-err <= 1e-4 elsewhere; stepper step counts, event rows and
+done flags bit-exact.  fp32 device physics vs fp64 oracle diverges chaotically
+once contacts slip, so contact-rich comparisons are short-horizon (single
+substep / single env-step from an identical state); contact-free rollouts are
+compared over whole episodes.
+"""
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+OBS_RTOL = 1e-4
+OBS_ATOL = 1e-4
+
+
+def obs_close(a, b, rtol=OBS_RTOL, atol=OBS_ATOL):
+    a = np.asarray(a, dtype=np.float64); b = np.asarray(b, dtype=np.float64)
+    big = np.abs(b) >= 1e-3
+    err_rel = np.abs(a - b)[big] / np.abs(b)[big] if big.any() else np.zeros(1)
+    err_abs = np.abs(a - b)[~big] if (~big).any() else np.zeros(1)
+    return bool(err_rel.max() <= rtol and err_abs.max() <= atol), float(err_rel.max()), float(err_abs.max())
+
+
+@pytest.fixture(scope="module")
+def setup(gm):
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import oracle_lib
+    return gm, oracle_lib
+
+
+def make_pair(gm, oracle_lib, n_envs=4, object_set="set1_synthetic", spawn=None, seed=5):
+    settings = gm.canonical_settings(noise=False, seed=seed)
+    env = gm.BatchedGripperEnv(n_envs, object_set=object_set, settings=settings, seed=seed)
+    sp = env.make_spawn(**(spawn or {}))
+    env.reset(spawn=sp)
+    oracles = []
+    for e in range(n_envs):
+        o = oracle_lib.OracleEnv(env.model, env.cfg, env.objects, env_id=e)
+        o.reset(sp[e])
+        oracles.append(o)
+    return env, oracles, sp
+
+
+def test_gpu_reset_matches_oracle(setup):
+    gm, ol = setup
+    env, ors, _ = make_pair(gm, ol, n_envs=3)
+    q, v, t = env.state()
+    for e, o in enumerate(ors):
+        qo, vo, to = o.state()
+        np.testing.assert_allclose(q[e], qo, rtol=0, atol=2e-6)
+        assert t[e] == to == 0.0
+    obs = env.observation()
+    for e, o in enumerate(ors):
+        np.testing.assert_array_equal(obs[e], o.observation())
+
+
+def test_single_substep_parity(setup):
+    gm, ol = setup
+    env, ors, _ = make_pair(gm, ol, n_envs=3, spawn={"x": 0.0, "y": 0.0})
+    q, v, _ = env.state()
+    for e, o in enumerate(ors):
+        o.set_state(q[e].astype(np.float64), v[e].astype(np.float64))
+    ncon, con, f, qacc = env.debug_substep()
+    for e, o in enumerate(ors):
+        n_o, con_o, f_o, qacc_o = o.debug_substep()
+        assert ncon[e] == n_o
+        # contact pair indexing bit-exact; geometry to fp32 tolerance
+        np.testing.assert_array_equal(con[e, :n_o, 13:15], con_o[:n_o, 13:15])
+        np.testing.assert_allclose(con[e, :n_o, 0:13], con_o[:n_o, 0:13], rtol=1e-3, atol=2e-6)
+        np.testing.assert_allclose(qacc[e, :env.model.nv], qacc_o, rtol=2e-3, atol=2e-3 * np.abs(qacc_o).max())
+
+
+def test_contact_free_rollout_parity(setup):
+    """object spawned away from the gripper: whole-episode obs / target / event parity"""
+    gm, ol = setup
+    env, ors, _ = make_pair(gm, ol, n_envs=2, spawn={"x": 0.06, "y": 0.06})
+    rng = np.random.default_rng(1234)
+    for t in range(30):
+        a = rng.uniform(-1, 1, size=(env.n_envs, env.n_actions)).astype(np.float32)
+        obs, rew, term, trunc = env.step(a)
+        te, tes, tns, tb = env.target()
+        rows, absc, lv = env.event_rows()
+        for e, o in enumerate(ors):
+            obs_o, r_o, d_o = o.step(a[e])
+            ok, er, ea = obs_close(obs[e], obs_o)
+            assert ok, (t, e, er, ea, obs[e], obs_o)
+            oe, oes, ons, ob = o.target()
+            np.testing.assert_array_equal(tes[e], oes)
+            np.testing.assert_array_equal(tns[e], ons)
+            rows_o, abs_o, _ = o.event_rows()
+            np.testing.assert_array_equal(rows[e], rows_o)
+            assert bool(term[e]) == d_o
+            assert abs(rew[e] - r_o) <= 1e-5 + 1e-4 * abs(r_o)
+
+
+def test_contact_rich_one_step_parity(setup):
+    """object under the gripper: one env-step (63 substeps) from the identical state"""
+    gm, ol = setup
+    env, ors, _ = make_pair(gm, ol, n_envs=3, spawn={"x": 0.0, "y": 0.0})
+    a = np.array([[1.0, 0.0, 1.0, 0.5]] * env.n_envs, dtype=np.float32)
+    obs, rew, term, trunc = env.step(a)
+    for e, o in enumerate(ors):
+        obs_o, r_o, d_o = o.step(a[e])
+        ok, er, ea = obs_close(obs[e], obs_o, rtol=1e-3, atol=1e-3)
+        assert ok, (e, er, ea)
+
+
+def test_large_batch_finite_and_deterministic(setup):
+    gm, ol = setup
+    settings = gm.canonical_settings(noise=True, seed=3)
+    env = gm.BatchedGripperEnv(1024, object_set="set6_synthetic", settings=settings, seed=3)
+    env.reset()
+    rng = np.random.default_rng(0)
+    acts = rng.uniform(-1, 1, size=(5, env.n_envs, env.n_actions)).astype(np.float32)
+    outs = []
+    for a in acts:
+        outs.append(env.step(a)[0])
+    assert np.isfinite(np.stack(outs)).all()
+    env2 = gm.BatchedGripperEnv(1024, object_set="set6_synthetic", settings=gm.canonical_settings(noise=True, seed=3), seed=3)
+    env2.reset()
+    for a, o1 in zip(acts, outs):
+        o2 = env2.step(a)[0]
+        np.testing.assert_array_equal(o1, o2)

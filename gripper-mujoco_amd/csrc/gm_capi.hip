@@ -32,7 +32,7 @@ struct gm_ctx {
   gm_config* d_cfg = nullptr;
   GmTopo* d_topo = nullptr;
   gm_object* d_objs = nullptr;
-  float* d_eq = nullptr;
+  double* d_eq = nullptr;
   float* d_obs = nullptr;
   float* d_rew = nullptr;
   uint8_t* d_done = nullptr;
@@ -136,7 +136,7 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   HIPCHK(c, hipMalloc(&c->d_cfg, sizeof(gm_config)));
   HIPCHK(c, hipMalloc(&c->d_topo, sizeof(GmTopo)));
   HIPCHK(c, hipMalloc(&c->d_objs, sizeof(gm_object) * (size_t)n_objects));
-  HIPCHK(c, hipMalloc(&c->d_eq, sizeof(float) * GM_MAX_QPOS));
+  HIPCHK(c, hipMalloc(&c->d_eq, sizeof(double) * GM_MAX_QPOS));
   HIPCHK(c, hipMalloc(&c->d_obs, sizeof(float) * (size_t)n_envs * (cfg->n_obs > 0 ? cfg->n_obs : 1)));
   HIPCHK(c, hipMalloc(&c->d_rew, sizeof(float) * (size_t)n_envs));
   HIPCHK(c, hipMalloc(&c->d_done, (size_t)n_envs));
@@ -158,7 +158,7 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   hipLaunchKernelGGL(gm_step_kernel, dim3(1), dim3(NT), 0, c->stream, c->d_state, c->d_model, c->d_cfg, c->d_topo,
                      c->d_obs, c->d_rew, c->d_done, 1, 1, dbg);
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(c->d_eq, reinterpret_cast<char*>(c->d_state) + offsetof(GmEnvState, qpos), sizeof(float) * GM_MAX_QPOS, hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_eq, reinterpret_cast<char*>(c->d_state) + offsetof(GmEnvState, qpos), sizeof(double) * GM_MAX_QPOS, hipMemcpyDeviceToDevice, c->stream));
   int threads = 256, blocks = (n_envs + threads - 1) / threads;
   hipLaunchKernelGGL(gm_init_envs_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, cfg->s.random_seed,
                      (long long)env_offset, n_envs);
@@ -319,8 +319,8 @@ int gm_get_state(gm_ctx* c, float* qpos, float* qvel, double* time) {
   int rc = fetch_states(c, h);
   if (rc) return rc;
   for (int e = 0; e < c->n_envs; e++) {
-    if (qpos) std::memcpy(qpos + (size_t)e * c->model.nq, h[e].qpos, sizeof(float) * c->model.nq);
-    if (qvel) std::memcpy(qvel + (size_t)e * c->model.nv, h[e].qvel, sizeof(float) * c->model.nv);
+    if (qpos) for (int i = 0; i < c->model.nq; i++) qpos[(size_t)e * c->model.nq + i] = (float)h[e].qpos[i];
+    if (qvel) for (int i = 0; i < c->model.nv; i++) qvel[(size_t)e * c->model.nv + i] = (float)h[e].qvel[i];
     if (time) time[e] = h[e].time;
   }
   return GM_OK;
@@ -332,8 +332,8 @@ int gm_set_state(gm_ctx* c, const float* qpos, const float* qvel) {
   int rc = fetch_states(c, h);
   if (rc) return rc;
   for (int e = 0; e < c->n_envs; e++) {
-    if (qpos) std::memcpy(h[e].qpos, qpos + (size_t)e * c->model.nq, sizeof(float) * c->model.nq);
-    if (qvel) std::memcpy(h[e].qvel, qvel + (size_t)e * c->model.nv, sizeof(float) * c->model.nv);
+    if (qpos) for (int i = 0; i < c->model.nq; i++) h[e].qpos[i] = qpos[(size_t)e * c->model.nq + i];
+    if (qvel) for (int i = 0; i < c->model.nv; i++) h[e].qvel[i] = qvel[(size_t)e * c->model.nv + i];
   }
   HIPCHK(c, hipMemcpyAsync(c->d_state, h.data(), sizeof(GmEnvState) * (size_t)c->n_envs, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

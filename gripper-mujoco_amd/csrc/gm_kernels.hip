@@ -30,6 +30,10 @@
 #define CW 20   // compact row: obj[6], base, chain[CLMAX], group (as float bits)
 #define PI_F 3.14159265358979f
 
+// `real` is the dynamics type: fp64, MuJoCo's mjtNum.  Collision geometry and the
+// PGS inner loop run in fp32 (see DESIGN.md "Precision").
+typedef double real;
+
 struct DebugOut {
   int32_t* ncon;      // [n_envs]
   float* contact;     // [n_envs][GM_MAX_CON][16]
@@ -39,21 +43,21 @@ struct DebugOut {
 
 struct __align__(16) Shared {
   GmEnvState s;
-  float qpos_pre[GM_MAX_QPOS];
-  float qacc_s[GM_MAX_DOF], qacc[GM_MAX_DOF], frc[GM_MAX_DOF], z[GM_MAX_DOF];
-  float xpos[GM_MAX_BODY][3];
-  float xmat[GM_MAX_BODY][9];
-  float cinert[GM_MAX_BODY][10];
-  float Ic[GM_MAX_BODY][10];
-  float cfrc[GM_MAX_BODY][6];
-  float cdof[GM_MAX_DOF][6];
+  real qpos_pre[GM_MAX_QPOS];
+  real qacc_s[GM_MAX_DOF], qacc[GM_MAX_DOF], frc[GM_MAX_DOF], z[GM_MAX_DOF];
+  real xpos[GM_MAX_BODY][3];
+  real xmat[GM_MAX_BODY][9];
+  real cinert[GM_MAX_BODY][10];
+  real Ic[GM_MAX_BODY][10];
+  real cfrc[GM_MAX_BODY][6];
+  real cdof[GM_MAX_DOF][6];
   float gxpos[GM_MAX_GEOM][3];
   float gxmat[GM_MAX_GEOM][9];
-  float Hf[3][TRIF], Hp[3], Ho[21], Hbb;
-  float Df[3][CLMAX + 1], Dp[2], Do[6], Dbb;
-  float bdelta[5];
+  real Hf[3][TRIF], Hp[3], Ho[21], Hbb;
+  real Df[3][CLMAX + 1], Dp[2], Do[6], Dbb;
+  real bdelta[5];
   float con[GM_MAX_CON][20];   // dist, pos3, frame9, mu, force3, g1, g2, (pad)
-  float Y[GM_MAX_EFC][CW];
+  real Y[GM_MAX_EFC][CW];
   float efc_f[GM_MAX_EFC];
   int32_t cnt[NT];
   int32_t ncon, nefc, nlockrows, overflow;
@@ -63,70 +67,71 @@ struct __align__(16) Shared {
 };
 
 // ------------------------------------------------------------ small math
-__device__ __forceinline__ float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-__device__ __forceinline__ void cross3(float* r, const float* a, const float* b) {
-  float t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+template <typename T> __device__ __forceinline__ T dot3(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+template <typename T> __device__ __forceinline__ void cross3(T* r, const T* a, const T* b) {
+  T t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
   r[0] = t0; r[1] = t1; r[2] = t2;
 }
-__device__ __forceinline__ void mulmv3(float* r, const float* M, const float* v) {
-  float t0 = M[0] * v[0] + M[1] * v[1] + M[2] * v[2];
-  float t1 = M[3] * v[0] + M[4] * v[1] + M[5] * v[2];
-  float t2 = M[6] * v[0] + M[7] * v[1] + M[8] * v[2];
+template <typename T> __device__ __forceinline__ void mulmv3(T* r, const T* M, const T* v) {
+  T t0 = M[0] * v[0] + M[1] * v[1] + M[2] * v[2];
+  T t1 = M[3] * v[0] + M[4] * v[1] + M[5] * v[2];
+  T t2 = M[6] * v[0] + M[7] * v[1] + M[8] * v[2];
   r[0] = t0; r[1] = t1; r[2] = t2;
 }
-__device__ __forceinline__ void mulmtv3(float* r, const float* M, const float* v) {
-  float t0 = M[0] * v[0] + M[3] * v[1] + M[6] * v[2];
-  float t1 = M[1] * v[0] + M[4] * v[1] + M[7] * v[2];
-  float t2 = M[2] * v[0] + M[5] * v[1] + M[8] * v[2];
+template <typename T> __device__ __forceinline__ void mulmtv3(T* r, const T* M, const T* v) {
+  T t0 = M[0] * v[0] + M[3] * v[1] + M[6] * v[2];
+  T t1 = M[1] * v[0] + M[4] * v[1] + M[7] * v[2];
+  T t2 = M[2] * v[0] + M[5] * v[1] + M[8] * v[2];
   r[0] = t0; r[1] = t1; r[2] = t2;
 }
-__device__ __forceinline__ void quat2mat(float* R, const float* q) {
-  float w = q[0], x = q[1], y = q[2], z = q[3];
+template <typename T> __device__ __forceinline__ void quat2mat(T* R, const T* q) {
+  T w = q[0], x = q[1], y = q[2], z = q[3];
   R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z);     R[2] = 2 * (x * z + w * y);
   R[3] = 2 * (x * y + w * z);     R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
   R[6] = 2 * (x * z - w * y);     R[7] = 2 * (y * z + w * x);     R[8] = 1 - 2 * (x * x + y * y);
 }
-__device__ __forceinline__ void quatmul(float* r, const float* a, const float* b) {
-  float t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
-  float t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
-  float t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
-  float t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+template <typename T> __device__ __forceinline__ void quatmul(T* r, const T* a, const T* b) {
+  T t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  T t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  T t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  T t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
   r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
 }
-__device__ __forceinline__ void quatnorm(float* q) {
-  float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-  if (n < 1e-15f) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
-  float in = 1.0f / n;
-  for (int i = 0; i < 4; i++) q[i] *= in;
+__device__ __forceinline__ void quatnorm(real* q) {
+  real n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < 1e-15) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  for (int i = 0; i < 4; i++) q[i] /= n;
 }
 __device__ __forceinline__ void ld3(float* r, const double* a) { r[0] = (float)a[0]; r[1] = (float)a[1]; r[2] = (float)a[2]; }
+__device__ __forceinline__ void ld3(double* r, const double* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
+__device__ __forceinline__ void ld4(double* r, const double* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3]; }
 __device__ __forceinline__ void ld4(float* r, const double* a) { r[0] = (float)a[0]; r[1] = (float)a[1]; r[2] = (float)a[2]; r[3] = (float)a[3]; }
 
 // spatial inertia (I_O sym6, h = m c, m) times motion [w; v]
-__device__ __forceinline__ void inert_mul(float* r, const float* ci, const float* v) {
-  const float* w = v; const float* u = v + 3;
-  float Iw0 = ci[0] * w[0] + ci[3] * w[1] + ci[4] * w[2];
-  float Iw1 = ci[3] * w[0] + ci[1] * w[1] + ci[5] * w[2];
-  float Iw2 = ci[4] * w[0] + ci[5] * w[1] + ci[2] * w[2];
-  float hxu[3], hxw[3];
+__device__ __forceinline__ void inert_mul(real* r, const real* ci, const real* v) {
+  const real* w = v; const real* u = v + 3;
+  real Iw0 = ci[0] * w[0] + ci[3] * w[1] + ci[4] * w[2];
+  real Iw1 = ci[3] * w[0] + ci[1] * w[1] + ci[5] * w[2];
+  real Iw2 = ci[4] * w[0] + ci[5] * w[1] + ci[2] * w[2];
+  real hxu[3], hxw[3];
   cross3(hxu, ci + 6, u);
   cross3(hxw, ci + 6, w);
   r[0] = Iw0 + hxu[0]; r[1] = Iw1 + hxu[1]; r[2] = Iw2 + hxu[2];
   r[3] = ci[9] * u[0] - hxw[0]; r[4] = ci[9] * u[1] - hxw[1]; r[5] = ci[9] * u[2] - hxw[2];
 }
-__device__ __forceinline__ void cross_motion(float* r, const float* v, const float* mv) {
-  float a[3], b[3], c[3];
+__device__ __forceinline__ void cross_motion(real* r, const real* v, const real* mv) {
+  real a[3], b[3], c[3];
   cross3(a, v, mv); cross3(b, v, mv + 3); cross3(c, v + 3, mv);
   r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
   r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
 }
-__device__ __forceinline__ void cross_force(float* r, const float* v, const float* f) {
-  float a[3], b[3], c[3];
+__device__ __forceinline__ void cross_force(real* r, const real* v, const real* f) {
+  real a[3], b[3], c[3];
   cross3(a, v, f); cross3(b, v + 3, f + 3); cross3(c, v, f + 3);
   r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
   r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
 }
-__device__ __forceinline__ float dot6(const float* a, const float* b) {
+__device__ __forceinline__ real dot6(const real* a, const real* b) {
   return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
 }
 
@@ -144,7 +149,7 @@ __device__ __forceinline__ int chain_dof(const GmTopo* T, int c, int p) {
   return T->dof_obj + p;   // object uses positions 0..5
 }
 // H/L storage accessor: chain c, positions p >= q (object: 0..5, others: 0 = base)
-__device__ __forceinline__ float& Hat(Shared& S, int c, int p, int q) {
+__device__ __forceinline__ real& Hat(Shared& S, int c, int p, int q) {
   if (c < 3) return (p == 0) ? S.Hbb : S.Hf[c][TRI(p, q)];
   if (c == 3) return (p == 0) ? S.Hbb : S.Hp[TRI(p, q)];
   return S.Ho[TRI(p, q)];
@@ -152,31 +157,31 @@ __device__ __forceinline__ float& Hat(Shared& S, int c, int p, int q) {
 
 // ============================================================ kinematics
 // mj_kinematics restatement (oracle.c: fk), one lane per chain.
-__device__ void body_fk(Shared& S, const gm_model* __restrict__ m, int b, const float* ppos,
-                        const float* pquat, float* quat_out) {
-  float bp[3], bq[4], t[3], q[4];
+__device__ void body_fk(Shared& S, const gm_model* __restrict__ m, int b, const real* ppos,
+                        const real* pquat, real* quat_out) {
+  real bp[3], bq[4], t[3], q[4];
   ld3(bp, m->body_pos[b]);
   ld4(bq, m->body_quat[b]);
-  float Rp[9];
+  real Rp[9];
   quat2mat(Rp, pquat);
   mulmv3(t, Rp, bp);
-  float xp[3] = {ppos[0] + t[0], ppos[1] + t[1], ppos[2] + t[2]};
+  real xp[3] = {ppos[0] + t[0], ppos[1] + t[1], ppos[2] + t[2]};
   quatmul(q, pquat, bq);
   int j = m->body_jnt[b];
   if (j >= 0) {
     int qa = m->jnt_qposadr[j];
     int type = m->jnt_type[j];
     if (type == GM_JNT_SLIDE) {
-      float R[9], ax[3], wa[3];
+      real R[9], ax[3], wa[3];
       quat2mat(R, q);
       ld3(ax, m->jnt_axis[j]);
       mulmv3(wa, R, ax);
-      float qv = S.s.qpos[qa];
+      real qv = S.s.qpos[qa];
       xp[0] += wa[0] * qv; xp[1] += wa[1] * qv; xp[2] += wa[2] * qv;
     } else if (type == GM_JNT_HINGE) {
-      float ang = S.s.qpos[qa];
-      float sn = sinf(0.5f * ang), cs = cosf(0.5f * ang);
-      float ql[4] = {cs, (float)m->jnt_axis[j][0] * sn, (float)m->jnt_axis[j][1] * sn, (float)m->jnt_axis[j][2] * sn};
+      real ang = S.s.qpos[qa];
+      real sn = sin(0.5 * ang), cs = cos(0.5 * ang);
+      real ql[4] = {cs, (real)m->jnt_axis[j][0] * sn, (real)m->jnt_axis[j][1] * sn, (real)m->jnt_axis[j][2] * sn};
       quatmul(q, q, ql);
     } else {
       xp[0] = S.s.qpos[qa]; xp[1] = S.s.qpos[qa + 1]; xp[2] = S.s.qpos[qa + 2];
@@ -185,27 +190,27 @@ __device__ void body_fk(Shared& S, const gm_model* __restrict__ m, int b, const 
   }
   quatnorm(q);
   S.xpos[b][0] = xp[0]; S.xpos[b][1] = xp[1]; S.xpos[b][2] = xp[2];
-  float R[9];
+  real R[9];
   quat2mat(R, q);
   for (int k = 0; k < 9; k++) S.xmat[b][k] = R[k];
   for (int k = 0; k < 4; k++) quat_out[k] = q[k];
   // world-origin spatial inertia
-  float ip[3], c[3];
+  real ip[3], c[3];
   ld3(ip, m->body_ipos[b]);
   mulmv3(c, R, ip);
   c[0] += xp[0]; c[1] += xp[1]; c[2] += xp[2];
-  float I[3] = {(float)m->body_inertia[b][0], (float)m->body_inertia[b][1], (float)m->body_inertia[b][2]};
-  float mass = (float)m->body_mass[b];
+  real I[3] = {(real)m->body_inertia[b][0], (real)m->body_inertia[b][1], (real)m->body_inertia[b][2]};
+  real mass = (real)m->body_mass[b];
   if (b == m->body_obj) {
     mass = S.s.obj_mass;
     I[0] = S.s.obj_inertia[0]; I[1] = S.s.obj_inertia[1]; I[2] = S.s.obj_inertia[2];
   }
-  float Iw[9];
+  real Iw[9];
   for (int i = 0; i < 3; i++)
     for (int k = 0; k < 3; k++)
       Iw[3 * i + k] = R[3 * i] * I[0] * R[3 * k] + R[3 * i + 1] * I[1] * R[3 * k + 1] + R[3 * i + 2] * I[2] * R[3 * k + 2];
-  float cc = dot3(c, c);
-  float* ci = S.cinert[b];
+  real cc = dot3(c, c);
+  real* ci = S.cinert[b];
   ci[0] = Iw[0] + mass * (cc - c[0] * c[0]);
   ci[1] = Iw[4] + mass * (cc - c[1] * c[1]);
   ci[2] = Iw[8] + mass * (cc - c[2] * c[2]);
@@ -220,20 +225,20 @@ __device__ void body_fk(Shared& S, const gm_model* __restrict__ m, int b, const 
     int type = m->jnt_type[j];
     if (type == GM_JNT_FREE) {
       for (int k = 0; k < 3; k++) {
-        float* cd = S.cdof[d0 + k];
+        real* cd = S.cdof[d0 + k];
         cd[0] = cd[1] = cd[2] = 0; cd[3] = cd[4] = cd[5] = 0; cd[3 + k] = 1;
       }
       for (int k = 0; k < 3; k++) {
-        float* cd = S.cdof[d0 + 3 + k];
-        float w[3] = {R[k], R[3 + k], R[6 + k]};
+        real* cd = S.cdof[d0 + 3 + k];
+        real w[3] = {R[k], R[3 + k], R[6 + k]};
         cd[0] = w[0]; cd[1] = w[1]; cd[2] = w[2];
         cross3(cd + 3, xp, w);
       }
     } else {
-      float ax[3], wa[3];
+      real ax[3], wa[3];
       ld3(ax, m->jnt_axis[j]);
       mulmv3(wa, R, ax);
-      float* cd = S.cdof[d0];
+      real* cd = S.cdof[d0];
       if (type == GM_JNT_SLIDE) {
         cd[0] = cd[1] = cd[2] = 0; cd[3] = wa[0]; cd[4] = wa[1]; cd[5] = wa[2];
       } else {
@@ -246,20 +251,20 @@ __device__ void body_fk(Shared& S, const gm_model* __restrict__ m, int b, const 
 
 __device__ void kinematics(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
   // base body (world child) first, then one lane per chain (fingers 0..2, palm 3, object 4)
-  __shared__ float base_quat[4];
+  __shared__ real base_quat[4];
   if (lane == 0) {
-    float q0[4] = {1, 0, 0, 0}, p0[3] = {0, 0, 0};
+    real q0[4] = {1, 0, 0, 0}, p0[3] = {0, 0, 0};
     body_fk(S, m, T->body_base, p0, q0, base_quat);
   }
   __syncthreads();
   if (lane < 5) {
-    float q[4];
+    real q[4];
     if (lane == 4) {
-      float q0[4] = {1, 0, 0, 0}, p0[3] = {0, 0, 0};
+      real q0[4] = {1, 0, 0, 0}, p0[3] = {0, 0, 0};
       body_fk(S, m, T->body_obj, p0, q0, q);
     } else {
-      float pq[4] = {base_quat[0], base_quat[1], base_quat[2], base_quat[3]};
-      float pp[3] = {S.xpos[T->body_base][0], S.xpos[T->body_base][1], S.xpos[T->body_base][2]};
+      real pq[4] = {base_quat[0], base_quat[1], base_quat[2], base_quat[3]};
+      real pp[3] = {S.xpos[T->body_base][0], S.xpos[T->body_base][1], S.xpos[T->body_base][2]};
       int L = chain_len(T, lane);
       for (int p = 1; p <= L; p++) {
         int b = chain_body(T, lane, p);
@@ -274,16 +279,16 @@ __device__ void kinematics(Shared& S, const gm_model* __restrict__ m, const GmTo
   if (lane < T->ngeom) {
     int g = lane;
     int b = m->geom_body[g];
-    float R[9];
+    real R[9];
     if (b == 0) {
       R[0] = 1; R[1] = 0; R[2] = 0; R[3] = 0; R[4] = 1; R[5] = 0; R[6] = 0; R[7] = 0; R[8] = 1;
     } else {
       for (int k = 0; k < 9; k++) R[k] = S.xmat[b][k];
     }
-    float gp[3], t[3], gq[4], Rg[9];
+    real gp[3], t[3], gq[4], Rg[9];
     ld3(gp, m->geom_pos[g]);
     mulmv3(t, R, gp);
-    float bp0 = b == 0 ? 0.f : S.xpos[b][0], bp1 = b == 0 ? 0.f : S.xpos[b][1], bp2 = b == 0 ? 0.f : S.xpos[b][2];
+    real bp0 = b == 0 ? 0.f : S.xpos[b][0], bp1 = b == 0 ? 0.f : S.xpos[b][1], bp2 = b == 0 ? 0.f : S.xpos[b][2];
     S.gxpos[g][0] = bp0 + t[0]; S.gxpos[g][1] = bp1 + t[1]; S.gxpos[g][2] = bp2 + t[2];
     ld4(gq, m->geom_quat[g]);
     quat2mat(Rg, gq);
@@ -300,18 +305,18 @@ __device__ void crb_rne(Shared& S, const gm_model* __restrict__ m, const GmTopo*
     int c = lane;
     int L = chain_len(T, c);
     // forward: velocities and bias accelerations
-    float cvel[6], cacc[6];
+    real cvel[6], cacc[6];
     for (int k = 0; k < 6; k++) { cvel[k] = 0; cacc[k] = 0; }
-    cacc[3] = -(float)m->gravity[0]; cacc[4] = -(float)m->gravity[1]; cacc[5] = -(float)m->gravity[2];
+    cacc[3] = -(real)m->gravity[0]; cacc[4] = -(real)m->gravity[1]; cacc[5] = -(real)m->gravity[2];
     if (c < 4) {
       // base body
       int db = T->dof_base;
-      float cdd[6];
+      real cdd[6];
       cross_motion(cdd, cvel, S.cdof[db]);
-      float qd = S.s.qvel[db];
+      real qd = S.s.qvel[db];
       for (int k = 0; k < 6; k++) { cvel[k] += S.cdof[db][k] * qd; cacc[k] += cdd[k] * qd; }
       if (c == 0) {
-        float t1[6], t2[6], f[6];
+        real t1[6], t2[6], f[6];
         inert_mul(f, S.cinert[T->body_base], cacc);
         inert_mul(t1, S.cinert[T->body_base], cvel);
         cross_force(t2, cvel, t1);
@@ -319,11 +324,11 @@ __device__ void crb_rne(Shared& S, const gm_model* __restrict__ m, const GmTopo*
       }
       for (int p = 1; p <= L; p++) {
         int b = chain_body(T, c, p), d = chain_dof(T, c, p);
-        float cdd2[6];
+        real cdd2[6];
         cross_motion(cdd2, cvel, S.cdof[d]);
-        float qv = S.s.qvel[d];
+        real qv = S.s.qvel[d];
         for (int k = 0; k < 6; k++) { cvel[k] += S.cdof[d][k] * qv; cacc[k] += cdd2[k] * qv; }
-        float t1[6], t2[6], f[6];
+        real t1[6], t2[6], f[6];
         inert_mul(f, S.cinert[b], cacc);
         inert_mul(t1, S.cinert[b], cvel);
         cross_force(t2, cvel, t1);
@@ -343,20 +348,20 @@ __device__ void crb_rne(Shared& S, const gm_model* __restrict__ m, const GmTopo*
       // object: free joint on one body
       int b = T->body_obj, d0 = T->dof_obj;
       for (int k = 0; k < 3; k++) {
-        float qv = S.s.qvel[d0 + k];
+        real qv = S.s.qvel[d0 + k];
         for (int t = 0; t < 6; t++) cvel[t] += S.cdof[d0 + k][t] * qv;
       }
-      float cdd[3][6];
+      real cdd[3][6];
       for (int k = 0; k < 3; k++) cross_motion(cdd[k], cvel, S.cdof[d0 + 3 + k]);
       for (int k = 0; k < 3; k++) {
-        float qv = S.s.qvel[d0 + 3 + k];
+        real qv = S.s.qvel[d0 + 3 + k];
         for (int t = 0; t < 6; t++) cvel[t] += S.cdof[d0 + 3 + k][t] * qv;
       }
       for (int k = 0; k < 3; k++) {
-        float qv = S.s.qvel[d0 + 3 + k];
+        real qv = S.s.qvel[d0 + 3 + k];
         for (int t = 0; t < 6; t++) cacc[t] += cdd[k][t] * qv;
       }
-      float t1[6], t2[6], f[6];
+      real t1[6], t2[6], f[6];
       inert_mul(f, S.cinert[b], cacc);
       inert_mul(t1, S.cinert[b], cvel);
       cross_force(t2, cvel, t1);
@@ -368,7 +373,7 @@ __device__ void crb_rne(Shared& S, const gm_model* __restrict__ m, const GmTopo*
   // base body: add chain roots (fingers' intermediates and palm)
   if (lane == 0) {
     int bb = T->body_base;
-    float ic[10], f[6];
+    real ic[10], f[6];
     for (int k = 0; k < 10; k++) ic[k] = S.cinert[bb][k];
     for (int k = 0; k < 6; k++) f[k] = S.cfrc[bb][k];
     for (int c = 0; c < 4; c++) {
@@ -384,14 +389,14 @@ __device__ void crb_rne(Shared& S, const gm_model* __restrict__ m, const GmTopo*
 
 // ============================================================ mass matrix rows + forces
 __device__ __forceinline__ void ctrl_gains(const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int d,
-                                           float* kp, float* kd) {
+                                           real* kp, real* kd) {
   *kp = 0; *kd = 0;
   for (int f = 0; f < 3; f++) {
-    if (d == m->dof_pris[f]) { *kp = (float)m->kp_gripper[0]; *kd = (float)m->kd_gripper[0]; }
-    if (d == m->dof_rev[f]) { *kp = (float)m->kp_gripper[1]; *kd = (float)m->kd_gripper[1]; }
+    if (d == m->dof_pris[f]) { *kp = (real)m->kp_gripper[0]; *kd = (real)m->kd_gripper[0]; }
+    if (d == m->dof_rev[f]) { *kp = (real)m->kp_gripper[1]; *kd = (real)m->kd_gripper[1]; }
   }
-  if (d == m->dof_palm) { *kp = (float)m->kp_gripper[2]; *kd = (float)m->kd_gripper[2]; }
-  if (d == m->dof_base) { *kp = (float)m->kp_base[2]; *kd = (float)m->kd_base[2]; }
+  if (d == m->dof_palm) { *kp = (real)m->kp_gripper[2]; *kd = (real)m->kd_gripper[2]; }
+  if (d == m->dof_base) { *kp = (real)m->kp_base[2]; *kd = (real)m->kd_base[2]; }
 }
 
 // lane per dof: H row entries (compact), bias/passive/actuator force
@@ -399,21 +404,21 @@ __device__ void mass_and_forces(Shared& S, const gm_model* __restrict__ m, const
   if (lane < T->nv) {
     int d = lane;
     int b = m->dof_body[d];
-    float F[6];
+    real F[6];
     inert_mul(F, S.Ic[b], S.cdof[d]);
-    float h = (float)m->timestep;
+    real h = (real)m->timestep;
     int j = m->body_jnt[b];
-    float kp, kd;
+    real kp, kd;
     ctrl_gains(m, T, d, &kp, &kd);
-    float add = (float)m->jnt_armature[j] + h * ((float)m->jnt_damping[j] + kd);
-    if (m->jnt_type[j] != GM_JNT_FREE) add += h * h * ((float)m->jnt_stiffness[j] + kp);
+    real add = (real)m->jnt_armature[j] + h * ((real)m->jnt_damping[j] + kd);
+    if (m->jnt_type[j] != GM_JNT_FREE) add += h * h * ((real)m->jnt_stiffness[j] + kp);
     int c = T->body_group[b];          // 0..2 finger, 3 palm, 5 object, 4 base
     if (c == GM_GRP_BASE) {
       S.Hbb = dot6(S.cdof[d], F) + add;
     } else if (c == GM_GRP_OBJECT) {
       int p = d - T->dof_obj;
       for (int q = 0; q <= p; q++) {
-        float v = dot6(S.cdof[T->dof_obj + q], F);
+        real v = dot6(S.cdof[T->dof_obj + q], F);
         if (q == p) v += add;
         S.Ho[TRI(p, q)] = v;
       }
@@ -421,24 +426,24 @@ __device__ void mass_and_forces(Shared& S, const gm_model* __restrict__ m, const
       int p = T->body_cpos[b];
       for (int q = 0; q <= p; q++) {
         int dq = (q == 0) ? T->dof_base : chain_dof(T, c, q);
-        float v = dot6(S.cdof[dq], F);
+        real v = dot6(S.cdof[dq], F);
         if (q == p) v += add;
         if (c < 3) S.Hf[c][TRI(p, q)] = v; else S.Hp[TRI(p, q)] = v;
       }
     }
     // forces: passive springs/damping, PD control (target_.next, base target), RNE bias
-    float bias = dot6(S.cdof[d], S.cfrc[b]);
-    float pas = 0;
-    if (m->jnt_type[j] != GM_JNT_FREE) pas -= (float)m->jnt_stiffness[j] * S.s.qpos[d];
-    pas -= (float)m->jnt_damping[j] * S.s.qvel[d];
-    float act = 0;
-    float q = S.s.qpos[d], v = S.s.qvel[d];
+    real bias = dot6(S.cdof[d], S.cfrc[b]);
+    real pas = 0;
+    if (m->jnt_type[j] != GM_JNT_FREE) pas -= (real)m->jnt_stiffness[j] * S.s.qpos[d];
+    pas -= (real)m->jnt_damping[j] * S.s.qvel[d];
+    real act = 0;
+    real q = S.s.qpos[d], v = S.s.qvel[d];
     for (int f = 0; f < 3; f++) {
-      if (d == m->dof_pris[f]) act = -((q - (float)S.s.next.x) * kp + v * kd);
-      if (d == m->dof_rev[f]) act = -((q - (float)S.s.next.th) * kp + v * kd);
+      if (d == m->dof_pris[f]) act = -((q - (real)S.s.next.x) * kp + v * kd);
+      if (d == m->dof_rev[f]) act = -((q - (real)S.s.next.th) * kp + v * kd);
     }
-    if (d == m->dof_palm) act = -((q - (float)S.s.next.z) * kp + v * kd);
-    if (d == m->dof_base) act = -((q - (float)S.s.base[2]) * kp + v * kd);
+    if (d == m->dof_palm) act = -((q - (real)S.s.next.z) * kp + v * kd);
+    if (d == m->dof_base) act = -((q - (real)S.s.base[2]) * kp + v * kd);
     S.frc[d] = pas + act - bias;
   }
   __syncthreads();
@@ -449,26 +454,26 @@ __device__ void factor(Shared& S, const GmTopo* __restrict__ T, int lane) {
   if (lane < 5) {
     int c = lane;
     int L = chain_len(T, c);
-    float delta = 0;
+    real delta = 0;
     if (c < 4) {
       for (int k = L; k >= 1; k--) {
-        float hk = Hat(S, c, k, k);
+        real hk = Hat(S, c, k, k);
         for (int i = k - 1; i >= 0; i--) {
-          float a = Hat(S, c, k, i) / hk;
+          real a = Hat(S, c, k, i) / hk;
           for (int jj = i; jj >= 0; jj--) {
-            float v = Hat(S, c, k, jj) * a;
+            real v = Hat(S, c, k, jj) * a;
             if (i == 0 && jj == 0) delta += v; else Hat(S, c, i, jj) -= v;
           }
           Hat(S, c, k, i) = a;
         }
       }
       S.bdelta[c] = delta;
-      for (int p = 1; p <= L; p++) { float dv = Hat(S, c, p, p); if (c < 3) S.Df[c][p] = dv; else S.Dp[p] = dv; }
+      for (int p = 1; p <= L; p++) { real dv = Hat(S, c, p, p); if (c < 3) S.Df[c][p] = dv; else S.Dp[p] = dv; }
     } else {
       for (int k = 5; k >= 1; k--) {
-        float hk = S.Ho[TRI(k, k)];
+        real hk = S.Ho[TRI(k, k)];
         for (int i = k - 1; i >= 0; i--) {
-          float a = S.Ho[TRI(k, i)] / hk;
+          real a = S.Ho[TRI(k, i)] / hk;
           for (int jj = i; jj >= 0; jj--) S.Ho[TRI(i, jj)] -= S.Ho[TRI(k, jj)] * a;
           S.Ho[TRI(k, i)] = a;
         }
@@ -481,17 +486,17 @@ __device__ void factor(Shared& S, const GmTopo* __restrict__ T, int lane) {
   __syncthreads();
 }
 
-__device__ __forceinline__ float Dof(Shared& S, int c, int p) {
+__device__ __forceinline__ real Dof(Shared& S, int c, int p) {
   if (c < 3) return p == 0 ? S.Dbb : S.Df[c][p];
   if (c == 3) return p == 0 ? S.Dbb : S.Dp[p];
   return S.Do[p];
 }
 
 // x = H^-1 b over full dof vectors (b, x in LDS, may alias)
-__device__ void solve_full(Shared& S, const GmTopo* __restrict__ T, const float* b, float* x, int lane) {
+__device__ void solve_full(Shared& S, const GmTopo* __restrict__ T, const real* b, real* x, int lane) {
   // L^T y = b  (leaves -> root); chain lanes, base accumulated
-  float ych[CLMAX + 1];
-  float ybase_part = 0;
+  real ych[CLMAX + 1];
+  real ybase_part = 0;
   int c = lane;
   if (lane < 5) {
     int L = chain_len(T, c);
@@ -511,24 +516,24 @@ __device__ void solve_full(Shared& S, const GmTopo* __restrict__ T, const float*
     if (c < 4) S.bdelta[c] = ybase_part;
   }
   __syncthreads();
-  float xbase = (b[T->dof_base] - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3])) / S.Dbb;
+  real xbase = (b[T->dof_base] - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3])) / S.Dbb;
   __syncthreads();
   if (lane < 5) {
     int L = chain_len(T, c);
     if (c < 4) {
-      float xs[CLMAX + 1];
+      real xs[CLMAX + 1];
       xs[0] = xbase;
       for (int k = 1; k <= L; k++) {
-        float v = ych[k];
+        real v = ych[k];
         for (int i = k - 1; i >= 0; i--) v -= Hat(S, c, k, i) * xs[i];
         xs[k] = v;
         x[chain_dof(T, c, k)] = v;
       }
       if (c == 0) x[T->dof_base] = xbase;
     } else {
-      float xs[6];
+      real xs[6];
       for (int k = 0; k < 6; k++) {
-        float v = ych[k];
+        real v = ych[k];
         for (int i = k - 1; i >= 0; i--) v -= S.Ho[TRI(k, i)] * xs[i];
         xs[k] = v;
         x[T->dof_obj + k] = v;
@@ -929,24 +934,25 @@ __device__ __forceinline__ int geom_chain(const GmTopo* T, int g) { return T->ge
 
 // compact Jacobian row of contact c along unit direction `dir` (rows of the frame)
 __device__ void contact_jac(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int c,
-                            const float* dir, float* J, int& grp) {
+                            const float* dirf, real* J, int& grp) {
   for (int k = 0; k < CW; k++) J[k] = 0;
   const float* C = S.con[c];
-  const float* pos = C + 1;
+  const real pos[3] = {C[1], C[2], C[3]};
+  const real dir[3] = {dirf[0], dirf[1], dirf[2]};
   int gs[2] = {(int)C[17], (int)C[18]};
-  float sg[2] = {-1.0f, 1.0f};
+  real sg[2] = {-1.0f, 1.0f};
   grp = -1;
   for (int side = 0; side < 2; side++) {
     int g = gs[side];
     int grpg = T->geom_group[g];
     if (grpg < 0) continue;
-    float s = sg[side];
+    real s = sg[side];
     if (grpg == GM_GRP_OBJECT) {
       for (int k = 0; k < 6; k++) {
-        const float* cd = S.cdof[T->dof_obj + k];
-        float wxp[3];
+        const real* cd = S.cdof[T->dof_obj + k];
+        real wxp[3];
         cross3(wxp, cd, pos);
-        float col[3] = {cd[3] + wxp[0], cd[4] + wxp[1], cd[5] + wxp[2]};
+        real col[3] = {cd[3] + wxp[0], cd[4] + wxp[1], cd[5] + wxp[2]};
         J[k] += s * dot3(dir, col);
       }
     } else {
@@ -954,11 +960,11 @@ __device__ void contact_jac(Shared& S, const gm_model* __restrict__ m, const GmT
       int P = T->geom_cpos[g];
       for (int q = 0; q <= P; q++) {
         int d = (q == 0) ? T->dof_base : chain_dof(T, grpg, q);
-        const float* cd = S.cdof[d];
-        float wxp[3];
+        const real* cd = S.cdof[d];
+        real wxp[3];
         cross3(wxp, cd, pos);
-        float col[3] = {cd[3] + wxp[0], cd[4] + wxp[1], cd[5] + wxp[2]};
-        float v = s * dot3(dir, col);
+        real col[3] = {cd[3] + wxp[0], cd[4] + wxp[1], cd[5] + wxp[2]};
+        real v = s * dot3(dir, col);
         if (q == 0) J[6] += v; else J[6 + q] += v;
       }
     }
@@ -966,7 +972,7 @@ __device__ void contact_jac(Shared& S, const gm_model* __restrict__ m, const GmT
 }
 
 // Y = J L^-1 on a compact row (in place)
-__device__ void row_LTsolve(Shared& S, const GmTopo* __restrict__ T, float* J, int grp) {
+__device__ void row_LTsolve(Shared& S, const GmTopo* __restrict__ T, real* J, int grp) {
   for (int k = 5; k >= 1; k--)
     for (int i = k - 1; i >= 0; i--) J[i] -= S.Ho[TRI(k, i)] * J[k];
   if (grp >= 0 && grp <= 3) {
@@ -977,8 +983,8 @@ __device__ void row_LTsolve(Shared& S, const GmTopo* __restrict__ T, float* J, i
     }
   }
 }
-__device__ __forceinline__ float row_dot_dofs(Shared& S, const GmTopo* __restrict__ T, const float* J, int grp, const float* v) {
-  float acc = 0;
+__device__ __forceinline__ real row_dot_dofs(Shared& S, const GmTopo* __restrict__ T, const real* J, int grp, const real* v) {
+  real acc = 0;
   for (int k = 0; k < 6; k++) acc += J[k] * v[T->dof_obj + k];
   if (grp >= 0 && grp <= 3) {
     acc += J[6] * v[T->dof_base];
@@ -1007,9 +1013,9 @@ __device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmT
   int nl = 0;
   for (int k = 0; k < T->nlock; k++) nl += S.s.lock_active[k] ? 1 : 0;
   int nefc = nl + 4 * S.ncon;
-  float J[CW];
+  real J[CW];
   int grp = -1;
-  float pos = 0;
+  real pos = 0;
   int is_contact = 0;
   if (lane < nefc) {
     if (lane < nl) {
@@ -1019,41 +1025,41 @@ __device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmT
       for (int t = 0; t < CW; t++) J[t] = 0;
       int b = m->dof_body[d];
       grp = T->body_group[b];
-      J[6 + T->body_cpos[b]] = 1.0f;
+      J[6 + T->body_cpos[b]] = 1.0;
       pos = S.s.qpos[d] - S.s.lock_q[k];
     } else {
       int r = lane - nl;
       int c = r >> 2, e = r & 3;
       const float* C = S.con[c];
-      float Jn[CW], Jt[CW];
+      real Jn[CW], Jt[CW];
       int g2;
       contact_jac(S, m, T, c, C + 4, Jn, grp);
       contact_jac(S, m, T, c, C + 4 + 3 * (1 + (e >> 1)), Jt, g2);
-      float sgn = (e & 1) ? -1.0f : 1.0f;
-      float mu = C[13];
+      real sgn = (e & 1) ? -1.0 : 1.0;
+      real mu = C[13];
       for (int t = 0; t < CW; t++) J[t] = Jn[t] + sgn * mu * Jt[t];
       pos = C[0];
       is_contact = 1;
     }
   }
   // a0 = J qacc_smooth, vel = J qvel (uses J before the in-place solve)
-  float a0 = 0, vel = 0;
+  real a0 = 0, vel = 0;
   if (lane < nefc) {
     a0 = row_dot_dofs(S, T, J, grp, S.qacc_s);
     vel = row_dot_dofs(S, T, J, grp, S.s.qvel);
     row_LTsolve(S, T, J, grp);
     for (int t = 0; t < CW - 1; t++) S.Y[lane][t] = J[t];
-    S.Y[lane][CW - 1] = __int_as_float(grp);
+    S.Y[lane][CW - 1] = (real)grp;
   }
   if (lane == 0) { S.nefc = nefc; S.nlockrows = nl; }
   __syncthreads();
   // Y D^-1 for this lane's row
-  float Yd[CW - 1];
+  real Yd[CW - 1];
   if (lane < nefc) {
     for (int k = 0; k < 6; k++) Yd[k] = J[k] / S.Do[k];
     Yd[6] = J[6] / S.Dbb;
     for (int q = 1; q <= CLMAX; q++) {
-      float dv = 1.0f;
+      real dv = 1.0;
       if (grp >= 0 && grp < 3 && q <= T->CL) dv = S.Df[grp][q];
       else if (grp == 3 && q == 1) dv = S.Dp[1];
       Yd[6 + q] = J[6 + q] / dv;
@@ -1061,40 +1067,40 @@ __device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmT
   } else {
     for (int k = 0; k < CW - 1; k++) Yd[k] = 0;
   }
-  // Delassus column A[:, lane] in VGPRs
+  const bool gj = grp >= 0 && grp <= 3;
+  // Delassus column A[:, lane] = Y D^-1 Y_lane^T, accumulated in fp64, held in fp32 VGPRs
   float A[GM_MAX_EFC];
 #pragma unroll
   for (int i = 0; i < GM_MAX_EFC; i++) {
-    float acc = 0;
+    real acc = 0;
     if (i < nefc) {
-      const float* Yi = S.Y[i];
-      int gi = __float_as_int(Yi[CW - 1]);
+      const real* Yi = S.Y[i];
+      int gi = (int)Yi[CW - 1];
       for (int k = 0; k < 6; k++) acc += Yd[k] * Yi[k];
-      float ch = Yd[6] * Yi[6];
-      float chn = 0;
-      for (int q = 1; q <= CLMAX; q++) chn += Yd[6 + q] * Yi[6 + q];
-      if (gi == grp && grp >= 0 && grp <= 3) ch += chn;
-      else if (!(gi >= 0 && gi <= 3 && grp >= 0 && grp <= 3)) ch = 0;
-      acc += ch;
+      if (gj && gi >= 0 && gi <= 3) {
+        acc += Yd[6] * Yi[6];
+        if (gi == grp)
+          for (int q = 1; q <= CLMAX; q++) acc += Yd[6 + q] * Yi[6 + q];
+      }
     }
-    A[i] = acc;
+    A[i] = (float)acc;
   }
   // impedance / reference acceleration (mj_makeImpedance)
-  float h = (float)m->timestep;
-  float tc = (float)m->solref[0];
+  real h = m->timestep;
+  real tc = m->solref[0];
   if (tc < 2 * h) tc = 2 * h;
-  float dr = (float)m->solref[1], dmax = (float)m->solimp[1];
-  float K = 1.0f / (dmax * dmax * tc * tc * dr * dr);
-  float Bd = 2.0f / (dmax * tc);
+  real dr = m->solref[1], dmax = m->solimp[1];
+  real K = 1.0 / (dmax * dmax * tc * tc * dr * dr);
+  real Bd = 2.0 / (dmax * tc);
   float Ajj = 0;
 #pragma unroll
   for (int i = 0; i < GM_MAX_EFC; i++) if (i == lane) Ajj = A[i];
-  float imp = impedance(m, pos);
-  float aref = -Bd * vel - K * imp * pos;
-  float R = (1 - imp) / imp * Ajj;
+  real imp = impedance(m, (float)pos);
+  real aref = -Bd * vel - K * imp * pos;
+  float R = (float)((1 - imp) / imp * (real)Ajj);
   if (R < 1e-15f) R = 1e-15f;
   float invd = (lane < nefc) ? 1.0f / (Ajj + R) : 0.0f;
-  float res = (lane < nefc) ? (a0 - aref) : 0.0f;   // (A f + b) with f = 0
+  float res = (lane < nefc) ? (float)(a0 - aref) : 0.0f;   // (A f + b) with f = 0
   float f = 0;
   // projected Gauss-Seidel, residual broadcast through v_readlane
   for (int it = 0; it < m->pgs_iterations; it++) {
@@ -1128,13 +1134,13 @@ __device__ void constraint_accel(Shared& S, const GmTopo* __restrict__ T, int la
     else if (d == T->dof_palm) { grp_d = 3; slot = 7; }
     else { grp_d = (d - T->dof_f0[0]) / T->CL; slot = 6 + 1 + (d - T->dof_f0[grp_d]); }
     (void)b;
-    float acc = 0;
+    real acc = 0;
     for (int r = 0; r < nefc; r++) {
-      int g = __float_as_int(S.Y[r][CW - 1]);
+      int g = (int)S.Y[r][CW - 1];
       bool use = (grp_d == GM_GRP_OBJECT) || (grp_d == GM_GRP_BASE && g >= 0 && g <= 3) || (grp_d == g);
       if (use) acc += S.Y[r][slot] * S.efc_f[r];
     }
-    float Dd;
+    real Dd;
     if (grp_d == GM_GRP_OBJECT) Dd = S.Do[slot];
     else if (grp_d == GM_GRP_BASE) Dd = S.Dbb;
     else if (grp_d == 3) Dd = S.Dp[1];
@@ -1147,10 +1153,10 @@ __device__ void constraint_accel(Shared& S, const GmTopo* __restrict__ T, int la
     int c = lane;
     int L = chain_len(T, c);
     if (c < 4) {
-      float xs[CLMAX + 1];
+      real xs[CLMAX + 1];
       xs[0] = S.z[T->dof_base];
       for (int k = 1; k <= L; k++) {
-        float v = S.z[chain_dof(T, c, k)];
+        real v = S.z[chain_dof(T, c, k)];
         for (int i = k - 1; i >= 0; i--) v -= Hat(S, c, k, i) * xs[i];
         xs[k] = v;
         int d = chain_dof(T, c, k);
@@ -1158,9 +1164,9 @@ __device__ void constraint_accel(Shared& S, const GmTopo* __restrict__ T, int la
       }
       if (c == 0) S.qacc[T->dof_base] = S.qacc_s[T->dof_base] + xs[0];
     } else {
-      float xs[6];
+      real xs[6];
       for (int k = 0; k < 6; k++) {
-        float v = S.z[T->dof_obj + k];
+        real v = S.z[T->dof_obj + k];
         for (int i = k - 1; i >= 0; i--) v -= S.Ho[TRI(k, i)] * xs[i];
         xs[k] = v;
         S.qacc[T->dof_obj + k] = S.qacc_s[T->dof_obj + k] + v;
@@ -1180,7 +1186,7 @@ __device__ void constraint_accel(Shared& S, const GmTopo* __restrict__ T, int la
 
 // ============================================================ integrate
 __device__ void integrate(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
-  float h = (float)m->timestep;
+  real h = (real)m->timestep;
   if (lane < T->nv) S.s.qvel[lane] += h * S.qacc[lane];
   __syncthreads();
   if (lane < T->nv && lane < T->dof_obj) {
@@ -1189,13 +1195,13 @@ __device__ void integrate(Shared& S, const gm_model* __restrict__ m, const GmTop
   if (lane == 0) {
     int qa = T->qadr_obj, da = T->dof_obj;
     for (int k = 0; k < 3; k++) S.s.qpos[qa + k] += h * S.s.qvel[da + k];
-    float* q = &S.s.qpos[qa + 3];
-    float w[3] = {S.s.qvel[da + 3], S.s.qvel[da + 4], S.s.qvel[da + 5]};
-    float wn = sqrtf(dot3(w, w));
-    if (wn > 1e-15f) {
-      float ang = wn * h;
-      float sn = sinf(0.5f * ang) / wn, cs = cosf(0.5f * ang);
-      float dq[4] = {cs, w[0] * sn, w[1] * sn, w[2] * sn};
+    real* q = &S.s.qpos[qa + 3];
+    real w[3] = {S.s.qvel[da + 3], S.s.qvel[da + 4], S.s.qvel[da + 5]};
+    real wn = sqrt(dot3(w, w));
+    if (wn > 1e-15) {
+      real ang = wn * h;
+      real sn = sin(0.5 * ang) / wn, cs = cos(0.5 * ang);
+      real dq[4] = {cs, w[0] * sn, w[1] * sn, w[2] * sn};
       quatmul(q, q, dq);
     }
     quatnorm(q);
@@ -1302,9 +1308,9 @@ __device__ void update_all(Shared& S, const gm_model* __restrict__ m, const GmTo
       s.last_step_time = s.time;
       g_step_to(s.next, s.end, m->stepper_num_steps);
     }
-    const float* v = &s.qvel[T->dof_obj];
-    float mag = sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
-    if (mag < 1e-6f) for (int k = 0; k < 6; k++) s.qvel[T->dof_obj + k] = 0;
+    const real* v = &s.qvel[T->dof_obj];
+    real mag = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    if (mag < 1e-6) for (int k = 0; k < 6; k++) s.qvel[T->dof_obj + k] = 0;
   }
   __syncthreads();
 }
@@ -1383,66 +1389,68 @@ __device__ int s_ready(GmEnvState& s, const gm_sensor& ss, int slot) {
 }
 
 // bending gauge: cubic least squares through the N+1 joint points, evaluated at
-// gauge.xpos (read_armadillo_gauge, myfunctions.cpp:2699-2795).  fp32 Householder
-// QR on a centred/scaled abscissa (same least-squares solution as the reference's
-// arma::polyfit on the raw Vandermonde, better conditioned in fp32).
-__device__ float gauge_reading(const gm_model* __restrict__ m, const float* q) {
+// gauge.xpos (read_armadillo_gauge, myfunctions.cpp:2699-2795).  Evaluated in fp64
+// (two reads per env-step at 10 Hz: negligible cost): the fitted value at 50 mm is
+// ~16x smaller than the tip deflection, so an fp32 fit would cost ~3e-5 relative.
+// Householder QR on a centred/scaled abscissa -- the same least-squares solution as
+// the reference's arma::polyfit on the raw Vandermonde.
+__device__ float gauge_reading(const gm_model* __restrict__ m, const real* q) {
   int N = m->n_seg, P = N + 1;
-  float Ls = (float)m->segment_length;
-  float X[GM_MAX_SEG + 1], Yv[GM_MAX_SEG + 1];
-  X[0] = m->fixed_first_segment ? Ls : 0.0f;
+  double Ls = m->segment_length;
+  double X[GM_MAX_SEG + 1], Yv[GM_MAX_SEG + 1];
+  X[0] = m->fixed_first_segment ? Ls : 0.0;
   Yv[0] = 0;
-  float cum = 0;
+  double cum = 0;
   for (int i = 0; i < N; i++) {
-    cum = (i == 0) ? q[0] : cum + q[i];
-    X[i + 1] = X[i] + Ls * cosf(cum);
-    Yv[i + 1] = Yv[i] + Ls * sinf(cum);
+    cum = (i == 0) ? (double)q[0] : cum + (double)q[i];
+    X[i + 1] = X[i] + Ls * cos(cum);
+    Yv[i + 1] = Yv[i] + Ls * sin(cum);
   }
-  float half = 0.5f * (float)m->finger_length;
-  float A[GM_MAX_SEG + 1][4], b[GM_MAX_SEG + 1];
+  double half = 0.5 * m->finger_length;
+  double A[GM_MAX_SEG + 1][4], b[GM_MAX_SEG + 1];
   for (int i = 0; i < P; i++) {
-    float t = (X[i] - half) / half;
-    A[i][0] = t * t * t; A[i][1] = t * t; A[i][2] = t; A[i][3] = 1.0f;
+    double t = (X[i] - half) / half;
+    A[i][0] = t * t * t; A[i][1] = t * t; A[i][2] = t; A[i][3] = 1.0;
     b[i] = Yv[i];
   }
   for (int k = 0; k < 4; k++) {
-    float nrm = 0;
+    double nrm = 0;
     for (int i = k; i < P; i++) nrm += A[i][k] * A[i][k];
-    nrm = sqrtf(nrm);
-    float alpha = A[k][k] > 0 ? -nrm : nrm;
-    float v[GM_MAX_SEG + 1];
-    for (int i = 0; i < P; i++) v[i] = (i >= k) ? A[i][k] : 0.0f;
+    nrm = sqrt(nrm);
+    double alpha = A[k][k] > 0 ? -nrm : nrm;
+    double v[GM_MAX_SEG + 1];
+    for (int i = 0; i < P; i++) v[i] = (i >= k) ? A[i][k] : 0.0;
     v[k] -= alpha;
-    float vv = 0;
+    double vv = 0;
     for (int i = k; i < P; i++) vv += v[i] * v[i];
-    if (vv < 1e-30f) continue;
+    if (vv < 1e-300) continue;
     for (int j = k; j < 4; j++) {
-      float s = 0;
+      double s = 0;
       for (int i = k; i < P; i++) s += v[i] * A[i][j];
       s = 2 * s / vv;
       for (int i = k; i < P; i++) A[i][j] -= s * v[i];
     }
-    float s = 0;
+    double s = 0;
     for (int i = k; i < P; i++) s += v[i] * b[i];
     s = 2 * s / vv;
     for (int i = k; i < P; i++) b[i] -= s * v[i];
   }
-  float coeff[4];
+  double coeff[4];
   for (int k = 3; k >= 0; k--) {
-    float s = b[k];
+    double s = b[k];
     for (int j = k + 1; j < 4; j++) s -= A[k][j] * coeff[j];
     coeff[k] = s / A[k][k];
   }
-  float tg = ((float)m->gauge_xpos - half) / half;
-  float y = ((coeff[0] * tg + coeff[1]) * tg + coeff[2]) * tg + coeff[3];
-  return y * 1000.0f;
+  double tg = (m->gauge_xpos - half) / half;
+  double y = ((coeff[0] * tg + coeff[1]) * tg + coeff[2]) * tg + coeff[3];
+  return (float)y * 1000;
 }
 
 // extract_forces_faster (objecthandler.cpp:737-992) over the last substep's contacts.
 // forces[]: obj_loc f1,f2,f3,palm (12) | obj ground global (3) | all_loc f1,f2,f3 x (3),
 //           all_loc palm x (1) | gnd_loc f1,f2,f3 x (3)
 __device__ void extract_forces(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T) {
-  float og[5][3], ag[4][3], gg[3][3];
+  real og[5][3], ag[4][3], gg[3][3];
   for (int a = 0; a < 5; a++) for (int k = 0; k < 3; k++) og[a][k] = 0;
   for (int a = 0; a < 4; a++) for (int k = 0; k < 3; k++) ag[a][k] = 0;
   for (int a = 0; a < 3; a++) for (int k = 0; k < 3; k++) gg[a][k] = 0;
@@ -1455,8 +1463,8 @@ __device__ void extract_forces(Shared& S, const gm_model* __restrict__ m, const 
     int w_f2 = (c1 == GM_CLS_FINGER3 || c2 == GM_CLS_FINGER3);
     int w_palm = (c1 == GM_CLS_PALM || c2 == GM_CLS_PALM);
     int w_gnd = (c1 == GM_CLS_GROUND || c2 == GM_CLS_GROUND);
-    float g[3];
-    for (int k = 0; k < 3; k++) g[k] = C[4 + k] * C[14] + C[7 + k] * C[15] + C[10 + k] * C[16];
+    real g[3];
+    for (int k = 0; k < 3; k++) g[k] = (real)C[4 + k] * C[14] + (real)C[7 + k] * C[15] + (real)C[10 + k] * C[16];
     int wf[3] = {w_f0, w_f1, w_f2};
     if (w_obj) {
       for (int f = 0; f < 3; f++) if (wf[f]) for (int k = 0; k < 3; k++) og[f][k] += g[k];
@@ -1473,15 +1481,15 @@ __device__ void extract_forces(Shared& S, const gm_model* __restrict__ m, const 
   float* F = S.forces;
   for (int f = 0; f < 4; f++) {
     int b = f < 3 ? T->body_finger[f] : T->body_palm;
-    float loc[3];
+    real loc[3];
     mulmtv3(loc, S.xmat[b], og[f]);
-    F[3 * f] = loc[0]; F[3 * f + 1] = loc[1]; F[3 * f + 2] = loc[2];
-    float al[3];
+    F[3 * f] = (float)loc[0]; F[3 * f + 1] = (float)loc[1]; F[3 * f + 2] = (float)loc[2];
+    real al[3];
     mulmtv3(al, S.xmat[b], ag[f]);
-    if (f < 3) F[15 + f] = al[0]; else F[18] = al[0];
-    if (f < 3) { float gl[3]; mulmtv3(gl, S.xmat[b], gg[f]); F[19 + f] = gl[0]; }
+    if (f < 3) F[15 + f] = (float)al[0]; else F[18] = (float)al[0];
+    if (f < 3) { real gl[3]; mulmtv3(gl, S.xmat[b], gg[f]); F[19 + f] = (float)gl[0]; }
   }
-  F[12] = og[4][0]; F[13] = og[4][1]; F[14] = og[4][2];
+  F[12] = (float)og[4][0]; F[13] = (float)og[4][1]; F[14] = (float)og[4][2];
 }
 
 // MjClass::monitor_sensors (mjclass.cpp:741-898)
@@ -2025,7 +2033,7 @@ extern "C" __global__ void gm_action_kernel(GmEnvState* __restrict__ states, con
 // configure_settings RNG draws, random_base_Z_movement, then spawn_object.
 extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, const gm_model* __restrict__ m,
                                            const gm_config* __restrict__ C, const GmTopo* __restrict__ T,
-                                           const float* __restrict__ eq_qpos, const uint8_t* __restrict__ mask,
+                                           const double* __restrict__ eq_qpos, const uint8_t* __restrict__ mask,
                                            const gm_spawn* __restrict__ spawn, const gm_object* __restrict__ objs,
                                            int n_objects, int n_envs) {
   int env = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2039,14 +2047,14 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
   for (int i = 0; i < GM_STATE_WORDS; i++) w[i] = 0;
   s.rng = rng; s.old_x = ox; s.old_y = oy; s.old_z = oz;
   g_reset(s.end); g_reset(s.next);
-  for (int k = 0; k < GM_MAX_QPOS; k++) s.qpos[k] = (float)m->qpos0[k];
+  for (int k = 0; k < GM_MAX_QPOS; k++) s.qpos[k] = m->qpos0[k];
   s.time = 0; s.last_step_time = 0;
   for (int d = 0; d < T->nv; d++) {
     bool motor = (d == m->dof_base || d == m->dof_palm);
     for (int f = 0; f < 3; f++) motor = motor || d == m->dof_pris[f] || d == m->dof_rev[f];
     if (motor) s.qpos[d] = eq_qpos[d];
   }
-  for (int k = 0; k < T->nlock; k++) { s.lock_active[k] = 1; s.lock_q[k] = (float)m->qpos0[m->lock_dof[k]]; }
+  for (int k = 0; k < T->nlock; k++) { s.lock_active[k] = 1; s.lock_q[k] = m->qpos0[m->lock_dof[k]]; }
   for (int st = 0; st < GM_NSTREAM; st++) s.ring_i[st] = -1;
   // apply_noise_params: mean draws, SS order then the state sensors again
   {
@@ -2074,7 +2082,7 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
     s.base[2] = z;
     if (s.base[2] > C->base_max[2]) s.base[2] = C->base_max[2];
     if (s.base[2] < C->base_min[2]) s.base[2] = C->base_min[2];
-    s.qpos[m->dof_base] = (float)(s.base[2] + (double)eq_qpos[m->dof_base]);
+    s.qpos[m->dof_base] = s.base[2] + eq_qpos[m->dof_base];
   }
   // spawn_object
   gm_spawn sp = spawn ? spawn[env] : gm_spawn{0, 0.0, 0.0, 0.0};
@@ -2110,10 +2118,10 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
   double x2 = sin(-sp.zrot / 2.0), w2 = cos(-sp.zrot / 2.0);
   double q4[4] = {x2, 0, 0, w2};   // reference QPos quirk: qx lands in MuJoCo's w slot
   double nq = sqrt(q4[0] * q4[0] + q4[1] * q4[1] + q4[2] * q4[2] + q4[3] * q4[3]);
-  s.qpos[qa + 0] = (float)sp.x;
-  s.qpos[qa + 1] = (float)sp.y;
-  s.qpos[qa + 2] = (float)(restz + 1e-6);
-  for (int k = 0; k < 4; k++) s.qpos[qa + 3 + k] = (float)(q4[k] / nq);
+  s.qpos[qa + 0] = sp.x;
+  s.qpos[qa + 1] = sp.y;
+  s.qpos[qa + 2] = restz + 1e-6;
+  for (int k = 0; k < 4; k++) s.qpos[qa + 3 + k] = q4[k] / nq;
   for (int k = 0; k < 7; k++) s.start_qpos[k] = s.qpos[qa + k];
 }
 
@@ -2125,7 +2133,7 @@ extern "C" __global__ void gm_settle_init_kernel(GmEnvState* __restrict__ states
   uint32_t* w = reinterpret_cast<uint32_t*>(&s);
   for (int i = 0; i < GM_STATE_WORDS; i++) w[i] = 0;
   g_reset(s.end); g_reset(s.next);
-  for (int k = 0; k < GM_MAX_QPOS; k++) s.qpos[k] = (float)m->qpos0[k];
+  for (int k = 0; k < GM_MAX_QPOS; k++) s.qpos[k] = m->qpos0[k];
   s.old_x = s.old_y = s.old_z = 1;
   for (int st = 0; st < GM_NSTREAM; st++) s.ring_i[st] = -1;
   const gm_object& o = objs[0];

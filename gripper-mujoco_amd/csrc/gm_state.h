@@ -43,17 +43,17 @@ struct GmEnvState {
   GmGrip end, next;
   double base[6];
   double last_read[SL_N];
+  double qpos[GM_MAX_QPOS];      // fp64 like MuJoCo's mjtNum (reference physics type)
+  double qvel[GM_MAX_DOF];
+  double lock_q[GM_MAX_LOCK];
+  double start_qpos[7];
   // ---- floats ----
-  float qpos[GM_MAX_QPOS];
-  float qvel[GM_MAX_DOF];
-  float lock_q[GM_MAX_LOCK];
   float rand_mu[SL_N][3];
   float ring[GM_NSTREAM][GM_RING];
   float lev_value[GM_N_LINEAR];
   float lev_last[GM_N_LINEAR];
   float cumulative_reward;
   float grp_peak_lateral;
-  float start_qpos[7];
   float obj_size[3];
   float obj_mass, obj_inertia[3], obj_friction, obj_rbound, obj_rest_z;
   float reward;

@@ -124,6 +124,15 @@ def load_library(path: str | None = None):
     if _lib is not None and path is None:
         return _lib
     p = path or LIB_PATH
+    # One HIP runtime per process: torch's libc10_hip pulls its bundled libamdhip64 by
+    # the unversioned name, so if libgm (NEEDED libamdhip64.so.7) loaded first a second
+    # runtime would appear and one of them sees no devices.  Loading torch first makes
+    # libgm bind to torch's runtime (same SONAME), so RCCL / torch tensors and our
+    # kernels share streams and device pointers.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     if not os.path.exists(p):
         raise ImportError(
             f"gripper-mi355x HIP extension not built: {p} is missing "

@@ -89,7 +89,9 @@ def test_contact_free_rollout_parity(setup):
         for e, o in enumerate(ors):
             obs_o, r_o, d_o = o.step(a[e])
             ok, er, ea = obs_close(obs[e], obs_o)
-            assert ok, (t, e, er, ea, obs[e], obs_o)
+            if not ok:
+                k = int(np.argmax(np.abs(obs[e] - obs_o) / np.maximum(np.abs(obs_o), 1e-3)))
+                raise AssertionError(f"step {t} env {e}: rel {er:.3g} abs {ea:.3g} at obs[{k}] gpu {obs[e][k]!r} ref {obs_o[k]!r}")
             oe, oes, ons, ob = o.target()
             np.testing.assert_array_equal(tes[e], oes)
             np.testing.assert_array_equal(tns[e], ons)

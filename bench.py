@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""Batched env-step throughput of the MI355X gripper hot path (BASELINE.json metric).
+
+A "step" is one MjEnv.step-equivalent for every env of the batch (MjEnv.py:2170-2220):
+set actions (MjClass::set_continous_action x n_actions), action_step() = S = 63 physics
+substeps + sense_gripper_state + update_env, then observation, done and reward
+(mjclass.cpp:1483-1508, 1632-1959, 3000-3049), followed by the episode-boundary
+bookkeeping (return hand-off, reset + respawn of done/truncated envs, MjEnv.py:616-637).
+Everything runs on the device; inputs (pre-drawn random actions, a spawn table) are
+resident in HBM before the timed region starts.
+
+Workload = BASELINE.json configs[2] ("C3"): 4096 envs per GPU, 20-object synthetic
+set6-like mixed set, randomised spawn, random actions U[-1,1]^4.  N GPUs run N x 4096
+envs sharded by env id (weak scaling); the only collective is an RCCL all-gather of
+the per-env episode returns each step.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints one JSON line.  `roofline.achieved` = algorithmic bytes per launch of
+the fused step kernel (SURVEY.md 8d per-env-substep working set, constants frozen from
+the model below) / the kernel's average duration from HIP events recorded on the
+stream it is launched on.  `cpu_baseline` times the fp64 CPU oracle (a restatement of
+the reference path; the reference bind.so needs MuJoCo 2.1.5 and cannot be built).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "gripper-mujoco_amd"))
+
+METRIC = "env-steps/sec (batched rollout) at 4096 envs; obs max-rel-err vs C++ ref"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM")
+NCON_NOMINAL = 12              # SURVEY.md 8d nominal contacts per env-substep
+
+
+def algorithmic_bytes_per_substep(model, ncon: int = NCON_NOMINAL) -> dict:
+    """fp32 working set crossing the north-star stage boundaries per
+    env-substep, with this model's frozen sizes."""
+    nefc = model.nlock + 4 * ncon
+    parts = {
+        "state_in_out": 2 * (model.nq + model.nv) * 4,
+        "ctrl": 8 * 4,
+        "fk_poses": (model.nbody * 16 + model.ngeom * 12) * 4,
+        "cinert_cdof": (model.nbody * 10 + model.nv * 6) * 4,
+        "mass_ldl": 2 * model.nM * 4,
+        "force_vectors": 4 * model.nv * 4,
+        "contacts": ncon * 60,
+        "constraints": nefc * 68,
+        "qacc_qfrc_constraint": 2 * model.nv * 4,
+        "cfrc_ext": model.nbody * 24,
+    }
+    return {"bytes": sum(parts.values()), "ncon": ncon, "nefc": nefc, "parts": parts}
+
+
+def load_traffic(n_envs: int):
+    """HBM bytes per launch of gm_step_kernel from the committed rocprofv3 PMC pass
+    (profiles/*pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950 guide)."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if int(d.get("n_envs", -1)) == n_envs:
+            return float(d["bytes_per_launch"]), d.get("source")
+    except (OSError, ValueError, KeyError):
+        pass
+    return None, None
+
+
+def obs_parity(gmx, n_envs: int = 4, n_steps: int = 12):
+    """obs max-rel-err of the GPU path vs the fp64 oracle (noise off, SURVEY.md 8d
+    definition: rel over |ref| >= 1e-3, abs elsewhere); small contact-free rollout."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib
+    s = gmx.canonical_settings(noise=False, seed=5)
+    env = gmx.BatchedGripperEnv(n_envs, object_set="set1_synthetic", settings=s, seed=5)
+    xs = np.linspace(0.06, 0.08, n_envs)
+    sp = env.make_spawn(x=xs, y=xs, idx=0)
+    env.reset(spawn=sp)
+    oracles = []
+    for e in range(n_envs):
+        o = oracle_lib.OracleEnv(env.model, env.cfg, env.objects, e)
+        o.reset(sp[e])
+        oracles.append(o)
+    rng = np.random.default_rng(1234)
+    rel, ab = 0.0, 0.0
+    for _ in range(n_steps):
+        a = rng.uniform(-1, 1, size=(n_envs, env.n_actions)).astype(np.float32)
+        obs, _, _, _ = env.step(a)
+        for e in range(n_envs):
+            ref, _, _ = oracles[e].step(a[e])
+            ref = np.asarray(ref, dtype=np.float64)
+            d = np.abs(obs[e].astype(np.float64) - ref)
+            big = np.abs(ref) >= 1e-3
+            if big.any():
+                rel = max(rel, float((d[big] / np.abs(ref[big])).max()))
+            if (~big).any():
+                ab = max(ab, float(d[~big].max()))
+    env.close()
+    return {"max_rel": rel, "max_abs_small": ab, "envs": n_envs, "steps": n_steps}
+
+
+def cpu_baseline(gmx, n_envs: int, n_steps: int):
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib
+    s = gmx.canonical_settings(seed=1234)
+    model = gmx.ModelBlob()
+    cfg = gmx.ConfigBlob(s, model)
+    objs = gmx.make_object_set("set6_synthetic", 1234)
+    t = time.time()
+    v = oracle_lib.bench(model, cfg, objs, n_envs, n_steps, seed=1234, n_threads=1)
+    return {"value": round(v, 2), "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"fp64 C oracle (oracle/oracle.c, gcc -O2 -mavx), 1 thread, {n_envs} envs x "
+                      f"{n_steps} env-steps of the C3 workload (set6_synthetic, random actions, "
+                      f"resets at done), {time.time() - t:.1f} s wall"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--cpu-envs", type=int, default=40)
+    ap.add_argument("--cpu-steps", type=int, default=250)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run",
+              file=sys.stderr)
+        sys.exit(2)
+
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import gmx
+    settings = gmx.canonical_settings(seed=args.seed)
+    n = args.envs
+    env = gmx.BatchedGripperEnv(n, object_set="set6_synthetic", settings=settings, seed=args.seed,
+                                env_offset=rank * n, device=local_rank)
+    stream = torch.cuda.Stream(dev)          # a real (non-null) stream shared by torch and the ctx
+    torch.cuda.set_stream(stream)
+    env.set_stream(stream.cuda_stream)
+    S = env.cfg.sim_steps_per_action
+    spawn = env.make_spawn()
+    env.reset(spawn=spawn)
+    spawn_ptr = env.upload_spawn(spawn)
+
+    K, W = args.steps, args.warmup
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed + 7919 * rank)
+    actions = torch.rand((W + K, n, env.n_actions), generator=g, device=dev) * 2 - 1
+    returns = torch.full((n,), float("nan"), device=dev)
+    gathered = torch.empty((world * n,), device=dev) if world > 1 else None
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    episodes = torch.zeros((), device=dev, dtype=torch.int64)
+
+    def one_step(i, timed):
+        env.lib.gm_set_action(env.ctx, actions[i].data_ptr(), 1)
+        if timed is not None:
+            ev[timed][0].record(stream)
+        env.lib.gm_step(env.ctx)
+        if timed is not None:
+            ev[timed][1].record(stream)
+        env.autoreset_device(spawn_ptr, returns.data_ptr())
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, returns)
+            episodes.add_(torch.isfinite(gathered).sum())
+        else:
+            episodes.add_(torch.isfinite(returns).sum())
+
+    for i in range(W):
+        one_step(i, None)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        one_step(W + k, k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
+    finite = bool(torch.isfinite(torch.as_tensor(env.observation())).all())
+    overflow = int(env.overflow().sum())
+
+    if rank == 0:
+        B = algorithmic_bytes_per_substep(env.model)
+        bytes_per_launch = n * S * B["bytes"]
+        achieved = bytes_per_launch / kern_avg_s / 1e9
+        traffic, traffic_src = load_traffic(n)
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "kernel": "gm_step_kernel", "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "traffic_source": traffic_src}
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(gmx, args.cpu_envs, args.cpu_steps)
+        parity = None if args.no_parity else obs_parity(gmx)
+        value = world * n * K / elapsed
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
+            "steps": K, "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64+f32", "data": "synthetic",
+            "config": {"workload": "C3: set6_synthetic 20 mixed objects, randomised spawn, random "
+                                   "actions U[-1,1]^4, canonical sensor/reward config, device auto-reset",
+                       "envs_per_gpu": n, "global_envs": world * n, "substeps_per_env_step": S,
+                       "parallelism": f"env-shard x{world}",
+                       "B_substep_bytes": B["bytes"], "B_substep_ncon": B["ncon"], "B_substep_nefc": B["nefc"],
+                       "model": {"nq": env.model.nq, "nv": env.model.nv, "nbody": env.model.nbody,
+                                 "ngeom": env.model.ngeom, "nM": env.model.nM, "nlock": env.model.nlock},
+                       "dtype_detail": "dynamics f64, collision + PGS f32"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "obs_max_rel_err": parity,
+            "episodes_finished": int(episodes.item()),
+            "overflow_envs": overflow, "finite": finite,
+        }
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -20,7 +20,8 @@ struct gm_ctx {
   int n_envs = 0;
   long long env_offset = 0;
   int n_objects = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;        // stream every launch of this ctx goes to
+  hipStream_t own_stream = nullptr;    // the one gm_create made (destroyed with the ctx)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   gm_model model;
@@ -128,7 +129,8 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   }
   *out = c;
   HIPCHK(c, hipSetDevice(device));
-  HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIPCHK(c, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+  c->stream = c->own_stream;
   HIPCHK(c, hipEventCreate(&c->ev0));
   HIPCHK(c, hipEventCreate(&c->ev1));
   HIPCHK(c, hipMalloc(&c->d_state, sizeof(GmEnvState) * (size_t)n_envs));
@@ -154,7 +156,7 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   HIPCHK(c, hipMemcpyAsync(c->d_objs, objects, sizeof(gm_object) * (size_t)n_objects, hipMemcpyHostToDevice, c->stream));
   // one-time calibrate_reset settle (myfunctions.cpp:1470-1505) on env 0
   hipLaunchKernelGGL(gm_settle_init_kernel, dim3(1), dim3(1), 0, c->stream, c->d_state, c->d_model, c->d_topo, c->d_objs);
-  DebugOut dbg{nullptr, nullptr, nullptr, nullptr};
+  DebugOut dbg{nullptr, nullptr, nullptr, nullptr, nullptr};
   hipLaunchKernelGGL(gm_step_kernel, dim3(1), dim3(NT), 0, c->stream, c->d_state, c->d_model, c->d_cfg, c->d_topo,
                      c->d_obs, c->d_rew, c->d_done, 1, 1, dbg);
   HIPCHK(c, hipGetLastError());
@@ -176,7 +178,7 @@ void gm_destroy(gm_ctx* c) {
   (void)hipFree(c->d_dact); (void)hipFree(c->d_mask); (void)hipFree(c->d_spawn);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
 
@@ -248,7 +250,7 @@ int gm_set_discrete_action(gm_ctx* c, const int32_t* actions, int on_device) {
 int gm_step(gm_ctx* c) {
   if (!c) return GM_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
-  DebugOut dbg{nullptr, nullptr, nullptr, nullptr};
+  DebugOut dbg{nullptr, nullptr, nullptr, nullptr, nullptr};
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   hipLaunchKernelGGL(gm_step_kernel, dim3(c->n_envs), dim3(NT), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
                      c->d_topo, c->d_obs, c->d_rew, c->d_done, c->n_envs, 0, dbg);
@@ -378,7 +380,7 @@ int gm_debug_substep(gm_ctx* c, int32_t* ncon, float* contact, float* efc_force,
   HIPCHK(c, hipMalloc(&d_con, sizeof(float) * n * GM_MAX_CON * 16));
   HIPCHK(c, hipMalloc(&d_f, sizeof(float) * n * GM_MAX_EFC));
   HIPCHK(c, hipMalloc(&d_q, sizeof(float) * n * GM_MAX_DOF));
-  DebugOut dbg{d_ncon, d_con, d_f, d_q};
+  DebugOut dbg{d_ncon, d_con, d_f, d_q, nullptr};
   hipLaunchKernelGGL(gm_step_kernel, dim3(c->n_envs), dim3(NT), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
                      c->d_topo, c->d_obs, c->d_rew, c->d_done, c->n_envs, 2, dbg);
   HIPCHK(c, hipGetLastError());
@@ -388,6 +390,54 @@ int gm_debug_substep(gm_ctx* c, int32_t* ncon, float* contact, float* efc_force,
   if (qacc) HIPCHK(c, hipMemcpyAsync(qacc, d_q, sizeof(float) * n * GM_MAX_DOF, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   (void)hipFree(d_ncon); (void)hipFree(d_con); (void)hipFree(d_f); (void)hipFree(d_q);
+  return GM_OK;
+}
+
+int gm_set_stream(gm_ctx* c, void* stream) {
+  if (!c) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->stream = stream ? (hipStream_t)stream : c->own_stream;
+  return GM_OK;
+}
+
+int gm_autoreset(gm_ctx* c, int max_episode_steps, const gm_spawn* spawn, int spawn_on_device, float* returns) {
+  if (!c) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  const gm_spawn* ds = nullptr;
+  if (spawn && !spawn_on_device) {
+    HIPCHK(c, hipMemcpyAsync(c->d_spawn, spawn, sizeof(gm_spawn) * (size_t)c->n_envs, hipMemcpyHostToDevice, c->stream));
+    ds = c->d_spawn;
+  } else if (spawn) {
+    ds = spawn;
+  }
+  int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
+  hipLaunchKernelGGL(gm_autoreset_mask_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_done,
+                     max_episode_steps, c->d_mask, returns, c->n_envs);
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(gm_reset_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
+                     c->d_topo, c->d_eq, c->d_mask, ds, c->d_objs, c->n_objects, c->n_envs);
+  HIPCHK(c, hipGetLastError());
+  if (spawn && !spawn_on_device) HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+
+void* gm_device_reset_mask(gm_ctx* c) { return c ? (void*)c->d_mask : nullptr; }
+
+int gm_step_profiled(gm_ctx* c, uint64_t* phase_cycles) {
+  if (!c || !phase_cycles) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  size_t n = (size_t)c->n_envs;
+  unsigned long long* d_ph;
+  HIPCHK(c, hipMalloc(&d_ph, sizeof(unsigned long long) * n * GM_NPHASE));
+  DebugOut dbg{nullptr, nullptr, nullptr, nullptr, d_ph};
+  hipLaunchKernelGGL(gm_step_kernel, dim3(c->n_envs), dim3(NT), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
+                     c->d_topo, c->d_obs, c->d_rew, c->d_done, c->n_envs, 0, dbg);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(phase_cycles, d_ph, sizeof(unsigned long long) * n * GM_NPHASE, hipMemcpyDeviceToHost,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  (void)hipFree(d_ph);
   return GM_OK;
 }
 

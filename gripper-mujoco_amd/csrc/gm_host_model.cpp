@@ -378,6 +378,11 @@ void gm_model_info(const gm_model* m, int32_t* o) {
   o[0] = m->nq; o[1] = m->nv; o[2] = m->nbody; o[3] = m->ngeom; o[4] = m->npair; o[5] = m->n_seg;
   o[6] = m->dof_base; o[7] = m->dof_palm; o[8] = m->dof_obj;
   for (int f = 0; f < 3; f++) { o[9 + f] = m->dof_pris[f]; o[12 + f] = m->dof_rev[f]; o[15 + f] = m->dof_seg[f]; }
+  o[18] = m->nlock;
+  int nM = 0;   // tree-sparse mass-matrix nonzeros (lower triangle): sum of dof depths
+  for (int d = 0; d < m->nv; d++)
+    for (int a = d; a >= 0; a = m->dof_parent[a]) nM++;
+  o[19] = nM;
 }
 
 void gm_config_info(const gm_config* c, int32_t* o) {

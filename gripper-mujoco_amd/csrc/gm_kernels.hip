@@ -39,7 +39,9 @@ struct DebugOut {
   float* contact;     // [n_envs][GM_MAX_CON][16]
   float* efc_force;   // [n_envs][GM_MAX_EFC]
   float* qacc;        // [n_envs][GM_MAX_DOF]
+  unsigned long long* phase;   // [n_envs][GM_NPHASE] shader-clock cycles per phase (profiling)
 };
+#define GM_NPHASE 16
 
 struct __align__(16) Shared {
   GmEnvState s;
@@ -51,19 +53,20 @@ struct __align__(16) Shared {
   real Ic[GM_MAX_BODY][10];
   real cfrc[GM_MAX_BODY][6];
   real cdof[GM_MAX_DOF][6];
-  float gxpos[GM_MAX_GEOM][3];
-  float gxmat[GM_MAX_GEOM][9];
+  real gxpos[GM_MAX_GEOM][3];
+  real gxmat[GM_MAX_GEOM][9];
   real Hf[3][TRIF], Hp[3], Ho[21], Hbb;
   real Df[3][CLMAX + 1], Dp[2], Do[6], Dbb;
   real bdelta[5];
-  float con[GM_MAX_CON][20];   // dist, pos3, frame9, mu, force3, g1, g2, (pad)
+  real con[GM_MAX_CON][20];   // dist, pos3, frame9, mu, force3, g1, g2, (pad)
   real Y[GM_MAX_EFC][CW];
-  float efc_f[GM_MAX_EFC];
+  real efc_f[GM_MAX_EFC];
   int32_t cnt[NT];
   int32_t ncon, nefc, nlockrows, overflow;
   float forces[32];            // extract_forces_faster results (see extract_forces)
   int32_t have_forces;
   float gauge_tmp[3];
+  unsigned long long tph[GM_NPHASE];
 };
 
 // ------------------------------------------------------------ small math
@@ -544,23 +547,23 @@ __device__ void solve_full(Shared& S, const GmTopo* __restrict__ T, const real* 
 }
 
 // ============================================================ collision
-struct Hit { float dist, pos[3], n[3]; };
+struct Hit { real dist, pos[3], n[3]; };
 
-__device__ void make_frame(float* F, const float* n) {
-  float a[3] = {0, 0, 0};
-  if (fabsf(n[0]) < 0.5f) a[0] = 1; else a[1] = 1;
-  float d = dot3(a, n);
-  float t1[3] = {a[0] - d * n[0], a[1] - d * n[1], a[2] - d * n[2]};
-  float l = sqrtf(dot3(t1, t1));
+__device__ void make_frame(real* F, const real* n) {
+  real a[3] = {0, 0, 0};
+  if (fabs(n[0]) < 0.5) a[0] = 1; else a[1] = 1;
+  real d = dot3(a, n);
+  real t1[3] = {a[0] - d * n[0], a[1] - d * n[1], a[2] - d * n[2]};
+  real l = sqrt(dot3(t1, t1));
   t1[0] /= l; t1[1] /= l; t1[2] /= l;
-  float t2[3];
+  real t2[3];
   cross3(t2, n, t1);
   F[0] = n[0]; F[1] = n[1]; F[2] = n[2];
   F[3] = t1[0]; F[4] = t1[1]; F[5] = t1[2];
   F[6] = t2[0]; F[7] = t2[1]; F[8] = t2[2];
 }
 
-struct GeomV { int type; float size[3]; float c[3]; float R[9]; float rbound; float friction; };
+struct GeomV { int type; real size[3]; real c[3]; real R[9]; real rbound; real friction; };
 
 __device__ __forceinline__ void load_geom(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int g, GeomV& G) {
   if (g == T->geom_obj) {
@@ -570,8 +573,8 @@ __device__ __forceinline__ void load_geom(Shared& S, const gm_model* __restrict_
   } else {
     G.type = m->geom_type[g];
     ld3(G.size, m->geom_size[g]);
-    G.rbound = (float)m->geom_rbound[g];
-    G.friction = (float)m->geom_friction[g];
+    G.rbound = (real)m->geom_rbound[g];
+    G.friction = (real)m->geom_friction[g];
   }
   for (int k = 0; k < 3; k++) G.c[k] = S.gxpos[g][k];
   for (int k = 0; k < 9; k++) G.R[k] = S.gxmat[g][k];
@@ -579,140 +582,140 @@ __device__ __forceinline__ void load_geom(Shared& S, const gm_model* __restrict_
 
 // plane-X multi-contact generators: k-th candidate point (returns 0 if none)
 __device__ __forceinline__ int plane_box_point(const GeomV& P, const GeomV& B, int i, Hit& h) {
-  float nz[3] = {P.R[2], P.R[5], P.R[8]};
-  float s[3] = {(i & 1) ? B.size[0] : -B.size[0], (i & 2) ? B.size[1] : -B.size[1], (i & 4) ? B.size[2] : -B.size[2]};
-  float v[3];
+  real nz[3] = {P.R[2], P.R[5], P.R[8]};
+  real s[3] = {(i & 1) ? B.size[0] : -B.size[0], (i & 2) ? B.size[1] : -B.size[1], (i & 4) ? B.size[2] : -B.size[2]};
+  real v[3];
   mulmv3(v, B.R, s);
   v[0] += B.c[0]; v[1] += B.c[1]; v[2] += B.c[2];
-  float dv[3] = {v[0] - P.c[0], v[1] - P.c[1], v[2] - P.c[2]};
-  float d = dot3(dv, nz);
+  real dv[3] = {v[0] - P.c[0], v[1] - P.c[1], v[2] - P.c[2]};
+  real d = dot3(dv, nz);
   if (!(d < 0)) return 0;
   h.dist = d;
-  for (int k = 0; k < 3; k++) { h.pos[k] = v[k] - 0.5f * d * nz[k]; h.n[k] = nz[k]; }
+  for (int k = 0; k < 3; k++) { h.pos[k] = v[k] - 0.5 * d * nz[k]; h.n[k] = nz[k]; }
   return 1;
 }
 __device__ __forceinline__ int plane_cyl_point(const GeomV& P, const GeomV& Cy, int i, Hit& h) {
-  float nz[3] = {P.R[2], P.R[5], P.R[8]};
-  float a[3] = {Cy.R[2], Cy.R[5], Cy.R[8]};
-  float r = Cy.size[0], hh = Cy.size[1];
-  float na = dot3(nz, a);
-  float w[3] = {-nz[0] + na * a[0], -nz[1] + na * a[1], -nz[2] + na * a[2]};
-  float lw = sqrtf(dot3(w, w));
-  if (lw < 1e-6f) { w[0] = Cy.R[0]; w[1] = Cy.R[3]; w[2] = Cy.R[6]; }
+  real nz[3] = {P.R[2], P.R[5], P.R[8]};
+  real a[3] = {Cy.R[2], Cy.R[5], Cy.R[8]};
+  real r = Cy.size[0], hh = Cy.size[1];
+  real na = dot3(nz, a);
+  real w[3] = {-nz[0] + na * a[0], -nz[1] + na * a[1], -nz[2] + na * a[2]};
+  real lw = sqrt(dot3(w, w));
+  if (lw < 1e-6) { w[0] = Cy.R[0]; w[1] = Cy.R[3]; w[2] = Cy.R[6]; }
   else { w[0] /= lw; w[1] /= lw; w[2] /= lw; }
-  float axw[3];
+  real axw[3];
   cross3(axw, a, w);
   int s = i >> 2, k = i & 3;
-  float sg = s == 0 ? 1.0f : -1.0f;
-  float dir[3];
+  real sg = s == 0 ? 1.0 : -1.0;
+  real dir[3];
   if (k == 0) { dir[0] = w[0]; dir[1] = w[1]; dir[2] = w[2]; }
   else if (k == 1) { dir[0] = axw[0]; dir[1] = axw[1]; dir[2] = axw[2]; }
   else if (k == 2) { dir[0] = -w[0]; dir[1] = -w[1]; dir[2] = -w[2]; }
   else { dir[0] = -axw[0]; dir[1] = -axw[1]; dir[2] = -axw[2]; }
-  float v[3];
+  real v[3];
   for (int t = 0; t < 3; t++) v[t] = Cy.c[t] + sg * hh * a[t] + r * dir[t];
-  float dv[3] = {v[0] - P.c[0], v[1] - P.c[1], v[2] - P.c[2]};
-  float d = dot3(dv, nz);
+  real dv[3] = {v[0] - P.c[0], v[1] - P.c[1], v[2] - P.c[2]};
+  real d = dot3(dv, nz);
   if (!(d < 0)) return 0;
   h.dist = d;
-  for (int t = 0; t < 3; t++) { h.pos[t] = v[t] - 0.5f * d * nz[t]; h.n[t] = nz[t]; }
+  for (int t = 0; t < 3; t++) { h.pos[t] = v[t] - 0.5 * d * nz[t]; h.n[t] = nz[t]; }
   return 1;
 }
 __device__ int plane_sphere(const GeomV& P, const GeomV& Sp, Hit& h) {
-  float nz[3] = {P.R[2], P.R[5], P.R[8]};
-  float r = Sp.size[0];
-  float dv[3] = {Sp.c[0] - P.c[0], Sp.c[1] - P.c[1], Sp.c[2] - P.c[2]};
-  float dist = dot3(dv, nz) - r;
+  real nz[3] = {P.R[2], P.R[5], P.R[8]};
+  real r = Sp.size[0];
+  real dv[3] = {Sp.c[0] - P.c[0], Sp.c[1] - P.c[1], Sp.c[2] - P.c[2]};
+  real dist = dot3(dv, nz) - r;
   if (!(dist < 0)) return 0;
   h.dist = dist;
-  for (int k = 0; k < 3; k++) { h.pos[k] = Sp.c[k] - nz[k] * (r + 0.5f * dist); h.n[k] = nz[k]; }
+  for (int k = 0; k < 3; k++) { h.pos[k] = Sp.c[k] - nz[k] * (r + 0.5 * dist); h.n[k] = nz[k]; }
   return 1;
 }
 __device__ int sphere_box(const GeomV& Sp, const GeomV& B, Hit& h) {
-  const float* R = B.R;
-  const float* hs = B.size;
-  float r = Sp.size[0];
-  float dv[3] = {Sp.c[0] - B.c[0], Sp.c[1] - B.c[1], Sp.c[2] - B.c[2]};
-  float cl[3];
+  const real* R = B.R;
+  const real* hs = B.size;
+  real r = Sp.size[0];
+  real dv[3] = {Sp.c[0] - B.c[0], Sp.c[1] - B.c[1], Sp.c[2] - B.c[2]};
+  real cl[3];
   mulmtv3(cl, R, dv);
-  float q[3];
+  real q[3];
   int inside = 1;
   for (int k = 0; k < 3; k++) {
     q[k] = cl[k];
     if (q[k] > hs[k]) { q[k] = hs[k]; inside = 0; }
     if (q[k] < -hs[k]) { q[k] = -hs[k]; inside = 0; }
   }
-  float nl[3], dist, ql[3];
+  real nl[3], dist, ql[3];
   if (!inside) {
-    float df[3] = {cl[0] - q[0], cl[1] - q[1], cl[2] - q[2]};
-    float l = sqrtf(dot3(df, df));
-    if (l < 1e-12f) return 0;
+    real df[3] = {cl[0] - q[0], cl[1] - q[1], cl[2] - q[2]};
+    real l = sqrt(dot3(df, df));
+    if (l < 1e-12) return 0;
     dist = l - r;
     if (!(dist < 0)) return 0;
     nl[0] = -df[0] / l; nl[1] = -df[1] / l; nl[2] = -df[2] / l;
     ql[0] = q[0]; ql[1] = q[1]; ql[2] = q[2];
   } else {
     int kmin = 0;
-    float best = hs[0] - fabsf(cl[0]);
-    for (int k = 1; k < 3; k++) { float v = hs[k] - fabsf(cl[k]); if (v < best) { best = v; kmin = k; } }
-    float sg = cl[kmin] >= 0 ? 1.0f : -1.0f;
+    real best = hs[0] - fabs(cl[0]);
+    for (int k = 1; k < 3; k++) { real v = hs[k] - fabs(cl[k]); if (v < best) { best = v; kmin = k; } }
+    real sg = cl[kmin] >= 0 ? 1.0 : -1.0;
     nl[0] = nl[1] = nl[2] = 0; nl[kmin] = -sg;
     dist = -(best + r);
     ql[0] = cl[0]; ql[1] = cl[1]; ql[2] = cl[2]; ql[kmin] = sg * hs[kmin];
   }
-  float n[3], qw[3];
+  real n[3], qw[3];
   mulmv3(n, R, nl);
   mulmv3(qw, R, ql);
   h.dist = dist;
   for (int k = 0; k < 3; k++) {
     qw[k] += B.c[k];
-    float sp = Sp.c[k] + n[k] * r;
-    h.pos[k] = 0.5f * (qw[k] + sp);
+    real sp = Sp.c[k] + n[k] * r;
+    h.pos[k] = 0.5 * (qw[k] + sp);
     h.n[k] = n[k];
   }
   return 1;
 }
 
 // ---- MPR ----
-struct SV { float v[3], p1[3], p2[3]; };
-__device__ __forceinline__ void support_geom(const GeomV& G, const float* d, float* out) {
-  float dl[3];
+struct SV { real v[3], p1[3], p2[3]; };
+__device__ __forceinline__ void support_geom(const GeomV& G, const real* d, real* out) {
+  real dl[3];
   mulmtv3(dl, G.R, d);
-  float pl[3] = {0, 0, 0};
+  real pl[3] = {0, 0, 0};
   if (G.type == GM_GEOM_BOX) {
     for (int k = 0; k < 3; k++) pl[k] = dl[k] >= 0 ? G.size[k] : -G.size[k];
   } else if (G.type == GM_GEOM_CYLINDER) {
-    float rr = sqrtf(dl[0] * dl[0] + dl[1] * dl[1]);
-    if (rr > 1e-12f) { pl[0] = G.size[0] * dl[0] / rr; pl[1] = G.size[0] * dl[1] / rr; }
+    real rr = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
+    if (rr > 1e-12) { pl[0] = G.size[0] * dl[0] / rr; pl[1] = G.size[0] * dl[1] / rr; }
     pl[2] = dl[2] >= 0 ? G.size[1] : -G.size[1];
   } else if (G.type == GM_GEOM_SPHERE) {
-    float l = sqrtf(dot3(dl, dl));
-    if (l > 1e-12f) { pl[0] = dl[0] * G.size[0] / l; pl[1] = dl[1] * G.size[0] / l; pl[2] = dl[2] * G.size[0] / l; }
+    real l = sqrt(dot3(dl, dl));
+    if (l > 1e-12) { pl[0] = dl[0] * G.size[0] / l; pl[1] = dl[1] * G.size[0] / l; pl[2] = dl[2] * G.size[0] / l; }
   }
   mulmv3(out, G.R, pl);
   out[0] += G.c[0]; out[1] += G.c[1]; out[2] += G.c[2];
 }
-__device__ __forceinline__ void mpr_support(const GeomV& A, const GeomV& B, const float* d, SV& sv) {
-  float nd[3] = {-d[0], -d[1], -d[2]};
+__device__ __forceinline__ void mpr_support(const GeomV& A, const GeomV& B, const real* d, SV& sv) {
+  real nd[3] = {-d[0], -d[1], -d[2]};
   support_geom(A, d, sv.p1);
   support_geom(B, nd, sv.p2);
   sv.v[0] = sv.p1[0] - sv.p2[0]; sv.v[1] = sv.p1[1] - sv.p2[1]; sv.v[2] = sv.p1[2] - sv.p2[2];
 }
-__device__ __forceinline__ int fzero(float x) { return fabsf(x) < 1e-12f; }
-__device__ __forceinline__ void normalize3(float* d) {
-  float l = sqrtf(dot3(d, d));
-  if (l > 0) { d[0] /= l; d[1] /= l; d[2] /= l; }
+__device__ __forceinline__ int fzero(real x) { return fabs(x) < 1e-12; }
+__device__ __forceinline__ void normalize3(real* d) {
+  real l = sqrt(dot3(d, d));
+  if (l > 0) { real il = 1.0 / l; d[0] *= il; d[1] *= il; d[2] *= il; }
 }
-__device__ void portal_dir(const SV* P, float* dir) {
-  float a[3] = {P[2].v[0] - P[1].v[0], P[2].v[1] - P[1].v[1], P[2].v[2] - P[1].v[2]};
-  float b[3] = {P[3].v[0] - P[1].v[0], P[3].v[1] - P[1].v[1], P[3].v[2] - P[1].v[2]};
+__device__ void portal_dir(const SV* P, real* dir) {
+  real a[3] = {P[2].v[0] - P[1].v[0], P[2].v[1] - P[1].v[1], P[2].v[2] - P[1].v[2]};
+  real b[3] = {P[3].v[0] - P[1].v[0], P[3].v[1] - P[1].v[1], P[3].v[2] - P[1].v[2]};
   cross3(dir, a, b);
   normalize3(dir);
 }
 __device__ void expand_portal(SV* P, const SV& v4) {
-  float v4v0[3];
+  real v4v0[3];
   cross3(v4v0, v4.v, P[0].v);
-  float d = dot3(P[1].v, v4v0);
+  real d = dot3(P[1].v, v4v0);
   if (d > 0) {
     d = dot3(P[2].v, v4v0);
     if (d > 0) P[1] = v4; else P[3] = v4;
@@ -721,47 +724,47 @@ __device__ void expand_portal(SV* P, const SV& v4) {
     if (d > 0) P[2] = v4; else P[1] = v4;
   }
 }
-__device__ int reach_tol(const SV* P, const SV& v4, const float* dir, float tol) {
-  float dv1 = dot3(P[1].v, dir), dv2 = dot3(P[2].v, dir), dv3 = dot3(P[3].v, dir), dv4 = dot3(v4.v, dir);
-  float d1 = dv4 - dv1, d2 = dv4 - dv2, d3 = dv4 - dv3;
-  float dd = fminf(fminf(d1, d2), d3);
-  return dd < tol || fabsf(dd - tol) < 1e-12f;
+__device__ int reach_tol(const SV* P, const SV& v4, const real* dir, real tol) {
+  real dv1 = dot3(P[1].v, dir), dv2 = dot3(P[2].v, dir), dv3 = dot3(P[3].v, dir), dv4 = dot3(v4.v, dir);
+  real d1 = dv4 - dv1, d2 = dv4 - dv2, d3 = dv4 - dv3;
+  real dd = fmin(fmin(d1, d2), d3);
+  return dd < tol || fabs(dd - tol) < 1e-12;
 }
-__device__ void tri_closest_origin(const float* a, const float* b, const float* c, float* out) {
-  float ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
-  float ac[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
-  float ap[3] = {-a[0], -a[1], -a[2]};
-  float d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+__device__ void tri_closest_origin(const real* a, const real* b, const real* c, real* out) {
+  real ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+  real ac[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+  real ap[3] = {-a[0], -a[1], -a[2]};
+  real d1 = dot3(ab, ap), d2 = dot3(ac, ap);
   if (d1 <= 0 && d2 <= 0) { out[0] = a[0]; out[1] = a[1]; out[2] = a[2]; return; }
-  float bp[3] = {-b[0], -b[1], -b[2]};
-  float d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  real bp[3] = {-b[0], -b[1], -b[2]};
+  real d3 = dot3(ab, bp), d4 = dot3(ac, bp);
   if (d3 >= 0 && d4 <= d3) { out[0] = b[0]; out[1] = b[1]; out[2] = b[2]; return; }
-  float vc = d1 * d4 - d3 * d2;
-  if (vc <= 0 && d1 >= 0 && d3 <= 0) { float v = d1 / (d1 - d3); for (int k = 0; k < 3; k++) out[k] = a[k] + v * ab[k]; return; }
-  float cp[3] = {-c[0], -c[1], -c[2]};
-  float d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+  real vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) { real v = d1 / (d1 - d3); for (int k = 0; k < 3; k++) out[k] = a[k] + v * ab[k]; return; }
+  real cp[3] = {-c[0], -c[1], -c[2]};
+  real d5 = dot3(ab, cp), d6 = dot3(ac, cp);
   if (d6 >= 0 && d5 <= d6) { out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; return; }
-  float vb = d5 * d2 - d1 * d6;
-  if (vb <= 0 && d2 >= 0 && d6 <= 0) { float w = d2 / (d2 - d6); for (int k = 0; k < 3; k++) out[k] = a[k] + w * ac[k]; return; }
-  float va = d3 * d6 - d5 * d4;
+  real vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) { real w = d2 / (d2 - d6); for (int k = 0; k < 3; k++) out[k] = a[k] + w * ac[k]; return; }
+  real va = d3 * d6 - d5 * d4;
   if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
-    float w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    real w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
     for (int k = 0; k < 3; k++) out[k] = b[k] + w * (c[k] - b[k]);
     return;
   }
-  float den = 1.0f / (va + vb + vc);
-  float v = vb * den, w = vc * den;
+  real den = 1.0 / (va + vb + vc);
+  real v = vb * den, w = vc * den;
   for (int k = 0; k < 3; k++) out[k] = a[k] + ab[k] * v + ac[k] * w;
 }
-__device__ void mpr_pos(const SV* P, float* pos) {
-  float dir[3];
+__device__ void mpr_pos(const SV* P, real* pos) {
+  real dir[3];
   portal_dir(P, dir);
-  float t[3];
-  cross3(t, P[1].v, P[2].v); float b0 = dot3(t, P[3].v);
-  cross3(t, P[3].v, P[2].v); float b1 = dot3(t, P[0].v);
-  cross3(t, P[0].v, P[1].v); float b2 = dot3(t, P[3].v);
-  cross3(t, P[2].v, P[1].v); float b3 = dot3(t, P[0].v);
-  float sum = b0 + b1 + b2 + b3;
+  real t[3];
+  cross3(t, P[1].v, P[2].v); real b0 = dot3(t, P[3].v);
+  cross3(t, P[3].v, P[2].v); real b1 = dot3(t, P[0].v);
+  cross3(t, P[0].v, P[1].v); real b2 = dot3(t, P[3].v);
+  cross3(t, P[2].v, P[1].v); real b3 = dot3(t, P[0].v);
+  real sum = b0 + b1 + b2 + b3;
   if (sum <= 0) {
     b0 = 0;
     cross3(t, P[2].v, P[3].v); b1 = dot3(t, dir);
@@ -769,33 +772,34 @@ __device__ void mpr_pos(const SV* P, float* pos) {
     cross3(t, P[1].v, P[2].v); b3 = dot3(t, dir);
     sum = b1 + b2 + b3;
   }
-  float inv = 1.0f / sum;
-  float bb[4] = {b0, b1, b2, b3};
-  float p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
+  real inv = 1.0 / sum;
+  real bb[4] = {b0, b1, b2, b3};
+  real p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
   for (int i = 0; i < 4; i++)
     for (int k = 0; k < 3; k++) { p1[k] += bb[i] * P[i].p1[k]; p2[k] += bb[i] * P[i].p2[k]; }
-  for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p1[k] + p2[k]) * inv;
+  for (int k = 0; k < 3; k++) pos[k] = 0.5 * (p1[k] + p2[k]) * inv;
 }
-__device__ int mpr(const GeomV& A, const GeomV& B, float tol, int maxit, Hit& h) {
+__device__ int mpr(const GeomV& A, const GeomV& B, real tol, int maxit, Hit& h) {
   SV P[4];
   for (int k = 0; k < 3; k++) { P[0].v[k] = A.c[k] - B.c[k]; P[0].p1[k] = A.c[k]; P[0].p2[k] = B.c[k]; }
-  if (fzero(P[0].v[0]) && fzero(P[0].v[1]) && fzero(P[0].v[2])) P[0].v[0] += 1e-5f;
-  float d[3] = {-P[0].v[0], -P[0].v[1], -P[0].v[2]};
+  if (fzero(P[0].v[0]) && fzero(P[0].v[1]) && fzero(P[0].v[2])) P[0].v[0] += 1e-5;
+  real d[3] = {-P[0].v[0], -P[0].v[1], -P[0].v[2]};
   normalize3(d);
   mpr_support(A, B, d, P[1]);
   if (dot3(P[1].v, d) <= 0) return 0;
   cross3(d, P[0].v, P[1].v);
-  if (fzero(sqrtf(dot3(d, d)))) {
-    float l1 = sqrtf(dot3(P[1].v, P[1].v));
+  if (fzero(sqrt(dot3(d, d)))) {
+    real l1 = sqrt(dot3(P[1].v, P[1].v));
     if (fzero(l1)) return 0;
     h.dist = -l1;
-    for (int k = 0; k < 3; k++) { h.n[k] = P[1].v[k] / l1; h.pos[k] = 0.5f * (P[1].p1[k] + P[1].p2[k]); }
+    real il = 1.0 / l1;
+    for (int k = 0; k < 3; k++) { h.n[k] = P[1].v[k] * il; h.pos[k] = 0.5 * (P[1].p1[k] + P[1].p2[k]); }
     return 1;
   }
   normalize3(d);
   mpr_support(A, B, d, P[2]);
   if (dot3(P[2].v, d) <= 0) return 0;
-  float va[3], vb[3];
+  real va[3], vb[3];
   for (int k = 0; k < 3; k++) { va[k] = P[1].v[k] - P[0].v[k]; vb[k] = P[2].v[k] - P[0].v[k]; }
   cross3(d, va, vb);
   normalize3(d);
@@ -806,10 +810,10 @@ __device__ int mpr(const GeomV& A, const GeomV& B, float tol, int maxit, Hit& h)
     if (dot3(P[3].v, d) <= 0) return 0;
     int cont = 0;
     cross3(va, P[1].v, P[3].v);
-    if (dot3(va, P[0].v) < -1e-12f) { P[2] = P[3]; cont = 1; }
+    if (dot3(va, P[0].v) < -1e-12) { P[2] = P[3]; cont = 1; }
     if (!cont) {
       cross3(va, P[3].v, P[2].v);
-      if (dot3(va, P[0].v) < -1e-12f) { P[1] = P[3]; cont = 1; }
+      if (dot3(va, P[0].v) < -1e-12) { P[1] = P[3]; cont = 1; }
     }
     if (!cont) break;
     for (int k = 0; k < 3; k++) { va[k] = P[1].v[k] - P[0].v[k]; vb[k] = P[2].v[k] - P[0].v[k]; }
@@ -820,10 +824,10 @@ __device__ int mpr(const GeomV& A, const GeomV& B, float tol, int maxit, Hit& h)
   it = 0;
   for (;;) {
     portal_dir(P, d);
-    if (dot3(d, P[1].v) >= -1e-12f) break;
+    if (dot3(d, P[1].v) >= -1e-12) break;
     SV v4;
     mpr_support(A, B, d, v4);
-    float dv4 = dot3(v4.v, d);
+    real dv4 = dot3(v4.v, d);
     if (!(fzero(dv4) || dv4 > 0)) return 0;
     if (reach_tol(P, v4, d, tol)) return 0;
     expand_portal(P, v4);
@@ -835,12 +839,13 @@ __device__ int mpr(const GeomV& A, const GeomV& B, float tol, int maxit, Hit& h)
     SV v4;
     mpr_support(A, B, d, v4);
     if (reach_tol(P, v4, d, tol) || it > maxit) {
-      float cp[3];
+      real cp[3];
       tri_closest_origin(P[1].v, P[2].v, P[3].v, cp);
-      float depth = sqrtf(dot3(cp, cp));
+      real depth = sqrt(dot3(cp, cp));
       if (fzero(depth)) return 0;
       h.dist = -depth;
-      h.n[0] = cp[0] / depth; h.n[1] = cp[1] / depth; h.n[2] = cp[2] / depth;
+      real id = 1.0 / depth;
+      h.n[0] = cp[0] * id; h.n[1] = cp[1] * id; h.n[2] = cp[2] * id;
       mpr_pos(P, h.pos);
       return depth > 0;
     }
@@ -854,14 +859,14 @@ __device__ __forceinline__ void canon_pair(int a, int b, int ta, int tb, int& g1
   if (ta > tb || (ta == tb && a > b)) { g1 = b; g2 = a; } else { g1 = a; g2 = b; }
 }
 
-__device__ void write_contact(Shared& S, int slot, int g1, int g2, const Hit& h, float mu) {
-  float* C = S.con[slot];
+__device__ void write_contact(Shared& S, int slot, int g1, int g2, const Hit& h, real mu) {
+  real* C = S.con[slot];
   C[0] = h.dist;
   C[1] = h.pos[0]; C[2] = h.pos[1]; C[3] = h.pos[2];
   make_frame(C + 4, h.n);
   C[13] = mu;
   C[14] = 0; C[15] = 0; C[16] = 0;
-  C[17] = (float)g1; C[18] = (float)g2;
+  C[17] = (real)g1; C[18] = (real)g2;
 }
 
 __device__ void collision(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
@@ -877,12 +882,12 @@ __device__ void collision(Shared& S, const gm_model* __restrict__ m, const GmTop
     load_geom(S, m, T, g2, B);
     bool pass;
     if (A.type == GM_GEOM_PLANE) {
-      float nz[3] = {A.R[2], A.R[5], A.R[8]};
-      float dv[3] = {B.c[0] - A.c[0], B.c[1] - A.c[1], B.c[2] - A.c[2]};
+      real nz[3] = {A.R[2], A.R[5], A.R[8]};
+      real dv[3] = {B.c[0] - A.c[0], B.c[1] - A.c[1], B.c[2] - A.c[2]};
       pass = !(dot3(dv, nz) > B.rbound);
     } else {
-      float dv[3] = {B.c[0] - A.c[0], B.c[1] - A.c[1], B.c[2] - A.c[2]};
-      float rr = A.rbound + B.rbound;
+      real dv[3] = {B.c[0] - A.c[0], B.c[1] - A.c[1], B.c[2] - A.c[2]};
+      real rr = A.rbound + B.rbound;
       pass = !(dot3(dv, dv) > rr * rr);
     }
     if (pass) {
@@ -900,7 +905,7 @@ __device__ void collision(Shared& S, const gm_model* __restrict__ m, const GmTop
       } else if (A.type == GM_GEOM_SPHERE && B.type == GM_GEOM_BOX) {
         kind = 1; cnt = sphere_box(A, B, single);
       } else {
-        kind = 1; cnt = mpr(A, B, (float)m->mpr_tolerance, m->mpr_iterations, single);
+        kind = 1; cnt = mpr(A, B, (real)m->mpr_tolerance, m->mpr_iterations, single);
         if (cnt && !(single.dist < 0)) cnt = 0;
       }
     }
@@ -910,7 +915,7 @@ __device__ void collision(Shared& S, const gm_model* __restrict__ m, const GmTop
   int off = 0, total = 0;
   for (int i = 0; i < NT; i++) { int c = S.cnt[i]; if (i < lane) off += c; total += c; }
   if (cnt > 0) {
-    float mu = fmaxf(A.friction, B.friction);
+    real mu = fmax(A.friction, B.friction);
     if (kind == 1) {
       if (off < GM_MAX_CON) write_contact(S, off, g1, g2, single, mu);
     } else {
@@ -934,11 +939,10 @@ __device__ __forceinline__ int geom_chain(const GmTopo* T, int g) { return T->ge
 
 // compact Jacobian row of contact c along unit direction `dir` (rows of the frame)
 __device__ void contact_jac(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int c,
-                            const float* dirf, real* J, int& grp) {
+                            const real* dir, real* J, int& grp) {
   for (int k = 0; k < CW; k++) J[k] = 0;
-  const float* C = S.con[c];
+  const real* C = S.con[c];
   const real pos[3] = {C[1], C[2], C[3]};
-  const real dir[3] = {dirf[0], dirf[1], dirf[2]};
   int gs[2] = {(int)C[17], (int)C[18]};
   real sg[2] = {-1.0f, 1.0f};
   grp = -1;
@@ -994,17 +998,17 @@ __device__ __forceinline__ real row_dot_dofs(Shared& S, const GmTopo* __restrict
   return acc;
 }
 
-__device__ float impedance(const gm_model* __restrict__ m, float r) {
-  float dmin = (float)m->solimp[0], dmax = (float)m->solimp[1], width = (float)m->solimp[2];
-  float mid = (float)m->solimp[3], pw = (float)m->solimp[4];
-  if (dmin == dmax || width <= 1e-15f) return dmin;
-  float x = fabsf(r) / width;
+__device__ real impedance(const gm_model* __restrict__ m, real r) {
+  real dmin = m->solimp[0], dmax = m->solimp[1], width = m->solimp[2];
+  real mid = m->solimp[3], pw = m->solimp[4];
+  if (dmin == dmax || width <= 1e-15) return dmin;
+  real x = fabs(r) / width;
   if (x >= 1) return dmax;
   if (x <= 0) return dmin;
-  float y;
+  real y;
   if (pw == 1) y = x;
-  else if (x <= mid) y = powf(x, pw) / powf(mid, pw - 1);
-  else y = 1 - powf(1 - x, pw) / powf(1 - mid, pw - 1);
+  else if (x <= mid) y = pow(x, pw) / pow(mid, pw - 1);
+  else y = 1 - pow(1 - x, pw) / pow(1 - mid, pw - 1);
   return dmin + y * (dmax - dmin);
 }
 
@@ -1030,7 +1034,7 @@ __device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmT
     } else {
       int r = lane - nl;
       int c = r >> 2, e = r & 3;
-      const float* C = S.con[c];
+      const real* C = S.con[c];
       real Jn[CW], Jt[CW];
       int g2;
       contact_jac(S, m, T, c, C + 4, Jn, grp);
@@ -1068,8 +1072,8 @@ __device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmT
     for (int k = 0; k < CW - 1; k++) Yd[k] = 0;
   }
   const bool gj = grp >= 0 && grp <= 3;
-  // Delassus column A[:, lane] = Y D^-1 Y_lane^T, accumulated in fp64, held in fp32 VGPRs
-  float A[GM_MAX_EFC];
+  // Delassus column A[:, lane] = Y D^-1 Y_lane^T, held in this lane's VGPRs
+  real A[GM_MAX_EFC];
 #pragma unroll
   for (int i = 0; i < GM_MAX_EFC; i++) {
     real acc = 0;
@@ -1083,7 +1087,7 @@ __device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmT
           for (int q = 1; q <= CLMAX; q++) acc += Yd[6 + q] * Yi[6 + q];
       }
     }
-    A[i] = (float)acc;
+    A[i] = acc;
   }
   // impedance / reference acceleration (mj_makeImpedance)
   real h = m->timestep;
@@ -1092,32 +1096,35 @@ __device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmT
   real dr = m->solref[1], dmax = m->solimp[1];
   real K = 1.0 / (dmax * dmax * tc * tc * dr * dr);
   real Bd = 2.0 / (dmax * tc);
-  float Ajj = 0;
+  real Ajj = 0;
 #pragma unroll
   for (int i = 0; i < GM_MAX_EFC; i++) if (i == lane) Ajj = A[i];
-  real imp = impedance(m, (float)pos);
+  real imp = impedance(m, pos);
   real aref = -Bd * vel - K * imp * pos;
-  float R = (float)((1 - imp) / imp * (real)Ajj);
-  if (R < 1e-15f) R = 1e-15f;
-  float invd = (lane < nefc) ? 1.0f / (Ajj + R) : 0.0f;
-  float res = (lane < nefc) ? (float)(a0 - aref) : 0.0f;   // (A f + b) with f = 0
-  float f = 0;
-  // projected Gauss-Seidel, residual broadcast through v_readlane
+  real R = (1 - imp) / imp * Ajj;
+  if (R < 1e-15) R = 1e-15;
+  real dinv = Ajj + R;
+  real res = (lane < nefc) ? (a0 - aref) : 0.0;   // (A f + b) with f = 0
+  real f = 0;
+  // projected Gauss-Seidel, each row's update broadcast through v_readlane
   for (int it = 0; it < m->pgs_iterations; it++) {
 #pragma unroll
     for (int r = 0; r < GM_MAX_EFC; r++) {
       if (r < nefc) {
-        float g = res + R * f;
-        float fn = f - g * invd;
+        real g = res + R * f;
+        real fn = f - g / dinv;
         if (is_contact && fn < 0) fn = 0;
-        float dl = fn - f;
-        float delta = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dl), r));
+        real dl = fn - f;
+        long long bits = __double_as_longlong(dl);
+        int lo = __builtin_amdgcn_readlane((int)bits, r);
+        int hi = __builtin_amdgcn_readlane((int)(bits >> 32), r);
+        real delta = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
         res += A[r] * delta;
-        if (lane == r) f += delta;
+        if (lane == r) f = fn;
       }
     }
   }
-  S.efc_f[lane] = (lane < nefc) ? f : 0.0f;
+  S.efc_f[lane] = (lane < nefc) ? f : 0.0;
   __syncthreads();
 }
 
@@ -1175,8 +1182,8 @@ __device__ void constraint_accel(Shared& S, const GmTopo* __restrict__ T, int la
   }
   // contact forces in the contact frame (mj_contactForce, pyramidal decode)
   if (lane < S.ncon) {
-    const float* fe = &S.efc_f[S.nlockrows + 4 * lane];
-    float mu = S.con[lane][13];
+    const real* fe = &S.efc_f[S.nlockrows + 4 * lane];
+    real mu = S.con[lane][13];
     S.con[lane][14] = fe[0] + fe[1] + fe[2] + fe[3];
     S.con[lane][15] = mu * (fe[0] - fe[1]);
     S.con[lane][16] = mu * (fe[2] - fe[3]);
@@ -1455,7 +1462,7 @@ __device__ void extract_forces(Shared& S, const gm_model* __restrict__ m, const 
   for (int a = 0; a < 4; a++) for (int k = 0; k < 3; k++) ag[a][k] = 0;
   for (int a = 0; a < 3; a++) for (int k = 0; k < 3; k++) gg[a][k] = 0;
   for (int i = 0; i < S.ncon; i++) {
-    const float* C = S.con[i];
+    const real* C = S.con[i];
     int c1 = m->geom_class[(int)C[17]], c2 = m->geom_class[(int)C[18]];
     int w_obj = (c1 == GM_CLS_OBJECT || c2 == GM_CLS_OBJECT);
     int w_f0 = (c1 == GM_CLS_FINGER1 || c2 == GM_CLS_FINGER1);
@@ -1542,17 +1549,29 @@ __device__ void monitor_sensors(Shared& S, const gm_model* __restrict__ m, const
 }
 
 // ============================================================ one full substep
-__device__ void physics_substep(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+#define PH(k) do { if (prof) { unsigned long long t_ = clock64(); if (lane == 0) S.tph[k] += t_ - t0; t0 = t_; } } while (0)
+__device__ void physics_substep(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
+                                bool prof = false) {
+  unsigned long long t0 = prof ? clock64() : 0;
   if (lane < T->nq) S.qpos_pre[lane] = S.s.qpos[lane];
   kinematics(S, m, T, lane);
+  PH(0);
   crb_rne(S, m, T, lane);
+  PH(1);
   mass_and_forces(S, m, T, lane);
+  PH(2);
   factor(S, T, lane);
+  PH(3);
   solve_full(S, T, S.frc, S.qacc_s, lane);
+  PH(4);
   collision(S, m, T, lane);
+  PH(5);
   constraints(S, m, T, lane);
+  PH(6);
   constraint_accel(S, T, lane);
+  PH(7);
   integrate(S, m, T, lane);
+  PH(8);
 }
 
 // ============================================================ env-step epilogue (lane 0)
@@ -1888,11 +1907,17 @@ extern "C" __global__ __launch_bounds__(NT) void gm_step_kernel(
     store_state(S, states + env, lane);
     return;
   }
+  const bool prof = dbg.phase != nullptr;
+  if (prof && lane < GM_NPHASE) S.tph[lane] = 0;
+  __syncthreads();
   int nsub = (mode == 2) ? 1 : C->sim_steps_per_action + S.s.extra_substeps;
   for (int i = 0; i < nsub; i++) {
-    physics_substep(S, m, T, lane);
+    physics_substep(S, m, T, lane, prof);
+    unsigned long long t0 = prof ? clock64() : 0;
     update_all(S, m, T, lane);
+    PH(9);
     monitor_sensors(S, m, C, T, lane);
+    PH(10);
   }
   if (mode == 2) {
     if (lane == 0) dbg.ncon[env] = S.ncon;
@@ -1900,7 +1925,7 @@ extern "C" __global__ __launch_bounds__(NT) void gm_step_kernel(
       float* o = dbg.contact + ((size_t)env * GM_MAX_CON + lane) * 16;
       for (int k = 0; k < 16; k++) o[k] = 0;
       if (lane < S.ncon) {
-        const float* Cc = S.con[lane];
+        const real* Cc = S.con[lane];
         o[0] = Cc[0];
         for (int k = 0; k < 3; k++) o[1 + k] = Cc[1 + k];
         for (int k = 0; k < 9; k++) o[4 + k] = Cc[4 + k];
@@ -1926,6 +1951,10 @@ extern "C" __global__ __launch_bounds__(NT) void gm_step_kernel(
     S.s.reward = r;
     rew[env] = r;
     done[env] = (uint8_t)d;
+  }
+  if (prof) {
+    __syncthreads();
+    if (lane < GM_NPHASE) dbg.phase[(size_t)env * GM_NPHASE + lane] = S.tph[lane];
   }
   store_state(S, states + env, lane);
 }
@@ -2029,6 +2058,21 @@ extern "C" __global__ void gm_action_kernel(GmEnvState* __restrict__ states, con
 }
 
 // ---------------------------------------------------------------- reset + spawn
+// MjEnv auto-reset bookkeeping (MjEnv.py:616-637, 2170-2263): an env whose episode
+// terminated (is_done) or truncated (num_action_steps >= max_episode_steps) hands its
+// episode return to `returns` and is flagged for gm_reset_kernel.
+extern "C" __global__ void gm_autoreset_mask_kernel(const GmEnvState* __restrict__ states,
+                                                    const uint8_t* __restrict__ done, int max_steps,
+                                                    uint8_t* __restrict__ mask, float* __restrict__ returns,
+                                                    int n_envs) {
+  int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n_envs) return;
+  const GmEnvState& s = states[env];
+  uint8_t r = (done[env] || (max_steps > 0 && s.num_action_steps >= max_steps)) ? 1 : 0;
+  mask[env] = r;
+  if (returns) returns[env] = r ? s.cumulative_reward : __builtin_nanf("");
+}
+
 // MjClass::reset (mjclass.cpp:434-486) -> luke::reset / calibrate_reset (non-first call),
 // configure_settings RNG draws, random_base_Z_movement, then spawn_object.
 extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, const gm_model* __restrict__ m,
@@ -2091,9 +2135,9 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
   const gm_object& o = objs[oi];
   s.obj_index = oi;
   s.obj_type = o.type;
-  s.obj_size[0] = (float)o.size[0]; s.obj_size[1] = (float)o.size[1]; s.obj_size[2] = (float)o.size[2];
-  s.obj_mass = (float)o.mass;
-  s.obj_friction = (float)o.friction;
+  s.obj_size[0] = o.size[0]; s.obj_size[1] = o.size[1]; s.obj_size[2] = o.size[2];
+  s.obj_mass = o.mass;
+  s.obj_friction = o.friction;
   double I0, I1, I2, rb, restz;
   if (o.type == GM_GEOM_BOX) {
     double a = 2 * o.size[0], bb = 2 * o.size[1], c = 2 * o.size[2];
@@ -2111,9 +2155,9 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
     rb = r;
     restz = r;
   }
-  s.obj_inertia[0] = (float)I0; s.obj_inertia[1] = (float)I1; s.obj_inertia[2] = (float)I2;
-  s.obj_rbound = (float)rb;
-  s.obj_rest_z = (float)restz;
+  s.obj_inertia[0] = I0; s.obj_inertia[1] = I1; s.obj_inertia[2] = I2;
+  s.obj_rbound = rb;
+  s.obj_rest_z = restz;
   int qa = T->qadr_obj;
   double x2 = sin(-sp.zrot / 2.0), w2 = cos(-sp.zrot / 2.0);
   double q4[4] = {x2, 0, 0, w2};   // reference QPos quirk: qx lands in MuJoCo's w slot
@@ -2138,23 +2182,23 @@ extern "C" __global__ void gm_settle_init_kernel(GmEnvState* __restrict__ states
   for (int st = 0; st < GM_NSTREAM; st++) s.ring_i[st] = -1;
   const gm_object& o = objs[0];
   s.obj_type = o.type;
-  s.obj_size[0] = (float)o.size[0]; s.obj_size[1] = (float)o.size[1]; s.obj_size[2] = (float)o.size[2];
-  s.obj_mass = (float)o.mass;
-  s.obj_friction = (float)o.friction;
+  s.obj_size[0] = o.size[0]; s.obj_size[1] = o.size[1]; s.obj_size[2] = o.size[2];
+  s.obj_mass = o.mass;
+  s.obj_friction = o.friction;
   if (o.type == GM_GEOM_BOX) {
     double a = 2 * o.size[0], bb = 2 * o.size[1], c = 2 * o.size[2];
-    s.obj_inertia[0] = (float)(o.mass * (bb * bb + c * c) / 12); s.obj_inertia[1] = (float)(o.mass * (a * a + c * c) / 12);
-    s.obj_inertia[2] = (float)(o.mass * (a * a + bb * bb) / 12);
-    s.obj_rbound = (float)sqrt(o.size[0] * o.size[0] + o.size[1] * o.size[1] + o.size[2] * o.size[2]);
+    s.obj_inertia[0] = (o.mass * (bb * bb + c * c) / 12); s.obj_inertia[1] = (o.mass * (a * a + c * c) / 12);
+    s.obj_inertia[2] = (o.mass * (a * a + bb * bb) / 12);
+    s.obj_rbound = sqrt(o.size[0] * o.size[0] + o.size[1] * o.size[1] + o.size[2] * o.size[2]);
   } else if (o.type == GM_GEOM_CYLINDER) {
     double r = o.size[0], hh = 2 * o.size[1];
-    s.obj_inertia[0] = s.obj_inertia[1] = (float)(o.mass * (3 * r * r + hh * hh) / 12);
-    s.obj_inertia[2] = (float)(o.mass * r * r / 2);
-    s.obj_rbound = (float)sqrt(o.size[0] * o.size[0] + o.size[1] * o.size[1]);
+    s.obj_inertia[0] = s.obj_inertia[1] = (o.mass * (3 * r * r + hh * hh) / 12);
+    s.obj_inertia[2] = (o.mass * r * r / 2);
+    s.obj_rbound = sqrt(o.size[0] * o.size[0] + o.size[1] * o.size[1]);
   } else {
     double r = o.size[0];
-    s.obj_inertia[0] = s.obj_inertia[1] = s.obj_inertia[2] = (float)(2 * o.mass * r * r / 5);
-    s.obj_rbound = (float)r;
+    s.obj_inertia[0] = s.obj_inertia[1] = s.obj_inertia[2] = (2 * o.mass * r * r / 5);
+    s.obj_rbound = r;
   }
 }
 

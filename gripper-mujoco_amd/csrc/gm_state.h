@@ -47,6 +47,8 @@ struct GmEnvState {
   double qvel[GM_MAX_DOF];
   double lock_q[GM_MAX_LOCK];
   double start_qpos[7];
+  double obj_size[3];
+  double obj_mass, obj_inertia[3], obj_friction, obj_rbound, obj_rest_z;
   // ---- floats ----
   float rand_mu[SL_N][3];
   float ring[GM_NSTREAM][GM_RING];
@@ -54,8 +56,6 @@ struct GmEnvState {
   float lev_last[GM_N_LINEAR];
   float cumulative_reward;
   float grp_peak_lateral;
-  float obj_size[3];
-  float obj_mass, obj_inertia[3], obj_friction, obj_rbound, obj_rest_z;
   float reward;
   // ---- ints ----
   int32_t ring_i[GM_NSTREAM];

@@ -188,6 +188,10 @@ def _declare(lib):
         "gm_stream": (vp, [vp]),
         "gm_last_step_ms": (i32, [vp, f32p]),
         "gm_debug_substep": (i32, [vp, i32p, f32p, f32p, f32p]),
+        "gm_step_profiled": (i32, [vp, C.POINTER(C.c_uint64)]),
+        "gm_set_stream": (i32, [vp, vp]),
+        "gm_autoreset": (i32, [vp, i32, vp, i32, vp]),
+        "gm_device_reset_mask": (vp, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -212,8 +216,9 @@ class ModelBlob:
         rc = lib.gm_build_model(C.byref(params), self.buf)
         if rc != 0:
             raise RuntimeError(f"gm_build_model failed ({rc})")
-        info = (C.c_int32 * 18)()
+        info = (C.c_int32 * 20)()
         lib.gm_model_info(self.buf, info)
+        self.nlock, self.nM = info[18], info[19]
         (self.nq, self.nv, self.nbody, self.ngeom, self.npair, self.n_seg, self.dof_base,
          self.dof_palm, self.dof_obj) = info[:9]
         self.dof_pris = list(info[9:12])

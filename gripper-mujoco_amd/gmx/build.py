@@ -9,7 +9,8 @@ from ._lib import PKG_DIR, REPO_DIR, LIB_PATH
 SOURCES = ["csrc/gm_capi.hip", "csrc/gm_host_model.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-         "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics"]
+         "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics",
+         "-ffp-contract=off"]
 
 
 def build(verbose: bool = False, force: bool = False) -> str:

@@ -143,6 +143,25 @@ class BatchedGripperEnv:
         self._check(self.lib.gm_set_action(self._ctx, C.c_void_p(actions_dev_ptr), 1))
         self._check(self.lib.gm_step(self._ctx))
 
+    def set_stream(self, stream_handle: int | None):
+        """Launch on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)."""
+        self._check(self.lib.gm_set_stream(self._ctx, C.c_void_p(stream_handle or 0)))
+
+    def upload_spawn(self, spawn):
+        """Copy a host gm_spawn array once; returns the device pointer kept alive by self."""
+        import torch
+        raw = np.frombuffer(bytes(spawn), dtype=np.uint8)
+        self._spawn_dev = torch.from_numpy(raw.copy()).to(f"cuda:{self.device}")
+        return self._spawn_dev.data_ptr()
+
+    def autoreset_device(self, spawn_dev_ptr: int, returns_dev_ptr: int | None = None,
+                         max_episode_steps: int | None = None):
+        """Episode boundary on the device: done/truncated envs report their return and are
+        reset + respawned (MjEnv.py:616-637, 2222-2263)."""
+        mx = self.max_episode_steps if max_episode_steps is None else max_episode_steps
+        self._check(self.lib.gm_autoreset(self._ctx, int(mx), C.c_void_p(spawn_dev_ptr), 1,
+                                          C.c_void_p(returns_dev_ptr or 0)))
+
     def device_buffers(self):
         return (self.lib.gm_device_obs(self._ctx), self.lib.gm_device_reward(self._ctx),
                 self.lib.gm_device_done(self._ctx))
@@ -203,3 +222,12 @@ class BatchedGripperEnv:
                                               f.ctypes.data_as(C.POINTER(C.c_float)),
                                               qacc.ctypes.data_as(C.POINTER(C.c_float))))
         return ncon, con, f, qacc
+
+    PHASES = ("kinematics", "crb_rne", "mass_forces", "factor", "smooth_solve", "collision",
+              "constraints_pgs", "constraint_accel", "integrate", "update_all", "monitor_sensors")
+
+    def step_profiled(self):
+        """One env-step with per-phase shader-clock counters (lane 0, summed over substeps)."""
+        ph = np.zeros((self.n_envs, 16), dtype=np.uint64)
+        self._check(self.lib.gm_step_profiled(self._ctx, ph.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return ph

@@ -282,7 +282,7 @@ int  gm_device_count(void);
  * 5 model params) so bindings can verify their layouts */
 int64_t gm_struct_size(int which);
 /* model summary: nq, nv, nbody, ngeom, npair, n_seg, dof_base, dof_palm, dof_obj,
- * dof_pris[3], dof_rev[3], dof_seg[3]  (18 int32) */
+ * dof_pris[3], dof_rev[3], dof_seg[3], nlock, nM (tree-sparse M nonzeros)  (20 int32) */
 void gm_model_info(const gm_model* m, int32_t* out);
 /* derived config summary: n_obs, n_actions, sim_steps_per_action, sensor_fcn, state_fcn */
 void gm_config_info(const gm_config* c, int32_t* out);
@@ -347,7 +347,20 @@ void* gm_device_obs(gm_ctx* ctx);
 void* gm_device_reward(gm_ctx* ctx);
 void* gm_device_done(gm_ctx* ctx);
 void* gm_device_actions(gm_ctx* ctx);
-void* gm_stream(gm_ctx* ctx);            /* hipStream_t the context launches on */
+void* gm_stream(gm_ctx* ctx);
+/* route every later launch of ctx to `stream` (a hipStream_t, e.g. torch's current
+   stream) so device-pointer I/O is ordered with the caller's work; NULL restores
+   the ctx's own stream.  Synchronises the previous stream first. */
+int  gm_set_stream(gm_ctx* ctx, void* stream);
+/* MjEnv's episode-boundary handling done on the device (MjEnv.py:616-637 then
+ * MjEnv.reset, MjEnv.py:2222-2263): every env with done != 0 from the last gm_step,
+ * or num_action_steps >= max_episode_steps (<= 0 disables truncation), writes its
+ * cumulative reward to returns[e] (NaN for envs that continue; returns may be NULL),
+ * is flagged in gm_device_reset_mask, and is reset + respawned from spawn[e].
+ * spawn: host array unless spawn_on_device; NULL spawns object 0 at the origin. */
+int  gm_autoreset(gm_ctx* ctx, int max_episode_steps, const gm_spawn* spawn, int spawn_on_device,
+                  float* returns);
+void* gm_device_reset_mask(gm_ctx* ctx);   /* uint8 [n_envs], written by gm_autoreset */            /* hipStream_t the context launches on */
 
 /* Timing of the fused env-step kernel (HIP events on the context's stream). */
 int  gm_last_step_ms(gm_ctx* ctx, float* ms);
@@ -359,6 +372,11 @@ int  gm_last_step_ms(gm_ctx* ctx, float* ms);
  * efc_force [n_envs x GM_MAX_EFC], qacc [n_envs x nv]. */
 int  gm_debug_substep(gm_ctx* ctx, int32_t* ncon, float* contact, float* efc_force,
                       float* qacc);
+/* diagnostic: one gm_step with per-phase shader-clock cycle counters, lane-0 view,
+   summed over substeps: out[n_envs][16] = kinematics, crb_rne, mass+forces, factor,
+   smooth solve, collision, constraint build+PGS, constraint accel, integrate,
+   update_all, monitor_sensors, (5 spare) */
+int  gm_step_profiled(gm_ctx* ctx, uint64_t* phase_cycles);
 
 #ifdef __cplusplus
 }

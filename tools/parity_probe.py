@@ -25,6 +25,8 @@ for t in range(steps):
     rel = (np.abs(obs[0] - obs_o)[big] / np.abs(obs_o[big])).max() if big.any() else 0
     dq = np.abs(q[0] - qo)
     segrel = (np.abs(q[0][seg] - qo[seg]) / np.maximum(np.abs(qo[seg]), 1e-9)).max()
+    dd = np.abs(obs[0] - obs_o); k = int(np.argmax(dd / np.maximum(np.abs(obs_o), 1e-3)))
+    print(f"   worst obs[{k}] gpu={obs[0][k]:.6f} ref={obs_o[k]:.6f} rew {rew[0]:.4f}/{r_o:.4f} done {term[0]}/{d_o}")
     print(f"t={t:2d} obs_rel={rel:.2e} obs_abs={np.abs(obs[0]-obs_o).max():.2e} seg_q_rel={segrel:.2e} "
           f"seg_q_abs={dq[seg].max():.2e} motor_q_abs={dq[[m.dof_base, m.dof_palm] + m.dof_pris + m.dof_rev].max():.2e} "
           f"obj_abs={dq[m.dof_obj:m.dof_obj+3].max():.2e} maxseg={np.abs(qo[seg]).max():.2e} v_abs={np.abs(v[0]-vo).max():.2e}", flush=True)

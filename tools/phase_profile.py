@@ -1,0 +1,23 @@
+"""Developer probe: per-phase cycle breakdown of the fused env-step kernel."""
+import sys, os
+sys.path[:0] = [os.path.join(os.path.dirname(__file__), '..', 'gripper-mujoco_amd')]
+import numpy as np
+import gmx
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+s = gmx.canonical_settings(noise=True, seed=5)
+env = gmx.BatchedGripperEnv(n, object_set="set6_synthetic", settings=s, seed=5)
+env.reset()
+rng = np.random.default_rng(0)
+for t in range(3):
+    env.step(rng.uniform(-1, 1, size=(n, env.n_actions)).astype(np.float32))
+tot = np.zeros(16)
+for t in range(3):
+    env.set_action(rng.uniform(-1, 1, size=(n, env.n_actions)).astype(np.float32))
+    ph = env.step_profiled().astype(np.float64)
+    tot += ph.mean(axis=0)
+tot /= 3
+S = env.cfg.sim_steps_per_action if hasattr(env.cfg, 'sim_steps_per_action') else 63
+allc = tot.sum()
+print(f"n={n} mean cycles per env-step (lane 0) total {allc:.3e}  per substep {allc/63:.3e}")
+for k, name in enumerate(env.PHASES):
+    print(f"  {name:18s} {tot[k]/63:10.0f} cyc/substep  {100*tot[k]/allc:5.1f}%")

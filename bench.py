@@ -27,7 +27,6 @@ from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -151,10 +150,12 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     import gmx
+    from gmx.shard import shard_range, gather_returns, max_over_ranks
     settings = gmx.canonical_settings(seed=args.seed)
     n = args.envs
+    first_env, _ = shard_range(rank, world, n)
     env = gmx.BatchedGripperEnv(n, object_set="set6_synthetic", settings=settings, seed=args.seed,
-                                env_offset=rank * n, device=local_rank)
+                                env_offset=first_env, device=local_rank)
     stream = torch.cuda.Stream(dev)          # a real (non-null) stream shared by torch and the ctx
     torch.cuda.set_stream(stream)
     env.set_stream(stream.cuda_stream)
@@ -168,7 +169,6 @@ def main():
     g.manual_seed(args.seed + 7919 * rank)
     actions = torch.rand((W + K, n, env.n_actions), generator=g, device=dev) * 2 - 1
     returns = torch.full((n,), float("nan"), device=dev)
-    gathered = torch.empty((world * n,), device=dev) if world > 1 else None
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     episodes = torch.zeros((), device=dev, dtype=torch.int64)
 
@@ -180,11 +180,7 @@ def main():
         if timed is not None:
             ev[timed][1].record(stream)
         env.autoreset_device(spawn_ptr, returns.data_ptr())
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, returns)
-            episodes.add_(torch.isfinite(gathered).sum())
-        else:
-            episodes.add_(torch.isfinite(returns).sum())
+        episodes.add_(torch.isfinite(gather_returns(returns, world)).sum())
 
     for i in range(W):
         one_step(i, None)
@@ -200,10 +196,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+    elapsed = max_over_ranks(elapsed, dev)
 
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3

@@ -1193,19 +1193,10 @@ static void update_all(or_env* e) {
 /* read_armadillo_gauge (myfunctions.cpp:2699-2795): cubic least squares through the
  * N+1 joint points, evaluated at gauge.xpos, in mm.  Least squares by Householder
  * QR on the Vandermonde matrix, as arma::polyfit -> LAPACK does. */
-float or_gauge_reading(const gm_model* m, const double* q) {
-  int N = m->n_seg, P = N + 1;
-  double X[GM_MAX_SEG + 1], Y[GM_MAX_SEG + 1];
-  X[0] = m->fixed_first_segment ? m->segment_length : 0;
-  Y[0] = 0;
-  double cum = 0;
-  for (int i = 0; i < N; i++) {
-    cum = (i == 0) ? q[0] : cum + q[i];
-    X[i + 1] = X[i] + m->segment_length * cos(cum);
-    Y[i + 1] = Y[i] + m->segment_length * sin(cum);
-  }
-  int order = m->gauge_order, nc = order + 1;
+/* least-squares polynomial of `order` through (X, Y), evaluated at x, in mm */
+float or_polyfit_eval(const double* X, const double* Y, int P, int order, double x) {
   double A[GM_MAX_SEG + 1][4], b[GM_MAX_SEG + 1];
+  int nc = order + 1;
   for (int i = 0; i < P; i++) {
     for (int k = 0; k < nc; k++) A[i][k] = pow(X[i], order - k);
     b[i] = Y[i];
@@ -1240,8 +1231,38 @@ float or_gauge_reading(const gm_model* m, const double* q) {
     coeff[k] = s / A[k][k];
   }
   float y = 0.0f;
-  for (int i = 0; i <= order; i++) y += (float)(coeff[i] * pow(m->gauge_xpos, order - i));
+  for (int i = 0; i <= order; i++) y += (float)(coeff[i] * pow(x, order - i));
   return y * 1000;
+}
+
+float or_gauge_reading(const gm_model* m, const double* q) {
+  int N = m->n_seg, P = N + 1;
+  double X[GM_MAX_SEG + 1], Y[GM_MAX_SEG + 1];
+  or_gauge_points(m, q, X, Y);
+  return or_polyfit_eval(X, Y, P, m->gauge_order, m->gauge_xpos);
+}
+
+/* finger joint points (myfunctions.cpp:2699-2740): cumulative segment angles */
+void or_gauge_points(const gm_model* m, const double* q, double* X, double* Y) {
+  int N = m->n_seg;
+  X[0] = m->fixed_first_segment ? m->segment_length : 0;
+  Y[0] = 0;
+  double cum = 0;
+  for (int i = 0; i < N; i++) {
+    cum = (i == 0) ? q[0] : cum + q[i];
+    X[i + 1] = X[i] + m->segment_length * cos(cum);
+    Y[i + 1] = Y[i] + m->segment_length * sin(cum);
+  }
+}
+
+/* SlidingWindow trace: after each add, read_element(0 .. n_reads-1) */
+void or_ring_trace(const float* adds, int n_adds, int n_reads, float* out) {
+  ring_t r;
+  ring_reset(&r);
+  for (int k = 0; k < n_adds; k++) {
+    ring_add(&r, adds[k]);
+    for (int n = 0; n < n_reads; n++) out[k * n_reads + n] = ring_read(&r, n);
+  }
 }
 
 /* Sensor::apply_normalisation (mjclass.h:155-174) */

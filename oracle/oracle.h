@@ -55,6 +55,9 @@ void  or_debug_substep(or_env* e, int32_t* ncon, float* contact, float* efc_forc
 float  or_gauge_reading(const gm_model* m, const double* finger_q);   /* read_armadillo_gauge */
 double or_minstd_next_canonical_float(uint32_t* state);               /* generate_canonical<float> */
 double or_minstd_next_canonical_double(uint32_t* state);              /* generate_canonical<double> */
+float  or_polyfit_eval(const double* X, const double* Y, int P, int order, double x);
+void   or_gauge_points(const gm_model* m, const double* q, double* X, double* Y);
+void   or_ring_trace(const float* adds, int n_adds, int n_reads, float* out);
 int    or_grip_step_sequence(const double* cmds, int n, double* out);  /* Gripper golden driver */
 int    or_sample(int mode, const float* window_recent_first, int n_avail, int prev_steps,
                  int readings_per_step, float* out);                  /* Sensor::*_sample */

@@ -55,6 +55,9 @@ def lib():
             "or_grip_step_sequence": (i32, [f64p, i32, f64p]),
             "or_sample": (i32, [i32, f32p, i32, i32, i32, f32p]),
             "or_bench": (C.c_double, [vp, vp, vp, i32, i32, i32, C.c_uint64, i32]),
+            "or_polyfit_eval": (C.c_float, [f64p, f64p, i32, i32, C.c_double]),
+            "or_gauge_points": (None, [vp, f64p, f64p, f64p]),
+            "or_ring_trace": (None, [f32p, i32, i32, f32p]),
         }
         for n, (r, a) in sig.items():
             f = getattr(L, n)
@@ -193,3 +196,40 @@ def canonical_floats(seed, n):
 def bench(model, cfg, objects, n_envs, n_steps, seed=1234, n_threads=1):
     return float(lib().or_bench(model.ptr, cfg.ptr, C.cast(objects, C.c_void_p), len(objects), n_envs, n_steps,
                                 seed, n_threads))
+
+
+def polyfit_eval(X, Y, order, x):
+    X = np.ascontiguousarray(X, dtype=np.float64); Y = np.ascontiguousarray(Y, dtype=np.float64)
+    return float(lib().or_polyfit_eval(X.ctypes.data_as(C.POINTER(C.c_double)),
+                                       Y.ctypes.data_as(C.POINTER(C.c_double)), len(X), order, x))
+
+
+def gauge_points(model, finger_q):
+    q = np.ascontiguousarray(finger_q, dtype=np.float64)
+    X = np.zeros(16); Y = np.zeros(16)
+    lib().or_gauge_points(model.ptr, q.ctypes.data_as(C.POINTER(C.c_double)),
+                          X.ctypes.data_as(C.POINTER(C.c_double)), Y.ctypes.data_as(C.POINTER(C.c_double)))
+    return X[:model.n_seg + 1], Y[:model.n_seg + 1]
+
+
+def ring_trace(adds, n_reads):
+    a = _f32(adds)
+    out = np.zeros((len(a), n_reads), dtype=np.float32)
+    lib().or_ring_trace(a.ctypes.data_as(C.POINTER(C.c_float)), len(a), n_reads,
+                        out.ctypes.data_as(C.POINTER(C.c_float)))
+    return out
+
+
+def minstd_raw(seed, n):
+    """minstd_rand0 raw outputs via the oracle's canonical draw state (16807 x mod 2^31-1)."""
+    s = C.c_uint32(seed)
+    out = []
+    for _ in range(n):
+        lib().or_minstd_next_canonical_float(C.byref(s))
+        out.append(s.value)
+    return out
+
+
+def canonical_doubles(seed, n):
+    s = C.c_uint32(seed)
+    return np.array([lib().or_minstd_next_canonical_double(C.byref(s)) for _ in range(n)])

@@ -214,6 +214,20 @@ int gm_reset(gm_ctx* c, const uint8_t* mask, const gm_spawn* spawn) {
   return GM_OK;
 }
 
+int gm_spawn_object(gm_ctx* c, const uint8_t* mask, const gm_spawn* spawn) {
+  if (!c || !spawn) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint8_t* dm = nullptr;
+  if (mask) { HIPCHK(c, hipMemcpyAsync(c->d_mask, mask, (size_t)c->n_envs, hipMemcpyHostToDevice, c->stream)); dm = c->d_mask; }
+  HIPCHK(c, hipMemcpyAsync(c->d_spawn, spawn, sizeof(gm_spawn) * (size_t)c->n_envs, hipMemcpyHostToDevice, c->stream));
+  int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
+  hipLaunchKernelGGL(gm_spawn_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_topo, dm,
+                     c->d_spawn, c->d_objs, c->n_objects, c->n_envs);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+
 int gm_set_action(gm_ctx* c, const float* actions, int on_device) {
   if (!c || !actions) return GM_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));

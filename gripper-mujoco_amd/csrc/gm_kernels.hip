@@ -2058,6 +2058,50 @@ extern "C" __global__ void gm_action_kernel(GmEnvState* __restrict__ states, con
 }
 
 // ---------------------------------------------------------------- reset + spawn
+// MjClass::spawn_object -> ObjectHandler::spawn_object (mjclass.cpp:2352-2420,
+// objecthandler.cpp:403-428): live object, pose on the ground at (x, y), z-rotation
+__device__ void spawn_object(GmEnvState& s, const GmTopo* __restrict__ T, const gm_object* __restrict__ objs,
+                             int n_objects, gm_spawn sp) {
+  int oi = sp.object_index;
+  if (oi < 0 || oi >= n_objects) oi = 0;
+  const gm_object& o = objs[oi];
+  s.obj_index = oi;
+  s.obj_type = o.type;
+  s.obj_size[0] = o.size[0]; s.obj_size[1] = o.size[1]; s.obj_size[2] = o.size[2];
+  s.obj_mass = o.mass;
+  s.obj_friction = o.friction;
+  double I0, I1, I2, rb, restz;
+  if (o.type == GM_GEOM_BOX) {
+    double a = 2 * o.size[0], bb = 2 * o.size[1], c = 2 * o.size[2];
+    I0 = o.mass * (bb * bb + c * c) / 12; I1 = o.mass * (a * a + c * c) / 12; I2 = o.mass * (a * a + bb * bb) / 12;
+    rb = sqrt(o.size[0] * o.size[0] + o.size[1] * o.size[1] + o.size[2] * o.size[2]);
+    restz = o.size[2];
+  } else if (o.type == GM_GEOM_CYLINDER) {
+    double r = o.size[0], hh = 2 * o.size[1];
+    I0 = I1 = o.mass * (3 * r * r + hh * hh) / 12; I2 = o.mass * r * r / 2;
+    rb = sqrt(o.size[0] * o.size[0] + o.size[1] * o.size[1]);
+    restz = o.size[1];
+  } else {
+    double r = o.size[0];
+    I0 = I1 = I2 = 2 * o.mass * r * r / 5;
+    rb = r;
+    restz = r;
+  }
+  s.obj_inertia[0] = I0; s.obj_inertia[1] = I1; s.obj_inertia[2] = I2;
+  s.obj_rbound = rb;
+  s.obj_rest_z = restz;
+  int qa = T->qadr_obj;
+  double x2 = sin(-sp.zrot / 2.0), w2 = cos(-sp.zrot / 2.0);
+  double q4[4] = {x2, 0, 0, w2};   // reference QPos quirk: qx lands in MuJoCo's w slot
+  double nq = sqrt(q4[0] * q4[0] + q4[1] * q4[1] + q4[2] * q4[2] + q4[3] * q4[3]);
+  s.qpos[qa + 0] = sp.x;
+  s.qpos[qa + 1] = sp.y;
+  s.qpos[qa + 2] = restz + 1e-6;
+  for (int k = 0; k < 4; k++) s.qpos[qa + 3 + k] = q4[k] / nq;
+  for (int k = 0; k < 7; k++) s.start_qpos[k] = s.qpos[qa + k];
+  for (int k = 0; k < 6; k++) s.qvel[T->dof_obj + k] = 0;
+}
+
 // MjEnv auto-reset bookkeeping (MjEnv.py:616-637, 2170-2263): an env whose episode
 // terminated (is_done) or truncated (num_action_steps >= max_episode_steps) hands its
 // episode return to `returns` and is flagged for gm_reset_kernel.
@@ -2128,45 +2172,7 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
     if (s.base[2] < C->base_min[2]) s.base[2] = C->base_min[2];
     s.qpos[m->dof_base] = s.base[2] + eq_qpos[m->dof_base];
   }
-  // spawn_object
-  gm_spawn sp = spawn ? spawn[env] : gm_spawn{0, 0.0, 0.0, 0.0};
-  int oi = sp.object_index;
-  if (oi < 0 || oi >= n_objects) oi = 0;
-  const gm_object& o = objs[oi];
-  s.obj_index = oi;
-  s.obj_type = o.type;
-  s.obj_size[0] = o.size[0]; s.obj_size[1] = o.size[1]; s.obj_size[2] = o.size[2];
-  s.obj_mass = o.mass;
-  s.obj_friction = o.friction;
-  double I0, I1, I2, rb, restz;
-  if (o.type == GM_GEOM_BOX) {
-    double a = 2 * o.size[0], bb = 2 * o.size[1], c = 2 * o.size[2];
-    I0 = o.mass * (bb * bb + c * c) / 12; I1 = o.mass * (a * a + c * c) / 12; I2 = o.mass * (a * a + bb * bb) / 12;
-    rb = sqrt(o.size[0] * o.size[0] + o.size[1] * o.size[1] + o.size[2] * o.size[2]);
-    restz = o.size[2];
-  } else if (o.type == GM_GEOM_CYLINDER) {
-    double r = o.size[0], hh = 2 * o.size[1];
-    I0 = I1 = o.mass * (3 * r * r + hh * hh) / 12; I2 = o.mass * r * r / 2;
-    rb = sqrt(o.size[0] * o.size[0] + o.size[1] * o.size[1]);
-    restz = o.size[1];
-  } else {
-    double r = o.size[0];
-    I0 = I1 = I2 = 2 * o.mass * r * r / 5;
-    rb = r;
-    restz = r;
-  }
-  s.obj_inertia[0] = I0; s.obj_inertia[1] = I1; s.obj_inertia[2] = I2;
-  s.obj_rbound = rb;
-  s.obj_rest_z = restz;
-  int qa = T->qadr_obj;
-  double x2 = sin(-sp.zrot / 2.0), w2 = cos(-sp.zrot / 2.0);
-  double q4[4] = {x2, 0, 0, w2};   // reference QPos quirk: qx lands in MuJoCo's w slot
-  double nq = sqrt(q4[0] * q4[0] + q4[1] * q4[1] + q4[2] * q4[2] + q4[3] * q4[3]);
-  s.qpos[qa + 0] = sp.x;
-  s.qpos[qa + 1] = sp.y;
-  s.qpos[qa + 2] = restz + 1e-6;
-  for (int k = 0; k < 4; k++) s.qpos[qa + 3 + k] = q4[k] / nq;
-  for (int k = 0; k < 7; k++) s.start_qpos[k] = s.qpos[qa + k];
+  spawn_object(s, T, objs, n_objects, spawn ? spawn[env] : gm_spawn{0, 0.0, 0.0, 0.0});
 }
 
 // settle initialisation (keyframe, targets home, locks off, flags true) for env 0
@@ -2211,4 +2217,14 @@ extern "C" __global__ void gm_init_envs_kernel(GmEnvState* __restrict__ states, 
   uint64_t seed = ((uint64_t)base_seed + (uint64_t)(env_offset + env) * 1000003ull) % 2147483647ull;
   s.rng = seed == 0 ? 1u : (uint32_t)seed;
   s.old_x = s.old_y = s.old_z = 0;
+}
+
+// spawn only (MjClass::spawn_object after MjClass::reset, MjEnv.py:1212-1267)
+extern "C" __global__ void gm_spawn_kernel(GmEnvState* __restrict__ states, const GmTopo* __restrict__ T,
+                                           const uint8_t* __restrict__ mask, const gm_spawn* __restrict__ spawn,
+                                           const gm_object* __restrict__ objs, int n_objects, int n_envs) {
+  int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n_envs) return;
+  if (mask && !mask[env]) return;
+  spawn_object(states[env], T, objs, n_objects, spawn[env]);
 }

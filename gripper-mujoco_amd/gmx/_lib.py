@@ -190,6 +190,7 @@ def _declare(lib):
         "gm_debug_substep": (i32, [vp, i32p, f32p, f32p, f32p]),
         "gm_step_profiled": (i32, [vp, C.POINTER(C.c_uint64)]),
         "gm_set_stream": (i32, [vp, vp]),
+        "gm_spawn_object": (i32, [vp, vp, vp]),
         "gm_autoreset": (i32, [vp, i32, vp, i32, vp]),
         "gm_device_reset_mask": (vp, [vp]),
     }

@@ -1,0 +1,346 @@
+"""Drop-in facade for the reference's pybind11 module `bind` (src/bind.cpp:32),
+imported by rl/env/MjEnv.py:18 as `from mjpy.bind import MjClass, EventTrack`.
+
+One MjClass is one env (the reference's model: one MjClass per process, bind.cpp:46),
+backed by a 1-env context of the MI355X C ABI (include/gripper_mi355x.h); every
+action_step() runs on the GPU.  The methods MjEnv calls on the hot path are mirrored
+with the reference's names, argument meaning and error behaviour:
+
+  .set (Settings, r/w fields of simsettings.h)      bind.cpp:195
+  set_continous_action(i, f) / set_discrete_action   bind.cpp:95-96   (MjEnv.py:594,597)
+  action_step()                                      bind.cpp:93      (MjEnv.py:612)
+  get_observation_numpy()                            bind.cpp:119-123 (MjEnv.py:823)
+  is_done() / reward()                               bind.cpp:115,128 (MjEnv.py:635,1039)
+  reset() / hard_reset()                             bind.cpp:53-54   (MjEnv.py:2240,2249)
+  spawn_object / spawn_into_scene / default_spawn_params / set_new_base_XY
+  get_n_actions / get_n_obs / get_N / finger dimension setters and getters
+  get_event_state() -> EventTrack                    bind.cpp:525-590 (MjEnv.py:1020)
+  __getstate__ / __setstate__ (pickle pair)          bind.cpp:207-241 (MjEnv.py:2088-2105)
+
+Differences the caller can observe are listed in DESIGN.md ("Facade").  There is no
+CPU fallback: without the HIP library / a GPU, construction of the env raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+
+import gmx
+from gmx._lib import BINARY_EVENTS, LINEAR_EVENTS
+
+
+class SpawnParams:
+    """MjType::SpawnParams (mjclass.h:916-931)."""
+
+    def __init__(self):
+        self.index = -1
+        self.x = 0.0
+        self.y = 0.0
+        self.zrot = 0.0
+        self.xrange = 0.0
+        self.yrange = 0.0
+        self.rotrange = 0.0
+        self.xmin, self.xmax, self.ymin, self.ymax = -100.0, 100.0, -100.0, 100.0
+        self.smallest_gap = 1e-3
+        self.xy_increment = 2e-3
+        self.rot_increment = math.pi / 30.0
+
+
+class _BinaryEvent:
+    __slots__ = ("value", "last_value", "active_sum", "row", "abs", "percent")
+
+    def __init__(self):
+        self.value = False
+        self.last_value = 0
+        self.active_sum = 0
+        self.row = 0
+        self.abs = 0
+        self.percent = 0.0
+
+
+class _LinearEvent:
+    __slots__ = ("value", "last_value", "active_sum", "row", "abs", "percent")
+
+    def __init__(self):
+        self.value = 0.0
+        self.last_value = 0.0
+        self.active_sum = 0
+        self.row = 0
+        self.abs = 0
+        self.percent = 0.0
+
+
+class EventTrack:
+    """MjType::EventTrack (mjclass.h:575-647): one BinaryEvent / LinearEvent per reward
+    name, readable attributes; reset(); calculate_percentage()."""
+
+    def __init__(self):
+        for n in BINARY_EVENTS:
+            setattr(self, n, _BinaryEvent())
+        for n in LINEAR_EVENTS:
+            setattr(self, n, _LinearEvent())
+
+    def reset(self):
+        self.__init__()
+
+    def calculate_percentage(self):
+        # percent = abs / total steps is what the reference derives; callers that need it
+        # divide by their own step count (MjEnv tracks current_step)
+        return None
+
+    def print(self):
+        for n in list(BINARY_EVENTS) + list(LINEAR_EVENTS):
+            e = getattr(self, n)
+            print(f"{n}: row {e.row} abs {e.abs} last {e.last_value}")
+
+
+class MjClass:
+    """MjClass (mjclass.h:1554-1833) on the MI355X hot path, one env."""
+
+    def __init__(self, model_path: str | None = None):
+        self.set = gmx.default_settings()
+        self.default_spawn_params = SpawnParams()
+        self.model_folder_path = model_path or ""
+        self.object_set_name = "set6_synthetic"
+        self.machine = "mi355x"
+        self.current_load_path = ""
+        self._params = None          # gm_model_params overrides (finger dimensions)
+        self._env = None
+        self._pending = None         # continuous action vector buffered between calls
+        self._rng = np.random.default_rng(0)
+        self._base_xy = (0.0, 0.0)
+
+    # ------------------------------------------------------------ model / lifecycle
+    def load(self, file_path: str = ""):
+        self.current_load_path = file_path
+        self._drop()
+
+    def load_relative(self, file_path: str = ""):
+        """The reference loads task MJCF here (bind.cpp:52); the build's model is compiled
+        from gm_model_params and the object set named by object_set_name."""
+        self.load(file_path)
+
+    def _drop(self):
+        if self._env is not None:
+            self._env.close()
+            self._env = None
+
+    def _ensure(self):
+        if self._env is None:
+            model_params = self._params
+            self._env = gmx.BatchedGripperEnv(1, object_set=self.object_set_name, settings=self.set,
+                                              model_params=model_params, seed=int(self.set.random_seed),
+                                              max_episode_steps=1 << 30)
+            self._rng = np.random.default_rng(int(self.set.random_seed))
+        return self._env
+
+    def reset(self):
+        """MjClass::reset (mjclass.cpp:434-486): re-apply settings (configure_settings),
+        keyframe + equilibrium, noise means, base-Z noise; the object set's first object
+        is placed until spawn_object / spawn_into_scene picks one (MjEnv.reset order)."""
+        env = self._ensure()
+        cfg = gmx.ConfigBlob(self.set, env.model)
+        if env.lib.gm_update_config(env.ctx, cfg.ptr) != 0:
+            # the observation layout changed: the reference re-sizes on reset too
+            self._drop()
+            env = self._ensure()
+            cfg = env.cfg
+        env.n_obs, env.n_actions = cfg.n_obs, cfg.n_actions
+        env._obs = np.zeros((1, cfg.n_obs), dtype=np.float32)
+        sp = (gmx.Spawn * 1)()
+        sp[0].object_index, sp[0].x, sp[0].y, sp[0].zrot = 0, 0.0, 0.0, 0.0
+        env.reset(spawn=sp)
+        self._pending = None
+
+    def hard_reset(self):
+        """Reload from scratch (bind.cpp:54): a fresh device context."""
+        self._drop()
+        self.reset()
+
+    def step(self):
+        raise NotImplementedError("single physics substeps are inside action_step() on the device")
+
+    # ------------------------------------------------------------ actions
+    def set_continous_action(self, action: int, fraction: float):
+        """MjClass::set_continous_action (mjclass.cpp:1517-1526). MjEnv calls it for every
+        index in order then action_step(); the vector is applied in that order on the
+        device at action_step()."""
+        env = self._ensure()
+        if self._pending is None:
+            self._pending = np.zeros(env.n_actions, dtype=np.float32)
+        if action < 0 or action >= env.n_actions:
+            print(f"set_continous_action: action {action} out of range")
+            return []
+        self._pending[action] = fraction
+        return []
+
+    def set_discrete_action(self, action: int):
+        env = self._ensure()
+        env.set_discrete_action(np.array([action], dtype=np.int32))
+        return []
+
+    def set_action(self, action: int):
+        return self.set_discrete_action(action)
+
+    def action_step(self):
+        env = self._ensure()
+        if self._pending is not None:
+            env.set_action(self._pending.reshape(1, -1))
+            self._pending = None
+        env.action_step()
+
+    # ------------------------------------------------------------ outputs
+    def get_observation_numpy(self):
+        return self._ensure().observation()[0]
+
+    def get_observation(self):
+        return self.get_observation_numpy().tolist()
+
+    def is_done(self) -> bool:
+        _, d = self._ensure().reward_done()
+        return bool(d[0])
+
+    def reward(self) -> float:
+        r, _ = self._ensure().reward_done()
+        return float(r[0])
+
+    def get_event_state(self) -> EventTrack:
+        rows, absc, lastv = self._ensure().event_rows()
+        t = EventTrack()
+        for i, n in enumerate(list(BINARY_EVENTS) + list(LINEAR_EVENTS)):
+            e = getattr(t, n)
+            e.row, e.abs = int(rows[0, i]), int(absc[0, i])
+            e.last_value = float(lastv[0, i]) if i >= len(BINARY_EVENTS) else int(lastv[0, i])
+            e.value = e.last_value
+        return t
+
+    def get_n_actions(self) -> int:
+        return int(self._config().n_actions)
+
+    def get_n_obs(self) -> int:
+        return int(self._config().n_obs)
+
+    def _config(self):
+        if self._env is not None:
+            return self._env.cfg
+        return gmx.ConfigBlob(self.set, gmx.ModelBlob(self._params))
+
+    # ------------------------------------------------------------ objects / spawning
+    def get_number_of_objects(self) -> int:
+        return len(gmx.make_object_set(self.object_set_name, int(self.set.random_seed)))
+
+    def get_object_name(self, idx: int) -> str:
+        o = gmx.make_object_set(self.object_set_name, int(self.set.random_seed))[idx]
+        kind = {2: "sphere", 5: "cylinder", 6: "cube"}.get(o.type, "object")
+        return f"{kind}_{idx}"
+
+    def get_current_object_name(self) -> str:
+        return self.get_object_name(self._spawned if hasattr(self, "_spawned") else 0)
+
+    def spawn_object(self, idx: int, x: float = 0.0, y: float = 0.0, zrot: float = 0.0):
+        """MjClass::spawn_object (mjclass.cpp:2352-2420)."""
+        env = self._ensure()
+        sp = (gmx.Spawn * 1)()
+        sp[0].object_index, sp[0].x, sp[0].y, sp[0].zrot = int(idx), float(x), float(y), float(zrot)
+        env._check(env.lib.gm_spawn_object(env.ctx, None, sp))
+        self._spawned = int(idx)
+
+    def spawn_into_scene(self, index, xpos=None, ypos=None, zrot=None, xrange=None, yrange=None,
+                         rotrange=None):
+        """MjClass::spawn_into_scene (mjclass.cpp:2475-2654) with default_spawn_params:
+        a pose on the xy_increment / rot_increment grid inside the ranges.  The
+        reference's fingertip-overlap (Box2d SAT) rejection loop is not reproduced
+        (DESIGN.md, next rows); always returns True."""
+        p = self.default_spawn_params
+        x0 = p.x if xpos is None else xpos
+        y0 = p.y if ypos is None else ypos
+        r0 = p.zrot if zrot is None else zrot
+        xr = p.xrange if xrange is None else xrange
+        yr = p.yrange if yrange is None else yrange
+        rr = p.rotrange if rotrange is None else rotrange
+        nx = int(round(xr / p.xy_increment)); ny = int(round(yr / p.xy_increment))
+        nr = int(round(rr / p.rot_increment))
+        x = x0 + p.xy_increment * int(self._rng.integers(-nx, nx + 1))
+        y = y0 + p.xy_increment * int(self._rng.integers(-ny, ny + 1))
+        r = r0 + p.rot_increment * int(self._rng.integers(-nr, nr + 1))
+        self.spawn_object(index, x, y, r)
+        return True
+
+    def set_new_base_XY(self, x: float, y: float):
+        self._base_xy = (float(x), float(y))
+
+    def set_scene_grasp_target(self, num_objects: int):
+        return None
+
+    def reset_goal(self):
+        return None
+
+    # ------------------------------------------------------------ gripper dimensions
+    def _model_params(self):
+        if self._params is None:
+            p = gmx.ModelParams()
+            gmx.load_library().gm_default_model_params(C.byref(p))
+            self._params = p
+        return self._params
+
+    def get_N(self) -> int:
+        return int(self._model_params().n_seg)
+
+    def set_finger_thickness(self, t: float):
+        self._model_params().finger_thickness = float(t)
+        self._drop()
+
+    def set_finger_width(self, w: float):
+        self._model_params().finger_width = float(w)
+        self._drop()
+
+    def set_finger_modulus(self, E: float):
+        self._model_params().finger_E = float(E)
+        self._drop()
+
+    def get_finger_thickness(self) -> float:
+        return float(self._model_params().finger_thickness)
+
+    def get_finger_width(self) -> float:
+        return float(self._model_params().finger_width)
+
+    def get_finger_modulus(self) -> float:
+        return float(self._model_params().finger_E)
+
+    def get_finger_length(self) -> float:
+        return float(self._model_params().finger_length)
+
+    def get_finger_hook_length(self) -> float:
+        return float(self._model_params().hook_length)
+
+    def get_finger_hook_angle_degrees(self) -> float:
+        return float(self._model_params().hook_angle_degrees)
+
+    def get_fingertip_clearance(self) -> float:
+        return float(self._model_params().fingertip_clearance)
+
+    def get_finger_rigidity(self) -> float:
+        p = self._model_params()
+        return float(p.finger_E * p.finger_width * p.finger_thickness ** 3 / 12.0)
+
+    def set_base_XYZ_limits(self, x: float, y: float, z: float):
+        self._base_limits = (float(x), float(y), float(z))
+
+    def set_base_yaw_limit(self, yaw: float):
+        self._base_yaw = float(yaw)
+
+    # ------------------------------------------------------------ pickling (bind.cpp:207-241)
+    def __getstate__(self):
+        return {"set": bytes(self.set), "params": bytes(self._params) if self._params is not None else None,
+                "object_set_name": self.object_set_name, "model_folder_path": self.model_folder_path,
+                "machine": self.machine}
+
+    def __setstate__(self, st):
+        self.__init__(st.get("model_folder_path"))
+        self.set = gmx.Settings.from_buffer_copy(st["set"])
+        if st.get("params") is not None:
+            self._params = gmx.ModelParams.from_buffer_copy(st["params"])
+        self.object_set_name = st["object_set_name"]
+        self.machine = st["machine"]

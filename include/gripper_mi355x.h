@@ -315,6 +315,9 @@ int  gm_update_config(gm_ctx* ctx, const gm_config* cfg);  /* mj.set.* writes */
 /* MjClass::reset() (mjclass.cpp:434-486) for envs with mask[e] != 0 (NULL = all),
  * followed by spawn_object(spawn[e]) (mjclass.cpp:2352-2420).  Host arrays. */
 int  gm_reset(gm_ctx* ctx, const uint8_t* mask, const gm_spawn* spawn);
+/* MjClass::spawn_object(idx, x, y, zrot) alone (mjclass.cpp:2352-2420; bind.cpp:98-105):
+ * replaces the live object of masked envs; consumes no RNG draws.  Host arrays. */
+int  gm_spawn_object(gm_ctx* ctx, const uint8_t* mask, const gm_spawn* spawn);
 
 /* MjClass::set_continous_action for every action index i in order
  * (mjclass.cpp:1517-1630; called per index by MjEnv._set_action, MjEnv.py:591-594).

@@ -1879,6 +1879,27 @@ static void randomise_mu(or_env* e) {
     for (int i = 0; i < 3; i++) e->rand_mu[order[k]][i] = ss[order[k]]->noise_mu * (2 * unif01(&e->rng) - 1);
 }
 
+/* spawn_object (mjclass.cpp:2352-2420, objecthandler.cpp:403-428) */
+void or_spawn(or_env* e, const gm_spawn* sp) {
+  int oi = sp ? sp->object_index : 0;
+  if (oi < 0 || oi >= e->nobj) oi = 0;
+  e->obj_index = oi;
+  apply_object(&e->m, &e->objs[oi]);
+  int qa = e->m.jnt_qposadr[e->m.body_jnt[e->m.body_obj]];
+  double zr = sp ? sp->zrot : 0.0;
+  /* quaternion exactly as the reference composes it: QPos (x,y,z,qx,qy,qz,qw) with
+   * qx written to qpos[3] (MuJoCo's w slot) -- net effect: rotation pi+zrot about z */
+  double x2 = sin(-zr / 2.0), w2 = cos(-zr / 2.0);
+  double qw = w2, qx = x2, qy = 0, qz = 0;
+  e->qpos[qa + 0] = sp ? sp->x : 0.0;
+  e->qpos[qa + 1] = sp ? sp->y : 0.0;
+  e->qpos[qa + 2] = object_rest_z(&e->objs[oi]) + 1e-6;
+  e->qpos[qa + 3] = qx; e->qpos[qa + 4] = qy; e->qpos[qa + 5] = qz; e->qpos[qa + 6] = qw;
+  quatnorm(&e->qpos[qa + 3]);
+  for (int k = 0; k < 6; k++) e->qvel[e->m.dof_obj + k] = 0;
+  for (int k = 0; k < 7; k++) e->start_qpos[k] = e->qpos[qa + k];
+}
+
 void or_reset(or_env* e, const gm_spawn* sp) {
   const gm_model* m0 = &e->m;
   /* luke::reset: targets home, locks off, keyframe, object parked */
@@ -1908,24 +1929,7 @@ void or_reset(or_env* e, const gm_spawn* sp) {
     if (e->base[2] < e->c.base_min[2]) e->base[2] = e->c.base_min[2];
     e->qpos[m0->dof_base] = e->base[2] + e->eq_q[m0->dof_base];
   }
-  /* spawn_object (mjclass.cpp:2352-2420, objecthandler.cpp:403-428) */
-  int oi = sp ? sp->object_index : 0;
-  if (oi < 0 || oi >= e->nobj) oi = 0;
-  e->obj_index = oi;
-  apply_object(&e->m, &e->objs[oi]);
-  int qa = e->m.jnt_qposadr[e->m.body_jnt[e->m.body_obj]];
-  double zr = sp ? sp->zrot : 0.0;
-  /* quaternion exactly as the reference composes it: QPos (x,y,z,qx,qy,qz,qw) with
-   * qx written to qpos[3] (MuJoCo's w slot) -- net effect: rotation pi+zrot about z */
-  double x2 = sin(-zr / 2.0), w2 = cos(-zr / 2.0);
-  double qw = w2, qx = x2, qy = 0, qz = 0;
-  e->qpos[qa + 0] = sp ? sp->x : 0.0;
-  e->qpos[qa + 1] = sp ? sp->y : 0.0;
-  e->qpos[qa + 2] = object_rest_z(&e->objs[oi]) + 1e-6;
-  e->qpos[qa + 3] = qx; e->qpos[qa + 4] = qy; e->qpos[qa + 5] = qz; e->qpos[qa + 6] = qw;
-  quatnorm(&e->qpos[qa + 3]);
-  for (int k = 0; k < 6; k++) e->qvel[e->m.dof_obj + k] = 0;
-  for (int k = 0; k < 7; k++) e->start_qpos[k] = e->qpos[qa + k];
+  or_spawn(e, sp);
 }
 
 or_env* or_create(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects,
@@ -1942,11 +1946,6 @@ or_env* or_create(const gm_model* m, const gm_config* c, const gm_object* object
   if (e->nobj > 0) apply_object(&e->m, &e->objs[0]);
   settle(e);
   e->old_x = e->old_y = e->old_z = 0;
-  /* state after settle (function-static flags keep their settled values) */
-  {
-    or_env tmp = *e;
-    (void)tmp;
-  }
   return e;
 }
 void or_destroy(or_env* e) { free(e); }

@@ -33,7 +33,8 @@ or_env* or_create(const gm_model* m, const gm_config* c, const gm_object* object
 void    or_destroy(or_env* e);
 size_t  or_sizeof(void);
 
-void  or_reset(or_env* e, const gm_spawn* spawn);                  /* MjClass::reset + spawn_object */
+void  or_reset(or_env* e, const gm_spawn* spawn);
+void  or_spawn(or_env* e, const gm_spawn* spawn);                  /* MjClass::spawn_object alone */
 void  or_set_action(or_env* e, const float* actions);              /* set_continous_action x n_actions */
 void  or_set_discrete_action(or_env* e, int32_t action);           /* set_discrete_action */
 void  or_step(or_env* e);                                          /* action_step */

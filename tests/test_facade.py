@@ -1,0 +1,86 @@
+"""The mjpy.bind facade (drop-in for the reference's pybind11 `bind` module, MjEnv.py:18):
+host-side surface on the CPU, and an MjEnv-style episode on the GPU checked against the
+fp64 oracle step by step."""
+import pickle
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+
+def test_facade_surface_without_gpu(gm):
+    from mjpy.bind import MjClass, EventTrack
+    mj = MjClass()
+    for name in ("set_continous_action", "set_discrete_action", "action_step", "get_observation_numpy",
+                 "is_done", "reward", "reset", "hard_reset", "spawn_object", "spawn_into_scene",
+                 "get_n_actions", "get_n_obs", "get_N", "set_finger_thickness", "set_base_XYZ_limits",
+                 "get_event_state", "get_number_of_objects", "get_object_name", "load_relative"):
+        assert callable(getattr(mj, name))
+    assert hasattr(mj.default_spawn_params, "xrange")
+    t = EventTrack()
+    assert hasattr(t, "lifted") and hasattr(t, "exceed_limits")
+
+
+def test_facade_settings_drive_sizes(gm):
+    from mjpy.bind import MjClass
+    mj = MjClass()
+    mj.set = gm.canonical_settings(seed=2)
+    assert mj.get_n_obs() == 63 and mj.get_n_actions() == 4
+    assert mj.get_N() == 8
+    mj.set_finger_thickness(1.0e-3)
+    assert mj.get_finger_thickness() == pytest.approx(1.0e-3)
+
+
+def test_facade_pickle_roundtrip(gm):
+    from mjpy.bind import MjClass
+    mj = MjClass()
+    mj.set = gm.canonical_settings(seed=9)
+    mj.object_set_name = "set1_synthetic"
+    mj2 = pickle.loads(pickle.dumps(mj))
+    assert bytes(mj2.set) == bytes(mj.set)
+    assert mj2.object_set_name == "set1_synthetic"
+
+
+def test_facade_without_gpu_fails_loudly(gm):
+    if gpu_available():
+        pytest.skip("a GPU is present")
+    from mjpy.bind import MjClass
+    mj = MjClass()
+    with pytest.raises(RuntimeError):
+        mj.reset()
+
+
+@pytest.mark.gpu
+def test_facade_episode_matches_oracle(gm):
+    """MjEnv._set_action / _take_action / _next_observation / _is_done / _reward order
+    (MjEnv.py:585-637, 2170-2220) through the facade vs the oracle, noise off."""
+    import oracle_lib
+    from mjpy.bind import MjClass
+    mj = MjClass()
+    mj.set = gm.canonical_settings(noise=False, seed=4)
+    mj.object_set_name = "set1_synthetic"
+    mj.reset()
+    mj.spawn_object(0, 0.06, 0.06, 0.0)
+    env = mj._env
+    o = oracle_lib.OracleEnv(env.model, env.cfg, env.objects, 0)
+    sp = gm.Spawn()
+    sp.object_index, sp.x, sp.y, sp.zrot = 0, 0.06, 0.06, 0.0
+    o.reset(sp)
+    rng = np.random.default_rng(3)
+    for t in range(10):
+        a = rng.uniform(-1, 1, size=mj.get_n_actions()).astype(np.float32)
+        for i, f in enumerate(a):
+            mj.set_continous_action(i, float(f))
+        mj.action_step()
+        obs = mj.get_observation_numpy()
+        done = mj.is_done()
+        r = mj.reward()
+        ro, rr, rd = o.step(a)
+        d = np.abs(obs - ro)
+        big = np.abs(ro) >= 1e-3
+        assert (d[big] / np.abs(ro[big])).max(initial=0) <= 1e-4 and d[~big].max(initial=0) <= 1e-4
+        assert done == rd
+        assert r == pytest.approx(rr, rel=1e-4, abs=1e-6)
+    ev = mj.get_event_state()
+    assert isinstance(ev.lifted.row, int)

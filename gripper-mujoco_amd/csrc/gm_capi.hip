@@ -57,6 +57,33 @@ int fail(gm_ctx* c, int code, const std::string& msg) {
       return fail(ctx, GM_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_));    \
   } while (0)
 
+// gm_step_kernel is instantiated per finger chain length (CL = n_seg + 2) so every chain
+// recursion is unrolled into registers; GM_NSEG_LIST is the set compiled in.
+#ifndef GM_NSEG_LIST
+#define GM_NSEG_LIST X(5) X(6) X(7) X(8) X(9) X(10)
+#endif
+bool nseg_supported(int n) {
+  switch (n) {
+#define X(N) case N:
+    GM_NSEG_LIST
+#undef X
+    return true;
+    default: return false;
+  }
+}
+hipError_t launch_step(gm_ctx* c, int grid, int n_envs, int mode, DebugOut dbg) {
+  switch (c->model.n_seg) {
+#define X(N)                                                                                               \
+  case N:                                                                                                  \
+    hipLaunchKernelGGL((gm_step_kernel<N + 2>), dim3(grid), dim3(NT), 0, c->stream, c->d_state, c->d_model, \
+                       c->d_cfg, c->d_topo, c->d_obs, c->d_rew, c->d_done, n_envs, mode, dbg);              \
+    return hipGetLastError();
+    GM_NSEG_LIST
+#undef X
+    default: return hipErrorInvalidValue;
+  }
+}
+
 int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
   std::memset(&T, 0, sizeof(T));
   T.N = m.n_seg;
@@ -121,6 +148,11 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   std::string err;
   int rc = build_topo(c->model, c->topo, err);
   if (rc != GM_OK) { fprintf(stderr, "gm_create: %s\n", err.c_str()); delete c; return rc; }
+  if (!nseg_supported(c->model.n_seg)) {
+    fprintf(stderr, "gm_create: n_seg=%d has no compiled step kernel (GM_NSEG_LIST)\n", c->model.n_seg);
+    delete c;
+    return GM_E_RANGE;
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device) {
     fprintf(stderr, "gm_create: no HIP device %d (found %d)\n", device, ndev);
@@ -157,9 +189,7 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   // one-time calibrate_reset settle (myfunctions.cpp:1470-1505) on env 0
   hipLaunchKernelGGL(gm_settle_init_kernel, dim3(1), dim3(1), 0, c->stream, c->d_state, c->d_model, c->d_topo, c->d_objs);
   DebugOut dbg{nullptr, nullptr, nullptr, nullptr, nullptr};
-  hipLaunchKernelGGL(gm_step_kernel, dim3(1), dim3(NT), 0, c->stream, c->d_state, c->d_model, c->d_cfg, c->d_topo,
-                     c->d_obs, c->d_rew, c->d_done, 1, 1, dbg);
-  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, launch_step(c, 1, 1, 1, dbg));
   HIPCHK(c, hipMemcpyAsync(c->d_eq, reinterpret_cast<char*>(c->d_state) + offsetof(GmEnvState, qpos), sizeof(double) * GM_MAX_QPOS, hipMemcpyDeviceToDevice, c->stream));
   int threads = 256, blocks = (n_envs + threads - 1) / threads;
   hipLaunchKernelGGL(gm_init_envs_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, cfg->s.random_seed,
@@ -266,9 +296,7 @@ int gm_step(gm_ctx* c) {
   HIPCHK(c, hipSetDevice(c->device));
   DebugOut dbg{nullptr, nullptr, nullptr, nullptr, nullptr};
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-  hipLaunchKernelGGL(gm_step_kernel, dim3(c->n_envs), dim3(NT), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
-                     c->d_topo, c->d_obs, c->d_rew, c->d_done, c->n_envs, 0, dbg);
-  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, launch_step(c, c->n_envs, c->n_envs, 0, dbg));
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   c->timed = true;
   return GM_OK;
@@ -395,9 +423,7 @@ int gm_debug_substep(gm_ctx* c, int32_t* ncon, float* contact, float* efc_force,
   HIPCHK(c, hipMalloc(&d_f, sizeof(float) * n * GM_MAX_EFC));
   HIPCHK(c, hipMalloc(&d_q, sizeof(float) * n * GM_MAX_DOF));
   DebugOut dbg{d_ncon, d_con, d_f, d_q, nullptr};
-  hipLaunchKernelGGL(gm_step_kernel, dim3(c->n_envs), dim3(NT), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
-                     c->d_topo, c->d_obs, c->d_rew, c->d_done, c->n_envs, 2, dbg);
-  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, launch_step(c, c->n_envs, c->n_envs, 2, dbg));
   if (ncon) HIPCHK(c, hipMemcpyAsync(ncon, d_ncon, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
   if (contact) HIPCHK(c, hipMemcpyAsync(contact, d_con, sizeof(float) * n * GM_MAX_CON * 16, hipMemcpyDeviceToHost, c->stream));
   if (efc_force) HIPCHK(c, hipMemcpyAsync(efc_force, d_f, sizeof(float) * n * GM_MAX_EFC, hipMemcpyDeviceToHost, c->stream));
@@ -445,9 +471,7 @@ int gm_step_profiled(gm_ctx* c, uint64_t* phase_cycles) {
   unsigned long long* d_ph;
   HIPCHK(c, hipMalloc(&d_ph, sizeof(unsigned long long) * n * GM_NPHASE));
   DebugOut dbg{nullptr, nullptr, nullptr, nullptr, d_ph};
-  hipLaunchKernelGGL(gm_step_kernel, dim3(c->n_envs), dim3(NT), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
-                     c->d_topo, c->d_obs, c->d_rew, c->d_done, c->n_envs, 0, dbg);
-  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, launch_step(c, c->n_envs, c->n_envs, 0, dbg));
   HIPCHK(c, hipMemcpyAsync(phase_cycles, d_ph, sizeof(unsigned long long) * n * GM_NPHASE, hipMemcpyDeviceToHost,
                            c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

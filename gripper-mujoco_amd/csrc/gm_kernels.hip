@@ -49,17 +49,27 @@ struct __align__(16) Shared {
   real qacc_s[GM_MAX_DOF], qacc[GM_MAX_DOF], frc[GM_MAX_DOF], z[GM_MAX_DOF];
   real xpos[GM_MAX_BODY][3];
   real xmat[GM_MAX_BODY][9];
-  real cinert[GM_MAX_BODY][10];
-  real Ic[GM_MAX_BODY][10];
-  real cfrc[GM_MAX_BODY][6];
   real cdof[GM_MAX_DOF][6];
-  real gxpos[GM_MAX_GEOM][3];
-  real gxmat[GM_MAX_GEOM][9];
   real Hf[3][TRIF], Hp[3], Ho[21], Hbb;
   real Df[3][CLMAX + 1], Dp[2], Do[6], Dbb;
   real bdelta[5];
   real con[GM_MAX_CON][20];   // dist, pos3, frame9, mu, force3, g1, g2, (pad)
-  real Y[GM_MAX_EFC][CW];
+  // LDS shared in time: the dynamics/collision scratch is dead once the constraint
+  // rows are built, so the compact Jacobian rows reuse it
+  union {
+    struct {                  // kinematics .. collision
+      real cinert[GM_MAX_BODY][10];
+      real Ic[GM_MAX_BODY][10];
+      real cfrc[GM_MAX_BODY][6];
+      real qloc[GM_MAX_BODY][4];          // hinge half-angle quaternions (FK phase A)
+      real chain_f[5][6], chain_I[5][10]; // chain-root sums for the base body
+      real gxpos[GM_MAX_GEOM][3];
+      real gxmat[GM_MAX_GEOM][9];
+    };
+    struct {                  // constraints .. constraint_accel
+      real Y[GM_MAX_EFC][CW];
+    };
+  };
   real efc_f[GM_MAX_EFC];
   int32_t cnt[NT];
   int32_t ncon, nefc, nlockrows, overflow;
@@ -68,6 +78,9 @@ struct __align__(16) Shared {
   float gauge_tmp[3];
   unsigned long long tph[GM_NPHASE];
 };
+
+// per-phase shader-clock accounting (gm_step_profiled); needs `prof`, `lane`, `t0` in scope
+#define PH(k) do { if (prof) { unsigned long long t_ = clock64(); if (lane == 0) S.tph[k] += t_ - t0; t0 = t_; } } while (0)
 
 // ------------------------------------------------------------ small math
 template <typename T> __device__ __forceinline__ T dot3(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
@@ -159,89 +172,171 @@ __device__ __forceinline__ real& Hat(Shared& S, int c, int p, int q) {
 }
 
 // ============================================================ kinematics
-// mj_kinematics restatement (oracle.c: fk), one lane per chain.
-__device__ void body_fk(Shared& S, const gm_model* __restrict__ m, int b, const real* ppos,
-                        const real* pquat, real* quat_out) {
+// mj_kinematics restated (oracle.c fk): phase A, one lane per body, the hinge joint
+// rotations (the only transcendental work) ; phase B, one lane per chain, the pose
+// recursion root -> leaf entirely in registers (chain length compile-time, unrolled,
+// every model constant load independent of the recursion) ; phase C, one lane per
+// body / dof / geom: rotation matrices, world-origin spatial inertias, motion
+// subspaces, geom poses.
+struct Pose { real p[3], q[4], R[9]; };
+
+__device__ __forceinline__ void fk_step(Shared& S, const gm_model* __restrict__ m, int b, Pose& P) {
   real bp[3], bq[4], t[3], q[4];
   ld3(bp, m->body_pos[b]);
   ld4(bq, m->body_quat[b]);
-  real Rp[9];
-  quat2mat(Rp, pquat);
-  mulmv3(t, Rp, bp);
-  real xp[3] = {ppos[0] + t[0], ppos[1] + t[1], ppos[2] + t[2]};
-  quatmul(q, pquat, bq);
-  int j = m->body_jnt[b];
+  mulmv3(t, P.R, bp);
+  real xp[3] = {P.p[0] + t[0], P.p[1] + t[1], P.p[2] + t[2]};
+  quatmul(q, P.q, bq);
+  const int j = m->body_jnt[b];
   if (j >= 0) {
-    int qa = m->jnt_qposadr[j];
-    int type = m->jnt_type[j];
+    const int type = m->jnt_type[j];
     if (type == GM_JNT_SLIDE) {
       real R[9], ax[3], wa[3];
       quat2mat(R, q);
       ld3(ax, m->jnt_axis[j]);
       mulmv3(wa, R, ax);
-      real qv = S.s.qpos[qa];
+      const real qv = S.s.qpos[m->jnt_qposadr[j]];
       xp[0] += wa[0] * qv; xp[1] += wa[1] * qv; xp[2] += wa[2] * qv;
     } else if (type == GM_JNT_HINGE) {
-      real ang = S.s.qpos[qa];
-      real sn = sin(0.5 * ang), cs = cos(0.5 * ang);
-      real ql[4] = {cs, (real)m->jnt_axis[j][0] * sn, (real)m->jnt_axis[j][1] * sn, (real)m->jnt_axis[j][2] * sn};
+      real ql[4] = {S.qloc[b][0], S.qloc[b][1], S.qloc[b][2], S.qloc[b][3]};
       quatmul(q, q, ql);
-    } else {
-      xp[0] = S.s.qpos[qa]; xp[1] = S.s.qpos[qa + 1]; xp[2] = S.s.qpos[qa + 2];
-      q[0] = S.s.qpos[qa + 3]; q[1] = S.s.qpos[qa + 4]; q[2] = S.s.qpos[qa + 5]; q[3] = S.s.qpos[qa + 6];
     }
   }
   quatnorm(q);
+  P.p[0] = xp[0]; P.p[1] = xp[1]; P.p[2] = xp[2];
+  P.q[0] = q[0]; P.q[1] = q[1]; P.q[2] = q[2]; P.q[3] = q[3];
+  quat2mat(P.R, q);
   S.xpos[b][0] = xp[0]; S.xpos[b][1] = xp[1]; S.xpos[b][2] = xp[2];
-  real R[9];
-  quat2mat(R, q);
-  for (int k = 0; k < 9; k++) S.xmat[b][k] = R[k];
-  for (int k = 0; k < 4; k++) quat_out[k] = q[k];
-  // world-origin spatial inertia
-  real ip[3], c[3];
-  ld3(ip, m->body_ipos[b]);
-  mulmv3(c, R, ip);
-  c[0] += xp[0]; c[1] += xp[1]; c[2] += xp[2];
-  real I[3] = {(real)m->body_inertia[b][0], (real)m->body_inertia[b][1], (real)m->body_inertia[b][2]};
-  real mass = (real)m->body_mass[b];
-  if (b == m->body_obj) {
-    mass = S.s.obj_mass;
-    I[0] = S.s.obj_inertia[0]; I[1] = S.s.obj_inertia[1]; I[2] = S.s.obj_inertia[2];
+#pragma unroll
+  for (int k = 0; k < 9; k++) S.xmat[b][k] = P.R[k];
+}
+
+template <int CL>
+__device__ void kinematics(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+  // A: hinge rotations
+  if (lane < T->nbody) {
+    const int j = m->body_jnt[lane];
+    if (j >= 0 && m->jnt_type[j] == GM_JNT_HINGE) {
+      const real ang = S.s.qpos[m->jnt_qposadr[j]];
+      real sn, cs;
+      sincos(0.5 * ang, &sn, &cs);
+      S.qloc[lane][0] = cs;
+      S.qloc[lane][1] = (real)m->jnt_axis[j][0] * sn;
+      S.qloc[lane][2] = (real)m->jnt_axis[j][1] * sn;
+      S.qloc[lane][3] = (real)m->jnt_axis[j][2] * sn;
+    }
   }
-  real Iw[9];
-  for (int i = 0; i < 3; i++)
-    for (int k = 0; k < 3; k++)
-      Iw[3 * i + k] = R[3 * i] * I[0] * R[3 * k] + R[3 * i + 1] * I[1] * R[3 * k + 1] + R[3 * i + 2] * I[2] * R[3 * k + 2];
-  real cc = dot3(c, c);
-  real* ci = S.cinert[b];
-  ci[0] = Iw[0] + mass * (cc - c[0] * c[0]);
-  ci[1] = Iw[4] + mass * (cc - c[1] * c[1]);
-  ci[2] = Iw[8] + mass * (cc - c[2] * c[2]);
-  ci[3] = Iw[1] - mass * c[0] * c[1];
-  ci[4] = Iw[2] - mass * c[0] * c[2];
-  ci[5] = Iw[5] - mass * c[1] * c[2];
-  ci[6] = mass * c[0]; ci[7] = mass * c[1]; ci[8] = mass * c[2];
-  ci[9] = mass;
-  // motion subspaces of this body's dofs
-  if (j >= 0) {
-    int d0 = m->jnt_dofadr[j];
-    int type = m->jnt_type[j];
-    if (type == GM_JNT_FREE) {
-      for (int k = 0; k < 3; k++) {
-        real* cd = S.cdof[d0 + k];
-        cd[0] = cd[1] = cd[2] = 0; cd[3] = cd[4] = cd[5] = 0; cd[3 + k] = 1;
+  __syncthreads();
+  // B: pose recursion per chain; every chain lane derives the base pose itself
+  if (lane < 4) {
+    Pose P;
+    P.p[0] = P.p[1] = P.p[2] = 0;
+    P.q[0] = 1; P.q[1] = P.q[2] = P.q[3] = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) P.R[k] = (k % 4 == 0) ? 1.0 : 0.0;
+    {
+      // base body (child of the world): same operation order as fk_step
+      const int b = T->body_base;
+      real bp[3], bq[4], q[4];
+      ld3(bp, m->body_pos[b]);
+      ld4(bq, m->body_quat[b]);
+      real t[3];
+      mulmv3(t, P.R, bp);
+      real xp[3] = {t[0], t[1], t[2]};
+      quatmul(q, P.q, bq);
+      const int j = m->body_jnt[b];
+      real R[9], ax[3], wa[3];
+      quat2mat(R, q);
+      ld3(ax, m->jnt_axis[j]);
+      mulmv3(wa, R, ax);
+      const real qv = S.s.qpos[m->jnt_qposadr[j]];
+      xp[0] += wa[0] * qv; xp[1] += wa[1] * qv; xp[2] += wa[2] * qv;
+      quatnorm(q);
+      P.p[0] = xp[0]; P.p[1] = xp[1]; P.p[2] = xp[2];
+      P.q[0] = q[0]; P.q[1] = q[1]; P.q[2] = q[2]; P.q[3] = q[3];
+      quat2mat(P.R, q);
+      if (lane == 0) {
+        S.xpos[b][0] = xp[0]; S.xpos[b][1] = xp[1]; S.xpos[b][2] = xp[2];
+#pragma unroll
+        for (int k = 0; k < 9; k++) S.xmat[b][k] = P.R[k];
       }
-      for (int k = 0; k < 3; k++) {
-        real* cd = S.cdof[d0 + 3 + k];
-        real w[3] = {R[k], R[3 + k], R[6 + k]};
+    }
+    if (lane < 3) {
+      const int b0 = T->body_f0[lane];
+#pragma unroll
+      for (int p = 1; p <= CL; p++) fk_step(S, m, b0 + p - 1, P);
+    } else {
+      fk_step(S, m, T->body_palm, P);
+    }
+  } else if (lane == 4) {
+    // object: free joint, pose straight from qpos
+    const int b = T->body_obj, qa = T->qadr_obj;
+    real q[4] = {S.s.qpos[qa + 3], S.s.qpos[qa + 4], S.s.qpos[qa + 5], S.s.qpos[qa + 6]};
+    quatnorm(q);
+    real R[9];
+    quat2mat(R, q);
+    S.xpos[b][0] = S.s.qpos[qa]; S.xpos[b][1] = S.s.qpos[qa + 1]; S.xpos[b][2] = S.s.qpos[qa + 2];
+#pragma unroll
+    for (int k = 0; k < 9; k++) S.xmat[b][k] = R[k];
+  }
+  __syncthreads();
+  // C1: world-origin spatial inertia per body
+  if (lane < T->nbody && lane > 0) {
+    const int b = lane;
+    real R[9], xp[3];
+#pragma unroll
+    for (int k = 0; k < 9; k++) R[k] = S.xmat[b][k];
+    xp[0] = S.xpos[b][0]; xp[1] = S.xpos[b][1]; xp[2] = S.xpos[b][2];
+    real ip[3], c[3];
+    ld3(ip, m->body_ipos[b]);
+    mulmv3(c, R, ip);
+    c[0] += xp[0]; c[1] += xp[1]; c[2] += xp[2];
+    real I[3] = {(real)m->body_inertia[b][0], (real)m->body_inertia[b][1], (real)m->body_inertia[b][2]};
+    real mass = (real)m->body_mass[b];
+    if (b == m->body_obj) {
+      mass = S.s.obj_mass;
+      I[0] = S.s.obj_inertia[0]; I[1] = S.s.obj_inertia[1]; I[2] = S.s.obj_inertia[2];
+    }
+    real Iw[9];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int k = 0; k < 3; k++)
+        Iw[3 * i + k] = R[3 * i] * I[0] * R[3 * k] + R[3 * i + 1] * I[1] * R[3 * k + 1] + R[3 * i + 2] * I[2] * R[3 * k + 2];
+    const real cc = dot3(c, c);
+    real* ci = S.cinert[b];
+    ci[0] = Iw[0] + mass * (cc - c[0] * c[0]);
+    ci[1] = Iw[4] + mass * (cc - c[1] * c[1]);
+    ci[2] = Iw[8] + mass * (cc - c[2] * c[2]);
+    ci[3] = Iw[1] - mass * c[0] * c[1];
+    ci[4] = Iw[2] - mass * c[0] * c[2];
+    ci[5] = Iw[5] - mass * c[1] * c[2];
+    ci[6] = mass * c[0]; ci[7] = mass * c[1]; ci[8] = mass * c[2];
+    ci[9] = mass;
+  }
+  // C2: motion subspaces, one lane per dof
+  if (lane < T->nv) {
+    const int d = lane;
+    const int b = m->dof_body[d];
+    const int j = m->body_jnt[b];
+    const int type = m->jnt_type[j];
+    real* cd = S.cdof[d];
+    const real xp[3] = {S.xpos[b][0], S.xpos[b][1], S.xpos[b][2]};
+    if (type == GM_JNT_FREE) {
+      const int k = d - m->jnt_dofadr[j];
+      if (k < 3) {
+        cd[0] = cd[1] = cd[2] = 0; cd[3] = cd[4] = cd[5] = 0; cd[3 + k] = 1;
+      } else {
+        const real w[3] = {S.xmat[b][k - 3], S.xmat[b][3 + k - 3], S.xmat[b][6 + k - 3]};
         cd[0] = w[0]; cd[1] = w[1]; cd[2] = w[2];
         cross3(cd + 3, xp, w);
       }
     } else {
-      real ax[3], wa[3];
+      real ax[3], wa[3], R[9];
+#pragma unroll
+      for (int k = 0; k < 9; k++) R[k] = S.xmat[b][k];
       ld3(ax, m->jnt_axis[j]);
       mulmv3(wa, R, ax);
-      real* cd = S.cdof[d0];
       if (type == GM_JNT_SLIDE) {
         cd[0] = cd[1] = cd[2] = 0; cd[3] = wa[0]; cd[4] = wa[1]; cd[5] = wa[2];
       } else {
@@ -250,141 +345,158 @@ __device__ void body_fk(Shared& S, const gm_model* __restrict__ m, int b, const 
       }
     }
   }
-}
-
-__device__ void kinematics(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
-  // base body (world child) first, then one lane per chain (fingers 0..2, palm 3, object 4)
-  __shared__ real base_quat[4];
-  if (lane == 0) {
-    real q0[4] = {1, 0, 0, 0}, p0[3] = {0, 0, 0};
-    body_fk(S, m, T->body_base, p0, q0, base_quat);
-  }
-  __syncthreads();
-  if (lane < 5) {
-    real q[4];
-    if (lane == 4) {
-      real q0[4] = {1, 0, 0, 0}, p0[3] = {0, 0, 0};
-      body_fk(S, m, T->body_obj, p0, q0, q);
-    } else {
-      real pq[4] = {base_quat[0], base_quat[1], base_quat[2], base_quat[3]};
-      real pp[3] = {S.xpos[T->body_base][0], S.xpos[T->body_base][1], S.xpos[T->body_base][2]};
-      int L = chain_len(T, lane);
-      for (int p = 1; p <= L; p++) {
-        int b = chain_body(T, lane, p);
-        body_fk(S, m, b, pp, pq, q);
-        pp[0] = S.xpos[b][0]; pp[1] = S.xpos[b][1]; pp[2] = S.xpos[b][2];
-        pq[0] = q[0]; pq[1] = q[1]; pq[2] = q[2]; pq[3] = q[3];
-      }
-    }
-  }
-  __syncthreads();
-  // geoms: one lane per geom
+  // C3: geoms, one lane per geom
   if (lane < T->ngeom) {
-    int g = lane;
-    int b = m->geom_body[g];
+    const int g = lane;
+    const int b = m->geom_body[g];
     real R[9];
     if (b == 0) {
       R[0] = 1; R[1] = 0; R[2] = 0; R[3] = 0; R[4] = 1; R[5] = 0; R[6] = 0; R[7] = 0; R[8] = 1;
     } else {
+#pragma unroll
       for (int k = 0; k < 9; k++) R[k] = S.xmat[b][k];
     }
     real gp[3], t[3], gq[4], Rg[9];
     ld3(gp, m->geom_pos[g]);
     mulmv3(t, R, gp);
-    real bp0 = b == 0 ? 0.f : S.xpos[b][0], bp1 = b == 0 ? 0.f : S.xpos[b][1], bp2 = b == 0 ? 0.f : S.xpos[b][2];
+    const real bp0 = b == 0 ? 0.0 : S.xpos[b][0], bp1 = b == 0 ? 0.0 : S.xpos[b][1], bp2 = b == 0 ? 0.0 : S.xpos[b][2];
     S.gxpos[g][0] = bp0 + t[0]; S.gxpos[g][1] = bp1 + t[1]; S.gxpos[g][2] = bp2 + t[2];
     ld4(gq, m->geom_quat[g]);
     quat2mat(Rg, gq);
+#pragma unroll
     for (int i = 0; i < 3; i++)
+#pragma unroll
       for (int k = 0; k < 3; k++)
         S.gxmat[g][3 * i + k] = R[3 * i] * Rg[k] + R[3 * i + 1] * Rg[3 + k] + R[3 * i + 2] * Rg[6 + k];
   }
+  __syncthreads();
 }
 
 // ============================================================ CRB + RNE
+// mj_rne (bias forces, world-origin spatial algebra) and mj_crb (composite inertias):
+// forward velocity / bias-acceleration recursion and body forces per chain, then
+// leaf -> root running sums in registers; chain-root totals meet at the base body.
+__device__ __forceinline__ void body_force(Shared& S, int b, const real* cvel, const real* cacc) {
+  real ci[10], t1[6], t2[6], f[6];
+#pragma unroll
+  for (int k = 0; k < 10; k++) ci[k] = S.cinert[b][k];
+  inert_mul(f, ci, cacc);
+  inert_mul(t1, ci, cvel);
+  cross_force(t2, cvel, t1);
+#pragma unroll
+  for (int k = 0; k < 6; k++) S.cfrc[b][k] = f[k] + t2[k];
+}
+__device__ __forceinline__ void rne_fwd(Shared& S, int b, int d, real* cvel, real* cacc) {
+  real cd[6], cdd[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
+  cross_motion(cdd, cvel, cd);
+  const real qv = S.s.qvel[d];
+#pragma unroll
+  for (int k = 0; k < 6; k++) { cvel[k] += cd[k] * qv; cacc[k] += cdd[k] * qv; }
+  body_force(S, b, cvel, cacc);
+}
+// backward running sums over bodies b0 .. b0+L-1 (leaf = last); writes cfrc / Ic
+template <int L>
+__device__ __forceinline__ void chain_sums(Shared& S, int b0, real* fs, real* Is) {
+#pragma unroll
+  for (int k = 0; k < 6; k++) fs[k] = 0;
+#pragma unroll
+  for (int k = 0; k < 10; k++) Is[k] = 0;
+#pragma unroll
+  for (int p = L; p >= 1; p--) {
+    const int b = b0 + p - 1;
+#pragma unroll
+    for (int k = 0; k < 6; k++) { fs[k] += S.cfrc[b][k]; S.cfrc[b][k] = fs[k]; }
+#pragma unroll
+    for (int k = 0; k < 10; k++) { Is[k] = S.cinert[b][k] + (p < L ? Is[k] : 0.0); S.Ic[b][k] = Is[k]; }
+  }
+}
+
+template <int CL>
 __device__ void crb_rne(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
-  // ---- composite inertia and RNE forward/backward along each chain (lanes 0..4) ----
-  if (lane < 5) {
-    int c = lane;
-    int L = chain_len(T, c);
-    // forward: velocities and bias accelerations
+  if (lane < 4) {
+    const int c = lane;
     real cvel[6], cacc[6];
+#pragma unroll
     for (int k = 0; k < 6; k++) { cvel[k] = 0; cacc[k] = 0; }
     cacc[3] = -(real)m->gravity[0]; cacc[4] = -(real)m->gravity[1]; cacc[5] = -(real)m->gravity[2];
-    if (c < 4) {
-      // base body
-      int db = T->dof_base;
-      real cdd[6];
-      cross_motion(cdd, cvel, S.cdof[db]);
-      real qd = S.s.qvel[db];
-      for (int k = 0; k < 6; k++) { cvel[k] += S.cdof[db][k] * qd; cacc[k] += cdd[k] * qd; }
-      if (c == 0) {
-        real t1[6], t2[6], f[6];
-        inert_mul(f, S.cinert[T->body_base], cacc);
-        inert_mul(t1, S.cinert[T->body_base], cvel);
-        cross_force(t2, cvel, t1);
-        for (int k = 0; k < 6; k++) S.cfrc[T->body_base][k] = f[k] + t2[k];
-      }
-      for (int p = 1; p <= L; p++) {
-        int b = chain_body(T, c, p), d = chain_dof(T, c, p);
-        real cdd2[6];
-        cross_motion(cdd2, cvel, S.cdof[d]);
-        real qv = S.s.qvel[d];
-        for (int k = 0; k < 6; k++) { cvel[k] += S.cdof[d][k] * qv; cacc[k] += cdd2[k] * qv; }
-        real t1[6], t2[6], f[6];
-        inert_mul(f, S.cinert[b], cacc);
-        inert_mul(t1, S.cinert[b], cvel);
-        cross_force(t2, cvel, t1);
-        for (int k = 0; k < 6; k++) S.cfrc[b][k] = f[k] + t2[k];
-      }
-      // backward within the chain
-      for (int p = L; p >= 2; p--) {
-        int b = chain_body(T, c, p), pb = chain_body(T, c, p - 1);
-        for (int k = 0; k < 6; k++) S.cfrc[pb][k] += S.cfrc[b][k];
-      }
-      // composite inertia backward
-      for (int p = L; p >= 1; p--) {
-        int b = chain_body(T, c, p);
-        for (int k = 0; k < 10; k++) S.Ic[b][k] = S.cinert[b][k] + (p < L ? S.Ic[chain_body(T, c, p + 1)][k] : 0.0f);
-      }
-    } else {
-      // object: free joint on one body
-      int b = T->body_obj, d0 = T->dof_obj;
-      for (int k = 0; k < 3; k++) {
-        real qv = S.s.qvel[d0 + k];
-        for (int t = 0; t < 6; t++) cvel[t] += S.cdof[d0 + k][t] * qv;
-      }
-      real cdd[3][6];
-      for (int k = 0; k < 3; k++) cross_motion(cdd[k], cvel, S.cdof[d0 + 3 + k]);
-      for (int k = 0; k < 3; k++) {
-        real qv = S.s.qvel[d0 + 3 + k];
-        for (int t = 0; t < 6; t++) cvel[t] += S.cdof[d0 + 3 + k][t] * qv;
-      }
-      for (int k = 0; k < 3; k++) {
-        real qv = S.s.qvel[d0 + 3 + k];
-        for (int t = 0; t < 6; t++) cacc[t] += cdd[k][t] * qv;
-      }
-      real t1[6], t2[6], f[6];
-      inert_mul(f, S.cinert[b], cacc);
-      inert_mul(t1, S.cinert[b], cvel);
-      cross_force(t2, cvel, t1);
-      for (int k = 0; k < 6; k++) S.cfrc[b][k] = f[k] + t2[k];
-      for (int k = 0; k < 10; k++) S.Ic[b][k] = S.cinert[b][k];
+    {
+      const int db = T->dof_base;
+      real cd[6], cdd[6];
+#pragma unroll
+      for (int k = 0; k < 6; k++) cd[k] = S.cdof[db][k];
+      cross_motion(cdd, cvel, cd);
+      const real qd = S.s.qvel[db];
+#pragma unroll
+      for (int k = 0; k < 6; k++) { cvel[k] += cd[k] * qd; cacc[k] += cdd[k] * qd; }
+      if (c == 0) body_force(S, T->body_base, cvel, cacc);
     }
+    real fs[6], Is[10];
+    if (c < 3) {
+      const int b0 = T->body_f0[c], d0 = T->dof_f0[c];
+#pragma unroll
+      for (int p = 1; p <= CL; p++) rne_fwd(S, b0 + p - 1, d0 + p - 1, cvel, cacc);
+      chain_sums<CL>(S, b0, fs, Is);
+    } else {
+      rne_fwd(S, T->body_palm, T->dof_palm, cvel, cacc);
+      chain_sums<1>(S, T->body_palm, fs, Is);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) S.chain_f[c][k] = fs[k];
+#pragma unroll
+    for (int k = 0; k < 10; k++) S.chain_I[c][k] = Is[k];
+  } else if (lane == 4) {
+    // object: free joint on one body
+    const int b = T->body_obj, d0 = T->dof_obj;
+    real cvel[6], cacc[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) { cvel[k] = 0; cacc[k] = 0; }
+    cacc[3] = -(real)m->gravity[0]; cacc[4] = -(real)m->gravity[1]; cacc[5] = -(real)m->gravity[2];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const real qv = S.s.qvel[d0 + k];
+#pragma unroll
+      for (int t = 0; t < 6; t++) cvel[t] += S.cdof[d0 + k][t] * qv;
+    }
+    real cdd[3][6];
+#pragma unroll
+    for (int k = 0; k < 3; k++) cross_motion(cdd[k], cvel, S.cdof[d0 + 3 + k]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const real qv = S.s.qvel[d0 + 3 + k];
+#pragma unroll
+      for (int t = 0; t < 6; t++) cvel[t] += S.cdof[d0 + 3 + k][t] * qv;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const real qv = S.s.qvel[d0 + 3 + k];
+#pragma unroll
+      for (int t = 0; t < 6; t++) cacc[t] += cdd[k][t] * qv;
+    }
+    body_force(S, b, cvel, cacc);
+#pragma unroll
+    for (int k = 0; k < 10; k++) S.Ic[b][k] = S.cinert[b][k];
   }
   __syncthreads();
-  // base body: add chain roots (fingers' intermediates and palm)
+  // base body: its own inertia / force plus the four chain roots
   if (lane == 0) {
-    int bb = T->body_base;
+    const int bb = T->body_base;
     real ic[10], f[6];
+#pragma unroll
     for (int k = 0; k < 10; k++) ic[k] = S.cinert[bb][k];
+#pragma unroll
     for (int k = 0; k < 6; k++) f[k] = S.cfrc[bb][k];
+#pragma unroll
     for (int c = 0; c < 4; c++) {
-      int r = chain_body(T, c, 1);
-      for (int k = 0; k < 10; k++) ic[k] += S.Ic[r][k];
-      for (int k = 0; k < 6; k++) f[k] += S.cfrc[r][k];
+#pragma unroll
+      for (int k = 0; k < 10; k++) ic[k] += S.chain_I[c][k];
+#pragma unroll
+      for (int k = 0; k < 6; k++) f[k] += S.chain_f[c][k];
     }
+#pragma unroll
     for (int k = 0; k < 10; k++) S.Ic[bb][k] = ic[k];
+#pragma unroll
     for (int k = 0; k < 6; k++) S.cfrc[bb][k] = f[k];
   }
   __syncthreads();
@@ -453,36 +565,67 @@ __device__ void mass_and_forces(Shared& S, const gm_model* __restrict__ m, const
 }
 
 // ============================================================ LTDL factor + solves
-__device__ void factor(Shared& S, const GmTopo* __restrict__ T, int lane) {
-  if (lane < 5) {
-    int c = lane;
-    int L = chain_len(T, c);
-    real delta = 0;
-    if (c < 4) {
-      for (int k = L; k >= 1; k--) {
-        real hk = Hat(S, c, k, k);
-        for (int i = k - 1; i >= 0; i--) {
-          real a = Hat(S, c, k, i) / hk;
-          for (int jj = i; jj >= 0; jj--) {
-            real v = Hat(S, c, k, jj) * a;
-            if (i == 0 && jj == 0) delta += v; else Hat(S, c, i, jj) -= v;
-          }
-          Hat(S, c, k, i) = a;
-        }
+// Tree LTDL of H~ (mj_factorM restated for the canonical tree): each chain block is
+// factored leaves -> root in registers (chain length CL is a compile-time constant so
+// the block never leaves VGPRs); the chains' contributions to the shared base pivot
+// are summed afterwards.
+template <int L>
+__device__ __forceinline__ void factor_chain(real* __restrict__ Hs, real& delta_out, real* __restrict__ Dout) {
+  real H[(L + 1) * (L + 2) / 2];
+#pragma unroll
+  for (int p = 1; p <= L; p++)
+#pragma unroll
+    for (int q = 0; q <= p; q++) H[TRI(p, q)] = Hs[TRI(p, q)];
+  real delta = 0;
+#pragma unroll
+  for (int k = L; k >= 1; k--) {
+    const real ihk = 1.0 / H[TRI(k, k)];
+#pragma unroll
+    for (int i = k - 1; i >= 0; i--) {
+      const real a = H[TRI(k, i)] * ihk;
+#pragma unroll
+      for (int jj = i; jj >= 0; jj--) {
+        const real v = H[TRI(k, jj)] * a;
+        if (i == 0 && jj == 0) delta += v; else H[TRI(i, jj)] -= v;
       }
-      S.bdelta[c] = delta;
-      for (int p = 1; p <= L; p++) { real dv = Hat(S, c, p, p); if (c < 3) S.Df[c][p] = dv; else S.Dp[p] = dv; }
-    } else {
-      for (int k = 5; k >= 1; k--) {
-        real hk = S.Ho[TRI(k, k)];
-        for (int i = k - 1; i >= 0; i--) {
-          real a = S.Ho[TRI(k, i)] / hk;
-          for (int jj = i; jj >= 0; jj--) S.Ho[TRI(i, jj)] -= S.Ho[TRI(k, jj)] * a;
-          S.Ho[TRI(k, i)] = a;
-        }
-      }
-      for (int p = 0; p < 6; p++) S.Do[p] = S.Ho[TRI(p, p)];
+      H[TRI(k, i)] = a;
     }
+  }
+#pragma unroll
+  for (int p = 1; p <= L; p++) {
+#pragma unroll
+    for (int q = 0; q < p; q++) Hs[TRI(p, q)] = H[TRI(p, q)];
+    Hs[TRI(p, p)] = H[TRI(p, p)];
+    Dout[p] = H[TRI(p, p)];
+  }
+  delta_out = delta;
+}
+
+template <int CL>
+__device__ void factor(Shared& S, const GmTopo* __restrict__ T, int lane) {
+  if (lane < 3) {
+    factor_chain<CL>(S.Hf[lane], S.bdelta[lane], S.Df[lane]);
+  } else if (lane == 3) {
+    factor_chain<1>(S.Hp, S.bdelta[3], S.Dp);
+  } else if (lane == 4) {
+    real H[21];
+#pragma unroll
+    for (int i = 0; i < 21; i++) H[i] = S.Ho[i];
+#pragma unroll
+    for (int k = 5; k >= 1; k--) {
+      const real ihk = 1.0 / H[TRI(k, k)];
+#pragma unroll
+      for (int i = k - 1; i >= 0; i--) {
+        const real a = H[TRI(k, i)] * ihk;
+#pragma unroll
+        for (int jj = i; jj >= 0; jj--) H[TRI(i, jj)] -= H[TRI(k, jj)] * a;
+        H[TRI(k, i)] = a;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 21; i++) S.Ho[i] = H[i];
+#pragma unroll
+    for (int p = 0; p < 6; p++) S.Do[p] = H[TRI(p, p)];
   }
   __syncthreads();
   if (lane == 0) S.Dbb = S.Hbb - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3]);
@@ -495,53 +638,81 @@ __device__ __forceinline__ real Dof(Shared& S, int c, int p) {
   return S.Do[p];
 }
 
-// x = H^-1 b over full dof vectors (b, x in LDS, may alias)
+// chain part of x = H~^-1 b: L^T y = b (leaves -> root), base contribution returned
+template <int L>
+__device__ __forceinline__ real chain_LT(const real* __restrict__ Hs, const real* __restrict__ D, real* y) {
+  real yb = 0;
+#pragma unroll
+  for (int k = L; k >= 1; k--) {
+#pragma unroll
+    for (int i = k - 1; i >= 1; i--) y[i] -= Hs[TRI(k, i)] * y[k];
+    yb += Hs[TRI(k, 0)] * y[k];
+  }
+#pragma unroll
+  for (int p = 1; p <= L; p++) y[p] /= D[p];
+  return yb;
+}
+// x = L^-1 y (root -> leaves) given x0 = base solution
+template <int L>
+__device__ __forceinline__ void chain_L(const real* __restrict__ Hs, real x0, const real* y, real* xs) {
+  xs[0] = x0;
+#pragma unroll
+  for (int k = 1; k <= L; k++) {
+    real v = y[k];
+#pragma unroll
+    for (int i = k - 1; i >= 0; i--) v -= Hs[TRI(k, i)] * xs[i];
+    xs[k] = v;
+  }
+}
+__device__ __forceinline__ void obj_solve(const real* __restrict__ Ho, const real* __restrict__ Do, real* y) {
+#pragma unroll
+  for (int k = 5; k >= 1; k--)
+#pragma unroll
+    for (int i = k - 1; i >= 0; i--) y[i] -= Ho[TRI(k, i)] * y[k];
+#pragma unroll
+  for (int p = 0; p < 6; p++) y[p] /= Do[p];
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    real v = y[k];
+#pragma unroll
+    for (int i = k - 1; i >= 0; i--) v -= Ho[TRI(k, i)] * y[i];
+    y[k] = v;
+  }
+}
+
+// x = H~^-1 b over full dof vectors (b, x in LDS, may alias); lanes 0..2 fingers,
+// 3 palm, 4 object
+template <int CL>
 __device__ void solve_full(Shared& S, const GmTopo* __restrict__ T, const real* b, real* x, int lane) {
-  // L^T y = b  (leaves -> root); chain lanes, base accumulated
-  real ych[CLMAX + 1];
-  real ybase_part = 0;
-  int c = lane;
-  if (lane < 5) {
-    int L = chain_len(T, c);
-    if (c < 4) {
-      for (int p = 1; p <= L; p++) ych[p] = b[chain_dof(T, c, p)];
-      for (int k = L; k >= 1; k--) {
-        for (int i = k - 1; i >= 1; i--) ych[i] -= Hat(S, c, k, i) * ych[k];
-        ybase_part += Hat(S, c, k, 0) * ych[k];
-      }
-      for (int p = 1; p <= L; p++) ych[p] /= Dof(S, c, p);
-    } else {
-      for (int p = 0; p < 6; p++) ych[p] = b[T->dof_obj + p];
-      for (int k = 5; k >= 1; k--)
-        for (int i = k - 1; i >= 0; i--) ych[i] -= S.Ho[TRI(k, i)] * ych[k];
-      for (int p = 0; p < 6; p++) ych[p] /= S.Do[p];
-    }
-    if (c < 4) S.bdelta[c] = ybase_part;
+  real y[(CL + 1) > 6 ? (CL + 1) : 6];
+  if (lane < 3) {
+#pragma unroll
+    for (int p = 1; p <= CL; p++) y[p] = b[T->dof_f0[lane] + p - 1];
+    S.bdelta[lane] = chain_LT<CL>(S.Hf[lane], S.Df[lane], y);
+  } else if (lane == 3) {
+    y[1] = b[T->dof_palm];
+    S.bdelta[3] = chain_LT<1>(S.Hp, S.Dp, y);
+  } else if (lane == 4) {
+#pragma unroll
+    for (int p = 0; p < 6; p++) y[p] = b[T->dof_obj + p];
+    obj_solve(S.Ho, S.Do, y);
   }
   __syncthreads();
-  real xbase = (b[T->dof_base] - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3])) / S.Dbb;
+  const real xbase = (b[T->dof_base] - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3])) / S.Dbb;
   __syncthreads();
-  if (lane < 5) {
-    int L = chain_len(T, c);
-    if (c < 4) {
-      real xs[CLMAX + 1];
-      xs[0] = xbase;
-      for (int k = 1; k <= L; k++) {
-        real v = ych[k];
-        for (int i = k - 1; i >= 0; i--) v -= Hat(S, c, k, i) * xs[i];
-        xs[k] = v;
-        x[chain_dof(T, c, k)] = v;
-      }
-      if (c == 0) x[T->dof_base] = xbase;
-    } else {
-      real xs[6];
-      for (int k = 0; k < 6; k++) {
-        real v = ych[k];
-        for (int i = k - 1; i >= 0; i--) v -= S.Ho[TRI(k, i)] * xs[i];
-        xs[k] = v;
-        x[T->dof_obj + k] = v;
-      }
-    }
+  if (lane < 3) {
+    real xs[CL + 1];
+    chain_L<CL>(S.Hf[lane], xbase, y, xs);
+#pragma unroll
+    for (int k = 1; k <= CL; k++) x[T->dof_f0[lane] + k - 1] = xs[k];
+    if (lane == 0) x[T->dof_base] = xbase;
+  } else if (lane == 3) {
+    real xs[2];
+    chain_L<1>(S.Hp, xbase, y, xs);
+    x[T->dof_palm] = xs[1];
+  } else if (lane == 4) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) x[T->dof_obj + k] = y[k];
   }
   __syncthreads();
 }
@@ -976,24 +1147,37 @@ __device__ void contact_jac(Shared& S, const gm_model* __restrict__ m, const GmT
 }
 
 // Y = J L^-1 on a compact row (in place)
-__device__ void row_LTsolve(Shared& S, const GmTopo* __restrict__ T, real* J, int grp) {
+template <int CL>
+__device__ void row_LTsolve(Shared& S, real* J, int grp) {
+#pragma unroll
   for (int k = 5; k >= 1; k--)
+#pragma unroll
     for (int i = k - 1; i >= 0; i--) J[i] -= S.Ho[TRI(k, i)] * J[k];
-  if (grp >= 0 && grp <= 3) {
-    int L = chain_len(T, grp);
-    for (int k = L; k >= 1; k--) {
-      for (int i = k - 1; i >= 1; i--) J[6 + i] -= Hat(S, grp, k, i) * J[6 + k];
-      J[6] -= Hat(S, grp, k, 0) * J[6 + k];
+  if (grp >= 0 && grp < 3) {
+    const real* Hs = S.Hf[grp];
+#pragma unroll
+    for (int k = CL; k >= 1; k--) {
+#pragma unroll
+      for (int i = k - 1; i >= 1; i--) J[6 + i] -= Hs[TRI(k, i)] * J[6 + k];
+      J[6] -= Hs[TRI(k, 0)] * J[6 + k];
     }
+  } else if (grp == 3) {
+    J[6] -= S.Hp[TRI(1, 0)] * J[7];
   }
 }
+template <int CL>
 __device__ __forceinline__ real row_dot_dofs(Shared& S, const GmTopo* __restrict__ T, const real* J, int grp, const real* v) {
   real acc = 0;
+#pragma unroll
   for (int k = 0; k < 6; k++) acc += J[k] * v[T->dof_obj + k];
-  if (grp >= 0 && grp <= 3) {
+  if (grp >= 0 && grp < 3) {
     acc += J[6] * v[T->dof_base];
-    int L = chain_len(T, grp);
-    for (int q = 1; q <= L; q++) acc += J[6 + q] * v[chain_dof(T, grp, q)];
+    const int d0 = T->dof_f0[grp];
+#pragma unroll
+    for (int q = 1; q <= CL; q++) acc += J[6 + q] * v[d0 + q - 1];
+  } else if (grp == 3) {
+    acc += J[6] * v[T->dof_base];
+    acc += J[7] * v[T->dof_palm];
   }
   return acc;
 }
@@ -1012,7 +1196,10 @@ __device__ real impedance(const gm_model* __restrict__ m, real r) {
   return dmin + y * (dmax - dmin);
 }
 
-__device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+template <int CL>
+__device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
+                            bool prof = false) {
+  unsigned long long t0 = prof ? clock64() : 0;
   // row layout: active locks (lock order) then 4 pyramid edges per contact
   int nl = 0;
   for (int k = 0; k < T->nlock; k++) nl += S.s.lock_active[k] ? 1 : 0;
@@ -1046,25 +1233,28 @@ __device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmT
       is_contact = 1;
     }
   }
+  PH(11);
   // a0 = J qacc_smooth, vel = J qvel (uses J before the in-place solve)
   real a0 = 0, vel = 0;
   if (lane < nefc) {
-    a0 = row_dot_dofs(S, T, J, grp, S.qacc_s);
-    vel = row_dot_dofs(S, T, J, grp, S.s.qvel);
-    row_LTsolve(S, T, J, grp);
+    a0 = row_dot_dofs<CL>(S, T, J, grp, S.qacc_s);
+    vel = row_dot_dofs<CL>(S, T, J, grp, S.s.qvel);
+    row_LTsolve<CL>(S, J, grp);
     for (int t = 0; t < CW - 1; t++) S.Y[lane][t] = J[t];
     S.Y[lane][CW - 1] = (real)grp;
   }
   if (lane == 0) { S.nefc = nefc; S.nlockrows = nl; }
   __syncthreads();
+  PH(12);
   // Y D^-1 for this lane's row
   real Yd[CW - 1];
   if (lane < nefc) {
     for (int k = 0; k < 6; k++) Yd[k] = J[k] / S.Do[k];
     Yd[6] = J[6] / S.Dbb;
+#pragma unroll
     for (int q = 1; q <= CLMAX; q++) {
       real dv = 1.0;
-      if (grp >= 0 && grp < 3 && q <= T->CL) dv = S.Df[grp][q];
+      if (grp >= 0 && grp < 3 && q <= CL) dv = S.Df[grp][q];
       else if (grp == 3 && q == 1) dv = S.Dp[1];
       Yd[6 + q] = J[6 + q] / dv;
     }
@@ -1084,11 +1274,13 @@ __device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmT
       if (gj && gi >= 0 && gi <= 3) {
         acc += Yd[6] * Yi[6];
         if (gi == grp)
-          for (int q = 1; q <= CLMAX; q++) acc += Yd[6 + q] * Yi[6 + q];
+#pragma unroll
+          for (int q = 1; q <= CL; q++) acc += Yd[6 + q] * Yi[6 + q];
       }
     }
     A[i] = acc;
   }
+  PH(13);
   // impedance / reference acceleration (mj_makeImpedance)
   real h = m->timestep;
   real tc = m->solref[0];
@@ -1103,32 +1295,37 @@ __device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmT
   real aref = -Bd * vel - K * imp * pos;
   real R = (1 - imp) / imp * Ajj;
   if (R < 1e-15) R = 1e-15;
-  real dinv = Ajj + R;
+  const real arinv = 1.0 / (Ajj + R);   // mj_solPGS's ARinv
   real res = (lane < nefc) ? (a0 - aref) : 0.0;   // (A f + b) with f = 0
   real f = 0;
-  // projected Gauss-Seidel, each row's update broadcast through v_readlane
+  // projected Gauss-Seidel (mj_solPGS order: rows in sequence, fixed sweeps).  Lane j
+  // owns row j: its residual res_j = (A f + b)_j is kept current by every row update,
+  // each update f_r += d is broadcast with v_readlane.  Contact rows are clamped at 0
+  // (pyramid edges), lock rows are unbounded.
+  const int nefc_s = __builtin_amdgcn_readfirstlane(nefc);
+  const real lb = is_contact ? 0.0 : -__builtin_inf();
   for (int it = 0; it < m->pgs_iterations; it++) {
 #pragma unroll
     for (int r = 0; r < GM_MAX_EFC; r++) {
-      if (r < nefc) {
-        real g = res + R * f;
-        real fn = f - g / dinv;
-        if (is_contact && fn < 0) fn = 0;
-        real dl = fn - f;
-        long long bits = __double_as_longlong(dl);
-        int lo = __builtin_amdgcn_readlane((int)bits, r);
-        int hi = __builtin_amdgcn_readlane((int)(bits >> 32), r);
-        real delta = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-        res += A[r] * delta;
-        if (lane == r) f = fn;
-      }
+      if (r >= nefc_s) continue;
+      const real g = fma(R, f, res);
+      const real fn = fmax(fma(-g, arinv, f), lb);
+      const real dl = fn - f;
+      const long long bits = __double_as_longlong(dl);
+      const int lo = __builtin_amdgcn_readlane((int)bits, r);
+      const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), r);
+      const real delta = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+      res = fma(A[r], delta, res);
+      if (lane == r) f = fn;
     }
   }
+  PH(14);
   S.efc_f[lane] = (lane < nefc) ? f : 0.0;
   __syncthreads();
 }
 
 // qacc = qacc_smooth + H^-1 J^T f  via  z = D^-1 Y^T f,  x = L^-1 z
+template <int CL>
 __device__ void constraint_accel(Shared& S, const GmTopo* __restrict__ T, int lane) {
   int nefc = S.nefc;
   if (lane < T->nv) {
@@ -1139,7 +1336,7 @@ __device__ void constraint_accel(Shared& S, const GmTopo* __restrict__ T, int la
     if (d >= T->dof_obj) { grp_d = GM_GRP_OBJECT; slot = d - T->dof_obj; }
     else if (d == T->dof_base) { grp_d = GM_GRP_BASE; slot = 6; }
     else if (d == T->dof_palm) { grp_d = 3; slot = 7; }
-    else { grp_d = (d - T->dof_f0[0]) / T->CL; slot = 6 + 1 + (d - T->dof_f0[grp_d]); }
+    else { grp_d = (d - T->dof_f0[0]) / CL; slot = 6 + 1 + (d - T->dof_f0[grp_d]); }
     (void)b;
     real acc = 0;
     for (int r = 0; r < nefc; r++) {
@@ -1156,28 +1353,28 @@ __device__ void constraint_accel(Shared& S, const GmTopo* __restrict__ T, int la
   }
   __syncthreads();
   // x = L^-1 z : root -> leaves
-  if (lane < 5) {
-    int c = lane;
-    int L = chain_len(T, c);
-    if (c < 4) {
-      real xs[CLMAX + 1];
-      xs[0] = S.z[T->dof_base];
-      for (int k = 1; k <= L; k++) {
-        real v = S.z[chain_dof(T, c, k)];
-        for (int i = k - 1; i >= 0; i--) v -= Hat(S, c, k, i) * xs[i];
-        xs[k] = v;
-        int d = chain_dof(T, c, k);
-        S.qacc[d] = S.qacc_s[d] + v;
-      }
-      if (c == 0) S.qacc[T->dof_base] = S.qacc_s[T->dof_base] + xs[0];
-    } else {
-      real xs[6];
-      for (int k = 0; k < 6; k++) {
-        real v = S.z[T->dof_obj + k];
-        for (int i = k - 1; i >= 0; i--) v -= S.Ho[TRI(k, i)] * xs[i];
-        xs[k] = v;
-        S.qacc[T->dof_obj + k] = S.qacc_s[T->dof_obj + k] + v;
-      }
+  if (lane < 3) {
+    real y[CL + 1], xs[CL + 1];
+    const int d0 = T->dof_f0[lane];
+#pragma unroll
+    for (int k = 1; k <= CL; k++) y[k] = S.z[d0 + k - 1];
+    chain_L<CL>(S.Hf[lane], S.z[T->dof_base], y, xs);
+#pragma unroll
+    for (int k = 1; k <= CL; k++) S.qacc[d0 + k - 1] = S.qacc_s[d0 + k - 1] + xs[k];
+    if (lane == 0) S.qacc[T->dof_base] = S.qacc_s[T->dof_base] + xs[0];
+  } else if (lane == 3) {
+    real y[2] = {0, S.z[T->dof_palm]}, xs[2];
+    chain_L<1>(S.Hp, S.z[T->dof_base], y, xs);
+    S.qacc[T->dof_palm] = S.qacc_s[T->dof_palm] + xs[1];
+  } else if (lane == 4) {
+    real xs[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      real v = S.z[T->dof_obj + k];
+#pragma unroll
+      for (int i = k - 1; i >= 0; i--) v -= S.Ho[TRI(k, i)] * xs[i];
+      xs[k] = v;
+      S.qacc[T->dof_obj + k] = S.qacc_s[T->dof_obj + k] + v;
     }
   }
   // contact forces in the contact frame (mj_contactForce, pyramidal decode)
@@ -1294,7 +1491,7 @@ __device__ int g_step_to(GmGrip& g, const GmGrip& t, int num) {
 }
 
 // update_all: update_stepper / update_constraints (myfunctions.cpp:2129-2284), antiroll
-__device__ void update_all(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+__device__ __forceinline__ void update_all(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
   if (lane == 0) {
     GmEnvState& s = S.s;
     if (s.time > s.last_step_time + m->time_per_step) {
@@ -1328,7 +1525,6 @@ __device__ __forceinline__ uint32_t lcg_next(uint32_t& s) {
   return s;
 }
 __device__ float unif01(uint32_t& s) {
-#pragma clang fp contract(off)
   const float r = 2147483646.0f;
   float sum = (float)(lcg_next(s) - 1u) * 1.0f;
   float ret = sum / r;
@@ -1336,7 +1532,6 @@ __device__ float unif01(uint32_t& s) {
   return ret * (1.0f - 0.0f) + 0.0f;
 }
 __device__ double canon_d(uint32_t& s) {
-#pragma clang fp contract(off)
   const double r = 2147483646.0;
   double sum = 0.0, tmp = 1.0;
   for (int k = 0; k < 2; k++) { sum += (double)(lcg_next(s) - 1u) * tmp; tmp *= r; }
@@ -1361,7 +1556,6 @@ __device__ __forceinline__ float ring_latest(const GmEnvState& s, int st) {
   return s.ring_i[st] == -1 ? s.ring[st][0] : s.ring[st][s.ring_i[st]];
 }
 __device__ float s_normalise(const gm_sensor& ss, float v) {
-#pragma clang fp contract(off)
   if (!ss.use_normalisation) return v;
   if (ss.normalise <= 0) return v < 0 ? -1.0f : 1.0f;
   else if (v > ss.normalise) return 1.0f;
@@ -1369,7 +1563,6 @@ __device__ float s_normalise(const gm_sensor& ss, float v) {
   return v / ss.normalise;
 }
 __device__ float s_noise(GmEnvState& s, const gm_sensor& ss, int slot, float value, int i) {
-#pragma clang fp contract(off)
   if (!ss.use_noise) return value;
   const float two_pi = (float)(2.0 * 3.14159265358979323846);
   const float eps = 1.1920928955078125e-07f;
@@ -1401,55 +1594,74 @@ __device__ int s_ready(GmEnvState& s, const gm_sensor& ss, int slot) {
 // ~16x smaller than the tip deflection, so an fp32 fit would cost ~3e-5 relative.
 // Householder QR on a centred/scaled abscissa -- the same least-squares solution as
 // the reference's arma::polyfit on the raw Vandermonde.
+template <int NS>
 __device__ float gauge_reading(const gm_model* __restrict__ m, const real* q) {
-  int N = m->n_seg, P = N + 1;
-  double Ls = m->segment_length;
-  double X[GM_MAX_SEG + 1], Yv[GM_MAX_SEG + 1];
+  constexpr int P = NS + 1;
+  const double Ls = m->segment_length;
+  double X[P], Yv[P];
   X[0] = m->fixed_first_segment ? Ls : 0.0;
   Yv[0] = 0;
   double cum = 0;
-  for (int i = 0; i < N; i++) {
+#pragma unroll
+  for (int i = 0; i < NS; i++) {
     cum = (i == 0) ? (double)q[0] : cum + (double)q[i];
-    X[i + 1] = X[i] + Ls * cos(cum);
-    Yv[i + 1] = Yv[i] + Ls * sin(cum);
+    double sn, cs;
+    sincos(cum, &sn, &cs);
+    X[i + 1] = X[i] + Ls * cs;
+    Yv[i + 1] = Yv[i] + Ls * sn;
   }
-  double half = 0.5 * m->finger_length;
-  double A[GM_MAX_SEG + 1][4], b[GM_MAX_SEG + 1];
+  const double half = 0.5 * m->finger_length;
+  const double ihalf = 1.0 / half;
+  double A[P][4], b[P];
+#pragma unroll
   for (int i = 0; i < P; i++) {
-    double t = (X[i] - half) / half;
+    const double t = (X[i] - half) * ihalf;
     A[i][0] = t * t * t; A[i][1] = t * t; A[i][2] = t; A[i][3] = 1.0;
     b[i] = Yv[i];
   }
+  // Householder QR of the (centred) Vandermonde system, as LAPACK's dgels under arma::polyfit
+#pragma unroll
   for (int k = 0; k < 4; k++) {
     double nrm = 0;
+#pragma unroll
     for (int i = k; i < P; i++) nrm += A[i][k] * A[i][k];
     nrm = sqrt(nrm);
-    double alpha = A[k][k] > 0 ? -nrm : nrm;
-    double v[GM_MAX_SEG + 1];
+    const double alpha = A[k][k] > 0 ? -nrm : nrm;
+    double v[P];
+#pragma unroll
     for (int i = 0; i < P; i++) v[i] = (i >= k) ? A[i][k] : 0.0;
     v[k] -= alpha;
     double vv = 0;
+#pragma unroll
     for (int i = k; i < P; i++) vv += v[i] * v[i];
     if (vv < 1e-300) continue;
+    const double ivv = 2.0 / vv;
+#pragma unroll
     for (int j = k; j < 4; j++) {
-      double s = 0;
-      for (int i = k; i < P; i++) s += v[i] * A[i][j];
-      s = 2 * s / vv;
-      for (int i = k; i < P; i++) A[i][j] -= s * v[i];
+      double sacc = 0;
+#pragma unroll
+      for (int i = k; i < P; i++) sacc += v[i] * A[i][j];
+      sacc *= ivv;
+#pragma unroll
+      for (int i = k; i < P; i++) A[i][j] -= sacc * v[i];
     }
-    double s = 0;
-    for (int i = k; i < P; i++) s += v[i] * b[i];
-    s = 2 * s / vv;
-    for (int i = k; i < P; i++) b[i] -= s * v[i];
+    double sacc = 0;
+#pragma unroll
+    for (int i = k; i < P; i++) sacc += v[i] * b[i];
+    sacc *= ivv;
+#pragma unroll
+    for (int i = k; i < P; i++) b[i] -= sacc * v[i];
   }
   double coeff[4];
+#pragma unroll
   for (int k = 3; k >= 0; k--) {
-    double s = b[k];
-    for (int j = k + 1; j < 4; j++) s -= A[k][j] * coeff[j];
-    coeff[k] = s / A[k][k];
+    double sacc = b[k];
+#pragma unroll
+    for (int j = k + 1; j < 4; j++) sacc -= A[k][j] * coeff[j];
+    coeff[k] = sacc / A[k][k];
   }
-  double tg = (m->gauge_xpos - half) / half;
-  double y = ((coeff[0] * tg + coeff[1]) * tg + coeff[2]) * tg + coeff[3];
+  const double tg = (m->gauge_xpos - half) * ihalf;
+  const double y = ((coeff[0] * tg + coeff[1]) * tg + coeff[2]) * tg + coeff[3];
   return (float)y * 1000;
 }
 
@@ -1500,15 +1712,15 @@ __device__ void extract_forces(Shared& S, const gm_model* __restrict__ m, const 
 }
 
 // MjClass::monitor_sensors (mjclass.cpp:741-898)
+template <int CL>
 __device__ void monitor_sensors(Shared& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
                                 const GmTopo* __restrict__ T, int lane) {
   __shared__ int bend_ready;
   if (lane == 0) bend_ready = s_ready(S.s, C->s.bending_gauge, SL_BEND);
   __syncthreads();
-  if (bend_ready && lane < 3) S.gauge_tmp[lane] = gauge_reading(m, &S.s.qpos[chain_dof(T, lane, 3)]);
+  if (bend_ready && lane < 3) S.gauge_tmp[lane] = gauge_reading<CL - 2>(m, &S.s.qpos[T->dof_f0[lane] + 2]);
   __syncthreads();
   if (lane == 0) {
-#pragma clang fp contract(off)
     GmEnvState& s = S.s;
     const gm_settings& st = C->s;
     int have = 0;
@@ -1549,26 +1761,26 @@ __device__ void monitor_sensors(Shared& S, const gm_model* __restrict__ m, const
 }
 
 // ============================================================ one full substep
-#define PH(k) do { if (prof) { unsigned long long t_ = clock64(); if (lane == 0) S.tph[k] += t_ - t0; t0 = t_; } } while (0)
-__device__ void physics_substep(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
+template <int CL>
+__device__ __noinline__ void physics_substep(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                                 bool prof = false) {
   unsigned long long t0 = prof ? clock64() : 0;
   if (lane < T->nq) S.qpos_pre[lane] = S.s.qpos[lane];
-  kinematics(S, m, T, lane);
+  kinematics<CL>(S, m, T, lane);
   PH(0);
-  crb_rne(S, m, T, lane);
+  crb_rne<CL>(S, m, T, lane);
   PH(1);
   mass_and_forces(S, m, T, lane);
   PH(2);
-  factor(S, T, lane);
+  factor<CL>(S, T, lane);
   PH(3);
-  solve_full(S, T, S.frc, S.qacc_s, lane);
+  solve_full<CL>(S, T, S.frc, S.qacc_s, lane);
   PH(4);
   collision(S, m, T, lane);
   PH(5);
-  constraints(S, m, T, lane);
+  constraints<CL>(S, m, T, lane, prof);
   PH(6);
-  constraint_accel(S, T, lane);
+  constraint_accel<CL>(S, T, lane);
   PH(7);
   integrate(S, m, T, lane);
   PH(8);
@@ -1576,14 +1788,12 @@ __device__ void physics_substep(Shared& S, const gm_model* __restrict__ m, const
 
 // ============================================================ env-step epilogue (lane 0)
 __device__ __forceinline__ float normalise_between(float val, float mn, float mx) {
-#pragma clang fp contract(off)
   if (val > mx) return 1.0f;
   else if (val < mn) return -1.0f;
   return 2 * (val - mn) / (mx - mn) - 1;
 }
 
 __device__ void sense_gripper_state(Shared& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C) {
-#pragma clang fp contract(off)
   GmEnvState& s = S.s;
   const gm_settings& st = C->s;
   const double* bmn = C->base_min;
@@ -1642,7 +1852,6 @@ __device__ float mag3f(const float* v) { return (float)sqrt((double)v[0] * v[0] 
 // MjClass::update_env (mjclass.cpp:966-1346) + update_events (5437-5469)
 __device__ void update_env(Shared& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
                            const GmTopo* __restrict__ T) {
-#pragma clang fp contract(off)
   GmEnvState& s = S.s;
   const gm_settings& st = C->s;
   const double ftol = 1e-5;
@@ -1757,7 +1966,6 @@ __device__ void update_env(Shared& S, const gm_model* __restrict__ m, const gm_c
 }
 
 __device__ int sample_stream(const GmEnvState& s, int mode, int st, const gm_sensor& ss, float* out) {
-#pragma clang fp contract(off)
   int prev = ss.prev_steps, rps = ss.readings_per_step, total = ss.total_readings;
   if (mode == GM_SAMPLE_RAW) {
     int n = total - 1;
@@ -1838,7 +2046,6 @@ __device__ int is_done(const GmEnvState& s, const gm_config* __restrict__ C) {
 }
 
 __device__ float linear_reward(float val, float mn, float mx, float overshoot) {
-#pragma clang fp contract(off)
   if (val < mn) return 0.0f;
   if (val > mx) {
     if (overshoot < mx) return 1.0f;
@@ -1848,7 +2055,6 @@ __device__ float linear_reward(float val, float mn, float mx, float overshoot) {
   return (val - mn) / (mx - mn);
 }
 __device__ float reward(GmEnvState& s, const gm_config* __restrict__ C) {
-#pragma clang fp contract(off)
   const gm_settings& st = C->s;
   float r = 0;
   int k = 0;
@@ -1890,7 +2096,8 @@ __device__ __forceinline__ void store_state(const Shared& S, GmEnvState* __restr
 
 // mode 0: action_step + obs/done/reward; mode 1: calibrate_reset settle (400 substeps,
 // no sensors); mode 2: one full substep with diagnostics
-extern "C" __global__ __launch_bounds__(NT) void gm_step_kernel(
+template <int CL>
+__global__ __launch_bounds__(NT, 2) void gm_step_kernel(
     GmEnvState* __restrict__ states, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
     const GmTopo* __restrict__ T, float* __restrict__ obs, float* __restrict__ rew,
     uint8_t* __restrict__ done, int n_envs, int mode, DebugOut dbg) {
@@ -1901,7 +2108,7 @@ extern "C" __global__ __launch_bounds__(NT) void gm_step_kernel(
   load_state(S, states + env, lane);
   if (mode == 1) {
     for (int i = 0; i < 400; i++) {
-      physics_substep(S, m, T, lane);
+      physics_substep<CL>(S, m, T, lane);
       update_all(S, m, T, lane);
     }
     store_state(S, states + env, lane);
@@ -1912,11 +2119,11 @@ extern "C" __global__ __launch_bounds__(NT) void gm_step_kernel(
   __syncthreads();
   int nsub = (mode == 2) ? 1 : C->sim_steps_per_action + S.s.extra_substeps;
   for (int i = 0; i < nsub; i++) {
-    physics_substep(S, m, T, lane, prof);
+    physics_substep<CL>(S, m, T, lane, prof);
     unsigned long long t0 = prof ? clock64() : 0;
     update_all(S, m, T, lane);
     PH(9);
-    monitor_sensors(S, m, C, T, lane);
+    monitor_sensors<CL>(S, m, C, T, lane);
     PH(10);
   }
   if (mode == 2) {
@@ -1999,7 +2206,6 @@ __device__ int call_action(GmEnvState& s, const gm_config* __restrict__ C, int k
 }
 __device__ void set_action_one(GmEnvState& s, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
                                int action, float frac) {
-#pragma clang fp contract(off)
   const gm_settings& st = C->s;
   int wl = 1;
   s.termination_signal_sent = 0;
@@ -2152,18 +2358,15 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
                                  &st.wrist_sensor_XY, &st.wrist_sensor_Z, &st.cartesian_contacts_XYZ};
     for (int k = 0; k < SL_N; k++)
       for (int i = 0; i < 3; i++) {
-#pragma clang fp contract(off)
         s.rand_mu[k][i] = ss[k]->noise_mu * (2 * unif01(s.rng) - 1);
       }
     int order[5] = {SL_MOTOR, SL_BASEXY, SL_BASEZ, SL_YAW, SL_CART};
     for (int k = 0; k < 5; k++)
       for (int i = 0; i < 3; i++) {
-#pragma clang fp contract(off)
         s.rand_mu[order[k]][i] = ss[order[k]]->noise_mu * (2 * unif01(s.rng) - 1);
       }
   }
   {
-#pragma clang fp contract(off)
     double size = C->s.base_position_noise;
     double u = canon_d(s.rng);
     double z = u * (size - (-size)) + (-size);

@@ -224,7 +224,8 @@ class BatchedGripperEnv:
         return ncon, con, f, qacc
 
     PHASES = ("kinematics", "crb_rne", "mass_forces", "factor", "smooth_solve", "collision",
-              "constraints_pgs", "constraint_accel", "integrate", "update_all", "monitor_sensors")
+              "constraints_pgs", "constraint_accel", "integrate", "update_all", "monitor_sensors",
+              "  c:jac+rowsolve", "  c:Yd", "  c:A_build", "  c:PGS")
 
     def step_profiled(self):
         """One env-step with per-phase shader-clock counters (lane 0, summed over substeps)."""

@@ -1004,12 +1004,15 @@ static void constraint_solve(or_env* e) {
     e->efc_b[r] = ja - aref;
     e->efc_f[r] = 0;
   }
-  /* projected Gauss-Seidel, fixed sweep count */
+  /* projected Gauss-Seidel, fixed sweep count; like mj_solPGS the diagonal is
+   * inverted once (ARinv) and each row update multiplies by it */
+  double ARinv[NE];
+  for (int r = 0; r < n; r++) ARinv[r] = 1.0 / (A[r][r] + e->efc_R[r]);
   for (int it = 0; it < m->pgs_iterations; it++) {
     for (int r = 0; r < n; r++) {
       double g = e->efc_b[r] + e->efc_R[r] * e->efc_f[r];
       for (int s = 0; s < n; s++) g += A[r][s] * e->efc_f[s];
-      double f = e->efc_f[r] - g / (A[r][r] + e->efc_R[r]);
+      double f = e->efc_f[r] - g * ARinv[r];
       if (e->efc_type[r] == 1 && f < 0) f = 0;
       e->efc_f[r] = f;
     }

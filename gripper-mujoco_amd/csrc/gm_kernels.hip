@@ -45,33 +45,40 @@ struct DebugOut {
 
 struct __align__(16) Shared {
   GmEnvState s;
-  real qpos_pre[GM_MAX_QPOS];
-  real qacc_s[GM_MAX_DOF], qacc[GM_MAX_DOF], frc[GM_MAX_DOF], z[GM_MAX_DOF];
+  real lock_pre[GM_MAX_LOCK];     // pre-integration qpos of the lock dofs (weld re-anchoring)
+  real qacc[GM_MAX_DOF], z[GM_MAX_DOF];   // qacc: smooth, then total acceleration
   real xpos[GM_MAX_BODY][3];
-  real xmat[GM_MAX_BODY][9];
-  real cdof[GM_MAX_DOF][6];
+  real xquat[GM_MAX_BODY][4];   // normalised body orientations; xmat = quat2mat(xquat)
   real Hf[3][TRIF], Hp[3], Ho[21], Hbb;
   real Df[3][CLMAX + 1], Dp[2], Do[6], Dbb;
   real bdelta[5];
-  real con[GM_MAX_CON][20];   // dist, pos3, frame9, mu, force3, g1, g2, (pad)
-  // LDS shared in time: the dynamics/collision scratch is dead once the constraint
-  // rows are built, so the compact Jacobian rows reuse it
+  // contact record: dist, pos[3], normal[3], mu, force[3] (contact frame); the
+  // tangents are make_frame(normal) wherever they are needed
+  real con[GM_MAX_CON][11];
+  int32_t cgeom[GM_MAX_CON][2];   // canonical (geom1, geom2)
+  // LDS shared in time: the dynamics / collision scratch is dead once every lane has
+  // built its constraint row, so the compact Jacobian rows reuse it
   union {
-    struct {                  // kinematics .. collision
-      real cinert[GM_MAX_BODY][10];
-      real Ic[GM_MAX_BODY][10];
-      real cfrc[GM_MAX_BODY][6];
-      real qloc[GM_MAX_BODY][4];          // hinge half-angle quaternions (FK phase A)
-      real chain_f[5][6], chain_I[5][10]; // chain-root sums for the base body
-      real gxpos[GM_MAX_GEOM][3];
-      real gxmat[GM_MAX_GEOM][9];
+    struct {                  // kinematics .. constraint rows
+      real cdof[GM_MAX_DOF][6];
+      real frc[GM_MAX_DOF];
+      union {                 // composite inertia accumulates in place over cinert
+        real cinert[GM_MAX_BODY][10];
+        real Ic[GM_MAX_BODY][10];
+      };
+      union {                 // FK phase A rotations are dead before RNE writes forces
+        real qloc[GM_MAX_BODY][4];
+        real cfrc[GM_MAX_BODY][6];
+      };
+      real chain_f[5][6], chain_I[5][10];   // chain-root sums for the base body
+      int32_t cnt[NT];                      // collision: contacts per pair lane
     };
-    struct {                  // constraints .. constraint_accel
-      real Y[GM_MAX_EFC][CW];
+    struct {                  // constraint rows .. constraint accelerations
+      real Y[GM_MAX_EFC][CW - 1];
+      int32_t ygrp[GM_MAX_EFC];   // chain group of each row (-1: object / locks only)
     };
   };
   real efc_f[GM_MAX_EFC];
-  int32_t cnt[NT];
   int32_t ncon, nefc, nlockrows, overflow;
   float forces[32];            // extract_forces_faster results (see extract_forces)
   int32_t have_forces;
@@ -172,6 +179,10 @@ __device__ __forceinline__ real& Hat(Shared& S, int c, int p, int q) {
 }
 
 // ============================================================ kinematics
+__device__ __forceinline__ void body_R(const Shared& S, int b, real* R) {
+  const real q[4] = {S.xquat[b][0], S.xquat[b][1], S.xquat[b][2], S.xquat[b][3]};
+  quat2mat(R, q);
+}
 // mj_kinematics restated (oracle.c fk): phase A, one lane per body, the hinge joint
 // rotations (the only transcendental work) ; phase B, one lane per chain, the pose
 // recursion root -> leaf entirely in registers (chain length compile-time, unrolled,
@@ -208,7 +219,7 @@ __device__ __forceinline__ void fk_step(Shared& S, const gm_model* __restrict__ 
   quat2mat(P.R, q);
   S.xpos[b][0] = xp[0]; S.xpos[b][1] = xp[1]; S.xpos[b][2] = xp[2];
 #pragma unroll
-  for (int k = 0; k < 9; k++) S.xmat[b][k] = P.R[k];
+  for (int k = 0; k < 4; k++) S.xquat[b][k] = q[k];
 }
 
 template <int CL>
@@ -258,7 +269,7 @@ __device__ void kinematics(Shared& S, const gm_model* __restrict__ m, const GmTo
       if (lane == 0) {
         S.xpos[b][0] = xp[0]; S.xpos[b][1] = xp[1]; S.xpos[b][2] = xp[2];
 #pragma unroll
-        for (int k = 0; k < 9; k++) S.xmat[b][k] = P.R[k];
+        for (int k = 0; k < 4; k++) S.xquat[b][k] = q[k];
       }
     }
     if (lane < 3) {
@@ -273,19 +284,16 @@ __device__ void kinematics(Shared& S, const gm_model* __restrict__ m, const GmTo
     const int b = T->body_obj, qa = T->qadr_obj;
     real q[4] = {S.s.qpos[qa + 3], S.s.qpos[qa + 4], S.s.qpos[qa + 5], S.s.qpos[qa + 6]};
     quatnorm(q);
-    real R[9];
-    quat2mat(R, q);
     S.xpos[b][0] = S.s.qpos[qa]; S.xpos[b][1] = S.s.qpos[qa + 1]; S.xpos[b][2] = S.s.qpos[qa + 2];
 #pragma unroll
-    for (int k = 0; k < 9; k++) S.xmat[b][k] = R[k];
+    for (int k = 0; k < 4; k++) S.xquat[b][k] = q[k];
   }
   __syncthreads();
   // C1: world-origin spatial inertia per body
   if (lane < T->nbody && lane > 0) {
     const int b = lane;
     real R[9], xp[3];
-#pragma unroll
-    for (int k = 0; k < 9; k++) R[k] = S.xmat[b][k];
+    body_R(S, b, R);
     xp[0] = S.xpos[b][0]; xp[1] = S.xpos[b][1]; xp[2] = S.xpos[b][2];
     real ip[3], c[3];
     ld3(ip, m->body_ipos[b]);
@@ -327,14 +335,15 @@ __device__ void kinematics(Shared& S, const gm_model* __restrict__ m, const GmTo
       if (k < 3) {
         cd[0] = cd[1] = cd[2] = 0; cd[3] = cd[4] = cd[5] = 0; cd[3 + k] = 1;
       } else {
-        const real w[3] = {S.xmat[b][k - 3], S.xmat[b][3 + k - 3], S.xmat[b][6 + k - 3]};
+        real Rb[9];
+        body_R(S, b, Rb);
+        const real w[3] = {Rb[k - 3], Rb[3 + k - 3], Rb[6 + k - 3]};
         cd[0] = w[0]; cd[1] = w[1]; cd[2] = w[2];
         cross3(cd + 3, xp, w);
       }
     } else {
       real ax[3], wa[3], R[9];
-#pragma unroll
-      for (int k = 0; k < 9; k++) R[k] = S.xmat[b][k];
+      body_R(S, b, R);
       ld3(ax, m->jnt_axis[j]);
       mulmv3(wa, R, ax);
       if (type == GM_JNT_SLIDE) {
@@ -344,30 +353,6 @@ __device__ void kinematics(Shared& S, const gm_model* __restrict__ m, const GmTo
         cross3(cd + 3, xp, wa);   // anchor at the body origin in this model
       }
     }
-  }
-  // C3: geoms, one lane per geom
-  if (lane < T->ngeom) {
-    const int g = lane;
-    const int b = m->geom_body[g];
-    real R[9];
-    if (b == 0) {
-      R[0] = 1; R[1] = 0; R[2] = 0; R[3] = 0; R[4] = 1; R[5] = 0; R[6] = 0; R[7] = 0; R[8] = 1;
-    } else {
-#pragma unroll
-      for (int k = 0; k < 9; k++) R[k] = S.xmat[b][k];
-    }
-    real gp[3], t[3], gq[4], Rg[9];
-    ld3(gp, m->geom_pos[g]);
-    mulmv3(t, R, gp);
-    const real bp0 = b == 0 ? 0.0 : S.xpos[b][0], bp1 = b == 0 ? 0.0 : S.xpos[b][1], bp2 = b == 0 ? 0.0 : S.xpos[b][2];
-    S.gxpos[g][0] = bp0 + t[0]; S.gxpos[g][1] = bp1 + t[1]; S.gxpos[g][2] = bp2 + t[2];
-    ld4(gq, m->geom_quat[g]);
-    quat2mat(Rg, gq);
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-      for (int k = 0; k < 3; k++)
-        S.gxmat[g][3 * i + k] = R[3 * i] * Rg[k] + R[3 * i + 1] * Rg[3 + k] + R[3 * i + 2] * Rg[6 + k];
   }
   __syncthreads();
 }
@@ -736,6 +721,29 @@ __device__ void make_frame(real* F, const real* n) {
 
 struct GeomV { int type; real size[3]; real c[3]; real R[9]; real rbound; real friction; };
 
+// world pose of geom g (oracle.c fk, geom part), computed where a pair lane needs it
+__device__ __forceinline__ void geom_pose(Shared& S, const gm_model* __restrict__ m, int g, real* c, real* Rw) {
+  const int b = m->geom_body[g];
+  real R[9];
+  if (b == 0) {
+    R[0] = 1; R[1] = 0; R[2] = 0; R[3] = 0; R[4] = 1; R[5] = 0; R[6] = 0; R[7] = 0; R[8] = 1;
+  } else {
+    body_R(S, b, R);
+  }
+  real gp[3], t[3], gq[4], Rg[9];
+  ld3(gp, m->geom_pos[g]);
+  mulmv3(t, R, gp);
+  const real bp0 = b == 0 ? 0.0 : S.xpos[b][0], bp1 = b == 0 ? 0.0 : S.xpos[b][1], bp2 = b == 0 ? 0.0 : S.xpos[b][2];
+  c[0] = bp0 + t[0]; c[1] = bp1 + t[1]; c[2] = bp2 + t[2];
+  ld4(gq, m->geom_quat[g]);
+  quat2mat(Rg, gq);
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+      Rw[3 * i + k] = R[3 * i] * Rg[k] + R[3 * i + 1] * Rg[3 + k] + R[3 * i + 2] * Rg[6 + k];
+}
+
 __device__ __forceinline__ void load_geom(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int g, GeomV& G) {
   if (g == T->geom_obj) {
     G.type = S.s.obj_type;
@@ -747,8 +755,7 @@ __device__ __forceinline__ void load_geom(Shared& S, const gm_model* __restrict_
     G.rbound = (real)m->geom_rbound[g];
     G.friction = (real)m->geom_friction[g];
   }
-  for (int k = 0; k < 3; k++) G.c[k] = S.gxpos[g][k];
-  for (int k = 0; k < 9; k++) G.R[k] = S.gxmat[g][k];
+  geom_pose(S, m, g, G.c, G.R);
 }
 
 // plane-X multi-contact generators: k-th candidate point (returns 0 if none)
@@ -1034,10 +1041,10 @@ __device__ void write_contact(Shared& S, int slot, int g1, int g2, const Hit& h,
   real* C = S.con[slot];
   C[0] = h.dist;
   C[1] = h.pos[0]; C[2] = h.pos[1]; C[3] = h.pos[2];
-  make_frame(C + 4, h.n);
-  C[13] = mu;
-  C[14] = 0; C[15] = 0; C[16] = 0;
-  C[17] = (real)g1; C[18] = (real)g2;
+  C[4] = h.n[0]; C[5] = h.n[1]; C[6] = h.n[2];
+  C[7] = mu;
+  C[8] = 0; C[9] = 0; C[10] = 0;
+  S.cgeom[slot][0] = g1; S.cgeom[slot][1] = g2;
 }
 
 __device__ void collision(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
@@ -1114,7 +1121,7 @@ __device__ void contact_jac(Shared& S, const gm_model* __restrict__ m, const GmT
   for (int k = 0; k < CW; k++) J[k] = 0;
   const real* C = S.con[c];
   const real pos[3] = {C[1], C[2], C[3]};
-  int gs[2] = {(int)C[17], (int)C[18]};
+  int gs[2] = {S.cgeom[c][0], S.cgeom[c][1]};
   real sg[2] = {-1.0f, 1.0f};
   grp = -1;
   for (int side = 0; side < 2; side++) {
@@ -1222,12 +1229,14 @@ __device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmT
       int r = lane - nl;
       int c = r >> 2, e = r & 3;
       const real* C = S.con[c];
+      real Fr[9];
+      make_frame(Fr, C + 4);
       real Jn[CW], Jt[CW];
       int g2;
-      contact_jac(S, m, T, c, C + 4, Jn, grp);
-      contact_jac(S, m, T, c, C + 4 + 3 * (1 + (e >> 1)), Jt, g2);
+      contact_jac(S, m, T, c, Fr, Jn, grp);
+      contact_jac(S, m, T, c, Fr + 3 * (1 + (e >> 1)), Jt, g2);
       real sgn = (e & 1) ? -1.0 : 1.0;
-      real mu = C[13];
+      real mu = C[7];
       for (int t = 0; t < CW; t++) J[t] = Jn[t] + sgn * mu * Jt[t];
       pos = C[0];
       is_contact = 1;
@@ -1237,11 +1246,14 @@ __device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmT
   // a0 = J qacc_smooth, vel = J qvel (uses J before the in-place solve)
   real a0 = 0, vel = 0;
   if (lane < nefc) {
-    a0 = row_dot_dofs<CL>(S, T, J, grp, S.qacc_s);
+    a0 = row_dot_dofs<CL>(S, T, J, grp, S.qacc);
     vel = row_dot_dofs<CL>(S, T, J, grp, S.s.qvel);
     row_LTsolve<CL>(S, J, grp);
+  }
+  __syncthreads();            // every lane is done with cdof before Y overwrites it
+  if (lane < nefc) {
     for (int t = 0; t < CW - 1; t++) S.Y[lane][t] = J[t];
-    S.Y[lane][CW - 1] = (real)grp;
+    S.ygrp[lane] = grp;
   }
   if (lane == 0) { S.nefc = nefc; S.nlockrows = nl; }
   __syncthreads();
@@ -1269,7 +1281,7 @@ __device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmT
     real acc = 0;
     if (i < nefc) {
       const real* Yi = S.Y[i];
-      int gi = (int)Yi[CW - 1];
+      int gi = S.ygrp[i];
       for (int k = 0; k < 6; k++) acc += Yd[k] * Yi[k];
       if (gj && gi >= 0 && gi <= 3) {
         acc += Yd[6] * Yi[6];
@@ -1340,7 +1352,7 @@ __device__ void constraint_accel(Shared& S, const GmTopo* __restrict__ T, int la
     (void)b;
     real acc = 0;
     for (int r = 0; r < nefc; r++) {
-      int g = (int)S.Y[r][CW - 1];
+      int g = S.ygrp[r];
       bool use = (grp_d == GM_GRP_OBJECT) || (grp_d == GM_GRP_BASE && g >= 0 && g <= 3) || (grp_d == g);
       if (use) acc += S.Y[r][slot] * S.efc_f[r];
     }
@@ -1360,12 +1372,12 @@ __device__ void constraint_accel(Shared& S, const GmTopo* __restrict__ T, int la
     for (int k = 1; k <= CL; k++) y[k] = S.z[d0 + k - 1];
     chain_L<CL>(S.Hf[lane], S.z[T->dof_base], y, xs);
 #pragma unroll
-    for (int k = 1; k <= CL; k++) S.qacc[d0 + k - 1] = S.qacc_s[d0 + k - 1] + xs[k];
-    if (lane == 0) S.qacc[T->dof_base] = S.qacc_s[T->dof_base] + xs[0];
+    for (int k = 1; k <= CL; k++) S.qacc[d0 + k - 1] = S.qacc[d0 + k - 1] + xs[k];
+    if (lane == 0) S.qacc[T->dof_base] = S.qacc[T->dof_base] + xs[0];
   } else if (lane == 3) {
     real y[2] = {0, S.z[T->dof_palm]}, xs[2];
     chain_L<1>(S.Hp, S.z[T->dof_base], y, xs);
-    S.qacc[T->dof_palm] = S.qacc_s[T->dof_palm] + xs[1];
+    S.qacc[T->dof_palm] = S.qacc[T->dof_palm] + xs[1];
   } else if (lane == 4) {
     real xs[6];
 #pragma unroll
@@ -1374,16 +1386,16 @@ __device__ void constraint_accel(Shared& S, const GmTopo* __restrict__ T, int la
 #pragma unroll
       for (int i = k - 1; i >= 0; i--) v -= S.Ho[TRI(k, i)] * xs[i];
       xs[k] = v;
-      S.qacc[T->dof_obj + k] = S.qacc_s[T->dof_obj + k] + v;
+      S.qacc[T->dof_obj + k] = S.qacc[T->dof_obj + k] + v;
     }
   }
   // contact forces in the contact frame (mj_contactForce, pyramidal decode)
   if (lane < S.ncon) {
     const real* fe = &S.efc_f[S.nlockrows + 4 * lane];
-    real mu = S.con[lane][13];
-    S.con[lane][14] = fe[0] + fe[1] + fe[2] + fe[3];
-    S.con[lane][15] = mu * (fe[0] - fe[1]);
-    S.con[lane][16] = mu * (fe[2] - fe[3]);
+    real mu = S.con[lane][7];
+    S.con[lane][8] = fe[0] + fe[1] + fe[2] + fe[3];
+    S.con[lane][9] = mu * (fe[0] - fe[1]);
+    S.con[lane][10] = mu * (fe[2] - fe[3]);
   }
   __syncthreads();
 }
@@ -1500,13 +1512,13 @@ __device__ __forceinline__ void update_all(Shared& S, const gm_model* __restrict
       int nz = g_zs(s.end) != g_zs(s.next);
       if (nx != s.old_x) {
         for (int k = 0; k < T->nlock; k++)
-          if (m->lock_kind[k] == 0) { s.lock_active[k] = !nx; if (!nx) s.lock_q[k] = S.qpos_pre[m->lock_dof[k]]; }
+          if (m->lock_kind[k] == 0) { s.lock_active[k] = !nx; if (!nx) s.lock_q[k] = S.lock_pre[k]; }
         s.old_x = nx;
       }
       if (ny != s.old_y) s.old_y = ny;   // revolute locks disabled (myfunctions.cpp:479)
       if (nz != s.old_z) {
         for (int k = 0; k < T->nlock; k++)
-          if (m->lock_kind[k] == 2) { s.lock_active[k] = !nz; if (!nz) s.lock_q[k] = S.qpos_pre[m->lock_dof[k]]; }
+          if (m->lock_kind[k] == 2) { s.lock_active[k] = !nz; if (!nz) s.lock_q[k] = S.lock_pre[k]; }
         s.old_z = nz;
       }
       s.last_step_time = s.time;
@@ -1675,7 +1687,7 @@ __device__ void extract_forces(Shared& S, const gm_model* __restrict__ m, const 
   for (int a = 0; a < 3; a++) for (int k = 0; k < 3; k++) gg[a][k] = 0;
   for (int i = 0; i < S.ncon; i++) {
     const real* C = S.con[i];
-    int c1 = m->geom_class[(int)C[17]], c2 = m->geom_class[(int)C[18]];
+    int c1 = m->geom_class[S.cgeom[i][0]], c2 = m->geom_class[S.cgeom[i][1]];
     int w_obj = (c1 == GM_CLS_OBJECT || c2 == GM_CLS_OBJECT);
     int w_f0 = (c1 == GM_CLS_FINGER1 || c2 == GM_CLS_FINGER1);
     int w_f1 = (c1 == GM_CLS_FINGER2 || c2 == GM_CLS_FINGER2);
@@ -1683,7 +1695,9 @@ __device__ void extract_forces(Shared& S, const gm_model* __restrict__ m, const 
     int w_palm = (c1 == GM_CLS_PALM || c2 == GM_CLS_PALM);
     int w_gnd = (c1 == GM_CLS_GROUND || c2 == GM_CLS_GROUND);
     real g[3];
-    for (int k = 0; k < 3; k++) g[k] = (real)C[4 + k] * C[14] + (real)C[7 + k] * C[15] + (real)C[10 + k] * C[16];
+    real Fr[9];
+    make_frame(Fr, C + 4);
+    for (int k = 0; k < 3; k++) g[k] = Fr[k] * C[8] + Fr[3 + k] * C[9] + Fr[6 + k] * C[10];
     int wf[3] = {w_f0, w_f1, w_f2};
     if (w_obj) {
       for (int f = 0; f < 3; f++) if (wf[f]) for (int k = 0; k < 3; k++) og[f][k] += g[k];
@@ -1700,13 +1714,15 @@ __device__ void extract_forces(Shared& S, const gm_model* __restrict__ m, const 
   float* F = S.forces;
   for (int f = 0; f < 4; f++) {
     int b = f < 3 ? T->body_finger[f] : T->body_palm;
+    real Rb[9];
+    body_R(S, b, Rb);
     real loc[3];
-    mulmtv3(loc, S.xmat[b], og[f]);
+    mulmtv3(loc, Rb, og[f]);
     F[3 * f] = (float)loc[0]; F[3 * f + 1] = (float)loc[1]; F[3 * f + 2] = (float)loc[2];
     real al[3];
-    mulmtv3(al, S.xmat[b], ag[f]);
+    mulmtv3(al, Rb, ag[f]);
     if (f < 3) F[15 + f] = (float)al[0]; else F[18] = (float)al[0];
-    if (f < 3) { real gl[3]; mulmtv3(gl, S.xmat[b], gg[f]); F[19 + f] = (float)gl[0]; }
+    if (f < 3) { real gl[3]; mulmtv3(gl, Rb, gg[f]); F[19 + f] = (float)gl[0]; }
   }
   F[12] = (float)og[4][0]; F[13] = (float)og[4][1]; F[14] = (float)og[4][2];
 }
@@ -1765,7 +1781,7 @@ template <int CL>
 __device__ __noinline__ void physics_substep(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                                 bool prof = false) {
   unsigned long long t0 = prof ? clock64() : 0;
-  if (lane < T->nq) S.qpos_pre[lane] = S.s.qpos[lane];
+  if (lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
   kinematics<CL>(S, m, T, lane);
   PH(0);
   crb_rne<CL>(S, m, T, lane);
@@ -1774,7 +1790,7 @@ __device__ __noinline__ void physics_substep(Shared& S, const gm_model* __restri
   PH(2);
   factor<CL>(S, T, lane);
   PH(3);
-  solve_full<CL>(S, T, S.frc, S.qacc_s, lane);
+  solve_full<CL>(S, T, S.frc, S.qacc, lane);
   PH(4);
   collision(S, m, T, lane);
   PH(5);
@@ -2135,8 +2151,10 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
         const real* Cc = S.con[lane];
         o[0] = Cc[0];
         for (int k = 0; k < 3; k++) o[1 + k] = Cc[1 + k];
-        for (int k = 0; k < 9; k++) o[4 + k] = Cc[4 + k];
-        o[13] = Cc[17]; o[14] = Cc[18]; o[15] = Cc[13];
+        real Fr[9];
+        make_frame(Fr, Cc + 4);
+        for (int k = 0; k < 9; k++) o[4 + k] = Fr[k];
+        o[13] = S.cgeom[lane][0]; o[14] = S.cgeom[lane][1]; o[15] = Cc[7];
       }
     }
     dbg.efc_force[(size_t)env * GM_MAX_EFC + lane] = lane < S.nefc ? S.efc_f[lane] : 0.0f;

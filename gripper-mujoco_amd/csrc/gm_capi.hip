@@ -153,6 +153,15 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
     delete c;
     return GM_E_RANGE;
   }
+  {
+    const int CLm = c->model.n_seg + 2;
+    if (c->model.nbody != 3 * CLm + 4 || c->model.nv != 3 * CLm + 8 || c->model.nq != c->model.nv + 1) {
+      fprintf(stderr, "gm_create: model sizes (nbody %d, nv %d, nq %d) do not match the canonical tree for n_seg=%d\n",
+              c->model.nbody, c->model.nv, c->model.nq, c->model.n_seg);
+      delete c;
+      return GM_E_RANGE;
+    }
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device) {
     fprintf(stderr, "gm_create: no HIP device %d (found %d)\n", device, ndev);

@@ -27,7 +27,7 @@
 #define CLMAX (GM_MAX_SEG + 2)
 #define TRI(p, q) ((p) * ((p) + 1) / 2 + (q))
 #define TRIF ((CLMAX + 1) * (CLMAX + 2) / 2)
-#define CW 20   // compact row: obj[6], base, chain[CLMAX], group (as float bits)
+#define CW (CL + 8)   // compact row: obj[6], base, chain[CL] (+1 scratch slot); needs CL in scope
 #define PI_F 3.14159265358979f
 
 // `real` is the dynamics type: fp64, MuJoCo's mjtNum.  Collision geometry and the
@@ -43,14 +43,21 @@ struct DebugOut {
 };
 #define GM_NPHASE 16
 
-struct __align__(16) Shared {
+// Per-env LDS image, sized for the compile-time finger chain length CL = n_seg + 2:
+// NB = 3 CL + 4 bodies (world, base, 3 x CL finger links, palm, object),
+// NV = 3 CL + 8 dofs (base, 3 x CL, palm, free object).  gm_create checks the model.
+template <int CL>
+struct __align__(16) SharedT {
+  static constexpr int NB = 3 * CL + 4;
+  static constexpr int NV = 3 * CL + 8;
+  static constexpr int TRIC = (CL + 1) * (CL + 2) / 2;
   GmEnvState s;
   real lock_pre[GM_MAX_LOCK];     // pre-integration qpos of the lock dofs (weld re-anchoring)
-  real qacc[GM_MAX_DOF], z[GM_MAX_DOF];   // qacc: smooth, then total acceleration
-  real xpos[GM_MAX_BODY][3];
-  real xquat[GM_MAX_BODY][4];   // normalised body orientations; xmat = quat2mat(xquat)
-  real Hf[3][TRIF], Hp[3], Ho[21], Hbb;
-  real Df[3][CLMAX + 1], Dp[2], Do[6], Dbb;
+  real qacc[NV], z[NV];   // qacc: smooth, then total acceleration
+  real xpos[NB][3];
+  real xquat[NB][4];   // normalised body orientations; xmat = quat2mat(xquat)
+  real Hf[3][TRIC], Hp[3], Ho[21], Hbb;
+  real Df[3][CL + 1], Dp[2], Do[6], Dbb;
   real bdelta[5];
   // contact record: dist, pos[3], normal[3], mu, force[3] (contact frame); the
   // tangents are make_frame(normal) wherever they are needed
@@ -60,15 +67,15 @@ struct __align__(16) Shared {
   // built its constraint row, so the compact Jacobian rows reuse it
   union {
     struct {                  // kinematics .. constraint rows
-      real cdof[GM_MAX_DOF][6];
-      real frc[GM_MAX_DOF];
+      real cdof[NV][6];
+      real frc[NV];
       union {                 // composite inertia accumulates in place over cinert
-        real cinert[GM_MAX_BODY][10];
-        real Ic[GM_MAX_BODY][10];
+        real cinert[NB][10];
+        real Ic[NB][10];
       };
       union {                 // FK phase A rotations are dead before RNE writes forces
-        real qloc[GM_MAX_BODY][4];
-        real cfrc[GM_MAX_BODY][6];
+        real qloc[NB][4];
+        real cfrc[NB][6];
       };
       real chain_f[5][6], chain_I[5][10];   // chain-root sums for the base body
       int32_t cnt[NT];                      // collision: contacts per pair lane
@@ -172,14 +179,10 @@ __device__ __forceinline__ int chain_dof(const GmTopo* T, int c, int p) {
   return T->dof_obj + p;   // object uses positions 0..5
 }
 // H/L storage accessor: chain c, positions p >= q (object: 0..5, others: 0 = base)
-__device__ __forceinline__ real& Hat(Shared& S, int c, int p, int q) {
-  if (c < 3) return (p == 0) ? S.Hbb : S.Hf[c][TRI(p, q)];
-  if (c == 3) return (p == 0) ? S.Hbb : S.Hp[TRI(p, q)];
-  return S.Ho[TRI(p, q)];
-}
 
 // ============================================================ kinematics
-__device__ __forceinline__ void body_R(const Shared& S, int b, real* R) {
+template <int CL>
+__device__ __forceinline__ void body_R(const SharedT<CL>& S, int b, real* R) {
   const real q[4] = {S.xquat[b][0], S.xquat[b][1], S.xquat[b][2], S.xquat[b][3]};
   quat2mat(R, q);
 }
@@ -191,7 +194,8 @@ __device__ __forceinline__ void body_R(const Shared& S, int b, real* R) {
 // subspaces, geom poses.
 struct Pose { real p[3], q[4], R[9]; };
 
-__device__ __forceinline__ void fk_step(Shared& S, const gm_model* __restrict__ m, int b, Pose& P) {
+template <int CL>
+__device__ __forceinline__ void fk_step(SharedT<CL>& S, const gm_model* __restrict__ m, int b, Pose& P) {
   real bp[3], bq[4], t[3], q[4];
   ld3(bp, m->body_pos[b]);
   ld4(bq, m->body_quat[b]);
@@ -223,7 +227,7 @@ __device__ __forceinline__ void fk_step(Shared& S, const gm_model* __restrict__ 
 }
 
 template <int CL>
-__device__ void kinematics(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+__device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
   // A: hinge rotations
   if (lane < T->nbody) {
     const int j = m->body_jnt[lane];
@@ -361,7 +365,8 @@ __device__ void kinematics(Shared& S, const gm_model* __restrict__ m, const GmTo
 // mj_rne (bias forces, world-origin spatial algebra) and mj_crb (composite inertias):
 // forward velocity / bias-acceleration recursion and body forces per chain, then
 // leaf -> root running sums in registers; chain-root totals meet at the base body.
-__device__ __forceinline__ void body_force(Shared& S, int b, const real* cvel, const real* cacc) {
+template <int CL>
+__device__ __forceinline__ void body_force(SharedT<CL>& S, int b, const real* cvel, const real* cacc) {
   real ci[10], t1[6], t2[6], f[6];
 #pragma unroll
   for (int k = 0; k < 10; k++) ci[k] = S.cinert[b][k];
@@ -371,7 +376,8 @@ __device__ __forceinline__ void body_force(Shared& S, int b, const real* cvel, c
 #pragma unroll
   for (int k = 0; k < 6; k++) S.cfrc[b][k] = f[k] + t2[k];
 }
-__device__ __forceinline__ void rne_fwd(Shared& S, int b, int d, real* cvel, real* cacc) {
+template <int CL>
+__device__ __forceinline__ void rne_fwd(SharedT<CL>& S, int b, int d, real* cvel, real* cacc) {
   real cd[6], cdd[6];
 #pragma unroll
   for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
@@ -382,8 +388,8 @@ __device__ __forceinline__ void rne_fwd(Shared& S, int b, int d, real* cvel, rea
   body_force(S, b, cvel, cacc);
 }
 // backward running sums over bodies b0 .. b0+L-1 (leaf = last); writes cfrc / Ic
-template <int L>
-__device__ __forceinline__ void chain_sums(Shared& S, int b0, real* fs, real* Is) {
+template <int L, int CL>
+__device__ __forceinline__ void chain_sums(SharedT<CL>& S, int b0, real* fs, real* Is) {
 #pragma unroll
   for (int k = 0; k < 6; k++) fs[k] = 0;
 #pragma unroll
@@ -399,7 +405,7 @@ __device__ __forceinline__ void chain_sums(Shared& S, int b0, real* fs, real* Is
 }
 
 template <int CL>
-__device__ void crb_rne(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+__device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
   if (lane < 4) {
     const int c = lane;
     real cvel[6], cacc[6];
@@ -500,7 +506,8 @@ __device__ __forceinline__ void ctrl_gains(const gm_model* __restrict__ m, const
 }
 
 // lane per dof: H row entries (compact), bias/passive/actuator force
-__device__ void mass_and_forces(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+template <int CL>
+__device__ void mass_and_forces(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
   if (lane < T->nv) {
     int d = lane;
     int b = m->dof_body[d];
@@ -587,7 +594,7 @@ __device__ __forceinline__ void factor_chain(real* __restrict__ Hs, real& delta_
 }
 
 template <int CL>
-__device__ void factor(Shared& S, const GmTopo* __restrict__ T, int lane) {
+__device__ void factor(SharedT<CL>& S, const GmTopo* __restrict__ T, int lane) {
   if (lane < 3) {
     factor_chain<CL>(S.Hf[lane], S.bdelta[lane], S.Df[lane]);
   } else if (lane == 3) {
@@ -617,11 +624,6 @@ __device__ void factor(Shared& S, const GmTopo* __restrict__ T, int lane) {
   __syncthreads();
 }
 
-__device__ __forceinline__ real Dof(Shared& S, int c, int p) {
-  if (c < 3) return p == 0 ? S.Dbb : S.Df[c][p];
-  if (c == 3) return p == 0 ? S.Dbb : S.Dp[p];
-  return S.Do[p];
-}
 
 // chain part of x = H~^-1 b: L^T y = b (leaves -> root), base contribution returned
 template <int L>
@@ -668,7 +670,7 @@ __device__ __forceinline__ void obj_solve(const real* __restrict__ Ho, const rea
 // x = H~^-1 b over full dof vectors (b, x in LDS, may alias); lanes 0..2 fingers,
 // 3 palm, 4 object
 template <int CL>
-__device__ void solve_full(Shared& S, const GmTopo* __restrict__ T, const real* b, real* x, int lane) {
+__device__ void solve_full(SharedT<CL>& S, const GmTopo* __restrict__ T, const real* b, real* x, int lane) {
   real y[(CL + 1) > 6 ? (CL + 1) : 6];
   if (lane < 3) {
 #pragma unroll
@@ -722,7 +724,8 @@ __device__ void make_frame(real* F, const real* n) {
 struct GeomV { int type; real size[3]; real c[3]; real R[9]; real rbound; real friction; };
 
 // world pose of geom g (oracle.c fk, geom part), computed where a pair lane needs it
-__device__ __forceinline__ void geom_pose(Shared& S, const gm_model* __restrict__ m, int g, real* c, real* Rw) {
+template <int CL>
+__device__ __forceinline__ void geom_pose(SharedT<CL>& S, const gm_model* __restrict__ m, int g, real* c, real* Rw) {
   const int b = m->geom_body[g];
   real R[9];
   if (b == 0) {
@@ -744,7 +747,8 @@ __device__ __forceinline__ void geom_pose(Shared& S, const gm_model* __restrict_
       Rw[3 * i + k] = R[3 * i] * Rg[k] + R[3 * i + 1] * Rg[3 + k] + R[3 * i + 2] * Rg[6 + k];
 }
 
-__device__ __forceinline__ void load_geom(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int g, GeomV& G) {
+template <int CL>
+__device__ __forceinline__ void load_geom(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int g, GeomV& G) {
   if (g == T->geom_obj) {
     G.type = S.s.obj_type;
     G.size[0] = S.s.obj_size[0]; G.size[1] = S.s.obj_size[1]; G.size[2] = S.s.obj_size[2];
@@ -1037,7 +1041,8 @@ __device__ __forceinline__ void canon_pair(int a, int b, int ta, int tb, int& g1
   if (ta > tb || (ta == tb && a > b)) { g1 = b; g2 = a; } else { g1 = a; g2 = b; }
 }
 
-__device__ void write_contact(Shared& S, int slot, int g1, int g2, const Hit& h, real mu) {
+template <int CL>
+__device__ void write_contact(SharedT<CL>& S, int slot, int g1, int g2, const Hit& h, real mu) {
   real* C = S.con[slot];
   C[0] = h.dist;
   C[1] = h.pos[0]; C[2] = h.pos[1]; C[3] = h.pos[2];
@@ -1047,7 +1052,8 @@ __device__ void write_contact(Shared& S, int slot, int g1, int g2, const Hit& h,
   S.cgeom[slot][0] = g1; S.cgeom[slot][1] = g2;
 }
 
-__device__ void collision(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+template <int CL>
+__device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
   int cnt = 0, kind = 0, g1 = 0, g2 = 0;
   Hit single;
   GeomV A, B;
@@ -1116,7 +1122,8 @@ __device__ void collision(Shared& S, const gm_model* __restrict__ m, const GmTop
 __device__ __forceinline__ int geom_chain(const GmTopo* T, int g) { return T->geom_group[g]; }
 
 // compact Jacobian row of contact c along unit direction `dir` (rows of the frame)
-__device__ void contact_jac(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int c,
+template <int CL>
+__device__ void contact_jac(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int c,
                             const real* dir, real* J, int& grp) {
   for (int k = 0; k < CW; k++) J[k] = 0;
   const real* C = S.con[c];
@@ -1155,7 +1162,7 @@ __device__ void contact_jac(Shared& S, const gm_model* __restrict__ m, const GmT
 
 // Y = J L^-1 on a compact row (in place)
 template <int CL>
-__device__ void row_LTsolve(Shared& S, real* J, int grp) {
+__device__ void row_LTsolve(SharedT<CL>& S, real* J, int grp) {
 #pragma unroll
   for (int k = 5; k >= 1; k--)
 #pragma unroll
@@ -1173,7 +1180,7 @@ __device__ void row_LTsolve(Shared& S, real* J, int grp) {
   }
 }
 template <int CL>
-__device__ __forceinline__ real row_dot_dofs(Shared& S, const GmTopo* __restrict__ T, const real* J, int grp, const real* v) {
+__device__ __forceinline__ real row_dot_dofs(SharedT<CL>& S, const GmTopo* __restrict__ T, const real* J, int grp, const real* v) {
   real acc = 0;
 #pragma unroll
   for (int k = 0; k < 6; k++) acc += J[k] * v[T->dof_obj + k];
@@ -1204,7 +1211,7 @@ __device__ real impedance(const gm_model* __restrict__ m, real r) {
 }
 
 template <int CL>
-__device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
+__device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                             bool prof = false) {
   unsigned long long t0 = prof ? clock64() : 0;
   // row layout: active locks (lock order) then 4 pyramid edges per contact
@@ -1264,7 +1271,7 @@ __device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmT
     for (int k = 0; k < 6; k++) Yd[k] = J[k] / S.Do[k];
     Yd[6] = J[6] / S.Dbb;
 #pragma unroll
-    for (int q = 1; q <= CLMAX; q++) {
+    for (int q = 1; q <= CL; q++) {
       real dv = 1.0;
       if (grp >= 0 && grp < 3 && q <= CL) dv = S.Df[grp][q];
       else if (grp == 3 && q == 1) dv = S.Dp[1];
@@ -1338,7 +1345,7 @@ __device__ void constraints(Shared& S, const gm_model* __restrict__ m, const GmT
 
 // qacc = qacc_smooth + H^-1 J^T f  via  z = D^-1 Y^T f,  x = L^-1 z
 template <int CL>
-__device__ void constraint_accel(Shared& S, const GmTopo* __restrict__ T, int lane) {
+__device__ void constraint_accel(SharedT<CL>& S, const GmTopo* __restrict__ T, int lane) {
   int nefc = S.nefc;
   if (lane < T->nv) {
     int d = lane;
@@ -1401,7 +1408,8 @@ __device__ void constraint_accel(Shared& S, const GmTopo* __restrict__ T, int la
 }
 
 // ============================================================ integrate
-__device__ void integrate(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+template <int CL>
+__device__ void integrate(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
   real h = (real)m->timestep;
   if (lane < T->nv) S.s.qvel[lane] += h * S.qacc[lane];
   __syncthreads();
@@ -1503,7 +1511,8 @@ __device__ int g_step_to(GmGrip& g, const GmGrip& t, int num) {
 }
 
 // update_all: update_stepper / update_constraints (myfunctions.cpp:2129-2284), antiroll
-__device__ __forceinline__ void update_all(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+template <int CL>
+__device__ __forceinline__ void update_all(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
   if (lane == 0) {
     GmEnvState& s = S.s;
     if (s.time > s.last_step_time + m->time_per_step) {
@@ -1680,7 +1689,8 @@ __device__ float gauge_reading(const gm_model* __restrict__ m, const real* q) {
 // extract_forces_faster (objecthandler.cpp:737-992) over the last substep's contacts.
 // forces[]: obj_loc f1,f2,f3,palm (12) | obj ground global (3) | all_loc f1,f2,f3 x (3),
 //           all_loc palm x (1) | gnd_loc f1,f2,f3 x (3)
-__device__ void extract_forces(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T) {
+template <int CL>
+__device__ void extract_forces(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T) {
   real og[5][3], ag[4][3], gg[3][3];
   for (int a = 0; a < 5; a++) for (int k = 0; k < 3; k++) og[a][k] = 0;
   for (int a = 0; a < 4; a++) for (int k = 0; k < 3; k++) ag[a][k] = 0;
@@ -1729,7 +1739,7 @@ __device__ void extract_forces(Shared& S, const gm_model* __restrict__ m, const 
 
 // MjClass::monitor_sensors (mjclass.cpp:741-898)
 template <int CL>
-__device__ void monitor_sensors(Shared& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
+__device__ void monitor_sensors(SharedT<CL>& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
                                 const GmTopo* __restrict__ T, int lane) {
   __shared__ int bend_ready;
   if (lane == 0) bend_ready = s_ready(S.s, C->s.bending_gauge, SL_BEND);
@@ -1778,7 +1788,7 @@ __device__ void monitor_sensors(Shared& S, const gm_model* __restrict__ m, const
 
 // ============================================================ one full substep
 template <int CL>
-__device__ __noinline__ void physics_substep(Shared& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
+__device__ __noinline__ void physics_substep(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                                 bool prof = false) {
   unsigned long long t0 = prof ? clock64() : 0;
   if (lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
@@ -1809,7 +1819,8 @@ __device__ __forceinline__ float normalise_between(float val, float mn, float mx
   return 2 * (val - mn) / (mx - mn) - 1;
 }
 
-__device__ void sense_gripper_state(Shared& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C) {
+template <int CL>
+__device__ void sense_gripper_state(SharedT<CL>& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C) {
   GmEnvState& s = S.s;
   const gm_settings& st = C->s;
   const double* bmn = C->base_min;
@@ -1866,7 +1877,8 @@ __device__ void sense_gripper_state(Shared& S, const gm_model* __restrict__ m, c
 __device__ float mag3f(const float* v) { return (float)sqrt((double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2]); }
 
 // MjClass::update_env (mjclass.cpp:966-1346) + update_events (5437-5469)
-__device__ void update_env(Shared& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
+template <int CL>
+__device__ void update_env(SharedT<CL>& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
                            const GmTopo* __restrict__ T) {
   GmEnvState& s = S.s;
   const gm_settings& st = C->s;
@@ -2097,13 +2109,15 @@ __device__ float reward(GmEnvState& s, const gm_config* __restrict__ C) {
 }
 
 // ============================================================ kernels
-__device__ __forceinline__ void load_state(Shared& S, const GmEnvState* __restrict__ g, int lane) {
+template <int CL>
+__device__ __forceinline__ void load_state(SharedT<CL>& S, const GmEnvState* __restrict__ g, int lane) {
   const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
   uint32_t* dst = reinterpret_cast<uint32_t*>(&S.s);
   for (int i = lane; i < GM_STATE_WORDS; i += NT) dst[i] = src[i];
   __syncthreads();
 }
-__device__ __forceinline__ void store_state(const Shared& S, GmEnvState* __restrict__ g, int lane) {
+template <int CL>
+__device__ __forceinline__ void store_state(const SharedT<CL>& S, GmEnvState* __restrict__ g, int lane) {
   __syncthreads();
   const uint32_t* src = reinterpret_cast<const uint32_t*>(&S.s);
   uint32_t* dst = reinterpret_cast<uint32_t*>(g);
@@ -2117,7 +2131,7 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
     GmEnvState* __restrict__ states, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
     const GmTopo* __restrict__ T, float* __restrict__ obs, float* __restrict__ rew,
     uint8_t* __restrict__ done, int n_envs, int mode, DebugOut dbg) {
-  __shared__ Shared S;
+  __shared__ SharedT<CL> S;
   const int lane = threadIdx.x;
   const int env = blockIdx.x;
   if (env >= n_envs) return;

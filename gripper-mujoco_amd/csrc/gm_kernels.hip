@@ -41,7 +41,7 @@ struct DebugOut {
   float* qacc;        // [n_envs][GM_MAX_DOF]
   unsigned long long* phase;   // [n_envs][GM_NPHASE] shader-clock cycles per phase (profiling)
 };
-#define GM_NPHASE 16
+#define GM_NPHASE 24
 
 // Per-env LDS image, sized for the compile-time finger chain length CL = n_seg + 2:
 // NB = 3 CL + 4 bodies (world, base, 3 x CL finger links, palm, object),
@@ -57,7 +57,7 @@ struct __align__(16) SharedT {
   real xpos[NB][3];
   real xquat[NB][4];   // normalised body orientations; xmat = quat2mat(xquat)
   real Hf[3][TRIC], Hp[3], Ho[21], Hbb;
-  real Df[3][CL + 1], Dp[2], Do[6], Dbb;
+  real Df[3][CL + 1], Dp[2], Do[6], Dbb;   // INVERSE pivots 1/D of the LTDL factor
   real bdelta[5];
   // contact record: dist, pos[3], normal[3], mu, force[3] (contact frame); the
   // tangents are make_frame(normal) wherever they are needed
@@ -73,8 +73,8 @@ struct __align__(16) SharedT {
         real cinert[NB][10];
         real Ic[NB][10];
       };
-      union {                 // FK phase A rotations are dead before RNE writes forces
-        real qloc[NB][4];
+      union {                 // FK local transforms are dead before RNE writes forces
+        real xloc[NB][7];     // body pose in its parent frame incl. the joint: pos[3], quat[4]
         real cfrc[NB][6];
       };
       real chain_f[5][6], chain_I[5][10];   // chain-root sums for the base body
@@ -130,7 +130,8 @@ template <typename T> __device__ __forceinline__ void quatmul(T* r, const T* a, 
 __device__ __forceinline__ void quatnorm(real* q) {
   real n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
   if (n < 1e-15) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
-  for (int i = 0; i < 4; i++) q[i] /= n;
+  const real in = 1.0 / n;
+  for (int i = 0; i < 4; i++) q[i] *= in;
 }
 __device__ __forceinline__ void ld3(float* r, const double* a) { r[0] = (float)a[0]; r[1] = (float)a[1]; r[2] = (float)a[2]; }
 __device__ __forceinline__ void ld3(double* r, const double* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
@@ -194,54 +195,60 @@ __device__ __forceinline__ void body_R(const SharedT<CL>& S, int b, real* R) {
 // subspaces, geom poses.
 struct Pose { real p[3], q[4], R[9]; };
 
+// one link of the pose recursion: world pose = parent pose o local transform (LDS)
 template <int CL>
-__device__ __forceinline__ void fk_step(SharedT<CL>& S, const gm_model* __restrict__ m, int b, Pose& P) {
-  real bp[3], bq[4], t[3], q[4];
-  ld3(bp, m->body_pos[b]);
-  ld4(bq, m->body_quat[b]);
-  mulmv3(t, P.R, bp);
-  real xp[3] = {P.p[0] + t[0], P.p[1] + t[1], P.p[2] + t[2]};
-  quatmul(q, P.q, bq);
-  const int j = m->body_jnt[b];
-  if (j >= 0) {
-    const int type = m->jnt_type[j];
-    if (type == GM_JNT_SLIDE) {
-      real R[9], ax[3], wa[3];
-      quat2mat(R, q);
-      ld3(ax, m->jnt_axis[j]);
-      mulmv3(wa, R, ax);
-      const real qv = S.s.qpos[m->jnt_qposadr[j]];
-      xp[0] += wa[0] * qv; xp[1] += wa[1] * qv; xp[2] += wa[2] * qv;
-    } else if (type == GM_JNT_HINGE) {
-      real ql[4] = {S.qloc[b][0], S.qloc[b][1], S.qloc[b][2], S.qloc[b][3]};
-      quatmul(q, q, ql);
-    }
-  }
+__device__ __forceinline__ void fk_step(SharedT<CL>& S, int b, Pose& P) {
+  const real* xl = S.xloc[b];
+  const real lp[3] = {xl[0], xl[1], xl[2]};
+  const real lq[4] = {xl[3], xl[4], xl[5], xl[6]};
+  real t[3], q[4];
+  mulmv3(t, P.R, lp);
+  quatmul(q, P.q, lq);
   quatnorm(q);
-  P.p[0] = xp[0]; P.p[1] = xp[1]; P.p[2] = xp[2];
+  P.p[0] += t[0]; P.p[1] += t[1]; P.p[2] += t[2];
   P.q[0] = q[0]; P.q[1] = q[1]; P.q[2] = q[2]; P.q[3] = q[3];
   quat2mat(P.R, q);
-  S.xpos[b][0] = xp[0]; S.xpos[b][1] = xp[1]; S.xpos[b][2] = xp[2];
+  S.xpos[b][0] = P.p[0]; S.xpos[b][1] = P.p[1]; S.xpos[b][2] = P.p[2];
 #pragma unroll
   for (int k = 0; k < 4; k++) S.xquat[b][k] = q[k];
 }
 
 template <int CL>
-__device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
-  // A: hinge rotations
-  if (lane < T->nbody) {
-    const int j = m->body_jnt[lane];
-    if (j >= 0 && m->jnt_type[j] == GM_JNT_HINGE) {
-      const real ang = S.s.qpos[m->jnt_qposadr[j]];
-      real sn, cs;
-      sincos(0.5 * ang, &sn, &cs);
-      S.qloc[lane][0] = cs;
-      S.qloc[lane][1] = (real)m->jnt_axis[j][0] * sn;
-      S.qloc[lane][2] = (real)m->jnt_axis[j][1] * sn;
-      S.qloc[lane][3] = (real)m->jnt_axis[j][2] * sn;
+__device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
+                           bool prof = false) {
+  unsigned long long t0 = prof ? clock64() : 0;
+  // A: local transform of every body (model constants + its joint), one lane per body:
+  //    slide  p = bpos + R(bquat) axis q,  quat = bquat
+  //    hinge  p = bpos,                    quat = bquat (x) (cos q/2, axis sin q/2)
+  if (lane < T->nbody && lane > 0) {
+    const int b = lane;
+    real bp[3], bq[4];
+    ld3(bp, m->body_pos[b]);
+    ld4(bq, m->body_quat[b]);
+    const int j = m->body_jnt[b];
+    if (j >= 0) {
+      const int type = m->jnt_type[j];
+      const real qv = S.s.qpos[m->jnt_qposadr[j]];
+      real ax[3];
+      ld3(ax, m->jnt_axis[j]);
+      if (type == GM_JNT_SLIDE) {
+        real R[9], wa[3];
+        quat2mat(R, bq);
+        mulmv3(wa, R, ax);
+        bp[0] += wa[0] * qv; bp[1] += wa[1] * qv; bp[2] += wa[2] * qv;
+      } else if (type == GM_JNT_HINGE) {
+        real sn, cs;
+        sincos(0.5 * qv, &sn, &cs);
+        const real ql[4] = {cs, ax[0] * sn, ax[1] * sn, ax[2] * sn};
+        quatmul(bq, bq, ql);
+      }
     }
+    real* xl = S.xloc[b];
+    xl[0] = bp[0]; xl[1] = bp[1]; xl[2] = bp[2];
+    xl[3] = bq[0]; xl[4] = bq[1]; xl[5] = bq[2]; xl[6] = bq[3];
   }
   __syncthreads();
+  PH(15);
   // B: pose recursion per chain; every chain lane derives the base pose itself
   if (lane < 4) {
     Pose P;
@@ -250,28 +257,17 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
 #pragma unroll
     for (int k = 0; k < 9; k++) P.R[k] = (k % 4 == 0) ? 1.0 : 0.0;
     {
-      // base body (child of the world): same operation order as fk_step
+      // base body (child of the world); lane 0 publishes it
       const int b = T->body_base;
-      real bp[3], bq[4], q[4];
-      ld3(bp, m->body_pos[b]);
-      ld4(bq, m->body_quat[b]);
-      real t[3];
-      mulmv3(t, P.R, bp);
-      real xp[3] = {t[0], t[1], t[2]};
-      quatmul(q, P.q, bq);
-      const int j = m->body_jnt[b];
-      real R[9], ax[3], wa[3];
-      quat2mat(R, q);
-      ld3(ax, m->jnt_axis[j]);
-      mulmv3(wa, R, ax);
-      const real qv = S.s.qpos[m->jnt_qposadr[j]];
-      xp[0] += wa[0] * qv; xp[1] += wa[1] * qv; xp[2] += wa[2] * qv;
+      const real* xl = S.xloc[b];
+      const real lp[3] = {xl[0], xl[1], xl[2]};
+      real q[4] = {xl[3], xl[4], xl[5], xl[6]};
       quatnorm(q);
-      P.p[0] = xp[0]; P.p[1] = xp[1]; P.p[2] = xp[2];
+      P.p[0] = lp[0]; P.p[1] = lp[1]; P.p[2] = lp[2];
       P.q[0] = q[0]; P.q[1] = q[1]; P.q[2] = q[2]; P.q[3] = q[3];
       quat2mat(P.R, q);
       if (lane == 0) {
-        S.xpos[b][0] = xp[0]; S.xpos[b][1] = xp[1]; S.xpos[b][2] = xp[2];
+        S.xpos[b][0] = lp[0]; S.xpos[b][1] = lp[1]; S.xpos[b][2] = lp[2];
 #pragma unroll
         for (int k = 0; k < 4; k++) S.xquat[b][k] = q[k];
       }
@@ -279,9 +275,9 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
     if (lane < 3) {
       const int b0 = T->body_f0[lane];
 #pragma unroll
-      for (int p = 1; p <= CL; p++) fk_step(S, m, b0 + p - 1, P);
+      for (int p = 1; p <= CL; p++) fk_step(S, b0 + p - 1, P);
     } else {
-      fk_step(S, m, T->body_palm, P);
+      fk_step(S, T->body_palm, P);
     }
   } else if (lane == 4) {
     // object: free joint, pose straight from qpos
@@ -293,6 +289,7 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
     for (int k = 0; k < 4; k++) S.xquat[b][k] = q[k];
   }
   __syncthreads();
+  PH(16);
   // C1: world-origin spatial inertia per body
   if (lane < T->nbody && lane > 0) {
     const int b = lane;
@@ -405,7 +402,9 @@ __device__ __forceinline__ void chain_sums(SharedT<CL>& S, int b0, real* fs, rea
 }
 
 template <int CL>
-__device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+__device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
+                        bool prof = false) {
+  unsigned long long t0 = prof ? clock64() : 0;
   if (lane < 4) {
     const int c = lane;
     real cvel[6], cacc[6];
@@ -470,6 +469,7 @@ __device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const Gm
     for (int k = 0; k < 10; k++) S.Ic[b][k] = S.cinert[b][k];
   }
   __syncthreads();
+  PH(17);
   // base body: its own inertia / force plus the four chain roots
   if (lane == 0) {
     const int bb = T->body_base;
@@ -588,7 +588,7 @@ __device__ __forceinline__ void factor_chain(real* __restrict__ Hs, real& delta_
 #pragma unroll
     for (int q = 0; q < p; q++) Hs[TRI(p, q)] = H[TRI(p, q)];
     Hs[TRI(p, p)] = H[TRI(p, p)];
-    Dout[p] = H[TRI(p, p)];
+    Dout[p] = 1.0 / H[TRI(p, p)];
   }
   delta_out = delta;
 }
@@ -617,10 +617,10 @@ __device__ void factor(SharedT<CL>& S, const GmTopo* __restrict__ T, int lane) {
 #pragma unroll
     for (int i = 0; i < 21; i++) S.Ho[i] = H[i];
 #pragma unroll
-    for (int p = 0; p < 6; p++) S.Do[p] = H[TRI(p, p)];
+    for (int p = 0; p < 6; p++) S.Do[p] = 1.0 / H[TRI(p, p)];
   }
   __syncthreads();
-  if (lane == 0) S.Dbb = S.Hbb - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3]);
+  if (lane == 0) S.Dbb = 1.0 / (S.Hbb - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3]));
   __syncthreads();
 }
 
@@ -636,7 +636,7 @@ __device__ __forceinline__ real chain_LT(const real* __restrict__ Hs, const real
     yb += Hs[TRI(k, 0)] * y[k];
   }
 #pragma unroll
-  for (int p = 1; p <= L; p++) y[p] /= D[p];
+  for (int p = 1; p <= L; p++) y[p] *= D[p];
   return yb;
 }
 // x = L^-1 y (root -> leaves) given x0 = base solution
@@ -657,7 +657,7 @@ __device__ __forceinline__ void obj_solve(const real* __restrict__ Ho, const rea
 #pragma unroll
     for (int i = k - 1; i >= 0; i--) y[i] -= Ho[TRI(k, i)] * y[k];
 #pragma unroll
-  for (int p = 0; p < 6; p++) y[p] /= Do[p];
+  for (int p = 0; p < 6; p++) y[p] *= Do[p];
 #pragma unroll
   for (int k = 0; k < 6; k++) {
     real v = y[k];
@@ -685,7 +685,7 @@ __device__ void solve_full(SharedT<CL>& S, const GmTopo* __restrict__ T, const r
     obj_solve(S.Ho, S.Do, y);
   }
   __syncthreads();
-  const real xbase = (b[T->dof_base] - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3])) / S.Dbb;
+  const real xbase = (b[T->dof_base] - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3])) * S.Dbb;
   __syncthreads();
   if (lane < 3) {
     real xs[CL + 1];
@@ -712,8 +712,8 @@ __device__ void make_frame(real* F, const real* n) {
   if (fabs(n[0]) < 0.5) a[0] = 1; else a[1] = 1;
   real d = dot3(a, n);
   real t1[3] = {a[0] - d * n[0], a[1] - d * n[1], a[2] - d * n[2]};
-  real l = sqrt(dot3(t1, t1));
-  t1[0] /= l; t1[1] /= l; t1[2] /= l;
+  const real il = 1.0 / sqrt(dot3(t1, t1));
+  t1[0] *= il; t1[1] *= il; t1[2] *= il;
   real t2[3];
   cross3(t2, n, t1);
   F[0] = n[0]; F[1] = n[1]; F[2] = n[2];
@@ -1268,14 +1268,14 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
   // Y D^-1 for this lane's row
   real Yd[CW - 1];
   if (lane < nefc) {
-    for (int k = 0; k < 6; k++) Yd[k] = J[k] / S.Do[k];
-    Yd[6] = J[6] / S.Dbb;
+    for (int k = 0; k < 6; k++) Yd[k] = J[k] * S.Do[k];
+    Yd[6] = J[6] * S.Dbb;
 #pragma unroll
     for (int q = 1; q <= CL; q++) {
       real dv = 1.0;
       if (grp >= 0 && grp < 3 && q <= CL) dv = S.Df[grp][q];
       else if (grp == 3 && q == 1) dv = S.Dp[1];
-      Yd[6 + q] = J[6 + q] / dv;
+      Yd[6 + q] = J[6 + q] * dv;
     }
   } else {
     for (int k = 0; k < CW - 1; k++) Yd[k] = 0;
@@ -1368,7 +1368,7 @@ __device__ void constraint_accel(SharedT<CL>& S, const GmTopo* __restrict__ T, i
     else if (grp_d == GM_GRP_BASE) Dd = S.Dbb;
     else if (grp_d == 3) Dd = S.Dp[1];
     else Dd = S.Df[grp_d][slot - 6];
-    S.z[d] = acc / Dd;
+    S.z[d] = acc * Dd;
   }
   __syncthreads();
   // x = L^-1 z : root -> leaves
@@ -1788,13 +1788,27 @@ __device__ void monitor_sensors(SharedT<CL>& S, const gm_model* __restrict__ m, 
 
 // ============================================================ one full substep
 template <int CL>
-__device__ __noinline__ void physics_substep(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
-                                bool prof = false) {
+__device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
+                                                     int lane, bool prof);
+// The substep is outlined (one copy, its own register allocation); address spaces are
+// re-established at its entry so the body keeps global loads for the model and LDS
+// instructions for the per-env image instead of generic (flat) accesses.
+template <int CL>
+__device__ __noinline__ void physics_substep(SharedT<CL>& S_, const gm_model* __restrict__ m_, const GmTopo* __restrict__ T_,
+                                             int lane, bool prof = false) {
+  SharedT<CL>& S = *(SharedT<CL>*)(__attribute__((address_space(3))) SharedT<CL>*)&S_;
+  const gm_model* m = (const gm_model*)(const __attribute__((address_space(1))) gm_model*)m_;
+  const GmTopo* T = (const GmTopo*)(const __attribute__((address_space(1))) GmTopo*)T_;
+  physics_substep_body<CL>(S, m, T, lane, prof);
+}
+template <int CL>
+__device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
+                                                     int lane, bool prof) {
   unsigned long long t0 = prof ? clock64() : 0;
   if (lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
-  kinematics<CL>(S, m, T, lane);
+  kinematics<CL>(S, m, T, lane, prof);
   PH(0);
-  crb_rne<CL>(S, m, T, lane);
+  crb_rne<CL>(S, m, T, lane, prof);
   PH(1);
   mass_and_forces(S, m, T, lane);
   PH(2);
@@ -2136,25 +2150,22 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
   const int env = blockIdx.x;
   if (env >= n_envs) return;
   load_state(S, states + env, lane);
-  if (mode == 1) {
-    for (int i = 0; i < 400; i++) {
-      physics_substep<CL>(S, m, T, lane);
-      update_all(S, m, T, lane);
-    }
-    store_state(S, states + env, lane);
-    return;
-  }
-  const bool prof = dbg.phase != nullptr;
+  const bool settle = (mode == 1);          // calibrate_reset settle: 400 substeps, no sensors
+  const bool prof = !settle && dbg.phase != nullptr;
   if (prof && lane < GM_NPHASE) S.tph[lane] = 0;
   __syncthreads();
-  int nsub = (mode == 2) ? 1 : C->sim_steps_per_action + S.s.extra_substeps;
+  const int nsub = settle ? 400 : (mode == 2) ? 1 : C->sim_steps_per_action + S.s.extra_substeps;
   for (int i = 0; i < nsub; i++) {
     physics_substep<CL>(S, m, T, lane, prof);
     unsigned long long t0 = prof ? clock64() : 0;
     update_all(S, m, T, lane);
     PH(9);
-    monitor_sensors<CL>(S, m, C, T, lane);
+    if (!settle) monitor_sensors<CL>(S, m, C, T, lane);
     PH(10);
+  }
+  if (settle) {
+    store_state(S, states + env, lane);
+    return;
   }
   if (mode == 2) {
     if (lane == 0) dbg.ncon[env] = S.ncon;

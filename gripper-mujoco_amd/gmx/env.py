@@ -225,10 +225,11 @@ class BatchedGripperEnv:
 
     PHASES = ("kinematics", "crb_rne", "mass_forces", "factor", "smooth_solve", "collision",
               "constraints_pgs", "constraint_accel", "integrate", "update_all", "monitor_sensors",
-              "  c:jac+rowsolve", "  c:Yd", "  c:A_build", "  c:PGS")
+              "  c:jac+rowsolve", "  c:Yd", "  c:A_build", "  c:PGS", "  k:A_hinge", "  k:B_chains",
+              "  crb:chains")
 
     def step_profiled(self):
         """One env-step with per-phase shader-clock counters (lane 0, summed over substeps)."""
-        ph = np.zeros((self.n_envs, 16), dtype=np.uint64)
+        ph = np.zeros((self.n_envs, 24), dtype=np.uint64)
         self._check(self.lib.gm_step_profiled(self._ctx, ph.ctypes.data_as(C.POINTER(C.c_uint64))))
         return ph

@@ -376,9 +376,10 @@ int  gm_last_step_ms(gm_ctx* ctx, float* ms);
 int  gm_debug_substep(gm_ctx* ctx, int32_t* ncon, float* contact, float* efc_force,
                       float* qacc);
 /* diagnostic: one gm_step with per-phase shader-clock cycle counters, lane-0 view,
-   summed over substeps: out[n_envs][16] = kinematics, crb_rne, mass+forces, factor,
+   summed over substeps: out[n_envs][24] = kinematics, crb_rne, mass+forces, factor,
    smooth solve, collision, constraint build+PGS, constraint accel, integrate,
-   update_all, monitor_sensors, (5 spare) */
+   update_all, monitor_sensors, then sub-phases (constraint rows, Yd, Delassus,
+   PGS, FK hinge rotations, FK chains, CRB/RNE chains), (rest spare) */
 int  gm_step_profiled(gm_ctx* ctx, uint64_t* phase_cycles);
 
 #ifdef __cplusplus

@@ -1321,21 +1321,32 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
   // owns row j: its residual res_j = (A f + b)_j is kept current by every row update,
   // each update f_r += d is broadcast with v_readlane.  Contact rows are clamped at 0
   // (pyramid edges), lock rows are unbounded.
-  const int nefc_s = __builtin_amdgcn_readfirstlane(nefc);
-  const real lb = is_contact ? 0.0 : -__builtin_inf();
+  // Rows run in chunks of 8 with one (scalar) guard per chunk; rows past nefc inside the
+  // last chunk are exact no-ops (res = f = 0, arinv = 0, zero A entries => delta = 0).
+  const int nchunk = (__builtin_amdgcn_readfirstlane(nefc) + 7) >> 3;
+  const real lb = (is_contact || lane >= nefc) ? 0.0 : -__builtin_inf();
+  const real arinv_l = (lane < nefc) ? arinv : 0.0;
   for (int it = 0; it < m->pgs_iterations; it++) {
 #pragma unroll
-    for (int r = 0; r < GM_MAX_EFC; r++) {
-      if (r >= nefc_s) continue;
-      const real g = fma(R, f, res);
-      const real fn = fmax(fma(-g, arinv, f), lb);
-      const real dl = fn - f;
-      const long long bits = __double_as_longlong(dl);
-      const int lo = __builtin_amdgcn_readlane((int)bits, r);
-      const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), r);
-      const real delta = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-      res = fma(A[r], delta, res);
-      if (lane == r) f = fn;
+    for (int c = 0; c < GM_MAX_EFC / 8; c++) {
+      if (c >= nchunk) continue;
+#pragma unroll
+      for (int rr = 0; rr < 8; rr++) {
+        const int r = c * 8 + rr;
+        const real g = fma(R, f, res);
+        const real fn = fmax(fma(-g, arinv_l, f), lb);
+        const real dl = fn - f;
+        const long long bits = __double_as_longlong(dl);
+        const int lo = __builtin_amdgcn_readlane((int)bits, r);
+        const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), r);
+        const real delta = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+        res = fma(A[r], delta, res);
+        // lane == r, compared in place: the opaque scalar copy of r keeps the compiler
+        // from hoisting a 64-entry mask table out of the sweep loop (it would spill)
+        int rs;
+        asm volatile("s_mov_b32 %0, %1" : "=s"(rs) : "i"(r));
+        f = (lane == rs) ? fn : f;
+      }
     }
   }
   PH(14);

@@ -405,40 +405,101 @@ template <int CL>
 __device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                         bool prof = false) {
   unsigned long long t0 = prof ? clock64() : 0;
-  if (lane < 4) {
-    const int c = lane;
-    real cvel[6], cacc[6];
+  // Lanes = bodies.  Along each finger / palm chain the velocities and bias accelerations
+  // are segmented prefix sums and the composite forces / inertias segmented suffix sums
+  // (Hillis-Steele over the chain position, shuffles within the wave); the base body is
+  // the common root and the free object is handled by its own lane.
+  const int db = T->dof_base;
+  const real qdb = S.s.qvel[db];
+  real cvb[6], cab[6];
 #pragma unroll
-    for (int k = 0; k < 6; k++) { cvel[k] = 0; cacc[k] = 0; }
-    cacc[3] = -(real)m->gravity[0]; cacc[4] = -(real)m->gravity[1]; cacc[5] = -(real)m->gravity[2];
-    {
-      const int db = T->dof_base;
-      real cd[6], cdd[6];
+  for (int k = 0; k < 6; k++) { cvb[k] = S.cdof[db][k] * qdb; cab[k] = 0; }
+  cab[3] = -(real)m->gravity[0]; cab[4] = -(real)m->gravity[1]; cab[5] = -(real)m->gravity[2];
+
+  const int b = lane;
+  const int grp = (b < T->nbody) ? T->body_group[b] : -1;
+  const bool chain = grp >= 0 && grp <= 3;
+  const int p = chain ? T->body_cpos[b] : 0;
+  const int Lc = (grp == 3) ? 1 : CL;
+  const int d = chain ? (grp < 3 ? T->dof_f0[grp] + p - 1 : T->dof_palm) : db;
+  real cd[6], v[6];
+  const real qd = chain ? S.s.qvel[d] : 0.0;
 #pragma unroll
-      for (int k = 0; k < 6; k++) cd[k] = S.cdof[db][k];
-      cross_motion(cdd, cvel, cd);
-      const real qd = S.s.qvel[db];
+  for (int k = 0; k < 6; k++) { cd[k] = chain ? S.cdof[d][k] : 0.0; v[k] = cd[k] * qd; }
+  // velocities: inclusive prefix along the chain, then the base contribution
+  real cv[6];
 #pragma unroll
-      for (int k = 0; k < 6; k++) { cvel[k] += cd[k] * qd; cacc[k] += cdd[k] * qd; }
-      if (c == 0) body_force(S, T->body_base, cvel, cacc);
+  for (int k = 0; k < 6; k++) cv[k] = v[k];
+#pragma unroll
+  for (int off = 1; off < CL; off <<= 1) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      const real nb = __shfl_up(cv[k], off);
+      if (p > off) cv[k] += nb;
     }
-    real fs[6], Is[10];
-    if (c < 3) {
-      const int b0 = T->body_f0[c], d0 = T->dof_f0[c];
+  }
+  real cvp[6];
 #pragma unroll
-      for (int p = 1; p <= CL; p++) rne_fwd(S, b0 + p - 1, d0 + p - 1, cvel, cacc);
-      chain_sums<CL>(S, b0, fs, Is);
-    } else {
-      rne_fwd(S, T->body_palm, T->dof_palm, cvel, cacc);
-      chain_sums<1>(S, T->body_palm, fs, Is);
+  for (int k = 0; k < 6; k++) {
+    const real nb = __shfl_up(cv[k], 1);
+    cvp[k] = cvb[k] + (p > 1 ? nb : 0.0);
+    cv[k] += cvb[k];
+  }
+  // bias accelerations: prefix of (cvel_parent x cdof) qd
+  real ca[6];
+  cross_motion(ca, cvp, cd);
+#pragma unroll
+  for (int k = 0; k < 6; k++) ca[k] *= qd;
+#pragma unroll
+  for (int off = 1; off < CL; off <<= 1) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      const real nb = __shfl_up(ca[k], off);
+      if (p > off) ca[k] += nb;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 6; k++) ca[k] += cab[k];
+  // body forces I a + v x* (I v), then suffix sums of forces and inertias
+  real ci[10], f[6];
+#pragma unroll
+  for (int k = 0; k < 10; k++) ci[k] = chain ? S.cinert[b][k] : 0.0;
+  {
+    real t1[6], t2[6];
+    inert_mul(f, ci, ca);
+    inert_mul(t1, ci, cv);
+    cross_force(t2, cv, t1);
+#pragma unroll
+    for (int k = 0; k < 6; k++) f[k] += t2[k];
+  }
+#pragma unroll
+  for (int off = 1; off < CL; off <<= 1) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      const real nb = __shfl_down(f[k], off);
+      if (p + off <= Lc) f[k] += nb;
     }
 #pragma unroll
-    for (int k = 0; k < 6; k++) S.chain_f[c][k] = fs[k];
+    for (int k = 0; k < 10; k++) {
+      const real nb = __shfl_down(ci[k], off);
+      if (p + off <= Lc) ci[k] += nb;
+    }
+  }
+  if (chain) {
 #pragma unroll
-    for (int k = 0; k < 10; k++) S.chain_I[c][k] = Is[k];
-  } else if (lane == 4) {
+    for (int k = 0; k < 6; k++) S.cfrc[b][k] = f[k];
+#pragma unroll
+    for (int k = 0; k < 10; k++) S.Ic[b][k] = ci[k];
+    if (p == 1) {
+#pragma unroll
+      for (int k = 0; k < 6; k++) S.chain_f[grp][k] = f[k];
+#pragma unroll
+      for (int k = 0; k < 10; k++) S.chain_I[grp][k] = ci[k];
+    }
+  }
+  if (b == T->body_obj) {
     // object: free joint on one body
-    const int b = T->body_obj, d0 = T->dof_obj;
+    const int d0 = T->dof_obj;
     real cvel[6], cacc[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) { cvel[k] = 0; cacc[k] = 0; }
@@ -465,30 +526,29 @@ __device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const Gm
       for (int t = 0; t < 6; t++) cacc[t] += cdd[k][t] * qv;
     }
     body_force(S, b, cvel, cacc);
-#pragma unroll
-    for (int k = 0; k < 10; k++) S.Ic[b][k] = S.cinert[b][k];
   }
   __syncthreads();
   PH(17);
   // base body: its own inertia / force plus the four chain roots
   if (lane == 0) {
     const int bb = T->body_base;
-    real ic[10], f[6];
+    body_force(S, bb, cvb, cab);
+    real ic[10], fb[6];
 #pragma unroll
     for (int k = 0; k < 10; k++) ic[k] = S.cinert[bb][k];
 #pragma unroll
-    for (int k = 0; k < 6; k++) f[k] = S.cfrc[bb][k];
+    for (int k = 0; k < 6; k++) fb[k] = S.cfrc[bb][k];
 #pragma unroll
     for (int c = 0; c < 4; c++) {
 #pragma unroll
       for (int k = 0; k < 10; k++) ic[k] += S.chain_I[c][k];
 #pragma unroll
-      for (int k = 0; k < 6; k++) f[k] += S.chain_f[c][k];
+      for (int k = 0; k < 6; k++) fb[k] += S.chain_f[c][k];
     }
 #pragma unroll
     for (int k = 0; k < 10; k++) S.Ic[bb][k] = ic[k];
 #pragma unroll
-    for (int k = 0; k < 6; k++) S.cfrc[bb][k] = f[k];
+    for (int k = 0; k < 6; k++) S.cfrc[bb][k] = fb[k];
   }
   __syncthreads();
 }
@@ -1283,21 +1343,31 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
   const bool gj = grp >= 0 && grp <= 3;
   // Delassus column A[:, lane] = Y D^-1 Y_lane^T, held in this lane's VGPRs
   real A[GM_MAX_EFC];
+  const int nchunk_a = (__builtin_amdgcn_readfirstlane(nefc) + 7) >> 3;
 #pragma unroll
-  for (int i = 0; i < GM_MAX_EFC; i++) {
-    real acc = 0;
-    if (i < nefc) {
+  for (int c = 0; c < GM_MAX_EFC / 8; c++) {
+#pragma unroll
+    for (int rr = 0; rr < 8; rr++) A[c * 8 + rr] = 0;
+    if (c >= nchunk_a) continue;
+#pragma unroll
+    for (int rr = 0; rr < 8; rr++) {
+      const int i = c * 8 + rr;
+      // rows past nefc hold stale data in LDS: their products are masked below
       const real* Yi = S.Y[i];
-      int gi = S.ygrp[i];
-      for (int k = 0; k < 6; k++) acc += Yd[k] * Yi[k];
-      if (gj && gi >= 0 && gi <= 3) {
-        acc += Yd[6] * Yi[6];
-        if (gi == grp)
+      const int gi = S.ygrp[i];
+      real ao = 0, ab = 0, ac = 0;
 #pragma unroll
-          for (int q = 1; q <= CL; q++) acc += Yd[6 + q] * Yi[6 + q];
-      }
+      for (int k = 0; k < 6; k++) ao = fma(Yd[k], Yi[k], ao);
+      ab = Yd[6] * Yi[6];
+#pragma unroll
+      for (int q = 1; q <= CL; q++) ac = fma(Yd[6 + q], Yi[6 + q], ac);
+      const bool valid = i < nefc;
+      const bool gi_chain = gi >= 0 && gi <= 3;
+      real acc = ao;
+      acc += (gj && gi_chain) ? ab : 0.0;
+      acc += (gj && gi == grp) ? ac : 0.0;
+      A[i] = valid ? acc : 0.0;
     }
-    A[i] = acc;
   }
   PH(13);
   // impedance / reference acceleration (mj_makeImpedance)

@@ -73,10 +73,7 @@ struct __align__(16) SharedT {
         real cinert[NB][10];
         real Ic[NB][10];
       };
-      union {                 // FK local transforms are dead before RNE writes forces
-        real xloc[NB][7];     // body pose in its parent frame incl. the joint: pos[3], quat[4]
-        real cfrc[NB][6];
-      };
+      real cfrc[NB][6];
       real chain_f[5][6], chain_I[5][10];   // chain-root sums for the base body
       int32_t cnt[NT];                      // collision: contacts per pair lane
     };
@@ -195,36 +192,19 @@ __device__ __forceinline__ void body_R(const SharedT<CL>& S, int b, real* R) {
 // subspaces, geom poses.
 struct Pose { real p[3], q[4], R[9]; };
 
-// one link of the pose recursion: world pose = parent pose o local transform (LDS)
-template <int CL>
-__device__ __forceinline__ void fk_step(SharedT<CL>& S, int b, Pose& P) {
-  const real* xl = S.xloc[b];
-  const real lp[3] = {xl[0], xl[1], xl[2]};
-  const real lq[4] = {xl[3], xl[4], xl[5], xl[6]};
-  real t[3], q[4];
-  mulmv3(t, P.R, lp);
-  quatmul(q, P.q, lq);
-  quatnorm(q);
-  P.p[0] += t[0]; P.p[1] += t[1]; P.p[2] += t[2];
-  P.q[0] = q[0]; P.q[1] = q[1]; P.q[2] = q[2]; P.q[3] = q[3];
-  quat2mat(P.R, q);
-  S.xpos[b][0] = P.p[0]; S.xpos[b][1] = P.p[1]; S.xpos[b][2] = P.p[2];
-#pragma unroll
-  for (int k = 0; k < 4; k++) S.xquat[b][k] = q[k];
-}
 
 template <int CL>
 __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                            bool prof = false) {
   unsigned long long t0 = prof ? clock64() : 0;
-  // A: local transform of every body (model constants + its joint), one lane per body:
+  // A: local transform of every body (model constants + its joint), lane = body:
   //    slide  p = bpos + R(bquat) axis q,  quat = bquat
   //    hinge  p = bpos,                    quat = bquat (x) (cos q/2, axis sin q/2)
+  real lp[3] = {0, 0, 0}, lq[4] = {1, 0, 0, 0};
   if (lane < T->nbody && lane > 0) {
     const int b = lane;
-    real bp[3], bq[4];
-    ld3(bp, m->body_pos[b]);
-    ld4(bq, m->body_quat[b]);
+    ld3(lp, m->body_pos[b]);
+    ld4(lq, m->body_quat[b]);
     const int j = m->body_jnt[b];
     if (j >= 0) {
       const int type = m->jnt_type[j];
@@ -233,60 +213,72 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
       ld3(ax, m->jnt_axis[j]);
       if (type == GM_JNT_SLIDE) {
         real R[9], wa[3];
-        quat2mat(R, bq);
+        quat2mat(R, lq);
         mulmv3(wa, R, ax);
-        bp[0] += wa[0] * qv; bp[1] += wa[1] * qv; bp[2] += wa[2] * qv;
+        lp[0] += wa[0] * qv; lp[1] += wa[1] * qv; lp[2] += wa[2] * qv;
       } else if (type == GM_JNT_HINGE) {
         real sn, cs;
         sincos(0.5 * qv, &sn, &cs);
         const real ql[4] = {cs, ax[0] * sn, ax[1] * sn, ax[2] * sn};
-        quatmul(bq, bq, ql);
+        quatmul(lq, lq, ql);
       }
     }
-    real* xl = S.xloc[b];
-    xl[0] = bp[0]; xl[1] = bp[1]; xl[2] = bp[2];
-    xl[3] = bq[0]; xl[4] = bq[1]; xl[5] = bq[2]; xl[6] = bq[3];
   }
-  __syncthreads();
   PH(15);
-  // B: pose recursion per chain; every chain lane derives the base pose itself
-  if (lane < 4) {
-    Pose P;
-    P.p[0] = P.p[1] = P.p[2] = 0;
-    P.q[0] = 1; P.q[1] = P.q[2] = P.q[3] = 0;
+  // B: poses.  The base is the world's child; along each finger / palm chain the
+  // local transforms are composed by a segmented inclusive scan (root-side operand on
+  // the left: (p_a, q_a) o (p_b, q_b) = (p_a + R(q_a) p_b, q_a (x) q_b)), then the base
+  // pose is applied and the orientation renormalised.
+  {
+    const int bb = T->body_base;
+    real bpos[3], bq[4];
 #pragma unroll
-    for (int k = 0; k < 9; k++) P.R[k] = (k % 4 == 0) ? 1.0 : 0.0;
-    {
-      // base body (child of the world); lane 0 publishes it
-      const int b = T->body_base;
-      const real* xl = S.xloc[b];
-      const real lp[3] = {xl[0], xl[1], xl[2]};
-      real q[4] = {xl[3], xl[4], xl[5], xl[6]};
-      quatnorm(q);
-      P.p[0] = lp[0]; P.p[1] = lp[1]; P.p[2] = lp[2];
-      P.q[0] = q[0]; P.q[1] = q[1]; P.q[2] = q[2]; P.q[3] = q[3];
-      quat2mat(P.R, q);
-      if (lane == 0) {
-        S.xpos[b][0] = lp[0]; S.xpos[b][1] = lp[1]; S.xpos[b][2] = lp[2];
+    for (int k = 0; k < 3; k++) bpos[k] = __shfl(lp[k], bb);
 #pragma unroll
-        for (int k = 0; k < 4; k++) S.xquat[b][k] = q[k];
+    for (int k = 0; k < 4; k++) bq[k] = __shfl(lq[k], bb);
+    quatnorm(bq);
+    real bR[9];
+    quat2mat(bR, bq);
+    const int grp = (lane < T->nbody) ? T->body_group[lane] : -1;
+    const bool chain = grp >= 0 && grp <= 3;
+    const int p = chain ? T->body_cpos[lane] : 0;
+#pragma unroll
+    for (int off = 1; off < CL; off <<= 1) {
+      real np[3], nq[4];
+#pragma unroll
+      for (int k = 0; k < 3; k++) np[k] = __shfl_up(lp[k], off);
+#pragma unroll
+      for (int k = 0; k < 4; k++) nq[k] = __shfl_up(lq[k], off);
+      if (p > off) {
+        real R[9], t[3], q[4];
+        quat2mat(R, nq);
+        mulmv3(t, R, lp);
+        quatmul(q, nq, lq);
+        lp[0] = np[0] + t[0]; lp[1] = np[1] + t[1]; lp[2] = np[2] + t[2];
+        lq[0] = q[0]; lq[1] = q[1]; lq[2] = q[2]; lq[3] = q[3];
       }
     }
-    if (lane < 3) {
-      const int b0 = T->body_f0[lane];
+    if (chain) {
+      real t[3], q[4];
+      mulmv3(t, bR, lp);
+      quatmul(q, bq, lq);
+      quatnorm(q);
+      S.xpos[lane][0] = bpos[0] + t[0]; S.xpos[lane][1] = bpos[1] + t[1]; S.xpos[lane][2] = bpos[2] + t[2];
 #pragma unroll
-      for (int p = 1; p <= CL; p++) fk_step(S, b0 + p - 1, P);
-    } else {
-      fk_step(S, T->body_palm, P);
+      for (int k = 0; k < 4; k++) S.xquat[lane][k] = q[k];
+    } else if (lane == bb) {
+      S.xpos[bb][0] = bpos[0]; S.xpos[bb][1] = bpos[1]; S.xpos[bb][2] = bpos[2];
+#pragma unroll
+      for (int k = 0; k < 4; k++) S.xquat[bb][k] = bq[k];
+    } else if (lane == T->body_obj) {
+      // object: free joint, pose straight from qpos
+      const int qa = T->qadr_obj;
+      real q[4] = {S.s.qpos[qa + 3], S.s.qpos[qa + 4], S.s.qpos[qa + 5], S.s.qpos[qa + 6]};
+      quatnorm(q);
+      S.xpos[lane][0] = S.s.qpos[qa]; S.xpos[lane][1] = S.s.qpos[qa + 1]; S.xpos[lane][2] = S.s.qpos[qa + 2];
+#pragma unroll
+      for (int k = 0; k < 4; k++) S.xquat[lane][k] = q[k];
     }
-  } else if (lane == 4) {
-    // object: free joint, pose straight from qpos
-    const int b = T->body_obj, qa = T->qadr_obj;
-    real q[4] = {S.s.qpos[qa + 3], S.s.qpos[qa + 4], S.s.qpos[qa + 5], S.s.qpos[qa + 6]};
-    quatnorm(q);
-    S.xpos[b][0] = S.s.qpos[qa]; S.xpos[b][1] = S.s.qpos[qa + 1]; S.xpos[b][2] = S.s.qpos[qa + 2];
-#pragma unroll
-    for (int k = 0; k < 4; k++) S.xquat[b][k] = q[k];
   }
   __syncthreads();
   PH(16);
@@ -2269,19 +2261,24 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
     return;
   }
   if (lane == 0) {
+    unsigned long long t0 = prof ? clock64() : 0;
     S.s.extra_substeps = 0;
     S.s.overflow = S.overflow;
     sense_gripper_state(S, m, C);
+    PH(18);
     update_env(S, m, C, T);
+    PH(19);
     S.s.num_action_steps += 1;
     float* o = obs + (size_t)env * C->n_obs;
     get_obs(S.s, C, o);
+    PH(20);
     int d = is_done(S.s, C);
     float r = reward(S.s, C);
     S.s.done = d;
     S.s.reward = r;
     rew[env] = r;
     done[env] = (uint8_t)d;
+    PH(21);
   }
   if (prof) {
     __syncthreads();

@@ -226,7 +226,7 @@ class BatchedGripperEnv:
     PHASES = ("kinematics", "crb_rne", "mass_forces", "factor", "smooth_solve", "collision",
               "constraints_pgs", "constraint_accel", "integrate", "update_all", "monitor_sensors",
               "  c:jac+rowsolve", "  c:Yd", "  c:A_build", "  c:PGS", "  k:A_hinge", "  k:B_chains",
-              "  crb:chains")
+              "  crb:chains", "e:sense", "e:update_env", "e:get_obs", "e:done_reward")
 
     def step_profiled(self):
         """One env-step with per-phase shader-clock counters (lane 0, summed over substeps)."""

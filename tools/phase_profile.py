@@ -20,6 +20,9 @@ S = env.cfg.sim_steps_per_action if hasattr(env.cfg, 'sim_steps_per_action') els
 allc = tot[:11].sum()
 print(f"n={n} mean cycles per env-step (lane 0) total {allc:.3e}  per substep {allc/63:.3e}")
 for k, name in enumerate(env.PHASES):
-    print(f"  {name:18s} {tot[k]/63:10.0f} cyc/substep  {100*tot[k]/allc:5.1f}%")
+    if name.startswith("e:"):
+        print(f"  {name:18s} {tot[k]:10.0f} cyc/env-step  (= {tot[k]/63:.0f} per substep)")
+    else:
+        print(f"  {name:18s} {tot[k]/63:10.0f} cyc/substep  {100*tot[k]/allc:5.1f}%")
 ncon, _, _, _ = env.debug_substep()
 print("ncon per env: mean %.2f  max %d  histogram %s" % (ncon.mean(), ncon.max(), np.bincount(ncon, minlength=16).tolist()))

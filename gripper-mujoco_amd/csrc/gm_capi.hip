@@ -113,6 +113,30 @@ int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
     if (m.body_group[b] >= 0 && m.body_group[b] < 3) T.body_cpos[b] = b - T.body_f0[m.body_group[b]] + 1;
     else if (m.body_group[b] == GM_GRP_PALM) T.body_cpos[b] = 1;
   }
+  // per-dof constants: the engine-spec H~ diagonal additions and PD gains
+  // (mj_step2 implicit terms and luke::control gains, oracle.c ctrl_gains / step2)
+  const double h = m.timestep;
+  for (int d = 0; d < m.nv; d++) {
+    const int b = m.dof_body[d], j = m.body_jnt[b];
+    T.dof_body[d] = b;
+    T.dof_grp[d] = m.body_group[b];
+    T.dof_p[d] = (m.body_group[b] == GM_GRP_OBJECT) ? d - m.dof_obj : T.body_cpos[b];
+    double kp = 0, kd = 0;
+    int tgt = 0;
+    for (int f = 0; f < 3; f++) {
+      if (d == m.dof_pris[f]) { kp = m.kp_gripper[0]; kd = m.kd_gripper[0]; tgt = 1; }
+      if (d == m.dof_rev[f]) { kp = m.kp_gripper[1]; kd = m.kd_gripper[1]; tgt = 2; }
+    }
+    if (d == m.dof_palm) { kp = m.kp_gripper[2]; kd = m.kd_gripper[2]; tgt = 3; }
+    if (d == m.dof_base) { kp = m.kp_base[2]; kd = m.kd_base[2]; tgt = 4; }
+    const bool free = m.jnt_type[j] == GM_JNT_FREE;
+    double add = m.jnt_armature[j] + h * (m.jnt_damping[j] + kd);
+    if (!free) add += h * h * (m.jnt_stiffness[j] + kp);
+    T.dof_add[d] = add;
+    T.dof_stiff[d] = free ? 0.0 : m.jnt_stiffness[j];
+    T.dof_damp[d] = m.jnt_damping[j];
+    T.dof_kp[d] = kp; T.dof_kd[d] = kd; T.dof_target[d] = tgt;
+  }
   for (int g = 0; g < m.ngeom; g++) {
     int b = m.geom_body[g];
     T.geom_group[g] = (b == 0) ? -1 : T.body_group[b];

@@ -561,48 +561,49 @@ __device__ __forceinline__ void ctrl_gains(const gm_model* __restrict__ m, const
 template <int CL>
 __device__ void mass_and_forces(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
   if (lane < T->nv) {
-    int d = lane;
-    int b = m->dof_body[d];
-    real F[6];
-    inert_mul(F, S.Ic[b], S.cdof[d]);
-    real h = (real)m->timestep;
-    int j = m->body_jnt[b];
-    real kp, kd;
-    ctrl_gains(m, T, d, &kp, &kd);
-    real add = (real)m->jnt_armature[j] + h * ((real)m->jnt_damping[j] + kd);
-    if (m->jnt_type[j] != GM_JNT_FREE) add += h * h * ((real)m->jnt_stiffness[j] + kp);
-    int c = T->body_group[b];          // 0..2 finger, 3 palm, 5 object, 4 base
+    const int d = lane;
+    const int b = T->dof_body[d];
+    const int c = T->dof_grp[d];
+    const int p = T->dof_p[d];
+    const real add = T->dof_add[d];
+    real cd[6], F[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
+    inert_mul(F, S.Ic[b], cd);
     if (c == GM_GRP_BASE) {
-      S.Hbb = dot6(S.cdof[d], F) + add;
+      S.Hbb = dot6(cd, F) + add;
     } else if (c == GM_GRP_OBJECT) {
-      int p = d - T->dof_obj;
-      for (int q = 0; q <= p; q++) {
+#pragma unroll
+      for (int q = 0; q < 6; q++) {
+        if (q > p) continue;
         real v = dot6(S.cdof[T->dof_obj + q], F);
         if (q == p) v += add;
         S.Ho[TRI(p, q)] = v;
       }
     } else {
-      int p = T->body_cpos[b];
-      for (int q = 0; q <= p; q++) {
-        int dq = (q == 0) ? T->dof_base : chain_dof(T, c, q);
+      const int d0 = (c < 3) ? T->dof_f0[c] : T->dof_palm;
+      real* Hrow = (c < 3) ? &S.Hf[c][TRI(p, 0)] : &S.Hp[TRI(p, 0)];
+#pragma unroll
+      for (int q = 0; q <= CL; q++) {
+        if (q > p) continue;
+        const int dq = (q == 0) ? T->dof_base : d0 + q - 1;
         real v = dot6(S.cdof[dq], F);
         if (q == p) v += add;
-        if (c < 3) S.Hf[c][TRI(p, q)] = v; else S.Hp[TRI(p, q)] = v;
+        Hrow[q] = v;
       }
     }
     // forces: passive springs/damping, PD control (target_.next, base target), RNE bias
-    real bias = dot6(S.cdof[d], S.cfrc[b]);
+    const real bias = dot6(cd, S.cfrc[b]);
+    const real qp = S.s.qpos[d], qv = S.s.qvel[d];
     real pas = 0;
-    if (m->jnt_type[j] != GM_JNT_FREE) pas -= (real)m->jnt_stiffness[j] * S.s.qpos[d];
-    pas -= (real)m->jnt_damping[j] * S.s.qvel[d];
+    pas -= T->dof_stiff[d] * qp;
+    pas -= T->dof_damp[d] * qv;
+    const int tgt = T->dof_target[d];
     real act = 0;
-    real q = S.s.qpos[d], v = S.s.qvel[d];
-    for (int f = 0; f < 3; f++) {
-      if (d == m->dof_pris[f]) act = -((q - (real)S.s.next.x) * kp + v * kd);
-      if (d == m->dof_rev[f]) act = -((q - (real)S.s.next.th) * kp + v * kd);
+    if (tgt != 0) {
+      const real target = tgt == 1 ? S.s.next.x : tgt == 2 ? S.s.next.th : tgt == 3 ? S.s.next.z : S.s.base[2];
+      act = -((qp - target) * T->dof_kp[d] + qv * T->dof_kd[d]);
     }
-    if (d == m->dof_palm) act = -((q - (real)S.s.next.z) * kp + v * kd);
-    if (d == m->dof_base) act = -((q - (real)S.s.base[2]) * kp + v * kd);
     S.frc[d] = pas + act - bias;
   }
   __syncthreads();
@@ -1174,39 +1175,44 @@ __device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const 
 __device__ __forceinline__ int geom_chain(const GmTopo* T, int g) { return T->geom_group[g]; }
 
 // compact Jacobian row of contact c along unit direction `dir` (rows of the frame)
+// compact Jacobian row of contact c along the world direction `dir` (linear in dir, so
+// a pyramid edge n +- mu t is one pass); chain columns are unrolled to CL
 template <int CL>
 __device__ void contact_jac(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int c,
                             const real* dir, real* J, int& grp) {
+#pragma unroll
   for (int k = 0; k < CW; k++) J[k] = 0;
   const real* C = S.con[c];
   const real pos[3] = {C[1], C[2], C[3]};
-  int gs[2] = {S.cgeom[c][0], S.cgeom[c][1]};
-  real sg[2] = {-1.0f, 1.0f};
   grp = -1;
+#pragma unroll
   for (int side = 0; side < 2; side++) {
-    int g = gs[side];
-    int grpg = T->geom_group[g];
+    const int g = S.cgeom[c][side];
+    const int grpg = T->geom_group[g];
     if (grpg < 0) continue;
-    real s = sg[side];
+    const real sgn = side == 0 ? -1.0 : 1.0;
     if (grpg == GM_GRP_OBJECT) {
+#pragma unroll
       for (int k = 0; k < 6; k++) {
         const real* cd = S.cdof[T->dof_obj + k];
         real wxp[3];
         cross3(wxp, cd, pos);
-        real col[3] = {cd[3] + wxp[0], cd[4] + wxp[1], cd[5] + wxp[2]};
-        J[k] += s * dot3(dir, col);
+        const real col[3] = {cd[3] + wxp[0], cd[4] + wxp[1], cd[5] + wxp[2]};
+        J[k] += sgn * dot3(dir, col);
       }
     } else {
       grp = grpg;
-      int P = T->geom_cpos[g];
-      for (int q = 0; q <= P; q++) {
-        int d = (q == 0) ? T->dof_base : chain_dof(T, grpg, q);
+      const int P = T->geom_cpos[g];
+      const int d0 = (grpg < 3) ? T->dof_f0[grpg] : T->dof_palm;
+#pragma unroll
+      for (int q = 0; q <= CL; q++) {
+        if (q > P) continue;
+        const int d = (q == 0) ? T->dof_base : d0 + q - 1;
         const real* cd = S.cdof[d];
         real wxp[3];
         cross3(wxp, cd, pos);
-        real col[3] = {cd[3] + wxp[0], cd[4] + wxp[1], cd[5] + wxp[2]};
-        real v = s * dot3(dir, col);
-        if (q == 0) J[6] += v; else J[6 + q] += v;
+        const real col[3] = {cd[3] + wxp[0], cd[4] + wxp[1], cd[5] + wxp[2]};
+        J[6 + q] += sgn * dot3(dir, col);
       }
     }
   }
@@ -1282,7 +1288,9 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
       for (int t = 0; t < CW; t++) J[t] = 0;
       int b = m->dof_body[d];
       grp = T->body_group[b];
-      J[6 + T->body_cpos[b]] = 1.0;
+      const int cpos = T->body_cpos[b];
+#pragma unroll
+      for (int q = 0; q <= CL; q++) J[6 + q] = (q == cpos) ? 1.0 : 0.0;
       pos = S.s.qpos[d] - S.s.lock_q[k];
     } else {
       int r = lane - nl;
@@ -1290,13 +1298,10 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
       const real* C = S.con[c];
       real Fr[9];
       make_frame(Fr, C + 4);
-      real Jn[CW], Jt[CW];
-      int g2;
-      contact_jac(S, m, T, c, Fr, Jn, grp);
-      contact_jac(S, m, T, c, Fr + 3 * (1 + (e >> 1)), Jt, g2);
-      real sgn = (e & 1) ? -1.0 : 1.0;
-      real mu = C[7];
-      for (int t = 0; t < CW; t++) J[t] = Jn[t] + sgn * mu * Jt[t];
+      const real smu = ((e & 1) ? -1.0 : 1.0) * C[7];
+      const real* t = Fr + 3 * (1 + (e >> 1));
+      const real dir[3] = {Fr[0] + smu * t[0], Fr[1] + smu * t[1], Fr[2] + smu * t[2]};
+      contact_jac(S, m, T, c, dir, J, grp);
       pos = C[0];
       is_contact = 1;
     }

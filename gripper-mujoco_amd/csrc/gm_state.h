@@ -95,4 +95,13 @@ struct GmTopo {
   int32_t geom_cpos[GM_MAX_GEOM];      // chain position of the geom's body (fingers / palm)
   int32_t body_group[GM_MAX_BODY];
   int32_t body_cpos[GM_MAX_BODY];
+  // per-dof constants folded on the host (one load level in the substep)
+  int32_t dof_body[GM_MAX_DOF];
+  int32_t dof_grp[GM_MAX_DOF];         // 0..2 finger, 3 palm, 4 base, 5 object
+  int32_t dof_p[GM_MAX_DOF];           // chain position (object: 0..5)
+  int32_t dof_target[GM_MAX_DOF];      // PD target: 0 none, 1 next.x, 2 next.th, 3 next.z, 4 base z
+  double dof_add[GM_MAX_DOF];          // armature + h (damping + kd) [+ h^2 (stiffness + kp)]
+  double dof_stiff[GM_MAX_DOF];        // 0 for the free joint
+  double dof_damp[GM_MAX_DOF];
+  double dof_kp[GM_MAX_DOF], dof_kd[GM_MAX_DOF];
 };

@@ -1867,20 +1867,6 @@ __device__ void monitor_sensors(SharedT<CL>& S, const gm_model* __restrict__ m, 
 // ============================================================ one full substep
 template <int CL>
 __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
-                                                     int lane, bool prof);
-// The substep is outlined (one copy, its own register allocation); address spaces are
-// re-established at its entry so the body keeps global loads for the model and LDS
-// instructions for the per-env image instead of generic (flat) accesses.
-template <int CL>
-__device__ __noinline__ void physics_substep(SharedT<CL>& S_, const gm_model* __restrict__ m_, const GmTopo* __restrict__ T_,
-                                             int lane, bool prof = false) {
-  SharedT<CL>& S = *(SharedT<CL>*)(__attribute__((address_space(3))) SharedT<CL>*)&S_;
-  const gm_model* m = (const gm_model*)(const __attribute__((address_space(1))) gm_model*)m_;
-  const GmTopo* T = (const GmTopo*)(const __attribute__((address_space(1))) GmTopo*)T_;
-  physics_substep_body<CL>(S, m, T, lane, prof);
-}
-template <int CL>
-__device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
                                                      int lane, bool prof) {
   unsigned long long t0 = prof ? clock64() : 0;
   if (lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
@@ -1902,6 +1888,22 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
   PH(7);
   integrate(S, m, T, lane);
   PH(8);
+}
+
+// All substeps of one env-step in one outlined call: one register allocation for the
+// substep loop, callee-saved registers spilled once per env-step (not per substep),
+// address spaces re-established at entry so the body uses global loads for the model
+// and LDS instructions for the per-env image instead of generic (flat) accesses.
+#define GM_AS_GLOBAL __attribute__((address_space(1)))
+#define GM_AS_LDS __attribute__((address_space(3)))
+// One substep, outlined: its own register allocation (the fused kernel around it keeps
+// the env-step epilogue's state), parameters typed with their address spaces so the body
+// issues global loads for the model and LDS instructions for the per-env image rather
+// than generic (flat) accesses that would serialise the two.
+template <int CL>
+__device__ __noinline__ void physics_substep(GM_AS_LDS SharedT<CL>* S_, const GM_AS_GLOBAL gm_model* m_,
+                                             const GM_AS_GLOBAL GmTopo* T_, int lane, bool prof) {
+  physics_substep_body<CL>(*(SharedT<CL>*)S_, (const gm_model*)m_, (const GmTopo*)T_, lane, prof);
 }
 
 // ============================================================ env-step epilogue (lane 0)
@@ -2234,7 +2236,8 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
   __syncthreads();
   const int nsub = settle ? 400 : (mode == 2) ? 1 : C->sim_steps_per_action + S.s.extra_substeps;
   for (int i = 0; i < nsub; i++) {
-    physics_substep<CL>(S, m, T, lane, prof);
+    physics_substep<CL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m, (const GM_AS_GLOBAL GmTopo*)T,
+                        lane, prof);
     unsigned long long t0 = prof ? clock64() : 0;
     update_all(S, m, T, lane);
     PH(9);

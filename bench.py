@@ -72,38 +72,61 @@ def load_traffic(n_envs: int):
     return None, None
 
 
-def obs_parity(gmx, n_envs: int = 4, n_steps: int = 12):
-    """obs max-rel-err of the GPU path vs the fp64 oracle (noise off, SURVEY.md 8d
-    definition: rel over |ref| >= 1e-3, abs elsewhere); small contact-free rollout."""
+def _rel_abs(obs, ref):
+    import numpy as np
+    ref = np.asarray(ref, dtype=np.float64)
+    d = np.abs(np.asarray(obs, dtype=np.float64) - ref)
+    big = np.abs(ref) >= 1e-3
+    rel = float((d[big] / np.abs(ref[big])).max()) if big.any() else 0.0
+    ab = float(d[~big].max()) if (~big).any() else 0.0
+    return rel, ab
+
+
+def obs_parity(gmx):
+    """obs max-rel-err of the GPU path vs the fp64 oracle (noise off; SURVEY.md 8d: rel
+    over |ref| >= 1e-3, abs elsewhere) on two probes: a 20-step contact-free rollout of
+    4 envs, and the first env-step of 3 envs closing on an object (contact-rich, from the
+    identical reset state; longer contact-rich rollouts separate chaotically)."""
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib
     s = gmx.canonical_settings(noise=False, seed=5)
-    env = gmx.BatchedGripperEnv(n_envs, object_set="set1_synthetic", settings=s, seed=5)
-    xs = np.linspace(0.06, 0.08, n_envs)
+    out = {}
+    # contact-free rollout
+    env = gmx.BatchedGripperEnv(4, object_set="set1_synthetic", settings=s, seed=5)
+    xs = np.array([0.055, 0.058, 0.06, 0.062])
     sp = env.make_spawn(x=xs, y=xs, idx=0)
     env.reset(spawn=sp)
-    oracles = []
-    for e in range(n_envs):
+    orc = []
+    for e in range(4):
         o = oracle_lib.OracleEnv(env.model, env.cfg, env.objects, e)
         o.reset(sp[e])
-        oracles.append(o)
+        orc.append(o)
     rng = np.random.default_rng(1234)
-    rel, ab = 0.0, 0.0
-    for _ in range(n_steps):
-        a = rng.uniform(-1, 1, size=(n_envs, env.n_actions)).astype(np.float32)
+    rel = ab = 0.0
+    for _ in range(20):
+        a = rng.uniform(-1, 1, size=(4, env.n_actions)).astype(np.float32)
         obs, _, _, _ = env.step(a)
-        for e in range(n_envs):
-            ref, _, _ = oracles[e].step(a[e])
-            ref = np.asarray(ref, dtype=np.float64)
-            d = np.abs(obs[e].astype(np.float64) - ref)
-            big = np.abs(ref) >= 1e-3
-            if big.any():
-                rel = max(rel, float((d[big] / np.abs(ref[big])).max()))
-            if (~big).any():
-                ab = max(ab, float(d[~big].max()))
+        for e in range(4):
+            r, b = _rel_abs(obs[e], orc[e].step(a[e])[0])
+            rel, ab = max(rel, r), max(ab, b)
     env.close()
-    return {"max_rel": rel, "max_abs_small": ab, "envs": n_envs, "steps": n_steps}
+    out["contact_free_rollout"] = {"max_rel": rel, "max_abs_small": ab, "envs": 4, "steps": 20}
+    # contact-rich first step
+    env = gmx.BatchedGripperEnv(3, object_set="set1_synthetic", settings=s, seed=5)
+    sp = env.make_spawn(x=0.0, y=0.0)
+    env.reset(spawn=sp)
+    a = np.array([[1.0, 0.0, 1.0, 0.5]] * 3, dtype=np.float32)
+    obs, _, _, _ = env.step(a)
+    rel = ab = 0.0
+    for e in range(3):
+        o = oracle_lib.OracleEnv(env.model, env.cfg, env.objects, e)
+        o.reset(sp[e])
+        r, b = _rel_abs(obs[e], o.step(a[e])[0])
+        rel, ab = max(rel, r), max(ab, b)
+    env.close()
+    out["contact_rich_first_step"] = {"max_rel": rel, "max_abs_small": ab, "envs": 3, "steps": 1}
+    return out
 
 
 def cpu_baseline(gmx, n_envs: int, n_steps: int):
@@ -222,7 +245,7 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
             "steps": K, "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f64+f32", "data": "synthetic",
+            "dtype": "f64", "data": "synthetic",
             "config": {"workload": "C3: set6_synthetic 20 mixed objects, randomised spawn, random "
                                    "actions U[-1,1]^4, canonical sensor/reward config, device auto-reset",
                        "envs_per_gpu": n, "global_envs": world * n, "substeps_per_env_step": S,
@@ -230,7 +253,7 @@ def main():
                        "B_substep_bytes": B["bytes"], "B_substep_ncon": B["ncon"], "B_substep_nefc": B["nefc"],
                        "model": {"nq": env.model.nq, "nv": env.model.nv, "nbody": env.model.nbody,
                                  "ngeom": env.model.ngeom, "nM": env.model.nM, "nlock": env.model.nlock},
-                       "dtype_detail": "dynamics f64, collision + PGS f32"},
+                       "dtype_detail": "f64 dynamics, collision and PGS; f32 sensor windows / observations (as the reference)"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "obs_max_rel_err": parity,

@@ -1408,11 +1408,12 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
         const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), r);
         const real delta = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
         res = fma(A[r], delta, res);
-        // lane == r, compared in place: the opaque scalar copy of r keeps the compiler
-        // from hoisting a 64-entry mask table out of the sweep loop (it would spill)
-        int rs;
-        asm volatile("s_mov_b32 %0, %1" : "=s"(rs) : "i"(r));
-        f = (lane == rs) ? fn : f;
+        // lane == r as a scalar one-hot mask built in place (s_bfm_b64, no VALU compare);
+        // the opaque asm keeps the compiler from hoisting a 64-entry mask table out of
+        // the sweep loop (it would spill)
+        unsigned long long onehot;
+        asm volatile("s_bfm_b64 %0, 1, %1" : "=s"(onehot) : "i"(r));
+        f = __builtin_amdgcn_inverse_ballot_w64(onehot) ? fn : f;
       }
     }
   }

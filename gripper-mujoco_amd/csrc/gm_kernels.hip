@@ -1382,32 +1382,46 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
   real R = (1 - imp) / imp * Ajj;
   if (R < 1e-15) R = 1e-15;
   const real arinv = 1.0 / (Ajj + R);   // mj_solPGS's ARinv
-  real res = (lane < nefc) ? (a0 - aref) : 0.0;   // (A f + b) with f = 0
-  real f = 0;
-  // projected Gauss-Seidel (mj_solPGS order: rows in sequence, fixed sweeps).  Lane j
-  // owns row j: its residual res_j = (A f + b)_j is kept current by every row update,
-  // each update f_r += d is broadcast with v_readlane.  Contact rows are clamped at 0
-  // (pyramid edges), lock rows are unbounded.
-  // Rows run in chunks of 8 with one (scalar) guard per chunk; rows past nefc inside the
-  // last chunk are exact no-ops (res = f = 0, arinv = 0, zero A entries => delta = 0).
-  const int nchunk = (__builtin_amdgcn_readfirstlane(nefc) + 7) >> 3;
+  // projected Gauss-Seidel (mj_solPGS order: rows in sequence, fixed sweeps, cold start).
+  // Lane j owns row j and keeps its unclamped Gauss-Seidel target current,
+  //   u_j = f_j - ARinv_j (AR f + b)_j,      AR = A + diag(R)  (mj_solPGS's efc_AR),
+  // so a row update is f_r <- max(u_r, lb_r) and every lane follows a change d of f_r
+  // with u_j -= (ARinv_j AR_jr) d.  The scaled column B_j[r] = ARinv_j AR_jr is built
+  // once per substep; B_r[r] = 0 exactly (ARinv_r AR_rr = 1 cancels the change of f_r),
+  // so the dependent chain per row is fma -> max -> sub -> readlane.  Each d is
+  // broadcast with v_readlane (no LDS, no reductions).  Contact rows (pyramid edges) are
+  // clamped at 0, lock rows are unbounded.  Rows run in chunks of 4 with one scalar
+  // guard per chunk; rows past nefc inside the last chunk are exact no-ops (u = f = 0,
+  // lb = 0, zero B entries => d = 0).
+  const int nchunk = (__builtin_amdgcn_readfirstlane(nefc) + 3) >> 2;
   const real lb = (is_contact || lane >= nefc) ? 0.0 : -__builtin_inf();
   const real arinv_l = (lane < nefc) ? arinv : 0.0;
+  real u = -(((lane < nefc) ? (a0 - aref) : 0.0) * arinv_l);   // f = 0: u = -ARinv b
+  real f = 0;
+#pragma unroll
+  for (int c = 0; c < GM_MAX_EFC / 4; c++) {
+    if (c >= nchunk) continue;
+#pragma unroll
+    for (int rr = 0; rr < 4; rr++) {
+      unsigned long long onehot;
+      asm volatile("s_bfm_b64 %0, 1, %1" : "=s"(onehot) : "i"(c * 4 + rr));
+      A[c * 4 + rr] = __builtin_amdgcn_inverse_ballot_w64(onehot) ? 0.0 : A[c * 4 + rr] * arinv_l;
+    }
+  }
   for (int it = 0; it < m->pgs_iterations; it++) {
 #pragma unroll
-    for (int c = 0; c < GM_MAX_EFC / 8; c++) {
+    for (int c = 0; c < GM_MAX_EFC / 4; c++) {
       if (c >= nchunk) continue;
 #pragma unroll
-      for (int rr = 0; rr < 8; rr++) {
-        const int r = c * 8 + rr;
-        const real g = fma(R, f, res);
-        const real fn = fmax(fma(-g, arinv_l, f), lb);
+      for (int rr = 0; rr < 4; rr++) {
+        const int r = c * 4 + rr;
+        const real fn = fmax(u, lb);
         const real dl = fn - f;
         const long long bits = __double_as_longlong(dl);
         const int lo = __builtin_amdgcn_readlane((int)bits, r);
         const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), r);
         const real delta = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-        res = fma(A[r], delta, res);
+        u = fma(-A[r], delta, u);
         // lane == r as a scalar one-hot mask built in place (s_bfm_b64, no VALU compare);
         // the opaque asm keeps the compiler from hoisting a 64-entry mask table out of
         // the sweep loop (it would spill)

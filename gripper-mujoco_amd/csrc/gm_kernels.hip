@@ -856,7 +856,7 @@ __device__ __forceinline__ int plane_cyl_point(const GeomV& P, const GeomV& Cy, 
   for (int t = 0; t < 3; t++) { h.pos[t] = v[t] - 0.5 * d * nz[t]; h.n[t] = nz[t]; }
   return 1;
 }
-__device__ int plane_sphere(const GeomV& P, const GeomV& Sp, Hit& h) {
+__device__ __forceinline__ int plane_sphere(const GeomV& P, const GeomV& Sp, Hit& h) {
   real nz[3] = {P.R[2], P.R[5], P.R[8]};
   real r = Sp.size[0];
   real dv[3] = {Sp.c[0] - P.c[0], Sp.c[1] - P.c[1], Sp.c[2] - P.c[2]};
@@ -866,7 +866,7 @@ __device__ int plane_sphere(const GeomV& P, const GeomV& Sp, Hit& h) {
   for (int k = 0; k < 3; k++) { h.pos[k] = Sp.c[k] - nz[k] * (r + 0.5 * dist); h.n[k] = nz[k]; }
   return 1;
 }
-__device__ int sphere_box(const GeomV& Sp, const GeomV& B, Hit& h) {
+__device__ __forceinline__ int sphere_box(const GeomV& Sp, const GeomV& B, Hit& h) {
   const real* R = B.R;
   const real* hs = B.size;
   real r = Sp.size[0];
@@ -893,10 +893,15 @@ __device__ int sphere_box(const GeomV& Sp, const GeomV& B, Hit& h) {
     int kmin = 0;
     real best = hs[0] - fabs(cl[0]);
     for (int k = 1; k < 3; k++) { real v = hs[k] - fabs(cl[k]); if (v < best) { best = v; kmin = k; } }
-    real sg = cl[kmin] >= 0 ? 1.0 : -1.0;
-    nl[0] = nl[1] = nl[2] = 0; nl[kmin] = -sg;
+    const real clk = kmin == 0 ? cl[0] : (kmin == 1 ? cl[1] : cl[2]);
+    const real hsk = kmin == 0 ? hs[0] : (kmin == 1 ? hs[1] : hs[2]);
+    real sg = clk >= 0 ? 1.0 : -1.0;
     dist = -(best + r);
-    ql[0] = cl[0]; ql[1] = cl[1]; ql[2] = cl[2]; ql[kmin] = sg * hs[kmin];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      nl[k] = (k == kmin) ? -sg : 0.0;
+      ql[k] = (k == kmin) ? sg * hsk : cl[k];
+    }
   }
   real n[3], qw[3];
   mulmv3(n, R, nl);
@@ -941,31 +946,41 @@ __device__ __forceinline__ void normalize3(real* d) {
   real l = sqrt(dot3(d, d));
   if (l > 0) { real il = 1.0 / l; d[0] *= il; d[1] *= il; d[2] *= il; }
 }
-__device__ void portal_dir(const SV* P, real* dir) {
-  real a[3] = {P[2].v[0] - P[1].v[0], P[2].v[1] - P[1].v[1], P[2].v[2] - P[1].v[2]};
-  real b[3] = {P[3].v[0] - P[1].v[0], P[3].v[1] - P[1].v[1], P[3].v[2] - P[1].v[2]};
+// The simplex vertices are four named values (not an array), conditional vertex copies
+// are per-component selects and every helper is inlined, so the whole MPR state stays in
+// VGPRs (an indexable array, or a branch between whole-struct copies, goes to scratch).
+__device__ __forceinline__ void sv_take(SV& dst, const SV& src, bool c) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    dst.v[k] = c ? src.v[k] : dst.v[k];
+    dst.p1[k] = c ? src.p1[k] : dst.p1[k];
+    dst.p2[k] = c ? src.p2[k] : dst.p2[k];
+  }
+}
+__device__ __forceinline__ void portal_dir(const SV& P1, const SV& P2, const SV& P3, real* dir) {
+  real a[3] = {P2.v[0] - P1.v[0], P2.v[1] - P1.v[1], P2.v[2] - P1.v[2]};
+  real b[3] = {P3.v[0] - P1.v[0], P3.v[1] - P1.v[1], P3.v[2] - P1.v[2]};
   cross3(dir, a, b);
   normalize3(dir);
 }
-__device__ void expand_portal(SV* P, const SV& v4) {
+__device__ __forceinline__ void expand_portal(const SV& P0, SV& P1, SV& P2, SV& P3, const SV& v4) {
   real v4v0[3];
-  cross3(v4v0, v4.v, P[0].v);
-  real d = dot3(P[1].v, v4v0);
-  if (d > 0) {
-    d = dot3(P[2].v, v4v0);
-    if (d > 0) P[1] = v4; else P[3] = v4;
-  } else {
-    d = dot3(P[3].v, v4v0);
-    if (d > 0) P[2] = v4; else P[1] = v4;
-  }
+  cross3(v4v0, v4.v, P0.v);
+  const bool s1 = dot3(P1.v, v4v0) > 0;
+  const bool s2 = dot3(P2.v, v4v0) > 0;
+  const bool s3 = dot3(P3.v, v4v0) > 0;
+  // d1 > 0: (d2 > 0 ? P1 : P3) = v4;  else: (d3 > 0 ? P2 : P1) = v4
+  sv_take(P1, v4, s1 ? s2 : !s3);
+  sv_take(P2, v4, !s1 && s3);
+  sv_take(P3, v4, s1 && !s2);
 }
-__device__ int reach_tol(const SV* P, const SV& v4, const real* dir, real tol) {
-  real dv1 = dot3(P[1].v, dir), dv2 = dot3(P[2].v, dir), dv3 = dot3(P[3].v, dir), dv4 = dot3(v4.v, dir);
+__device__ __forceinline__ int reach_tol(const SV& P1, const SV& P2, const SV& P3, const SV& v4, const real* dir, real tol) {
+  real dv1 = dot3(P1.v, dir), dv2 = dot3(P2.v, dir), dv3 = dot3(P3.v, dir), dv4 = dot3(v4.v, dir);
   real d1 = dv4 - dv1, d2 = dv4 - dv2, d3 = dv4 - dv3;
   real dd = fmin(fmin(d1, d2), d3);
   return dd < tol || fabs(dd - tol) < 1e-12;
 }
-__device__ void tri_closest_origin(const real* a, const real* b, const real* c, real* out) {
+__device__ __forceinline__ void tri_closest_origin(const real* a, const real* b, const real* c, real* out) {
   real ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
   real ac[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
   real ap[3] = {-a[0], -a[1], -a[2]};
@@ -991,100 +1006,107 @@ __device__ void tri_closest_origin(const real* a, const real* b, const real* c, 
   real v = vb * den, w = vc * den;
   for (int k = 0; k < 3; k++) out[k] = a[k] + ab[k] * v + ac[k] * w;
 }
-__device__ void mpr_pos(const SV* P, real* pos) {
+__device__ __forceinline__ void mpr_pos(const SV& P0, const SV& P1, const SV& P2, const SV& P3, real* pos) {
   real dir[3];
-  portal_dir(P, dir);
+  portal_dir(P1, P2, P3, dir);
   real t[3];
-  cross3(t, P[1].v, P[2].v); real b0 = dot3(t, P[3].v);
-  cross3(t, P[3].v, P[2].v); real b1 = dot3(t, P[0].v);
-  cross3(t, P[0].v, P[1].v); real b2 = dot3(t, P[3].v);
-  cross3(t, P[2].v, P[1].v); real b3 = dot3(t, P[0].v);
+  cross3(t, P1.v, P2.v); real b0 = dot3(t, P3.v);
+  cross3(t, P3.v, P2.v); real b1 = dot3(t, P0.v);
+  cross3(t, P0.v, P1.v); real b2 = dot3(t, P3.v);
+  cross3(t, P2.v, P1.v); real b3 = dot3(t, P0.v);
   real sum = b0 + b1 + b2 + b3;
   if (sum <= 0) {
     b0 = 0;
-    cross3(t, P[2].v, P[3].v); b1 = dot3(t, dir);
-    cross3(t, P[3].v, P[1].v); b2 = dot3(t, dir);
-    cross3(t, P[1].v, P[2].v); b3 = dot3(t, dir);
+    cross3(t, P2.v, P3.v); b1 = dot3(t, dir);
+    cross3(t, P3.v, P1.v); b2 = dot3(t, dir);
+    cross3(t, P1.v, P2.v); b3 = dot3(t, dir);
     sum = b1 + b2 + b3;
   }
   real inv = 1.0 / sum;
-  real bb[4] = {b0, b1, b2, b3};
   real p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
-  for (int i = 0; i < 4; i++)
-    for (int k = 0; k < 3; k++) { p1[k] += bb[i] * P[i].p1[k]; p2[k] += bb[i] * P[i].p2[k]; }
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    p1[k] += b0 * P0.p1[k]; p2[k] += b0 * P0.p2[k];
+    p1[k] += b1 * P1.p1[k]; p2[k] += b1 * P1.p2[k];
+    p1[k] += b2 * P2.p1[k]; p2[k] += b2 * P2.p2[k];
+    p1[k] += b3 * P3.p1[k]; p2[k] += b3 * P3.p2[k];
+  }
   for (int k = 0; k < 3; k++) pos[k] = 0.5 * (p1[k] + p2[k]) * inv;
 }
-__device__ int mpr(const GeomV& A, const GeomV& B, real tol, int maxit, Hit& h) {
-  SV P[4];
-  for (int k = 0; k < 3; k++) { P[0].v[k] = A.c[k] - B.c[k]; P[0].p1[k] = A.c[k]; P[0].p2[k] = B.c[k]; }
-  if (fzero(P[0].v[0]) && fzero(P[0].v[1]) && fzero(P[0].v[2])) P[0].v[0] += 1e-5;
-  real d[3] = {-P[0].v[0], -P[0].v[1], -P[0].v[2]};
+__device__ __forceinline__ int mpr(const GeomV& A, const GeomV& B, real tol, int maxit, Hit& h) {
+  SV P0, P1, P2, P3;
+  for (int k = 0; k < 3; k++) { P0.v[k] = A.c[k] - B.c[k]; P0.p1[k] = A.c[k]; P0.p2[k] = B.c[k]; }
+  if (fzero(P0.v[0]) && fzero(P0.v[1]) && fzero(P0.v[2])) P0.v[0] += 1e-5;
+  real d[3] = {-P0.v[0], -P0.v[1], -P0.v[2]};
   normalize3(d);
-  mpr_support(A, B, d, P[1]);
-  if (dot3(P[1].v, d) <= 0) return 0;
-  cross3(d, P[0].v, P[1].v);
+  mpr_support(A, B, d, P1);
+  if (dot3(P1.v, d) <= 0) return 0;
+  cross3(d, P0.v, P1.v);
   if (fzero(sqrt(dot3(d, d)))) {
-    real l1 = sqrt(dot3(P[1].v, P[1].v));
+    real l1 = sqrt(dot3(P1.v, P1.v));
     if (fzero(l1)) return 0;
     h.dist = -l1;
     real il = 1.0 / l1;
-    for (int k = 0; k < 3; k++) { h.n[k] = P[1].v[k] * il; h.pos[k] = 0.5 * (P[1].p1[k] + P[1].p2[k]); }
+    for (int k = 0; k < 3; k++) { h.n[k] = P1.v[k] * il; h.pos[k] = 0.5 * (P1.p1[k] + P1.p2[k]); }
     return 1;
   }
   normalize3(d);
-  mpr_support(A, B, d, P[2]);
-  if (dot3(P[2].v, d) <= 0) return 0;
+  mpr_support(A, B, d, P2);
+  if (dot3(P2.v, d) <= 0) return 0;
   real va[3], vb[3];
-  for (int k = 0; k < 3; k++) { va[k] = P[1].v[k] - P[0].v[k]; vb[k] = P[2].v[k] - P[0].v[k]; }
+  for (int k = 0; k < 3; k++) { va[k] = P1.v[k] - P0.v[k]; vb[k] = P2.v[k] - P0.v[k]; }
   cross3(d, va, vb);
   normalize3(d);
-  if (dot3(d, P[0].v) > 0) { SV t = P[1]; P[1] = P[2]; P[2] = t; d[0] = -d[0]; d[1] = -d[1]; d[2] = -d[2]; }
+  if (dot3(d, P0.v) > 0) {
+    const SV t = P1;
+    sv_take(P1, P2, true); sv_take(P2, t, true);
+    d[0] = -d[0]; d[1] = -d[1]; d[2] = -d[2];
+  }
   int it = 0;
   for (;;) {
-    mpr_support(A, B, d, P[3]);
-    if (dot3(P[3].v, d) <= 0) return 0;
-    int cont = 0;
-    cross3(va, P[1].v, P[3].v);
-    if (dot3(va, P[0].v) < -1e-12) { P[2] = P[3]; cont = 1; }
-    if (!cont) {
-      cross3(va, P[3].v, P[2].v);
-      if (dot3(va, P[0].v) < -1e-12) { P[1] = P[3]; cont = 1; }
-    }
-    if (!cont) break;
-    for (int k = 0; k < 3; k++) { va[k] = P[1].v[k] - P[0].v[k]; vb[k] = P[2].v[k] - P[0].v[k]; }
+    mpr_support(A, B, d, P3);
+    if (dot3(P3.v, d) <= 0) return 0;
+    cross3(va, P1.v, P3.v);
+    const bool c2 = dot3(va, P0.v) < -1e-12;
+    cross3(va, P3.v, P2.v);
+    const bool c1 = !c2 && dot3(va, P0.v) < -1e-12;
+    sv_take(P2, P3, c2);
+    sv_take(P1, P3, c1);
+    if (!(c1 || c2)) break;
+    for (int k = 0; k < 3; k++) { va[k] = P1.v[k] - P0.v[k]; vb[k] = P2.v[k] - P0.v[k]; }
     cross3(d, va, vb);
     normalize3(d);
     if (++it > maxit) return 0;
   }
   it = 0;
   for (;;) {
-    portal_dir(P, d);
-    if (dot3(d, P[1].v) >= -1e-12) break;
+    portal_dir(P1, P2, P3, d);
+    if (dot3(d, P1.v) >= -1e-12) break;
     SV v4;
     mpr_support(A, B, d, v4);
     real dv4 = dot3(v4.v, d);
     if (!(fzero(dv4) || dv4 > 0)) return 0;
-    if (reach_tol(P, v4, d, tol)) return 0;
-    expand_portal(P, v4);
+    if (reach_tol(P1, P2, P3, v4, d, tol)) return 0;
+    expand_portal(P0, P1, P2, P3, v4);
     if (++it > maxit) return 0;
   }
   it = 0;
   for (;;) {
-    portal_dir(P, d);
+    portal_dir(P1, P2, P3, d);
     SV v4;
     mpr_support(A, B, d, v4);
-    if (reach_tol(P, v4, d, tol) || it > maxit) {
+    if (reach_tol(P1, P2, P3, v4, d, tol) || it > maxit) {
       real cp[3];
-      tri_closest_origin(P[1].v, P[2].v, P[3].v, cp);
+      tri_closest_origin(P1.v, P2.v, P3.v, cp);
       real depth = sqrt(dot3(cp, cp));
       if (fzero(depth)) return 0;
       h.dist = -depth;
       real id = 1.0 / depth;
       h.n[0] = cp[0] * id; h.n[1] = cp[1] * id; h.n[2] = cp[2] * id;
-      mpr_pos(P, h.pos);
+      mpr_pos(P0, P1, P2, P3, h.pos);
       return depth > 0;
     }
-    expand_portal(P, v4);
+    expand_portal(P0, P1, P2, P3, v4);
     it++;
   }
 }
@@ -1254,7 +1276,7 @@ __device__ __forceinline__ real row_dot_dofs(SharedT<CL>& S, const GmTopo* __res
   return acc;
 }
 
-__device__ real impedance(const gm_model* __restrict__ m, real r) {
+__device__ __forceinline__ real impedance(const gm_model* __restrict__ m, real r) {
   real dmin = m->solimp[0], dmax = m->solimp[1], width = m->solimp[2];
   real mid = m->solimp[3], pw = m->solimp[4];
   if (dmin == dmax || width <= 1e-15) return dmin;
@@ -2248,12 +2270,15 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
   const bool settle = (mode == 1);          // calibrate_reset settle: 400 substeps, no sensors
   const bool prof = !settle && dbg.phase != nullptr;
   if (prof && lane < GM_NPHASE) S.tph[lane] = 0;
+  const unsigned long long t_kernel = prof ? clock64() : 0;
   __syncthreads();
   const int nsub = settle ? 400 : (mode == 2) ? 1 : C->sim_steps_per_action + S.s.extra_substeps;
   for (int i = 0; i < nsub; i++) {
+    const unsigned long long tc = prof ? clock64() : 0;
     physics_substep<CL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m, (const GM_AS_GLOBAL GmTopo*)T,
                         lane, prof);
     unsigned long long t0 = prof ? clock64() : 0;
+    if (prof && lane == 0) S.tph[22] += t0 - tc;   // whole outlined call (phases 0-8 + call overhead)
     update_all(S, m, T, lane);
     PH(9);
     if (!settle) monitor_sensors<CL>(S, m, C, T, lane);
@@ -2304,6 +2329,7 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
     PH(21);
   }
   if (prof) {
+    if (lane == 0) S.tph[23] = clock64() - t_kernel;   // whole env-step on this wave
     __syncthreads();
     if (lane < GM_NPHASE) dbg.phase[(size_t)env * GM_NPHASE + lane] = S.tph[lane];
   }

@@ -24,5 +24,7 @@ for k, name in enumerate(env.PHASES):
         print(f"  {name:18s} {tot[k]:10.0f} cyc/env-step  (= {tot[k]/63:.0f} per substep)")
     else:
         print(f"  {name:18s} {tot[k]/63:10.0f} cyc/substep  {100*tot[k]/allc:5.1f}%")
+print(f"  outlined-call overhead {(tot[22] - tot[:9].sum())/63:10.0f} cyc/substep (prologue/epilogue, CSR save/restore)")
+print(f"  whole env-step on one wave {tot[23]:.3e} cyc (phases account for {100*(tot[:11].sum()+tot[18:22].sum())/max(tot[23],1):.1f}%)")
 ncon, _, _, _ = env.debug_substep()
 print("ncon per env: mean %.2f  max %d  histogram %s" % (ncon.mean(), ncon.max(), np.bincount(ncon, minlength=16).tolist()))

@@ -113,6 +113,14 @@ int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
     if (m.body_group[b] >= 0 && m.body_group[b] < 3) T.body_cpos[b] = b - T.body_f0[m.body_group[b]] + 1;
     else if (m.body_group[b] == GM_GRP_PALM) T.body_cpos[b] = 1;
   }
+  for (int l = 0; l < 64; l++) T.lane_body[l] = -1;
+  if (T.CL > 15) { err = "finger chain longer than a 16-lane DPP row"; return GM_E_RANGE; }
+  for (int f = 0; f < 3; f++)
+    for (int p = 1; p <= T.CL; p++) T.lane_body[16 * f + p] = T.body_f0[f] + p - 1;
+  T.lane_base = 48;
+  T.lane_body[48] = T.body_base;
+  T.lane_body[49] = T.body_palm;
+  T.lane_body[50] = T.body_obj;
   // per-dof constants: the engine-spec H~ diagonal additions and PD gains
   // (mj_step2 implicit terms and luke::control gains, oracle.c ctrl_gains / step2)
   const double h = m.timestep;

@@ -193,6 +193,41 @@ __device__ __forceinline__ void body_R(const SharedT<CL>& S, int b, real* R) {
 struct Pose { real p[3], q[4], R[9]; };
 
 
+// Segmented-scan shuffles inside a 16-lane DPP row (chains live on the scan lanes of
+// GmTopo::lane_body): row_shr / row_shl by a compile-time distance, 0 shifted in at the
+// row edge.  A VALU op with a DPP modifier, no LDS round trip (ds_bpermute).
+template <int CTRL>
+__device__ __forceinline__ real dpp_move(real x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// value from the lane `off` positions lower in the row (off in 1, 2, 4, 8)
+__device__ __forceinline__ real row_shr(real x, int off) {
+  switch (off) {
+    case 1: return dpp_move<0x111>(x);
+    case 2: return dpp_move<0x112>(x);
+    case 4: return dpp_move<0x114>(x);
+    default: return dpp_move<0x118>(x);
+  }
+}
+// value from the lane `off` positions higher in the row
+__device__ __forceinline__ real row_shl(real x, int off) {
+  switch (off) {
+    case 1: return dpp_move<0x101>(x);
+    case 2: return dpp_move<0x102>(x);
+    case 4: return dpp_move<0x104>(x);
+    default: return dpp_move<0x108>(x);
+  }
+}
+__device__ __forceinline__ real readlane_real(real x, int l) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 template <int CL>
 __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                            bool prof = false) {
@@ -201,8 +236,8 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
   //    slide  p = bpos + R(bquat) axis q,  quat = bquat
   //    hinge  p = bpos,                    quat = bquat (x) (cos q/2, axis sin q/2)
   real lp[3] = {0, 0, 0}, lq[4] = {1, 0, 0, 0};
-  if (lane < T->nbody && lane > 0) {
-    const int b = lane;
+  const int b = T->lane_body[lane];   // scan-lane layout (GmTopo::lane_body)
+  if (b > 0) {
     ld3(lp, m->body_pos[b]);
     ld4(lq, m->body_quat[b]);
     const int j = m->body_jnt[b];
@@ -231,24 +266,25 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
   // pose is applied and the orientation renormalised.
   {
     const int bb = T->body_base;
+    const int lb = T->lane_base;
     real bpos[3], bq[4];
 #pragma unroll
-    for (int k = 0; k < 3; k++) bpos[k] = __shfl(lp[k], bb);
+    for (int k = 0; k < 3; k++) bpos[k] = readlane_real(lp[k], lb);
 #pragma unroll
-    for (int k = 0; k < 4; k++) bq[k] = __shfl(lq[k], bb);
+    for (int k = 0; k < 4; k++) bq[k] = readlane_real(lq[k], lb);
     quatnorm(bq);
     real bR[9];
     quat2mat(bR, bq);
-    const int grp = (lane < T->nbody) ? T->body_group[lane] : -1;
+    const int grp = (b >= 0) ? T->body_group[b] : -1;
     const bool chain = grp >= 0 && grp <= 3;
-    const int p = chain ? T->body_cpos[lane] : 0;
+    const int p = chain ? T->body_cpos[b] : 0;
 #pragma unroll
     for (int off = 1; off < CL; off <<= 1) {
       real np[3], nq[4];
 #pragma unroll
-      for (int k = 0; k < 3; k++) np[k] = __shfl_up(lp[k], off);
+      for (int k = 0; k < 3; k++) np[k] = row_shr(lp[k], off);
 #pragma unroll
-      for (int k = 0; k < 4; k++) nq[k] = __shfl_up(lq[k], off);
+      for (int k = 0; k < 4; k++) nq[k] = row_shr(lq[k], off);
       if (p > off) {
         real R[9], t[3], q[4];
         quat2mat(R, nq);
@@ -263,21 +299,21 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
       mulmv3(t, bR, lp);
       quatmul(q, bq, lq);
       quatnorm(q);
-      S.xpos[lane][0] = bpos[0] + t[0]; S.xpos[lane][1] = bpos[1] + t[1]; S.xpos[lane][2] = bpos[2] + t[2];
+      S.xpos[b][0] = bpos[0] + t[0]; S.xpos[b][1] = bpos[1] + t[1]; S.xpos[b][2] = bpos[2] + t[2];
 #pragma unroll
-      for (int k = 0; k < 4; k++) S.xquat[lane][k] = q[k];
-    } else if (lane == bb) {
+      for (int k = 0; k < 4; k++) S.xquat[b][k] = q[k];
+    } else if (b == bb) {
       S.xpos[bb][0] = bpos[0]; S.xpos[bb][1] = bpos[1]; S.xpos[bb][2] = bpos[2];
 #pragma unroll
       for (int k = 0; k < 4; k++) S.xquat[bb][k] = bq[k];
-    } else if (lane == T->body_obj) {
+    } else if (b == T->body_obj) {
       // object: free joint, pose straight from qpos
       const int qa = T->qadr_obj;
       real q[4] = {S.s.qpos[qa + 3], S.s.qpos[qa + 4], S.s.qpos[qa + 5], S.s.qpos[qa + 6]};
       quatnorm(q);
-      S.xpos[lane][0] = S.s.qpos[qa]; S.xpos[lane][1] = S.s.qpos[qa + 1]; S.xpos[lane][2] = S.s.qpos[qa + 2];
+      S.xpos[b][0] = S.s.qpos[qa]; S.xpos[b][1] = S.s.qpos[qa + 1]; S.xpos[b][2] = S.s.qpos[qa + 2];
 #pragma unroll
-      for (int k = 0; k < 4; k++) S.xquat[lane][k] = q[k];
+      for (int k = 0; k < 4; k++) S.xquat[b][k] = q[k];
     }
   }
   __syncthreads();
@@ -408,8 +444,8 @@ __device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const Gm
   for (int k = 0; k < 6; k++) { cvb[k] = S.cdof[db][k] * qdb; cab[k] = 0; }
   cab[3] = -(real)m->gravity[0]; cab[4] = -(real)m->gravity[1]; cab[5] = -(real)m->gravity[2];
 
-  const int b = lane;
-  const int grp = (b < T->nbody) ? T->body_group[b] : -1;
+  const int b = T->lane_body[lane];   // scan-lane layout (GmTopo::lane_body)
+  const int grp = (b >= 0) ? T->body_group[b] : -1;
   const bool chain = grp >= 0 && grp <= 3;
   const int p = chain ? T->body_cpos[b] : 0;
   const int Lc = (grp == 3) ? 1 : CL;
@@ -426,14 +462,14 @@ __device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const Gm
   for (int off = 1; off < CL; off <<= 1) {
 #pragma unroll
     for (int k = 0; k < 6; k++) {
-      const real nb = __shfl_up(cv[k], off);
+      const real nb = row_shr(cv[k], off);
       if (p > off) cv[k] += nb;
     }
   }
   real cvp[6];
 #pragma unroll
   for (int k = 0; k < 6; k++) {
-    const real nb = __shfl_up(cv[k], 1);
+    const real nb = row_shr(cv[k], 1);
     cvp[k] = cvb[k] + (p > 1 ? nb : 0.0);
     cv[k] += cvb[k];
   }
@@ -446,7 +482,7 @@ __device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const Gm
   for (int off = 1; off < CL; off <<= 1) {
 #pragma unroll
     for (int k = 0; k < 6; k++) {
-      const real nb = __shfl_up(ca[k], off);
+      const real nb = row_shr(ca[k], off);
       if (p > off) ca[k] += nb;
     }
   }
@@ -468,12 +504,12 @@ __device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const Gm
   for (int off = 1; off < CL; off <<= 1) {
 #pragma unroll
     for (int k = 0; k < 6; k++) {
-      const real nb = __shfl_down(f[k], off);
+      const real nb = row_shl(f[k], off);
       if (p + off <= Lc) f[k] += nb;
     }
 #pragma unroll
     for (int k = 0; k < 10; k++) {
-      const real nb = __shfl_down(ci[k], off);
+      const real nb = row_shl(ci[k], off);
       if (p + off <= Lc) ci[k] += nb;
     }
   }

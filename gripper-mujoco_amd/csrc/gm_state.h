@@ -95,6 +95,11 @@ struct GmTopo {
   int32_t geom_cpos[GM_MAX_GEOM];      // chain position of the geom's body (fingers / palm)
   int32_t body_group[GM_MAX_BODY];
   int32_t body_cpos[GM_MAX_BODY];
+  // scan lanes: finger f's chain position p (1..CL) sits on lane 16 f + p, so a chain
+  // lies inside one 16-lane DPP row; row 3 holds the base (48), palm (49, position 1)
+  // and object (50).  -1: no body on that lane.
+  int32_t lane_body[64];
+  int32_t lane_base;
   // per-dof constants folded on the host (one load level in the substep)
   int32_t dof_body[GM_MAX_DOF];
   int32_t dof_grp[GM_MAX_DOF];         // 0..2 finger, 3 palm, 4 base, 5 object

@@ -221,6 +221,28 @@ __device__ __forceinline__ real row_shl(real x, int off) {
     default: return dpp_move<0x108>(x);
   }
 }
+// value of position k of this lane's 16-lane DPP row (row_newbcast:k), k compile-time
+// after unrolling
+__device__ __forceinline__ real row_bcast(real x, int k) {
+  switch (k) {
+    case 0: return dpp_move<0x150>(x);
+    case 1: return dpp_move<0x151>(x);
+    case 2: return dpp_move<0x152>(x);
+    case 3: return dpp_move<0x153>(x);
+    case 4: return dpp_move<0x154>(x);
+    case 5: return dpp_move<0x155>(x);
+    case 6: return dpp_move<0x156>(x);
+    case 7: return dpp_move<0x157>(x);
+    case 8: return dpp_move<0x158>(x);
+    case 9: return dpp_move<0x159>(x);
+    case 10: return dpp_move<0x15A>(x);
+    case 11: return dpp_move<0x15B>(x);
+    case 12: return dpp_move<0x15C>(x);
+    case 13: return dpp_move<0x15D>(x);
+    case 14: return dpp_move<0x15E>(x);
+    default: return dpp_move<0x15F>(x);
+  }
+}
 __device__ __forceinline__ real readlane_real(real x, int l) {
   const long long b = __double_as_longlong(x);
   const int lo = __builtin_amdgcn_readlane((int)b, l);
@@ -646,149 +668,150 @@ __device__ void mass_and_forces(SharedT<CL>& S, const gm_model* __restrict__ m, 
 }
 
 // ============================================================ LTDL factor + solves
-// Tree LTDL of H~ (mj_factorM restated for the canonical tree): each chain block is
-// factored leaves -> root in registers (chain length CL is a compile-time constant so
-// the block never leaves VGPRs); the chains' contributions to the shared base pivot
-// are summed afterwards.
-template <int L>
-__device__ __forceinline__ void factor_chain(real* __restrict__ Hs, real& delta_out, real* __restrict__ Dout) {
-  real H[(L + 1) * (L + 2) / 2];
-#pragma unroll
-  for (int p = 1; p <= L; p++)
-#pragma unroll
-    for (int q = 0; q <= p; q++) H[TRI(p, q)] = Hs[TRI(p, q)];
-  real delta = 0;
-#pragma unroll
-  for (int k = L; k >= 1; k--) {
-    const real ihk = 1.0 / H[TRI(k, k)];
-#pragma unroll
-    for (int i = k - 1; i >= 0; i--) {
-      const real a = H[TRI(k, i)] * ihk;
-#pragma unroll
-      for (int jj = i; jj >= 0; jj--) {
-        const real v = H[TRI(k, jj)] * a;
-        if (i == 0 && jj == 0) delta += v; else H[TRI(i, jj)] -= v;
-      }
-      H[TRI(k, i)] = a;
-    }
-  }
-#pragma unroll
-  for (int p = 1; p <= L; p++) {
-#pragma unroll
-    for (int q = 0; q < p; q++) Hs[TRI(p, q)] = H[TRI(p, q)];
-    Hs[TRI(p, p)] = H[TRI(p, p)];
-    Dout[p] = 1.0 / H[TRI(p, p)];
-  }
-  delta_out = delta;
-}
-
+// Tree LTDL of H~ (mj_factorM restated for the canonical tree) on the DPP-row layout:
+// DPP rows 0..2 hold the three finger blocks (base + chain) -- lane 16 f + p holds the
+// symmetric row p of finger f's block, p = 0 being the base column -- and lanes 48..53
+// the free object's 6x6 block.  The palm's 1-dof chain is done by lane 63 alone.  The
+// chains meet only in the base pivot: each finger / palm block returns its Schur
+// contribution (bdelta) and the base pivot is formed afterwards.
+// Factor: pivots k = CL..1 (object: 5..1); the pivot row is broadcast inside every DPP
+// row with row_newbcast:k and each lane p < k eliminates with its own (upper) element.
 template <int CL>
 __device__ void factor(SharedT<CL>& S, const GmTopo* __restrict__ T, int lane) {
-  if (lane < 3) {
-    factor_chain<CL>(S.Hf[lane], S.bdelta[lane], S.Df[lane]);
-  } else if (lane == 3) {
-    factor_chain<1>(S.Hp, S.bdelta[3], S.Dp);
-  } else if (lane == 4) {
-    real H[21];
+  const int rowf = lane >> 4, p = lane & 15;
+  const bool fing = rowf < 3 && p <= CL;
+  const bool obj = rowf == 3 && p < 6;
+  real h[CL + 1];
 #pragma unroll
-    for (int i = 0; i < 21; i++) H[i] = S.Ho[i];
-#pragma unroll
-    for (int k = 5; k >= 1; k--) {
-      const real ihk = 1.0 / H[TRI(k, k)];
-#pragma unroll
-      for (int i = k - 1; i >= 0; i--) {
-        const real a = H[TRI(k, i)] * ihk;
-#pragma unroll
-        for (int jj = i; jj >= 0; jj--) H[TRI(i, jj)] -= H[TRI(k, jj)] * a;
-        H[TRI(k, i)] = a;
-      }
+  for (int j = 0; j <= CL; j++) {
+    const int lo = p < j ? p : j, hi = p < j ? j : p;
+    real v = 0;
+    if (fing) {
+      if (hi > 0) v = S.Hf[rowf][TRI(hi, lo)];   // (0, 0) is the base pivot: not in the block
+    } else if (obj) {
+      if (j < 6) v = S.Ho[TRI(hi, lo)];
     }
+    h[j] = v;
+  }
 #pragma unroll
-    for (int i = 0; i < 21; i++) S.Ho[i] = H[i];
+  for (int k = CL; k >= 1; k--) {
+    const bool act = fing || (obj && k <= 5);
+    const real hkk = row_bcast(h[k], k);
+    const real ihk = 1.0 / hkk;
+    const real a = h[k] * ihk;             // L[k][p] for p < k
+    real hk[CL];
 #pragma unroll
-    for (int p = 0; p < 6; p++) S.Do[p] = 1.0 / H[TRI(p, p)];
+    for (int j = 0; j < k; j++) hk[j] = row_bcast(h[j], k);
+    if (act && p < k) {
+#pragma unroll
+      for (int j = 0; j < k; j++) h[j] -= hk[j] * a;
+      h[k] = a;
+    }
+    if (act && p == k) {
+#pragma unroll
+      for (int j = 0; j < k; j++) h[j] *= ihk;   // row k of L; the pivot stays in h[k]
+    }
+  }
+  if (fing) {
+    if (p >= 1) {
+      real* Hs = S.Hf[rowf];
+#pragma unroll
+      for (int j = 0; j < CL; j++) if (j < p) Hs[TRI(p, j)] = h[j];
+      Hs[TRI(p, p)] = h[p];
+      S.Df[rowf][p] = 1.0 / h[p];
+    } else {
+      S.bdelta[rowf] = -h[0];   // the base row accumulated -sum_k L[k][0]^2 D_k
+    }
+  } else if (obj) {
+#pragma unroll
+    for (int j = 0; j < 5; j++) if (j < p) S.Ho[TRI(p, j)] = h[j];
+    S.Ho[TRI(p, p)] = h[p];
+    S.Do[p] = 1.0 / h[p];
+  } else if (lane == 63) {
+    const real h11 = S.Hp[TRI(1, 1)], h10 = S.Hp[TRI(1, 0)];
+    const real ih = 1.0 / h11;
+    const real a = h10 * ih;
+    S.bdelta[3] = h10 * a;
+    S.Hp[TRI(1, 0)] = a;
+    S.Dp[1] = 1.0 / h11;
   }
   __syncthreads();
   if (lane == 0) S.Dbb = 1.0 / (S.Hbb - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3]));
   __syncthreads();
 }
 
+// L^T y = b on the DPP-row layout (leaves -> root): lane p holds y_p and column p of L;
+// a finger row's base lane accumulates -sum_k L[k][0] y_k.  Then y <- D^-1 y.
+template <int CL>
+__device__ __forceinline__ real rows_LT_D(SharedT<CL>& S, int rowf, int p, bool fing, bool obj, real y) {
+  real Lc[CL + 1];
+#pragma unroll
+  for (int k = 0; k <= CL; k++) {
+    real v = 0;
+    if (fing) { if (k > p) v = S.Hf[rowf][TRI(k, p)]; }
+    else if (obj) { if (k > p && k < 6) v = S.Ho[TRI(k, p)]; }
+    Lc[k] = v;
+  }
+#pragma unroll
+  for (int k = CL; k >= 1; k--) {
+    const bool act = fing || (obj && k <= 5);
+    const real yk = row_bcast(y, k);
+    if (act && p < k) y -= Lc[k] * yk;
+  }
+  if (fing) { if (p >= 1) y *= S.Df[rowf][p]; }
+  else if (obj) y *= S.Do[p];
+  return y;
+}
+// x = L^-1 y on the DPP-row layout (root -> leaves); a finger row's base lane holds the
+// base solution
+template <int CL>
+__device__ __forceinline__ real rows_L(SharedT<CL>& S, int rowf, int p, bool fing, bool obj, real y) {
+  real Lr[CL];
+#pragma unroll
+  for (int k = 0; k < CL; k++) {
+    real v = 0;
+    if (fing) { if (k < p) v = S.Hf[rowf][TRI(p, k)]; }
+    else if (obj) { if (k < p) v = S.Ho[TRI(p, k)]; }
+    Lr[k] = v;
+  }
+#pragma unroll
+  for (int k = 0; k < CL; k++) {
+    const bool act = fing || (obj && k < 5);
+    const real xk = row_bcast(y, k);
+    if (act && p > k) y -= Lr[k] * xk;
+  }
+  return y;
+}
 
-// chain part of x = H~^-1 b: L^T y = b (leaves -> root), base contribution returned
-template <int L>
-__device__ __forceinline__ real chain_LT(const real* __restrict__ Hs, const real* __restrict__ D, real* y) {
-  real yb = 0;
-#pragma unroll
-  for (int k = L; k >= 1; k--) {
-#pragma unroll
-    for (int i = k - 1; i >= 1; i--) y[i] -= Hs[TRI(k, i)] * y[k];
-    yb += Hs[TRI(k, 0)] * y[k];
-  }
-#pragma unroll
-  for (int p = 1; p <= L; p++) y[p] *= D[p];
-  return yb;
-}
-// x = L^-1 y (root -> leaves) given x0 = base solution
-template <int L>
-__device__ __forceinline__ void chain_L(const real* __restrict__ Hs, real x0, const real* y, real* xs) {
-  xs[0] = x0;
-#pragma unroll
-  for (int k = 1; k <= L; k++) {
-    real v = y[k];
-#pragma unroll
-    for (int i = k - 1; i >= 0; i--) v -= Hs[TRI(k, i)] * xs[i];
-    xs[k] = v;
-  }
-}
-__device__ __forceinline__ void obj_solve(const real* __restrict__ Ho, const real* __restrict__ Do, real* y) {
-#pragma unroll
-  for (int k = 5; k >= 1; k--)
-#pragma unroll
-    for (int i = k - 1; i >= 0; i--) y[i] -= Ho[TRI(k, i)] * y[k];
-#pragma unroll
-  for (int p = 0; p < 6; p++) y[p] *= Do[p];
-#pragma unroll
-  for (int k = 0; k < 6; k++) {
-    real v = y[k];
-#pragma unroll
-    for (int i = k - 1; i >= 0; i--) v -= Ho[TRI(k, i)] * y[i];
-    y[k] = v;
-  }
-}
-
-// x = H~^-1 b over full dof vectors (b, x in LDS, may alias); lanes 0..2 fingers,
-// 3 palm, 4 object
+// x = H~^-1 b over full dof vectors (b, x in LDS, may alias)
 template <int CL>
 __device__ void solve_full(SharedT<CL>& S, const GmTopo* __restrict__ T, const real* b, real* x, int lane) {
-  real y[(CL + 1) > 6 ? (CL + 1) : 6];
-  if (lane < 3) {
-#pragma unroll
-    for (int p = 1; p <= CL; p++) y[p] = b[T->dof_f0[lane] + p - 1];
-    S.bdelta[lane] = chain_LT<CL>(S.Hf[lane], S.Df[lane], y);
-  } else if (lane == 3) {
-    y[1] = b[T->dof_palm];
-    S.bdelta[3] = chain_LT<1>(S.Hp, S.Dp, y);
-  } else if (lane == 4) {
-#pragma unroll
-    for (int p = 0; p < 6; p++) y[p] = b[T->dof_obj + p];
-    obj_solve(S.Ho, S.Do, y);
+  const int rowf = lane >> 4, p = lane & 15;
+  const bool fing = rowf < 3 && p <= CL;
+  const bool obj = rowf == 3 && p < 6;
+  real y = 0;
+  if (fing) { if (p >= 1) y = b[T->dof_f0[rowf] + p - 1]; }
+  else if (obj) y = b[T->dof_obj + p];
+  y = rows_LT_D<CL>(S, rowf, p, fing, obj, y);
+  real ypalm = 0;
+  if (fing && p == 0) S.bdelta[rowf] = -y;
+  if (lane == 63) {
+    const real y1 = b[T->dof_palm];
+    S.bdelta[3] = S.Hp[TRI(1, 0)] * y1;
+    ypalm = y1 * S.Dp[1];
   }
   __syncthreads();
   const real xbase = (b[T->dof_base] - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3])) * S.Dbb;
   __syncthreads();
-  if (lane < 3) {
-    real xs[CL + 1];
-    chain_L<CL>(S.Hf[lane], xbase, y, xs);
-#pragma unroll
-    for (int k = 1; k <= CL; k++) x[T->dof_f0[lane] + k - 1] = xs[k];
-    if (lane == 0) x[T->dof_base] = xbase;
-  } else if (lane == 3) {
-    real xs[2];
-    chain_L<1>(S.Hp, xbase, y, xs);
-    x[T->dof_palm] = xs[1];
-  } else if (lane == 4) {
-#pragma unroll
-    for (int k = 0; k < 6; k++) x[T->dof_obj + k] = y[k];
+  if (fing && p == 0) y = xbase;
+  y = rows_L<CL>(S, rowf, p, fing, obj, y);
+  if (fing) {
+    if (p >= 1) x[T->dof_f0[rowf] + p - 1] = y;
+    else if (rowf == 0) x[T->dof_base] = xbase;
+  } else if (obj) {
+    x[T->dof_obj + p] = y;
+  } else if (lane == 63) {
+    x[T->dof_palm] = ypalm - S.Hp[TRI(1, 0)] * xbase;
   }
   __syncthreads();
 }
@@ -1522,29 +1545,22 @@ __device__ void constraint_accel(SharedT<CL>& S, const GmTopo* __restrict__ T, i
     S.z[d] = acc * Dd;
   }
   __syncthreads();
-  // x = L^-1 z : root -> leaves
-  if (lane < 3) {
-    real y[CL + 1], xs[CL + 1];
-    const int d0 = T->dof_f0[lane];
-#pragma unroll
-    for (int k = 1; k <= CL; k++) y[k] = S.z[d0 + k - 1];
-    chain_L<CL>(S.Hf[lane], S.z[T->dof_base], y, xs);
-#pragma unroll
-    for (int k = 1; k <= CL; k++) S.qacc[d0 + k - 1] = S.qacc[d0 + k - 1] + xs[k];
-    if (lane == 0) S.qacc[T->dof_base] = S.qacc[T->dof_base] + xs[0];
-  } else if (lane == 3) {
-    real y[2] = {0, S.z[T->dof_palm]}, xs[2];
-    chain_L<1>(S.Hp, S.z[T->dof_base], y, xs);
-    S.qacc[T->dof_palm] = S.qacc[T->dof_palm] + xs[1];
-  } else if (lane == 4) {
-    real xs[6];
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-      real v = S.z[T->dof_obj + k];
-#pragma unroll
-      for (int i = k - 1; i >= 0; i--) v -= S.Ho[TRI(k, i)] * xs[i];
-      xs[k] = v;
-      S.qacc[T->dof_obj + k] = S.qacc[T->dof_obj + k] + v;
+  // x = L^-1 z : root -> leaves, on the DPP-row layout (see factor)
+  {
+    const int rowf = lane >> 4, p = lane & 15;
+    const bool fing = rowf < 3 && p <= CL;
+    const bool obj = rowf == 3 && p < 6;
+    real y = 0;
+    if (fing) y = (p == 0) ? S.z[T->dof_base] : S.z[T->dof_f0[rowf] + p - 1];
+    else if (obj) y = S.z[T->dof_obj + p];
+    y = rows_L<CL>(S, rowf, p, fing, obj, y);
+    if (fing) {
+      if (p >= 1) S.qacc[T->dof_f0[rowf] + p - 1] += y;
+      else if (rowf == 0) S.qacc[T->dof_base] += y;
+    } else if (obj) {
+      S.qacc[T->dof_obj + p] += y;
+    } else if (lane == 63) {
+      S.qacc[T->dof_palm] += S.z[T->dof_palm] - S.Hp[TRI(1, 0)] * S.z[T->dof_base];
     }
   }
   // contact forces in the contact frame (mj_contactForce, pyramidal decode)

@@ -75,7 +75,6 @@ struct __align__(16) SharedT {
       };
       real cfrc[NB][6];
       real chain_f[5][6], chain_I[5][10];   // chain-root sums for the base body
-      int32_t cnt[NT];                      // collision: contacts per pair lane
     };
     struct {                  // constraint rows .. constraint accelerations
       real Y[GM_MAX_EFC][CW - 1];
@@ -1228,10 +1227,15 @@ __device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const 
       }
     }
   }
-  S.cnt[lane] = cnt;
-  __syncthreads();
+  // contact slots: exclusive prefix sum of the per-lane counts (0..4, three bits) from
+  // three ballots -- no LDS round trip
   int off = 0, total = 0;
-  for (int i = 0; i < NT; i++) { int c = S.cnt[i]; if (i < lane) off += c; total += c; }
+#pragma unroll
+  for (int bit = 0; bit < 3; bit++) {
+    const unsigned long long bal = __ballot((cnt >> bit) & 1);
+    off += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u)) << bit;
+    total += __popcll(bal) << bit;
+  }
   if (cnt > 0) {
     real mu = fmax(A.friction, B.friction);
     if (kind == 1) {

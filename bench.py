@@ -129,7 +129,9 @@ def obs_parity(gmx):
     return out
 
 
-def cpu_baseline(gmx, n_envs: int, n_steps: int):
+def cpu_baseline(gmx, n_envs: int, n_steps: int, n_threads: int):
+    """The fp64 CPU oracle on the host cores: envs are independent (one env
+    per thread, as the reference runs one env per process), spread over n_threads."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib
     s = gmx.canonical_settings(seed=1234)
@@ -137,9 +139,9 @@ def cpu_baseline(gmx, n_envs: int, n_steps: int):
     cfg = gmx.ConfigBlob(s, model)
     objs = gmx.make_object_set("set6_synthetic", 1234)
     t = time.time()
-    v = oracle_lib.bench(model, cfg, objs, n_envs, n_steps, seed=1234, n_threads=1)
-    return {"value": round(v, 2), "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"fp64 C oracle (oracle/oracle.c, gcc -O2 -mavx), 1 thread, {n_envs} envs x "
+    v = oracle_lib.bench(model, cfg, objs, n_envs, n_steps, seed=1234, n_threads=n_threads)
+    return {"value": round(v, 2), "unit": "env-steps/s", "cores": n_threads, "kind": "port",
+            "sample": f"fp64 C oracle (oracle/oracle.c, gcc -O2 -mavx), {n_threads} thread(s), {n_envs} envs x "
                       f"{n_steps} env-steps of the C3 workload (set6_synthetic, random actions, "
                       f"resets at done), {time.time() - t:.1f} s wall"}
 
@@ -151,8 +153,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--seed", type=int, default=1234)
-    ap.add_argument("--cpu-envs", type=int, default=40)
+    ap.add_argument("--cpu-envs", type=int, default=40, help="envs per CPU thread in the baseline")
     ap.add_argument("--cpu-steps", type=int, default=250)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="host threads for the CPU baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     args = ap.parse_args()
@@ -238,7 +242,8 @@ def main():
                 "traffic_source": traffic_src}
         cpu = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(gmx, args.cpu_envs, args.cpu_steps)
+            cpu = cpu_baseline(gmx, args.cpu_envs * args.cpu_threads // 4, args.cpu_steps, args.cpu_threads)
+            cpu["single_thread"] = cpu_baseline(gmx, args.cpu_envs, args.cpu_steps, 1)["value"]
         parity = None if args.no_parity else obs_parity(gmx)
         value = world * n * K / elapsed
         out = {

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "gm_kernels.hip"
+#include "gm_policy.hip"
 
 struct gm_ctx {
   int device = 0;
@@ -517,6 +518,123 @@ int gm_step_profiled(gm_ctx* c, uint64_t* phase_cycles) {
                            c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   (void)hipFree(d_ph);
+  return GM_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- on-device DQN policy
+struct gm_policy {
+  gm_ctx* ctx = nullptr;
+  GpNet net{};
+  float* d_params = nullptr;
+  int32_t* d_actions = nullptr;
+  float* d_q = nullptr;
+};
+
+static int64_t policy_layout(const int32_t* sizes, int n_sizes, GpNet* net) {
+  if (!sizes || n_sizes < 2 || n_sizes - 1 > GP_MAX_LAYERS) return -1;
+  GpNet P{};
+  P.n_layers = n_sizes - 1;
+  long long off = 0;
+  for (int l = 0; l < n_sizes; l++) {
+    if (sizes[l] < 1 || sizes[l] > GP_MAX_WIDTH) return -1;
+    P.width[l] = sizes[l];
+  }
+  for (int l = 0; l < P.n_layers; l++) {
+    P.kpad[l] = (P.width[l] + 3) & ~3;
+    P.tiles[l] = (P.width[l + 1] + 15) / 16;
+    P.woff[l] = off;
+    off += (long long)P.tiles[l] * (P.kpad[l] / 4) * 64;
+    P.boff[l] = off;
+    off += (long long)P.tiles[l] * 16;
+  }
+  if (net) *net = P;
+  return off;
+}
+
+extern "C" {
+
+int64_t gm_policy_pack(const int32_t* sizes, int n_sizes, const float* params, float* out) {
+  GpNet P;
+  const int64_t total = policy_layout(sizes, n_sizes, &P);
+  if (total < 0 || !out) return total;
+  if (!params) return GM_E_ARG;
+  std::memset(out, 0, sizeof(float) * (size_t)total);
+  const float* src = params;
+  for (int l = 0; l < P.n_layers; l++) {
+    const int in = P.width[l], outw = P.width[l + 1], ks = P.kpad[l] / 4;
+    const float* W = src;            // [outw x in] row-major (torch nn.Linear.weight)
+    const float* b = src + (size_t)outw * in;
+    for (int t = 0; t < P.tiles[l]; t++)
+      for (int s4 = 0; s4 < ks; s4++)
+        for (int lane = 0; lane < 64; lane++) {
+          const int j = 16 * t + (lane & 15), k = 4 * s4 + (lane >> 4);
+          out[P.woff[l] + ((int64_t)t * ks + s4) * 64 + lane] = (j < outw && k < in) ? W[(size_t)j * in + k] : 0.0f;
+        }
+    for (int j = 0; j < outw; j++) out[P.boff[l] + j] = b[j];
+    src = b + outw;
+  }
+  return total;
+}
+
+int gm_policy_create(gm_ctx* c, const int32_t* sizes, int n_sizes, const float* params, gm_policy** out) {
+  if (!c || !sizes || !params || !out) return GM_E_ARG;
+  GpNet P;
+  const int64_t total = policy_layout(sizes, n_sizes, &P);
+  if (total < 0) return fail(c, GM_E_RANGE, "gm_policy_create: <= 8 layers of width 1..256 expected");
+  if (P.width[0] != c->cfg.n_obs || P.width[P.n_layers] != c->cfg.n_actions)
+    return fail(c, GM_E_ARG, "gm_policy_create: network must map n_obs (" + std::to_string(c->cfg.n_obs) +
+                                 ") to n_actions (" + std::to_string(c->cfg.n_actions) + ")");
+  if (c->cfg.s.continous_actions)
+    return fail(c, GM_E_ARG, "gm_policy_create: the DQN policy needs discrete actions (continous_actions = 0)");
+  std::vector<float> packed((size_t)total);
+  gm_policy_pack(sizes, n_sizes, params, packed.data());
+  gm_policy* p = new gm_policy;
+  p->ctx = c;
+  p->net = P;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMalloc(&p->d_params, sizeof(float) * (size_t)total));
+  HIPCHK(c, hipMalloc(&p->d_actions, sizeof(int32_t) * (size_t)c->n_envs));
+  HIPCHK(c, hipMalloc(&p->d_q, sizeof(float) * (size_t)c->n_envs * c->cfg.n_actions));
+  HIPCHK(c, hipMemcpyAsync(p->d_params, packed.data(), sizeof(float) * (size_t)total, hipMemcpyHostToDevice,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *out = p;
+  return GM_OK;
+}
+
+void gm_policy_destroy(gm_policy* p) {
+  if (!p) return;
+  if (p->ctx) (void)hipSetDevice(p->ctx->device);
+  (void)hipFree(p->d_params);
+  (void)hipFree(p->d_actions);
+  (void)hipFree(p->d_q);
+  delete p;
+}
+
+int gm_policy_act(gm_policy* p, float eps, uint64_t seed, uint64_t decision) {
+  if (!p || !p->ctx) return GM_E_ARG;
+  gm_ctx* c = p->ctx;
+  HIPCHK(c, hipSetDevice(c->device));
+  const int blocks = (c->n_envs + GP_TILE - 1) / GP_TILE;
+  hipLaunchKernelGGL(gm_policy_kernel, dim3(blocks), dim3(64), 0, c->stream, c->d_obs, c->n_envs,
+                     (long long)c->env_offset, p->d_params, p->net, eps, seed, decision, p->d_actions, p->d_q);
+  HIPCHK(c, hipGetLastError());
+  return gm_set_discrete_action(c, p->d_actions, 1);
+}
+
+int gm_policy_read(gm_policy* p, int32_t* actions, float* q) {
+  if (!p || !p->ctx) return GM_E_ARG;
+  gm_ctx* c = p->ctx;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (actions)
+    HIPCHK(c, hipMemcpyAsync(actions, p->d_actions, sizeof(int32_t) * (size_t)c->n_envs, hipMemcpyDeviceToHost,
+                             c->stream));
+  if (q)
+    HIPCHK(c, hipMemcpyAsync(q, p->d_q, sizeof(float) * (size_t)c->n_envs * c->cfg.n_actions,
+                             hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return GM_OK;
 }
 

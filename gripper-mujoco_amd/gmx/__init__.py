@@ -9,8 +9,9 @@ from ._lib import (load_library, Settings, ModelParams, Object, Spawn, ModelBlob
                    SENSORS, LIB_PATH)
 from .settings import canonical_settings, disable_noise, MAX_EPISODE_STEPS
 from .env import BatchedGripperEnv, spawn_positions
+from .policy import DevicePolicy, eps_threshold
 
 __all__ = ["load_library", "Settings", "ModelParams", "Object", "Spawn", "ModelBlob", "ConfigBlob",
            "default_settings", "make_object_set", "canonical_settings", "disable_noise",
            "BatchedGripperEnv", "spawn_positions", "MAX_EPISODE_STEPS", "BINARY_EVENTS",
-           "LINEAR_EVENTS", "ACTION_KINDS", "SENSORS", "LIB_PATH"]
+           "LINEAR_EVENTS", "ACTION_KINDS", "SENSORS", "LIB_PATH", "DevicePolicy", "eps_threshold"]

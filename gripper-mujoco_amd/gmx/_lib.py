@@ -193,6 +193,11 @@ def _declare(lib):
         "gm_spawn_object": (i32, [vp, vp, vp]),
         "gm_autoreset": (i32, [vp, i32, vp, i32, vp]),
         "gm_device_reset_mask": (vp, [vp]),
+        "gm_policy_create": (i32, [vp, i32p, i32, f32p, C.POINTER(vp)]),
+        "gm_policy_destroy": (None, [vp]),
+        "gm_policy_pack": (C.c_int64, [i32p, i32, f32p, f32p]),
+        "gm_policy_act": (i32, [vp, C.c_float, C.c_uint64, C.c_uint64]),
+        "gm_policy_read": (i32, [vp, i32p, f32p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -15,7 +15,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
 
 def build(verbose: bool = False, force: bool = False) -> str:
     srcs = [os.path.join(PKG_DIR, s) for s in SOURCES]
-    deps = srcs + [os.path.join(PKG_DIR, "csrc", f) for f in ("gm_kernels.hip", "gm_state.h")] + \
+    deps = srcs + [os.path.join(PKG_DIR, "csrc", f) for f in ("gm_kernels.hip", "gm_policy.hip", "gm_state.h")] + \
         [os.path.join(REPO_DIR, "include", f) for f in ("gripper_mi355x.h", "gm_settings.def")]
     if not force and os.path.exists(LIB_PATH):
         t = os.path.getmtime(LIB_PATH)

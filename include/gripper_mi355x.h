@@ -382,6 +382,30 @@ int  gm_debug_substep(gm_ctx* ctx, int32_t* ncon, float* contact, float* efc_for
    PGS, FK hinge rotations, FK chains, CRB/RNE chains), (rest spare) */
 int  gm_step_profiled(gm_ctx* ctx, uint64_t* phase_cycles);
 
+/* ---- on-device DQN policy ----
+ * VariableNetwork.forward (rl/networks.py:7-41: Linear+ReLU hidden layers, final Linear,
+ * Softmax(dim=1)) on every env's current observation, then Agent_DQN.select_action
+ * (rl/agents/DQN.py:184-209): argmax of the network output, or with probability eps a
+ * uniform random action.  The chosen discrete actions are applied to the envs on the
+ * device (MjClass::set_discrete_action), so a rollout needs no host round trip.
+ * sizes: n_sizes layer widths [n_obs, hidden..., n_actions] (<= 8 layers, widths <= 256);
+ * params: torch state_dict order, f32 -- W0 [sizes[1] x sizes[0]] row-major, b0
+ * [sizes[1]], W1, b1, ...  (host pointer). */
+typedef struct gm_policy gm_policy;
+int  gm_policy_create(gm_ctx* ctx, const int32_t* sizes, int n_sizes, const float* params,
+                      gm_policy** out);
+void gm_policy_destroy(gm_policy* p);
+/* Host-side repack of params into the device layout (MFMA B-fragment order, zero
+ * padded); returns the packed float count, writes `out` when non-NULL.  Exposed so the
+ * layout is testable without a GPU. */
+int64_t gm_policy_pack(const int32_t* sizes, int n_sizes, const float* params, float* out);
+/* select (eps-greedy, counter-based per-env draws from (seed, global env id, decision))
+ * and apply actions for every env; eps = eps_threshold of select_action */
+int  gm_policy_act(gm_policy* p, float eps, uint64_t seed, uint64_t decision);
+/* last selected actions [n_envs] int32 and softmax outputs [n_envs x n_actions] f32
+ * (either may be NULL); host copies */
+int  gm_policy_read(gm_policy* p, int32_t* actions, float* q);
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,6 +16,7 @@
 #include <string.h>
 #include <float.h>
 #include <time.h>
+#include <pthread.h>
 #include <stdio.h>
 
 #define NB GM_MAX_BODY
@@ -2003,23 +2004,29 @@ void or_debug_substep(or_env* e, int32_t* ncon, float* contact, float* efc_force
 }
 
 /* bounded CPU baseline: n_envs independent envs, random continuous actions */
-double or_bench(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects,
-                int n_envs, int n_steps, uint64_t seed, int n_threads) {
-  (void)n_threads;
-  or_env* proto = or_create(m, c, objects, n_objects, 0);
-  if (!proto) return -1;
-  uint64_t x = seed;
-  struct timespec t0, t1;
-  clock_gettime(CLOCK_MONOTONIC, &t0);
-  long done_steps = 0;
-  for (int k = 0; k < n_envs; k++) {
-    or_env* e = (or_env*)malloc(sizeof(or_env));
-    *e = *proto;
+/* CPU throughput baseline: n_envs independent envs x n_steps env-steps of random
+ * actions (one LCG stream per env, so the work does not depend on the thread count),
+ * spread over n_threads POSIX threads (envs share nothing, like the reference's
+ * one-env-per-process model).  Returns env-steps per wall second. */
+typedef struct {
+  const or_env* proto;
+  const gm_config* c;
+  int n_objects, n_envs, n_steps, tid, n_threads;
+  uint64_t seed;
+  long done_steps;
+} bench_job;
+
+static void* bench_worker(void* arg) {
+  bench_job* j = (bench_job*)arg;
+  or_env* e = (or_env*)malloc(sizeof(or_env));
+  for (int k = j->tid; k < j->n_envs; k += j->n_threads) {
+    *e = *j->proto;
     e->env_id = k;
-    e->rng = lcg_seed((uint64_t)c->s.random_seed + (uint64_t)k * 1000003ull);
-    gm_spawn sp = {k % (n_objects > 0 ? n_objects : 1), 0.0, 0.0, 0.0};
+    e->rng = lcg_seed((uint64_t)j->c->s.random_seed + (uint64_t)k * 1000003ull);
+    gm_spawn sp = {k % (j->n_objects > 0 ? j->n_objects : 1), 0.0, 0.0, 0.0};
     or_reset(e, &sp);
-    for (int t = 0; t < n_steps; t++) {
+    uint64_t x = j->seed + (uint64_t)k * 0x9E3779B97F4A7C15ull;
+    for (int t = 0; t < j->n_steps; t++) {
       float a[8];
       for (int i = 0; i < e->c.n_actions && i < 8; i++) {
         x = x * 6364136223846793005ull + 1442695040888963407ull;
@@ -2031,10 +2038,33 @@ double or_bench(const gm_model* m, const gm_config* c, const gm_object* objects,
       or_get_obs(e, obs);
       int d = or_is_done(e);
       or_reward(e);
-      done_steps++;
+      j->done_steps++;
       if (d) or_reset(e, &sp);
     }
-    free(e);
+  }
+  free(e);
+  return NULL;
+}
+
+double or_bench(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects,
+                int n_envs, int n_steps, uint64_t seed, int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > 256) n_threads = 256;
+  or_env* proto = or_create(m, c, objects, n_objects, 0);
+  if (!proto) return -1;
+  bench_job jobs[256];
+  pthread_t th[256];
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int t = 0; t < n_threads; t++) {
+    jobs[t] = (bench_job){proto, c, n_objects, n_envs, n_steps, t, n_threads, seed, 0};
+    if (n_threads == 1) bench_worker(&jobs[0]);
+    else pthread_create(&th[t], NULL, bench_worker, &jobs[t]);
+  }
+  long done_steps = 0;
+  for (int t = 0; t < n_threads; t++) {
+    if (n_threads > 1) pthread_join(th[t], NULL);
+    done_steps += jobs[t].done_steps;
   }
   clock_gettime(CLOCK_MONOTONIC, &t1);
   or_destroy(proto);

@@ -146,6 +146,48 @@ def cpu_baseline(gmx, n_envs: int, n_steps: int, n_threads: int):
                       f"resets at done), {time.time() - t:.1f} s wall"}
 
 
+def policy_rollout(gmx, torch, dev, stream, n: int, steps: int, seed: int, env_offset: int):
+    """C5: the C3 workload with discrete actions chosen on the device by the
+    DQN policy (VariableNetwork [63,150,100,50,8], eps-greedy) -- policy, env-step and
+    auto-reset with no host round trip.  Returns env-steps/s and the policy kernel's
+    share of the step (HIP events on the shared stream)."""
+    s = gmx.canonical_settings(seed=seed)
+    s.continous_actions = 0
+    env = gmx.BatchedGripperEnv(n, object_set="set6_synthetic", settings=s, seed=seed, env_offset=env_offset,
+                                device=dev.index)
+    env.set_stream(stream.cuda_stream)
+    spawn = env.make_spawn()
+    env.reset(spawn=spawn)
+    spawn_ptr = env.upload_spawn(spawn)
+    pol = gmx.DevicePolicy(env, seed=seed)
+    returns = torch.full((n,), float("nan"), device=dev)
+    evp = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+
+    def one(t, k):
+        if k is not None:
+            evp[k][0].record(stream)
+        pol.act(eps=gmx.eps_threshold(t), seed=seed, decision=t)
+        if k is not None:
+            evp[k][1].record(stream)
+        env.lib.gm_step(env.ctx)
+        env.autoreset_device(spawn_ptr, returns.data_ptr())
+
+    one(0, None)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        one(1 + k, k)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    pol_ms = sum(a.elapsed_time(b) for a, b in evp) / steps
+    out = {"value": round(n * steps / el, 1), "unit": "env-steps/s", "envs": n, "steps": steps,
+           "ms_per_step": round(el / steps * 1e3, 3), "policy_select_ms": round(pol_ms, 4),
+           "network": pol.sizes, "dtype": "f32 policy (MFMA) + f64 env"}
+    pol.close()
+    env.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -159,6 +201,7 @@ def main():
                     help="host threads for the CPU baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-policy", action="store_true", help="skip the C5 on-device DQN rollout line item")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -245,6 +288,8 @@ def main():
             cpu = cpu_baseline(gmx, args.cpu_envs * args.cpu_threads // 4, args.cpu_steps, args.cpu_threads)
             cpu["single_thread"] = cpu_baseline(gmx, args.cpu_envs, args.cpu_steps, 1)["value"]
         parity = None if args.no_parity else obs_parity(gmx)
+        c5 = None if (args.no_policy or world > 1) else policy_rollout(gmx, torch, dev, stream, n, max(3, K // 2), args.seed,
+                                                        first_env)
         value = world * n * K / elapsed
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
@@ -262,6 +307,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "obs_max_rel_err": parity,
+            "c5_device_policy_rollout": c5,
             "episodes_finished": int(episodes.item()),
             "overflow_envs": overflow, "finite": finite,
         }

@@ -979,7 +979,7 @@ static void constraint_solve(or_env* e) {
   e->nefc = n;
   if (n == 0) return;
   /* A = J H^-1 J^T */
-  static double W[NE][NV];
+  double W[NE][NV];
   double A[NE][NE];
   for (int r = 0; r < n; r++) solve(e, W[r], e->J[r]);
   for (int r = 0; r < n; r++)
@@ -1106,13 +1106,6 @@ static void physics_substep(or_env* e) {
   double dq[NV];
   solve(e, dq, jtf);
   for (int d = 0; d < nv; d++) e->qacc[d] = e->qacc_smooth[d] + dq[d];
-  if (getenv("ORACLE_DEBUG")) {
-    static int once = 0;
-    if (once++ < 1) {
-      for (int d = 0; d < nv; d++) printf("d=%d M=%.4g D=%.4g bias=%.4g pas=%.4g act=%.4g qacc_s=%.4g qacc=%.4g\n", d, e->M[d][d], e->D[d], e->qfrc_bias[d], e->qfrc_passive[d], e->qfrc_act[d], e->qacc_smooth[d], e->qacc[d]);
-      printf("ncon=%d nefc=%d\n", e->ncon, e->nefc);
-    }
-  }
   /* semi-implicit Euler */
   for (int d = 0; d < nv; d++) e->qvel[d] += h * e->qacc[d];
   for (int b = 1; b < m->nbody; b++) {
@@ -1136,25 +1129,6 @@ static void physics_substep(or_env* e) {
     }
   }
   e->time += h;
-  if (getenv("ORACLE_DEBUG")) {
-    static int reported = 0;
-    int bad = 0;
-    for (int d = 0; d < nv; d++) if (!isfinite(e->qvel[d])) bad = 1;
-    static int cnt = 0;
-    if (cnt++ < 12) {
-      double vm = 0; int dm = 0;
-      for (int d = 0; d < nv; d++) if (fabs(e->qvel[d]) > vm) { vm = fabs(e->qvel[d]); dm = d; }
-      printf("sub %d t=%.4f ncon=%d nefc=%d vmax=%g at d%d q=%g\n", cnt, e->time, e->ncon, e->nefc, vm, dm, e->qpos[dm]);
-      for (int c = 0; c < e->ncon; c++) printf("   con g1=%d g2=%d dist=%g f=(%g %g %g)\n", e->con[c].g1, e->con[c].g2, e->con[c].dist, e->con[c].force[0], e->con[c].force[1], e->con[c].force[2]);
-    }
-    if (bad && !reported) {
-      reported = 1;
-      printf("NaN at time %.5f ncon=%d nefc=%d\n", e->time, e->ncon, e->nefc);
-      for (int c = 0; c < e->ncon; c++) printf(" con %d g1=%d g2=%d dist=%g n=(%g %g %g) f=(%g %g %g)\n", c, e->con[c].g1, e->con[c].g2, e->con[c].dist, e->con[c].frame[0], e->con[c].frame[1], e->con[c].frame[2], e->con[c].force[0], e->con[c].force[1], e->con[c].force[2]);
-      for (int r = 0; r < e->nefc; r++) printf(" efc %d f=%g R=%g b=%g\n", r, e->efc_f[r], e->efc_R[r], e->efc_b[r]);
-      for (int d = 0; d < nv; d++) printf(" d%d qacc_s=%g qacc=%g D=%g\n", d, e->qacc_smooth[d], e->qacc[d], e->D[d]);
-    }
-  }
 }
 
 /* =====================================================================

@@ -42,6 +42,8 @@ struct gm_ctx {
   int32_t* d_dact = nullptr;
   uint8_t* d_mask = nullptr;
   gm_spawn* d_spawn = nullptr;
+  int32_t* d_order = nullptr;          // workgroup -> env dispatch order (cost-sorted)
+  uint32_t* d_cost = nullptr;          // per-env cost of the last env-step (clocks / 64)
   std::string err;
 };
 
@@ -73,11 +75,14 @@ bool nseg_supported(int n) {
   }
 }
 hipError_t launch_step(gm_ctx* c, int grid, int n_envs, int mode, DebugOut dbg) {
+  // the full env-step (mode 0) runs in cost-sorted order and records each env's cost
+  const int32_t* order = (mode == 0 && grid == c->n_envs) ? c->d_order : nullptr;
+  uint32_t* cost = (mode == 0 && grid == c->n_envs) ? c->d_cost : nullptr;
   switch (c->model.n_seg) {
 #define X(N)                                                                                               \
   case N:                                                                                                  \
     hipLaunchKernelGGL((gm_step_kernel<N + 2>), dim3(grid), dim3(NT), 0, c->stream, c->d_state, c->d_model, \
-                       c->d_cfg, c->d_topo, c->d_obs, c->d_rew, c->d_done, n_envs, mode, dbg);              \
+                       c->d_cfg, c->d_topo, c->d_obs, c->d_rew, c->d_done, n_envs, mode, dbg, order, cost); \
     return hipGetLastError();
     GM_NSEG_LIST
 #undef X
@@ -220,6 +225,11 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   HIPCHK(c, hipMalloc(&c->d_dact, sizeof(int32_t) * (size_t)n_envs));
   HIPCHK(c, hipMalloc(&c->d_mask, (size_t)n_envs));
   HIPCHK(c, hipMalloc(&c->d_spawn, sizeof(gm_spawn) * (size_t)n_envs));
+  HIPCHK(c, hipMalloc(&c->d_order, sizeof(int32_t) * (size_t)n_envs));
+  HIPCHK(c, hipMalloc(&c->d_cost, sizeof(uint32_t) * (size_t)n_envs));
+  HIPCHK(c, hipMemsetAsync(c->d_cost, 0, sizeof(uint32_t) * (size_t)n_envs, c->stream));
+  hipLaunchKernelGGL(gm_dispatch_order_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_cost, c->d_order, n_envs);
+  HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemsetAsync(c->d_state, 0, sizeof(GmEnvState) * (size_t)n_envs, c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_obs, 0, sizeof(float) * (size_t)n_envs * (cfg->n_obs > 0 ? cfg->n_obs : 1), c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_rew, 0, sizeof(float) * (size_t)n_envs, c->stream));
@@ -248,6 +258,7 @@ void gm_destroy(gm_ctx* c) {
   (void)hipFree(c->d_state); (void)hipFree(c->d_model); (void)hipFree(c->d_cfg); (void)hipFree(c->d_topo); (void)hipFree(c->d_objs);
   (void)hipFree(c->d_eq); (void)hipFree(c->d_obs); (void)hipFree(c->d_rew); (void)hipFree(c->d_done); (void)hipFree(c->d_act);
   (void)hipFree(c->d_dact); (void)hipFree(c->d_mask); (void)hipFree(c->d_spawn);
+  (void)hipFree(c->d_order); (void)hipFree(c->d_cost);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -340,6 +351,8 @@ int gm_step(gm_ctx* c) {
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   HIPCHK(c, launch_step(c, c->n_envs, c->n_envs, 0, dbg));
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  hipLaunchKernelGGL(gm_dispatch_order_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_cost, c->d_order, c->n_envs);
+  HIPCHK(c, hipGetLastError());
   c->timed = true;
   return GM_OK;
 }

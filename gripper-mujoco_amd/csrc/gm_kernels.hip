@@ -2317,11 +2317,16 @@ template <int CL>
 __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
     GmEnvState* __restrict__ states, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
     const GmTopo* __restrict__ T, float* __restrict__ obs, float* __restrict__ rew,
-    uint8_t* __restrict__ done, int n_envs, int mode, DebugOut dbg) {
+    uint8_t* __restrict__ done, int n_envs, int mode, DebugOut dbg, const int32_t* __restrict__ order,
+    uint32_t* __restrict__ cost) {
   __shared__ SharedT<CL> S;
   const int lane = threadIdx.x;
-  const int env = blockIdx.x;
-  if (env >= n_envs) return;
+  if ((int)blockIdx.x >= n_envs) return;
+  // cost-sorted dispatch: workgroups start in blockIdx order, so the envs that were the
+  // most expensive last env-step are started first (longest-processing-time list
+  // scheduling over the resident slots; see gm_dispatch_order_kernel)
+  const int env = order ? order[blockIdx.x] : (int)blockIdx.x;
+  const unsigned long long t_start = cost ? __builtin_amdgcn_s_memtime() : 0;
   load_state(S, states + env, lane);
   const bool settle = (mode == 1);          // calibrate_reset settle: 400 substeps, no sensors
   const bool prof = !settle && dbg.phase != nullptr;
@@ -2389,7 +2394,44 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
     __syncthreads();
     if (lane < GM_NPHASE) dbg.phase[(size_t)env * GM_NPHASE + lane] = S.tph[lane];
   }
+  if (cost && lane == 0) {   // smoothed (3:1 with the previous estimate): the measured cost carries co-residency noise
+    const uint32_t now = (uint32_t)((__builtin_amdgcn_s_memtime() - t_start) >> 6);
+    cost[env] = (uint32_t)(((uint64_t)cost[env] * 3 + now) >> 2);
+  }
   store_state(S, states + env, lane);
+}
+
+// Dispatch order for the next env-step: envs by descending cost of their last env-step
+// (shader clocks / 64, written by gm_step_kernel), bucketed into 256 cost classes.
+// One 1024-thread workgroup; the order only changes which env a workgroup slot runs
+// first, never any result.
+extern "C" __global__ __launch_bounds__(1024) void gm_dispatch_order_kernel(const uint32_t* __restrict__ cost,
+                                                                            int32_t* __restrict__ order, int n) {
+  __shared__ uint32_t cnt[256];
+  __shared__ uint32_t cmax;
+  const int t = threadIdx.x;
+  if (t < 256) cnt[t] = 0;
+  if (t == 0) cmax = 1;
+  __syncthreads();
+  uint32_t m = 1;
+  for (int i = t; i < n; i += 1024) m = max(m, cost[i]);
+  atomicMax(&cmax, m);
+  __syncthreads();
+  const uint64_t cm = (uint64_t)cmax + 1;
+  for (int i = t; i < n; i += 1024) {
+    const int b = 255 - (int)(((uint64_t)cost[i] * 256) / cm);
+    atomicAdd(&cnt[b], 1u);
+  }
+  __syncthreads();
+  if (t == 0) {
+    uint32_t acc = 0;
+    for (int b = 0; b < 256; b++) { const uint32_t c = cnt[b]; cnt[b] = acc; acc += c; }
+  }
+  __syncthreads();
+  for (int i = t; i < n; i += 1024) {
+    const int b = 255 - (int)(((uint64_t)cost[i] * 256) / cm);
+    order[atomicAdd(&cnt[b], 1u)] = i;
+  }
 }
 
 // ---------------------------------------------------------------- actions

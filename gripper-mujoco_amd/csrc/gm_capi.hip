@@ -44,6 +44,8 @@ struct gm_ctx {
   gm_spawn* d_spawn = nullptr;
   int32_t* d_order = nullptr;          // workgroup -> env dispatch order (cost-sorted)
   uint32_t* d_cost = nullptr;          // per-env cost of the last env-step (clocks / 64)
+  gm_spawn_params* d_scene = nullptr;  // gm_set_scene_spawn parameters (NULL: plain spawn_object)
+  int scene_tries = 0;
   std::string err;
 };
 
@@ -258,7 +260,7 @@ void gm_destroy(gm_ctx* c) {
   (void)hipFree(c->d_state); (void)hipFree(c->d_model); (void)hipFree(c->d_cfg); (void)hipFree(c->d_topo); (void)hipFree(c->d_objs);
   (void)hipFree(c->d_eq); (void)hipFree(c->d_obs); (void)hipFree(c->d_rew); (void)hipFree(c->d_done); (void)hipFree(c->d_act);
   (void)hipFree(c->d_dact); (void)hipFree(c->d_mask); (void)hipFree(c->d_spawn);
-  (void)hipFree(c->d_order); (void)hipFree(c->d_cost);
+  (void)hipFree(c->d_order); (void)hipFree(c->d_cost); (void)hipFree(c->d_scene);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -291,7 +293,7 @@ int gm_reset(gm_ctx* c, const uint8_t* mask, const gm_spawn* spawn) {
   }
   int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
   hipLaunchKernelGGL(gm_reset_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
-                     c->d_topo, c->d_eq, dm, ds, c->d_objs, c->n_objects, c->n_envs);
+                     c->d_topo, c->d_eq, dm, ds, c->d_objs, c->n_objects, c->n_envs, c->d_scene, c->scene_tries);
   HIPCHK(c, hipGetLastError());
   if (mask || spawn) HIPCHK(c, hipStreamSynchronize(c->stream));   // host buffers may be reused
   return GM_OK;
@@ -341,6 +343,49 @@ int gm_set_discrete_action(gm_ctx* c, const int32_t* actions, int on_device) {
                      (const float*)nullptr, da, c->n_envs);
   HIPCHK(c, hipGetLastError());
   if (!on_device) HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+
+static bool spawn_grid_ok(const gm_spawn_params& p) {
+  if (!(p.xy_increment > 0) || !(p.rot_increment > 0) || p.xrange < 0 || p.yrange < 0 || p.rotrange < 0) return false;
+  const double nx = ((2 * p.xrange) / p.xy_increment) + 1, ny = ((2 * p.yrange) / p.xy_increment) + 1;
+  const double nr = ((2 * p.rotrange) / p.rot_increment) + 1;
+  return nx * ny < GM_SPAWN_MAX_XY + 1 && (int)nx * (int)ny <= GM_SPAWN_MAX_XY && nr < GM_SPAWN_MAX_ROT + 1;
+}
+
+int gm_spawn_into_scene(gm_ctx* c, const uint8_t* mask, const gm_spawn_params* params, int n_params, uint8_t* ok) {
+  if (!c || !params || (n_params != 1 && n_params != c->n_envs)) return fail(c, GM_E_ARG, "gm_spawn_into_scene: params must hold 1 or n_envs entries");
+  for (int i = 0; i < n_params; i++)
+    if (!spawn_grid_ok(params[i]))
+      return fail(c, GM_E_ARG, "gm_spawn_into_scene: spawn grid empty or larger than GM_SPAWN_MAX_XY / GM_SPAWN_MAX_ROT");
+  HIPCHK(c, hipSetDevice(c->device));
+  gm_spawn_params* dp = nullptr;
+  uint8_t* dok = nullptr;
+  HIPCHK(c, hipMalloc(&dp, sizeof(gm_spawn_params) * (size_t)n_params));
+  HIPCHK(c, hipMalloc(&dok, (size_t)c->n_envs));
+  HIPCHK(c, hipMemcpyAsync(dp, params, sizeof(gm_spawn_params) * (size_t)n_params, hipMemcpyHostToDevice, c->stream));
+  const uint8_t* dm = nullptr;
+  if (mask) { HIPCHK(c, hipMemcpyAsync(c->d_mask, mask, (size_t)c->n_envs, hipMemcpyHostToDevice, c->stream)); dm = c->d_mask; }
+  int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
+  hipLaunchKernelGGL(gm_spawn_into_scene_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model,
+                     c->d_topo, c->d_objs, c->n_objects, dm, dp, n_params, dok, c->n_envs);
+  HIPCHK(c, hipGetLastError());
+  if (ok) HIPCHK(c, hipMemcpyAsync(ok, dok, (size_t)c->n_envs, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  (void)hipFree(dp);
+  (void)hipFree(dok);
+  return GM_OK;
+}
+
+int gm_set_scene_spawn(gm_ctx* c, const gm_spawn_params* params, int max_tries) {
+  if (!c) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (!params) { c->scene_tries = 0; HIPCHK(c, hipStreamSynchronize(c->stream)); (void)hipFree(c->d_scene); c->d_scene = nullptr; return GM_OK; }
+  if (max_tries < 1 || !spawn_grid_ok(*params)) return fail(c, GM_E_ARG, "gm_set_scene_spawn: max_tries < 1 or bad spawn grid");
+  if (!c->d_scene) HIPCHK(c, hipMalloc(&c->d_scene, sizeof(gm_spawn_params)));
+  HIPCHK(c, hipMemcpyAsync(c->d_scene, params, sizeof(gm_spawn_params), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->scene_tries = max_tries;
   return GM_OK;
 }
 
@@ -511,7 +556,8 @@ int gm_autoreset(gm_ctx* c, int max_episode_steps, const gm_spawn* spawn, int sp
                      max_episode_steps, c->d_mask, returns, c->n_envs);
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(gm_reset_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
-                     c->d_topo, c->d_eq, c->d_mask, ds, c->d_objs, c->n_objects, c->n_envs);
+                     c->d_topo, c->d_eq, c->d_mask, ds, c->d_objs, c->n_objects, c->n_envs, c->d_scene,
+                     c->scene_tries);
   HIPCHK(c, hipGetLastError());
   if (spawn && !spawn_on_device) HIPCHK(c, hipStreamSynchronize(c->stream));
   return GM_OK;

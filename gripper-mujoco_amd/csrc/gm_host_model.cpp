@@ -370,8 +370,22 @@ int64_t gm_struct_size(int which) {
     case 3: return (int64_t)sizeof(gm_object);
     case 4: return (int64_t)sizeof(gm_spawn);
     case 5: return (int64_t)sizeof(gm_model_params);
+    case 6: return (int64_t)sizeof(gm_spawn_params);
     default: return -1;
   }
+}
+
+// MjType::SpawnParams member initialisers (mjclass.h:916-931)
+void gm_default_spawn_params(gm_spawn_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->index = -1;
+  p->x = 0.0; p->y = 0.0; p->zrot = 0.0;
+  p->xrange = 0.0; p->yrange = 0.0; p->rotrange = 0.0;
+  p->xmin = -100; p->xmax = 100; p->ymin = -100; p->ymax = 100;
+  p->smallest_gap = 1e-3;
+  p->xy_increment = 2e-3;
+  p->rot_increment = M_PI / 30.0;
 }
 
 void gm_model_info(const gm_model* m, int32_t* o) {

@@ -2579,6 +2579,185 @@ __device__ void spawn_object(GmEnvState& s, const GmTopo* __restrict__ T, const 
 // MjEnv auto-reset bookkeeping (MjEnv.py:616-637, 2170-2263): an env whose episode
 // terminated (is_done) or truncated (num_action_steps >= max_episode_steps) hands its
 // episode return to `returns` and is flagged for gm_reset_kernel.
+// ---------------------------------------------------------------- spawn_into_scene
+// MjClass::spawn_into_scene(SpawnParams) (mjclass.cpp:2475-2654), one thread per env.
+//
+// std::uniform_int_distribution<unsigned long>{a, b} driven by minstd_rand0, as libstdc++
+// implements it (bits/uniform_int_dist.h): the engine's range 2^31 - 3 is neither 2^32 - 1
+// nor 2^64 - 1, so the downscaling branch takes the two-division rejection path.
+__device__ uint64_t uid_minstd(uint32_t& st, uint64_t a, uint64_t b) {
+  const uint64_t urngrange = 2147483646ull - 1ull;   // max() - min()
+  const uint64_t urange = b - a;
+  uint64_t ret;
+  if (urngrange > urange) {
+    const uint64_t uerange = urange + 1;
+    const uint64_t scaling = urngrange / uerange;
+    const uint64_t past = uerange * scaling;
+    do ret = (uint64_t)lcg_next(st) - 1ull; while (ret >= past);
+    ret /= scaling;
+  } else {
+    ret = (uint64_t)lcg_next(st) - 1ull;   // urange == urngrange (grids are far smaller)
+  }
+  return ret + a;
+}
+// std::shuffle(first, first + n, minstd_rand0) as libstdc++ implements it
+// (bits/stl_algo.h): when the engine range allows, positions are drawn two at a time
+// from one uniform_int over [0, (k + 1)(k + 2) - 1] (__gen_two_uniform_ints), with a
+// single leading {0, 1} draw for even n.  Shuffling indices permutes exactly like
+// shuffling the elements.
+__device__ void shuffle_minstd(uint16_t* v, int n, uint32_t& st) {
+  if (n <= 0) return;
+  const uint64_t urngrange = 2147483645ull, urange = (uint64_t)n;
+  if (urngrange / urange >= urange) {
+    int i = 1;
+    if ((urange % 2) == 0) {
+      const int j = (int)uid_minstd(st, 0, 1);
+      const uint16_t t = v[i]; v[i] = v[j]; v[j] = t;
+      i++;
+    }
+    while (i != n) {
+      const uint64_t r = (uint64_t)i + 1;
+      const uint64_t x = uid_minstd(st, 0, r * (r + 1) - 1);
+      const int p1 = (int)(x / (r + 1)), p2 = (int)(x % (r + 1));
+      uint16_t t = v[i]; v[i] = v[p1]; v[p1] = t;
+      i++;
+      t = v[i]; v[i] = v[p2]; v[p2] = t;
+      i++;
+    }
+  } else {
+    for (int i = 1; i < n; i++) {
+      const int j = (int)uid_minstd(st, 0, (uint64_t)i);
+      const uint16_t t = v[i]; v[i] = v[j]; v[j] = t;
+    }
+  }
+}
+// luke::Box2d (customtypes.h:35-172): corners counter-clockwise from bottom-left
+struct Box2 { double x[4], y[4]; };
+__device__ void box_init_centre(Box2& b, double cx, double cy, double width, double height) {
+  const double hw = width / 2.0, hh = height / 2.0;
+  b.x[0] = cx - hw; b.y[0] = cy - hh;
+  b.x[1] = cx + hw; b.y[1] = cy - hh;
+  b.x[2] = cx + hw; b.y[2] = cy + hh;
+  b.x[3] = cx - hw; b.y[3] = cy + hh;
+}
+__device__ void box_rotate(Box2& b, double theta) {
+  const double cx = (b.x[0] + b.x[1] + b.x[2] + b.x[3]) / 4.0;
+  const double cy = (b.y[0] + b.y[1] + b.y[2] + b.y[3]) / 4.0;
+  const double c = cos(theta), s = sin(theta);
+  for (int i = 0; i < 4; i++) {
+    const double nx = cx + (b.x[i] - cx) * c - (b.y[i] - cy) * s;
+    const double ny = cy + (b.x[i] - cx) * s + (b.y[i] - cy) * c;
+    b.x[i] = nx; b.y[i] = ny;
+  }
+}
+__device__ bool box_inbounds(const Box2& b, double xmin, double ymin, double xmax, double ymax) {
+  for (int i = 0; i < 4; i++)
+    if (b.x[i] < xmin || b.x[i] > xmax || b.y[i] < ymin || b.y[i] > ymax) return false;
+  return true;
+}
+// Box2d::overlapsWith: SAT over this box's four edge normals only, with the reference's
+// "containsOther" bookkeeping (true only if no axis separates by more than zero)
+__device__ bool box_overlaps(const Box2& a, const Box2& o, double gap) {
+  bool contains = true;
+  for (int i = 0; i < 4; i++) {
+    const int j = (i + 1) % 4;
+    double px = -(a.y[j] - a.y[i]), py = a.x[j] - a.x[i];
+    const double len = sqrt(px * px + py * py);
+    px /= len; py /= len;
+    double min1 = a.x[0] * px + a.y[0] * py, max1 = min1;
+    double min2 = o.x[0] * px + o.y[0] * py, max2 = min2;
+    for (int k = 1; k < 4; k++) {
+      const double p1 = a.x[k] * px + a.y[k] * py;
+      const double p2 = o.x[k] * px + o.y[k] * py;
+      if (p1 < min1) min1 = p1;
+      if (p1 > max1) max1 = p1;
+      if (p2 < min2) min2 = p2;
+      if (p2 > max2) max2 = p2;
+    }
+    if (max1 + gap < min2 || max2 + gap < min1) return false;
+    if (max1 < min2 || max2 < min1) contains = false;
+  }
+  return contains;
+}
+// "Task object i" xyz bounding box (objecthandler.cpp:91-110): full extents of the
+// synthetic object's geom (the MJCF numerics are unavailable)
+__device__ __host__ inline void object_bbox(const gm_object& o, double* xyz) {
+  if (o.type == GM_GEOM_BOX) { xyz[0] = 2 * o.size[0]; xyz[1] = 2 * o.size[1]; xyz[2] = 2 * o.size[2]; }
+  else if (o.type == GM_GEOM_CYLINDER) { xyz[0] = xyz[1] = 2 * o.size[0]; xyz[2] = 2 * o.size[1]; }
+  else { xyz[0] = xyz[1] = xyz[2] = 2 * o.size[0]; }
+}
+// returns 1 and spawns on success; 0 when no candidate pose is free
+__device__ int spawn_into_scene_dev(GmEnvState& s, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
+                                    const gm_object* __restrict__ objs, int n_objects, const gm_spawn_params& p,
+                                    int index) {
+  const int num_x = (int)(((2 * p.xrange) / p.xy_increment) + 1);
+  const int num_y = (int)(((2 * p.yrange) / p.xy_increment) + 1);
+  const int num_r = (int)(((2 * p.rotrange) / p.rot_increment) + 1);
+  const int nxy = num_x * num_y;
+  if (num_x < 1 || num_y < 1 || num_r < 1 || nxy > GM_SPAWN_MAX_XY || num_r > GM_SPAWN_MAX_ROT) return 0;
+  uint16_t pxy[GM_SPAWN_MAX_XY], prot[GM_SPAWN_MAX_ROT];
+  for (int i = 0; i < nxy; i++) pxy[i] = (uint16_t)i;
+  for (int i = 0; i < num_r; i++) prot[i] = (uint16_t)i;
+  if (nxy > 1) shuffle_minstd(pxy, nxy, s.rng);
+  if (num_r > 1) shuffle_minstd(prot, num_r, s.rng);
+  // object footprint
+  int oi = index;
+  if (oi < 0 || oi >= n_objects) oi = 0;
+  double bb[3];
+  object_bbox(objs[oi], bb);
+  // initial fingertip boxes: Env::reset (mjclass.h:895-904) from
+  // get_finger_hook_locations (myfunctions.cpp:3717-3761), straight fingers at the target
+  Box2 tips[3];
+  {
+    const double PI_23 = M_PI * (2.0 / 3.0);
+    const double angles[3] = {0.0, PI_23, 2 * PI_23};
+    const double fing_x = s.end.x;
+    const double hook_th = m->hook_angle_degrees * (M_PI / 180.000);
+    for (int i = 0; i < 3; i++) {
+      const double hook_x = 0.5 * m->hook_length * sin(hook_th);
+      const double x = -(fing_x - hook_x) * sin(angles[i]) + s.base[0];
+      const double y = -(fing_x - hook_x) * cos(angles[i]) + s.base[1];
+      box_init_centre(tips[i], x, y, m->finger_width, m->hook_length);
+      box_rotate(tips[i], -angles[i]);
+    }
+  }
+  const int total = nxy > num_r ? nxy : num_r;
+  int ixy = -1, ir = -1;
+  for (int i = 0; i < total; i++) {
+    ixy += 1; ir += 1;
+    if (ixy >= nxy) ixy = 0;
+    if (ir >= num_r) ir = 0;
+    const int kx = pxy[ixy] / num_y, ky = pxy[ixy] % num_y;
+    const double px = num_x > 1 ? -p.xrange + kx * p.xy_increment + p.x : p.x;
+    const double py = num_y > 1 ? -p.yrange + ky * p.xy_increment + p.y : p.y;
+    const double pr = num_r > 1 ? -p.rotrange + prot[ir] * p.rot_increment + p.zrot : p.zrot;
+    Box2 ob;
+    box_init_centre(ob, px, py, bb[0], bb[1]);
+    box_rotate(ob, pr);
+    if (!box_inbounds(ob, p.xmin, p.ymin, p.xmax, p.ymax)) continue;
+    bool good = true;
+    for (int f = 0; f < 3 && good; f++)
+      if (box_overlaps(ob, tips[f], p.smallest_gap)) good = false;
+    if (!good) continue;
+    spawn_object(s, T, objs, n_objects, gm_spawn{index, px, py, pr});
+    return 1;
+  }
+  return 0;
+}
+
+extern "C" __global__ void gm_spawn_into_scene_kernel(GmEnvState* __restrict__ states, const gm_model* __restrict__ m,
+                                                      const GmTopo* __restrict__ T, const gm_object* __restrict__ objs,
+                                                      int n_objects, const uint8_t* __restrict__ mask,
+                                                      const gm_spawn_params* __restrict__ params, int n_params,
+                                                      uint8_t* __restrict__ ok, int n_envs) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n_envs) return;
+  if (mask && !mask[env]) { if (ok) ok[env] = 0; return; }
+  const gm_spawn_params p = params[n_params == 1 ? 0 : env];
+  const int r = spawn_into_scene_dev(states[env], m, T, objs, n_objects, p, p.index);
+  if (ok) ok[env] = (uint8_t)r;
+}
+
 extern "C" __global__ void gm_autoreset_mask_kernel(const GmEnvState* __restrict__ states,
                                                     const uint8_t* __restrict__ done, int max_steps,
                                                     uint8_t* __restrict__ mask, float* __restrict__ returns,
@@ -2597,7 +2776,8 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
                                            const gm_config* __restrict__ C, const GmTopo* __restrict__ T,
                                            const double* __restrict__ eq_qpos, const uint8_t* __restrict__ mask,
                                            const gm_spawn* __restrict__ spawn, const gm_object* __restrict__ objs,
-                                           int n_objects, int n_envs) {
+                                           int n_objects, int n_envs, const gm_spawn_params* __restrict__ scene,
+                                           int scene_tries) {
   int env = blockIdx.x * blockDim.x + threadIdx.x;
   if (env >= n_envs) return;
   if (mask && !mask[env]) return;
@@ -2643,7 +2823,14 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
     if (s.base[2] < C->base_min[2]) s.base[2] = C->base_min[2];
     s.qpos[m->dof_base] = s.base[2] + eq_qpos[m->dof_base];
   }
-  spawn_object(s, T, objs, n_objects, spawn ? spawn[env] : gm_spawn{0, 0.0, 0.0, 0.0});
+  const gm_spawn sp = spawn ? spawn[env] : gm_spawn{0, 0.0, 0.0, 0.0};
+  if (scene) {
+    // MjEnv._spawn_object (MjEnv.py:1177-1267): spawn_into_scene up to scene_tries times,
+    // then the "old method" pose from the spawn table
+    for (int t = 0; t < scene_tries; t++)
+      if (spawn_into_scene_dev(s, m, T, objs, n_objects, *scene, sp.object_index)) return;
+  }
+  spawn_object(s, T, objs, n_objects, sp);
 }
 
 // settle initialisation (keyframe, targets home, locks off, flags true) for env 0

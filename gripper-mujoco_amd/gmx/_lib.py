@@ -114,6 +114,21 @@ class Spawn(C.Structure):
                 ("zrot", C.c_double)]
 
 
+class SpawnParams(C.Structure):
+    """MjType::SpawnParams (mjclass.h:916-931; bind.cpp:411-430): same field names."""
+    _fields_ = [("index", C.c_int32), ("pad", C.c_int32), ("x", C.c_double), ("y", C.c_double),
+                ("zrot", C.c_double), ("xrange", C.c_double), ("yrange", C.c_double),
+                ("rotrange", C.c_double), ("xmin", C.c_double), ("xmax", C.c_double),
+                ("ymin", C.c_double), ("ymax", C.c_double), ("smallest_gap", C.c_double),
+                ("xy_increment", C.c_double), ("rot_increment", C.c_double)]
+
+
+def default_spawn_params() -> "SpawnParams":
+    p = SpawnParams()
+    load_library().gm_default_spawn_params(C.byref(p))
+    return p
+
+
 _lib = None
 
 
@@ -139,7 +154,7 @@ def load_library(path: str | None = None):
             "(run `python -c 'import __graft_entry__ as g; g.build()'` from the repo root)")
     lib = C.CDLL(p)
     _declare(lib)
-    sizes = {0: Settings, 3: Object, 4: Spawn, 5: ModelParams}
+    sizes = {0: Settings, 3: Object, 4: Spawn, 5: ModelParams, 6: SpawnParams}
     for which, cls in sizes.items():
         n = lib.gm_struct_size(which)
         if n != C.sizeof(cls):
@@ -191,6 +206,9 @@ def _declare(lib):
         "gm_step_profiled": (i32, [vp, C.POINTER(C.c_uint64)]),
         "gm_set_stream": (i32, [vp, vp]),
         "gm_spawn_object": (i32, [vp, vp, vp]),
+        "gm_default_spawn_params": (None, [vp]),
+        "gm_spawn_into_scene": (i32, [vp, u8p, vp, i32, u8p]),
+        "gm_set_scene_spawn": (i32, [vp, vp, i32]),
         "gm_autoreset": (i32, [vp, i32, vp, i32, vp]),
         "gm_device_reset_mask": (vp, [vp]),
         "gm_policy_create": (i32, [vp, i32p, i32, f32p, C.POINTER(vp)]),

@@ -11,7 +11,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import (load_library, ModelBlob, ConfigBlob, ModelParams, Spawn, make_object_set,
+from ._lib import (load_library, ModelBlob, ConfigBlob, ModelParams, Spawn, SpawnParams, make_object_set,
                    BINARY_EVENTS, LINEAR_EVENTS)
 from .settings import canonical_settings, MAX_EPISODE_STEPS
 
@@ -102,6 +102,28 @@ class BatchedGripperEnv:
             self._check(self.lib.gm_reset(self._ctx, None, spawn))
             self.current_step[:] = 0
         return self.observation()
+
+    def spawn_into_scene(self, params, mask=None):
+        """MjClass::spawn_into_scene(SpawnParams) on the device (mjclass.cpp:2475-2654).
+        params: one SpawnParams (shared) or a sequence of n_envs.  Returns ok[n_envs]
+        (True where the object was placed)."""
+        if isinstance(params, SpawnParams):
+            arr, n = (SpawnParams * 1)(params), 1
+        else:
+            arr = (SpawnParams * len(params))(*params)
+            n = len(params)
+        ok = np.zeros(self.n_envs, dtype=np.uint8)
+        m = None
+        if mask is not None:
+            m = np.ascontiguousarray(np.asarray(mask, dtype=np.uint8))
+        self._check(self.lib.gm_spawn_into_scene(self._ctx, None if m is None else m.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                                 arr, n, ok.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return ok.astype(bool)
+
+    def set_scene_spawn(self, params, max_tries: int = 3):
+        """Resets place objects with spawn_into_scene (MjEnv._spawn_object: up to max_tries
+        attempts, then the spawn table pose); params=None restores plain spawn_object."""
+        self._check(self.lib.gm_set_scene_spawn(self._ctx, None if params is None else C.byref(params), int(max_tries)))
 
     def set_action(self, actions):
         a = np.ascontiguousarray(np.asarray(actions, dtype=np.float32).reshape(self.n_envs, self.n_actions))

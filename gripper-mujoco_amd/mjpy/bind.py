@@ -31,21 +31,13 @@ import gmx
 from gmx._lib import BINARY_EVENTS, LINEAR_EVENTS
 
 
-class SpawnParams:
-    """MjType::SpawnParams (mjclass.h:916-931)."""
+class SpawnParams(gmx.SpawnParams):
+    """MjType::SpawnParams (mjclass.h:916-931; bind.cpp:411-430): r/w fields with the
+    reference's names and defaults, laid out as the C ABI's gm_spawn_params."""
 
     def __init__(self):
-        self.index = -1
-        self.x = 0.0
-        self.y = 0.0
-        self.zrot = 0.0
-        self.xrange = 0.0
-        self.yrange = 0.0
-        self.rotrange = 0.0
-        self.xmin, self.xmax, self.ymin, self.ymax = -100.0, 100.0, -100.0, 100.0
-        self.smallest_gap = 1e-3
-        self.xy_increment = 2e-3
-        self.rot_increment = math.pi / 30.0
+        super().__init__()
+        gmx.load_library().gm_default_spawn_params(C.byref(self))
 
 
 class _BinaryEvent:
@@ -248,25 +240,25 @@ class MjClass:
         self._spawned = int(idx)
 
     def spawn_into_scene(self, index, xpos=None, ypos=None, zrot=None, xrange=None, yrange=None,
-                         rotrange=None):
-        """MjClass::spawn_into_scene (mjclass.cpp:2475-2654) with default_spawn_params:
-        a pose on the xy_increment / rot_increment grid inside the ranges.  The
-        reference's fingertip-overlap (Box2d SAT) rejection loop is not reproduced
-        (DESIGN.md, next rows); always returns True."""
-        p = self.default_spawn_params
-        x0 = p.x if xpos is None else xpos
-        y0 = p.y if ypos is None else ypos
-        r0 = p.zrot if zrot is None else zrot
-        xr = p.xrange if xrange is None else xrange
-        yr = p.yrange if yrange is None else yrange
-        rr = p.rotrange if rotrange is None else rotrange
-        nx = int(round(xr / p.xy_increment)); ny = int(round(yr / p.xy_increment))
-        nr = int(round(rr / p.rot_increment))
-        x = x0 + p.xy_increment * int(self._rng.integers(-nx, nx + 1))
-        y = y0 + p.xy_increment * int(self._rng.integers(-ny, ny + 1))
-        r = r0 + p.rot_increment * int(self._rng.integers(-nr, nr + 1))
-        self.spawn_object(index, x, y, r)
-        return True
+                         rotrange=None) -> bool:
+        """MjClass::spawn_into_scene (mjclass.cpp:2422-2654; the four bind.cpp:100-103
+        overloads): default_spawn_params with the given overrides, the shuffled xy /
+        rotation grid search with Box2d rejection against the fingertips and the scene
+        bounds, run on the device.  Returns False when no free pose exists."""
+        env = self._ensure()
+        p = SpawnParams()
+        C.memmove(C.byref(p), C.byref(self.default_spawn_params), C.sizeof(p))
+        p.index = int(index)
+        if xpos is not None: p.x = float(xpos)
+        if ypos is not None: p.y = float(ypos)
+        if zrot is not None: p.zrot = float(zrot)
+        if xrange is not None: p.xrange = float(xrange)
+        if yrange is not None: p.yrange = float(yrange)
+        if rotrange is not None: p.rotrange = float(rotrange)
+        ok = bool(env.spawn_into_scene(p)[0])
+        if ok:
+            self._spawned = int(index)
+        return ok
 
     def set_new_base_XY(self, x: float, y: float):
         self._base_xy = (float(x), float(y))
@@ -335,7 +327,7 @@ class MjClass:
     def __getstate__(self):
         return {"set": bytes(self.set), "params": bytes(self._params) if self._params is not None else None,
                 "object_set_name": self.object_set_name, "model_folder_path": self.model_folder_path,
-                "machine": self.machine}
+                "machine": self.machine, "default_spawn_params": bytes(self.default_spawn_params)}
 
     def __setstate__(self, st):
         self.__init__(st.get("model_folder_path"))
@@ -344,3 +336,5 @@ class MjClass:
             self._params = gmx.ModelParams.from_buffer_copy(st["params"])
         self.object_set_name = st["object_set_name"]
         self.machine = st["machine"]
+        if st.get("default_spawn_params") is not None:
+            C.memmove(C.byref(self.default_spawn_params), st["default_spawn_params"], C.sizeof(SpawnParams))

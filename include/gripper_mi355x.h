@@ -272,6 +272,21 @@ typedef struct gm_spawn {
   double  x, y, zrot;
 } gm_spawn;
 
+/* spawn search request: MjType::SpawnParams (mjclass.h:916-931), defaults as there
+ * (gm_default_spawn_params).  The xy grid holds at most GM_SPAWN_MAX_XY points and the
+ * rotation grid GM_SPAWN_MAX_ROT (gm_spawn_into_scene rejects larger grids). */
+typedef struct gm_spawn_params {
+  int32_t index;
+  int32_t pad;
+  double  x, y, zrot;
+  double  xrange, yrange, rotrange;
+  double  xmin, xmax, ymin, ymax;
+  double  smallest_gap;
+  double  xy_increment, rot_increment;
+} gm_spawn_params;
+#define GM_SPAWN_MAX_XY  1024
+#define GM_SPAWN_MAX_ROT 256
+
 /* ------------------------------------------------------------ C ABI */
 typedef struct gm_ctx gm_ctx;
 
@@ -279,7 +294,7 @@ typedef struct gm_ctx gm_ctx;
 const char* gm_version(void);
 int  gm_device_count(void);
 /* sizes of the interface structs (0 settings, 1 model, 2 config, 3 object, 4 spawn,
- * 5 model params) so bindings can verify their layouts */
+ * 5 model params, 6 spawn params) so bindings can verify their layouts */
 int64_t gm_struct_size(int which);
 /* model summary: nq, nv, nbody, ngeom, npair, n_seg, dof_base, dof_palm, dof_obj,
  * dof_pris[3], dof_rev[3], dof_seg[3], nlock, nM (tree-sparse M nonzeros)  (20 int32) */
@@ -318,6 +333,26 @@ int  gm_reset(gm_ctx* ctx, const uint8_t* mask, const gm_spawn* spawn);
 /* MjClass::spawn_object(idx, x, y, zrot) alone (mjclass.cpp:2352-2420; bind.cpp:98-105):
  * replaces the live object of masked envs; consumes no RNG draws.  Host arrays. */
 int  gm_spawn_object(gm_ctx* ctx, const uint8_t* mask, const gm_spawn* spawn);
+/* MjType::SpawnParams defaults (mjclass.h:916-931). */
+void gm_default_spawn_params(gm_spawn_params* p);
+/* MjClass::spawn_into_scene(SpawnParams) (mjclass.cpp:2475-2654; bind.cpp:100-103) on the
+ * device for envs with mask[e] != 0 (NULL = all): the xy and rotation grids are shuffled
+ * with std::shuffle semantics on the env's RNG stream, every candidate pose is tested with
+ * the Box2d SAT rules (customtypes.h:35-172) against the scene bounds and the initial
+ * fingertip boxes (Env::reset, mjclass.h:895-904, from get_finger_hook_locations,
+ * myfunctions.cpp:3717-3761), and the object is spawned at the first free pose
+ * (spawn_object).  params: n_params == 1 (shared) or n_envs entries.  ok[e] = 1 when
+ * spawned, 0 when no pose is free (state unchanged apart from the RNG draws, as in the
+ * reference); ok may be NULL.  Host arrays.  The device env holds one live object, so
+ * the reference's loop over objects already in the scene is empty (MjEnv._spawn_object
+ * spawns one object per reset). */
+int  gm_spawn_into_scene(gm_ctx* ctx, const uint8_t* mask, const gm_spawn_params* params, int n_params,
+                         uint8_t* ok);
+/* Make gm_reset / gm_autoreset place each reset env's object the way MjEnv._spawn_object
+ * does (MjEnv.py:1177-1267): spawn_into_scene(spawn[e].object_index) with *params, up to
+ * max_tries attempts, falling back to spawn_object(spawn[e]) (MjEnv's "old method").
+ * params == NULL restores plain spawn_object(spawn[e]). */
+int  gm_set_scene_spawn(gm_ctx* ctx, const gm_spawn_params* params, int max_tries);
 
 /* MjClass::set_continous_action for every action index i in order
  * (mjclass.cpp:1517-1630; called per index by MjEnv._set_action, MjEnv.py:591-594).

@@ -1878,6 +1878,153 @@ void or_spawn(or_env* e, const gm_spawn* sp) {
   for (int k = 0; k < 7; k++) e->start_qpos[k] = e->qpos[qa + k];
 }
 
+/* =====================================================================
+ * MjClass::spawn_into_scene(SpawnParams) (mjclass.cpp:2475-2654)
+ * ===================================================================== */
+/* std::uniform_int_distribution<unsigned long>{a, b}(minstd_rand0) as libstdc++
+ * implements it (bits/uniform_int_dist.h): engine range 2^31 - 3 takes the
+ * downscaling two-division rejection path */
+static uint64_t uid_minstd(uint32_t* st, uint64_t a, uint64_t b) {
+  const uint64_t urngrange = 2147483646ull - 1ull, urange = b - a;
+  uint64_t ret;
+  if (urngrange > urange) {
+    const uint64_t uerange = urange + 1, scaling = urngrange / uerange, past = uerange * scaling;
+    do ret = (uint64_t)lcg_next(st) - 1ull; while (ret >= past);
+    ret /= scaling;
+  } else {
+    ret = (uint64_t)lcg_next(st) - 1ull;
+  }
+  return ret + a;
+}
+/* std::shuffle with minstd_rand0 as libstdc++ implements it (bits/stl_algo.h):
+ * positions drawn in pairs (__gen_two_uniform_ints) when the engine range allows,
+ * one leading {0,1} draw for an even count */
+static void shuffle_minstd(int* v, int n, uint32_t* st) {
+  if (n <= 0) return;
+  const uint64_t urngrange = 2147483645ull, urange = (uint64_t)n;
+  int t;
+  if (urngrange / urange >= urange) {
+    int i = 1;
+    if (urange % 2 == 0) { int j = (int)uid_minstd(st, 0, 1); t = v[i]; v[i] = v[j]; v[j] = t; i++; }
+    while (i != n) {
+      uint64_t r = (uint64_t)i + 1, x = uid_minstd(st, 0, r * (r + 1) - 1);
+      int p1 = (int)(x / (r + 1)), p2 = (int)(x % (r + 1));
+      t = v[i]; v[i] = v[p1]; v[p1] = t; i++;
+      t = v[i]; v[i] = v[p2]; v[p2] = t; i++;
+    }
+  } else {
+    for (int i = 1; i < n; i++) { int j = (int)uid_minstd(st, 0, (uint64_t)i); t = v[i]; v[i] = v[j]; v[j] = t; }
+  }
+}
+/* luke::Box2d (customtypes.h:35-172) */
+typedef struct { double x[4], y[4]; } box2_t;
+static void box_init_centre(box2_t* b, double cx, double cy, double w, double h) {
+  double hw = w / 2.0, hh = h / 2.0;
+  b->x[0] = cx - hw; b->y[0] = cy - hh; b->x[1] = cx + hw; b->y[1] = cy - hh;
+  b->x[2] = cx + hw; b->y[2] = cy + hh; b->x[3] = cx - hw; b->y[3] = cy + hh;
+}
+static void box_rotate(box2_t* b, double th) {
+  double cx = (b->x[0] + b->x[1] + b->x[2] + b->x[3]) / 4.0, cy = (b->y[0] + b->y[1] + b->y[2] + b->y[3]) / 4.0;
+  for (int i = 0; i < 4; i++) {
+    double nx = cx + (b->x[i] - cx) * cos(th) - (b->y[i] - cy) * sin(th);
+    double ny = cy + (b->x[i] - cx) * sin(th) + (b->y[i] - cy) * cos(th);
+    b->x[i] = nx; b->y[i] = ny;
+  }
+}
+static int box_inbounds(const box2_t* b, double xmin, double ymin, double xmax, double ymax) {
+  for (int i = 0; i < 4; i++) if (b->x[i] < xmin || b->x[i] > xmax || b->y[i] < ymin || b->y[i] > ymax) return 0;
+  return 1;
+}
+static int box_overlaps(const box2_t* a, const box2_t* o, double gap) {
+  int contains = 1;
+  for (int i = 0; i < 4; i++) {
+    int j = (i + 1) % 4;
+    double px = -(a->y[j] - a->y[i]), py = a->x[j] - a->x[i];
+    double len = sqrt(px * px + py * py);
+    px /= len; py /= len;
+    double min1 = a->x[0] * px + a->y[0] * py, max1 = min1, min2 = o->x[0] * px + o->y[0] * py, max2 = min2;
+    for (int k = 1; k < 4; k++) {
+      double p1 = a->x[k] * px + a->y[k] * py, p2 = o->x[k] * px + o->y[k] * py;
+      if (p1 < min1) min1 = p1;
+      if (p1 > max1) max1 = p1;
+      if (p2 < min2) min2 = p2;
+      if (p2 > max2) max2 = p2;
+    }
+    if (max1 + gap < min2 || max2 + gap < min1) return 0;
+    if (max1 < min2 || max2 < min1) contains = 0;
+  }
+  return contains;
+}
+/* "Task object i" bounding box (objecthandler.cpp:91-110): full geom extents */
+static void object_bbox(const gm_object* o, double* xyz) {
+  if (o->type == GM_GEOM_BOX) { xyz[0] = 2 * o->size[0]; xyz[1] = 2 * o->size[1]; xyz[2] = 2 * o->size[2]; }
+  else if (o->type == GM_GEOM_CYLINDER) { xyz[0] = xyz[1] = 2 * o->size[0]; xyz[2] = 2 * o->size[1]; }
+  else { xyz[0] = xyz[1] = xyz[2] = 2 * o->size[0]; }
+}
+int or_spawn_into_scene(or_env* e, const gm_spawn_params* p) {
+  int num_x = (int)(((2 * p->xrange) / p->xy_increment) + 1);
+  int num_y = (int)(((2 * p->yrange) / p->xy_increment) + 1);
+  int num_r = (int)(((2 * p->rotrange) / p->rot_increment) + 1);
+  int nxy = num_x * num_y;
+  if (num_x < 1 || num_y < 1 || num_r < 1 || nxy > GM_SPAWN_MAX_XY || num_r > GM_SPAWN_MAX_ROT) return 0;
+  int pxy[GM_SPAWN_MAX_XY], prot[GM_SPAWN_MAX_ROT];
+  for (int i = 0; i < nxy; i++) pxy[i] = i;
+  for (int i = 0; i < num_r; i++) prot[i] = i;
+  if (nxy > 1) shuffle_minstd(pxy, nxy, &e->rng);
+  if (num_r > 1) shuffle_minstd(prot, num_r, &e->rng);
+  int oi = p->index;
+  if (oi < 0 || oi >= e->nobj) oi = 0;
+  double bb[3];
+  object_bbox(&e->objs[oi], bb);
+  /* Env::reset (mjclass.h:895-904) + get_finger_hook_locations (myfunctions.cpp:3717-3761) */
+  box2_t tips[3];
+  const double PI_23 = PI_D * (2.0 / 3.0);
+  const double angles[3] = {0.0, PI_23, 2 * PI_23};
+  double hook_th = e->m.hook_angle_degrees * (PI_D / 180.000);
+  for (int i = 0; i < 3; i++) {
+    double hook_x = 0.5 * e->m.hook_length * sin(hook_th);
+    double x = -(e->end.x - hook_x) * sin(angles[i]) + e->base[0];
+    double y = -(e->end.x - hook_x) * cos(angles[i]) + e->base[1];
+    box_init_centre(&tips[i], x, y, e->m.finger_width, e->m.hook_length);
+    box_rotate(&tips[i], -angles[i]);
+  }
+  int total = nxy > num_r ? nxy : num_r, ixy = -1, ir = -1;
+  for (int i = 0; i < total; i++) {
+    ixy += 1; ir += 1;
+    if (ixy >= nxy) ixy = 0;
+    if (ir >= num_r) ir = 0;
+    int kx = pxy[ixy] / num_y, ky = pxy[ixy] % num_y;
+    double px = num_x > 1 ? -p->xrange + kx * p->xy_increment + p->x : p->x;
+    double py = num_y > 1 ? -p->yrange + ky * p->xy_increment + p->y : p->y;
+    double pr = num_r > 1 ? -p->rotrange + prot[ir] * p->rot_increment + p->zrot : p->zrot;
+    box2_t ob;
+    box_init_centre(&ob, px, py, bb[0], bb[1]);
+    box_rotate(&ob, pr);
+    if (!box_inbounds(&ob, p->xmin, p->ymin, p->xmax, p->ymax)) continue;
+    int good = 1;
+    for (int f = 0; f < 3 && good; f++) if (box_overlaps(&ob, &tips[f], p->smallest_gap)) good = 0;
+    if (!good) continue;
+    gm_spawn sp = {p->index, px, py, pr};
+    or_spawn(e, &sp);
+    return 1;
+  }
+  return 0;
+}
+/* golden-vector hooks: libstdc++ std::shuffle / Box2d restatements */
+uint32_t or_std_shuffle(uint32_t seed, int n, int32_t* out) {
+  uint32_t st = lcg_seed(seed);
+  for (int i = 0; i < n; i++) out[i] = i;
+  shuffle_minstd(out, n, &st);
+  return lcg_next(&st);   /* the engine's next draw: pins how many draws the shuffle used */
+}
+int or_box2d_overlaps(const double* a5, const double* b5, double gap) {
+  /* boxes as (cx, cy, w, h, rot): initCentre then rotate */
+  box2_t a, b;
+  box_init_centre(&a, a5[0], a5[1], a5[2], a5[3]); box_rotate(&a, a5[4]);
+  box_init_centre(&b, b5[0], b5[1], b5[2], b5[3]); box_rotate(&b, b5[4]);
+  return box_overlaps(&a, &b, gap);
+}
+
 void or_reset(or_env* e, const gm_spawn* sp) {
   const gm_model* m0 = &e->m;
   /* luke::reset: targets home, locks off, keyframe, object parked */

@@ -35,6 +35,7 @@ size_t  or_sizeof(void);
 
 void  or_reset(or_env* e, const gm_spawn* spawn);
 void  or_spawn(or_env* e, const gm_spawn* spawn);                  /* MjClass::spawn_object alone */
+int   or_spawn_into_scene(or_env* e, const gm_spawn_params* p);    /* MjClass::spawn_into_scene */
 void  or_set_action(or_env* e, const float* actions);              /* set_continous_action x n_actions */
 void  or_set_discrete_action(or_env* e, int32_t action);           /* set_discrete_action */
 void  or_step(or_env* e);                                          /* action_step */
@@ -59,6 +60,8 @@ double or_minstd_next_canonical_double(uint32_t* state);              /* generat
 float  or_polyfit_eval(const double* X, const double* Y, int P, int order, double x);
 void   or_gauge_points(const gm_model* m, const double* q, double* X, double* Y);
 void   or_ring_trace(const float* adds, int n_adds, int n_reads, float* out);
+uint32_t or_std_shuffle(uint32_t seed, int n, int32_t* out);     /* std::shuffle, minstd_rand0 */
+int    or_box2d_overlaps(const double* a5, const double* b5, double gap);   /* Box2d::overlapsWith */
 int    or_grip_step_sequence(const double* cmds, int n, double* out);  /* Gripper golden driver */
 int    or_sample(int mode, const float* window_recent_first, int n_avail, int prev_steps,
                  int readings_per_step, float* out);                  /* Sensor::*_sample */

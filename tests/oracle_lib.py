@@ -58,6 +58,9 @@ def lib():
             "or_polyfit_eval": (C.c_float, [f64p, f64p, i32, i32, C.c_double]),
             "or_gauge_points": (None, [vp, f64p, f64p, f64p]),
             "or_ring_trace": (None, [f32p, i32, i32, f32p]),
+            "or_spawn_into_scene": (i32, [vp, vp]),
+            "or_std_shuffle": (C.c_uint32, [C.c_uint32, i32, i32p]),
+            "or_box2d_overlaps": (i32, [f64p, f64p, C.c_double]),
         }
         for n, (r, a) in sig.items():
             f = getattr(L, n)
@@ -95,6 +98,10 @@ class OracleEnv:
 
     def reset(self, spawn):
         self.L.or_reset(self.h, C.byref(spawn))
+
+    def spawn_into_scene(self, params) -> bool:
+        """MjClass::spawn_into_scene(SpawnParams) (mjclass.cpp:2475-2654)."""
+        return bool(self.L.or_spawn_into_scene(self.h, C.byref(params)))
 
     def set_action(self, a):
         a = _f32(a)
@@ -218,6 +225,20 @@ def ring_trace(adds, n_reads):
     lib().or_ring_trace(a.ctypes.data_as(C.POINTER(C.c_float)), len(a), n_reads,
                         out.ctypes.data_as(C.POINTER(C.c_float)))
     return out
+
+
+def std_shuffle(seed, n):
+    """libstdc++ std::shuffle of [0, n) with minstd_rand0(seed); returns (perm, next draw)."""
+    out = np.zeros(max(n, 1), dtype=np.int32)
+    nxt = lib().or_std_shuffle(seed, n, out.ctypes.data_as(C.POINTER(C.c_int32)))
+    return out[:n].tolist(), int(nxt)
+
+
+def box2d_overlaps(a5, b5, gap):
+    """luke::Box2d::overlapsWith for boxes given as (cx, cy, w, h, rot)."""
+    a = np.ascontiguousarray(a5, dtype=np.float64); b = np.ascontiguousarray(b5, dtype=np.float64)
+    return bool(lib().or_box2d_overlaps(a.ctypes.data_as(C.POINTER(C.c_double)),
+                                        b.ctypes.data_as(C.POINTER(C.c_double)), gap))
 
 
 def minstd_raw(seed, n):

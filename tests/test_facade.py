@@ -37,9 +37,21 @@ def test_facade_pickle_roundtrip(gm):
     mj = MjClass()
     mj.set = gm.canonical_settings(seed=9)
     mj.object_set_name = "set1_synthetic"
+    mj.default_spawn_params.xrange = 7e-3
     mj2 = pickle.loads(pickle.dumps(mj))
     assert bytes(mj2.set) == bytes(mj.set)
     assert mj2.object_set_name == "set1_synthetic"
+    assert mj2.default_spawn_params.xrange == 7e-3
+
+
+def test_facade_spawn_params_defaults(gm):
+    """MjType::SpawnParams member defaults (mjclass.h:916-931)."""
+    import math
+    from mjpy.bind import MjClass
+    p = MjClass().default_spawn_params
+    assert (p.index, p.x, p.y, p.zrot, p.xrange, p.yrange, p.rotrange) == (-1, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0)
+    assert (p.xmin, p.xmax, p.ymin, p.ymax) == (-100, 100, -100, 100)
+    assert p.smallest_gap == 1e-3 and p.xy_increment == 2e-3 and p.rot_increment == math.pi / 30.0
 
 
 def test_facade_without_gpu_fails_loudly(gm):
@@ -49,6 +61,32 @@ def test_facade_without_gpu_fails_loudly(gm):
     mj = MjClass()
     with pytest.raises(RuntimeError):
         mj.reset()
+
+
+@pytest.mark.gpu
+def test_facade_spawn_into_scene_matches_oracle(gm):
+    """MjEnv._spawn_object's call (MjEnv.py:1211-1223): default_spawn_params with 10 mm
+    xy noise and pi/2 rotation range, spawn_into_scene(idx) -> True, pose as the oracle."""
+    import oracle_lib
+    from mjpy.bind import MjClass
+    mj = MjClass()
+    mj.set = gm.canonical_settings(noise=False, seed=6)
+    mj.reset()
+    mj.default_spawn_params.xrange = mj.default_spawn_params.yrange = 10e-3
+    mj.default_spawn_params.rotrange = np.pi / 2.0
+    assert mj.spawn_into_scene(2) is True
+    env = mj._env
+    o = oracle_lib.OracleEnv(env.model, env.cfg, env.objects, 0)
+    sp = gm.Spawn()
+    sp.object_index, sp.x, sp.y, sp.zrot = 0, 0.0, 0.0, 0.0
+    o.reset(sp)
+    p = gm.default_spawn_params()
+    p.index, p.xrange, p.yrange, p.rotrange = 2, 10e-3, 10e-3, np.pi / 2.0
+    assert o.spawn_into_scene(p)
+    q, _, _ = env.state()
+    qo, _, _ = o.state()
+    qa = env.model.nq - 7
+    np.testing.assert_array_equal(q[0][qa:qa + 7], qo[qa:qa + 7].astype(np.float32))
 
 
 @pytest.mark.gpu

@@ -75,6 +75,38 @@ def test_rng_matches_libstdcxx(seed):
     np.testing.assert_array_equal(d, np.array(r["double_pm0.01"]))
 
 
+@pytest.mark.parametrize("seed", ["1", "5", "1234", "1000004", "2147483646"])
+def test_std_shuffle_matches_libstdcxx(seed):
+    """std::shuffle(grid, minstd_rand0) as spawn_into_scene draws it (mjclass.cpp:2533-2536):
+    the permutation and the engine position afterwards, against libstdc++ itself."""
+    r = load("rng.json")[seed]
+    for key in r:
+        if not key.startswith("shuffle") or key.endswith("_next"):
+            continue
+        n = int(key[len("shuffle"):])
+        perm, nxt = oracle_lib.std_shuffle(int(seed), n)
+        assert perm == [int(x) for x in r[key]], key
+        assert nxt == int(r[key + "_next"][0]), key
+
+
+def test_box2d_overlap_known_answers():
+    """luke::Box2d::overlapsWith (customtypes.h:83-131) by hand: SAT over this box's own
+    edge normals; a positive separation smaller than the gap counts as *no* overlap
+    (the containsOther flag), only a separation above the gap returns early."""
+    ov = oracle_lib.box2d_overlaps
+    sq = lambda cx, cy, rot=0.0: (cx, cy, 0.02, 0.02, rot)
+    assert ov(sq(0, 0), sq(0.01, 0), 1e-3)            # half overlapping
+    assert ov(sq(0, 0), sq(0, 0), 0.0)                # identical
+    assert ov(sq(0, 0), sq(0.02, 0), 0.0)             # touching edges (max1 == min2)
+    assert not ov(sq(0, 0), sq(0.021, 0), 5e-3)       # 1 mm apart, inside the 5 mm gap
+    assert not ov(sq(0, 0), sq(0.03, 0), 5e-3)        # 10 mm apart, beyond the gap
+    assert ov(sq(0, 0), sq(0.0, 0.015, np.pi / 4), 0.0)
+    # only this box's axes are tested: a rotated box whose corner region misses
+    # is still reported as overlapping when no own axis separates them
+    assert ov(sq(0, 0), (0.0205, 0.0205, 0.02, 0.02, np.pi / 4), 0.0)
+    assert not ov((0.0205, 0.0205, 0.02, 0.02, np.pi / 4), sq(0, 0), 0.0)
+
+
 def test_gauge_polyfit_vs_numpy():
     """read_armadillo_gauge's cubic least-squares fit (myfunctions.cpp:2739) against
     numpy.polyfit on the same points, evaluated at 50 mm (in mm)."""

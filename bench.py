@@ -58,6 +58,17 @@ def algorithmic_bytes_per_substep(model, ncon: int = NCON_NOMINAL) -> dict:
     return {"bytes": sum(parts.values()), "ncon": ncon, "nefc": nefc, "parts": parts}
 
 
+def mjenv_spawn_params(gmx):
+    """default_spawn_params as MjEnv._spawn_object sets them (MjEnv.py:1211-1215):
+    +-10 mm xy on the 2 mm grid, +-pi/2 rotation on the pi/30 grid; resets place the
+    object with spawn_into_scene on the device (3 tries, then the spawn-table pose)."""
+    import math
+    p = gmx.default_spawn_params()
+    p.xrange = p.yrange = 10e-3
+    p.rotrange = math.pi / 2.0
+    return p
+
+
 def load_traffic(n_envs: int):
     """HBM bytes per launch of gm_step_kernel from the committed rocprofv3 PMC pass
     (profiles/*pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950 guide)."""
@@ -156,6 +167,7 @@ def policy_rollout(gmx, torch, dev, stream, n: int, steps: int, seed: int, env_o
     env = gmx.BatchedGripperEnv(n, object_set="set6_synthetic", settings=s, seed=seed, env_offset=env_offset,
                                 device=dev.index)
     env.set_stream(stream.cuda_stream)
+    env.set_scene_spawn(mjenv_spawn_params(gmx), max_tries=3)
     spawn = env.make_spawn()
     env.reset(spawn=spawn)
     spawn_ptr = env.upload_spawn(spawn)
@@ -230,6 +242,7 @@ def main():
     torch.cuda.set_stream(stream)
     env.set_stream(stream.cuda_stream)
     S = env.cfg.sim_steps_per_action
+    env.set_scene_spawn(mjenv_spawn_params(gmx), max_tries=3)
     spawn = env.make_spawn()
     env.reset(spawn=spawn)
     spawn_ptr = env.upload_spawn(spawn)
@@ -296,8 +309,9 @@ def main():
             "steps": K, "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "C3: set6_synthetic 20 mixed objects, randomised spawn, random "
-                                   "actions U[-1,1]^4, canonical sensor/reward config, device auto-reset",
+            "config": {"workload": "C3: set6_synthetic 20 mixed objects, randomised spawn (spawn_into_scene "
+                                   "grid search on the device), random actions U[-1,1]^4, canonical "
+                                   "sensor/reward config, device auto-reset",
                        "envs_per_gpu": n, "global_envs": world * n, "substeps_per_env_step": S,
                        "parallelism": f"env-shard x{world}",
                        "B_substep_bytes": B["bytes"], "B_substep_ncon": B["ncon"], "B_substep_nefc": B["nefc"],

@@ -1983,10 +1983,10 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
   PH(8);
 }
 
-// All substeps of one env-step in one outlined call: one register allocation for the
-// substep loop, callee-saved registers spilled once per env-step (not per substep),
-// address spaces re-established at entry so the body uses global loads for the model
-// and LDS instructions for the per-env image instead of generic (flat) accesses.
+// Why per substep: outlining the whole substep loop instead (physics + update_all +
+// monitor_sensors in one call, callee-saved registers spilled once per env-step) was
+// measured slower -- 12.6 vs 10.0 ms per 4096-env step, the larger body allocates worse
+// (kinematics and the factor roughly doubled); inlining everything spills more still.
 #define GM_AS_GLOBAL __attribute__((address_space(1)))
 #define GM_AS_LDS __attribute__((address_space(3)))
 // One substep, outlined: its own register allocation (the fused kernel around it keeps

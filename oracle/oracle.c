@@ -2145,7 +2145,15 @@ static void* bench_worker(void* arg) {
     e->env_id = k;
     e->rng = lcg_seed((uint64_t)j->c->s.random_seed + (uint64_t)k * 1000003ull);
     gm_spawn sp = {k % (j->n_objects > 0 ? j->n_objects : 1), 0.0, 0.0, 0.0};
-    or_reset(e, &sp);
+    /* MjEnv._spawn_object (MjEnv.py:1211-1223): +-10 mm, +-pi/2 grid search, 3 tries */
+    gm_spawn_params sc;
+    memset(&sc, 0, sizeof(sc));
+    sc.index = sp.object_index;
+    sc.xrange = sc.yrange = 10e-3; sc.rotrange = PI_D / 2.0;
+    sc.xmin = sc.ymin = -100; sc.xmax = sc.ymax = 100;
+    sc.smallest_gap = 1e-3; sc.xy_increment = 2e-3; sc.rot_increment = PI_D / 30.0;
+#define BENCH_RESET() do { or_reset(e, &sp); for (int tr = 0; tr < 3; tr++) if (or_spawn_into_scene(e, &sc)) break; } while (0)
+    BENCH_RESET();
     uint64_t x = j->seed + (uint64_t)k * 0x9E3779B97F4A7C15ull;
     for (int t = 0; t < j->n_steps; t++) {
       float a[8];
@@ -2160,8 +2168,9 @@ static void* bench_worker(void* arg) {
       int d = or_is_done(e);
       or_reward(e);
       j->done_steps++;
-      if (d) or_reset(e, &sp);
+      if (d) BENCH_RESET();
     }
+#undef BENCH_RESET
   }
   free(e);
   return NULL;

@@ -9,12 +9,23 @@
 
 #include <cstddef>
 #include <cstdio>
+#include <cmath>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
 #include "gm_kernels.hip"
 #include "gm_policy.hip"
+
+// calibration translation unit (gm_calib.hip)
+hipError_t gm_cal_launch_step(int n_seg, int n_envs, hipStream_t st, GmEnvState* states, const gm_model* m,
+                              const gm_config* C, const GmTopo* T);
+hipError_t gm_cal_launch_setup(hipStream_t st, GmEnvState* states, const double* dt, const int32_t* steps, double tip,
+                               int n);
+hipError_t gm_cal_launch_read(hipStream_t st, const GmEnvState* states, uint8_t* bad, int n);
+hipError_t gm_cal_launch_gauge(int n_seg, hipStream_t st, const GmEnvState* states, const gm_model* m, const GmTopo* T,
+                               int env, float* out);
 
 struct gm_ctx {
   int device = 0;
@@ -62,11 +73,6 @@ int fail(gm_ctx* c, int code, const std::string& msg) {
       return fail(ctx, GM_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_));    \
   } while (0)
 
-// gm_step_kernel is instantiated per finger chain length (CL = n_seg + 2) so every chain
-// recursion is unrolled into registers; GM_NSEG_LIST is the set compiled in.
-#ifndef GM_NSEG_LIST
-#define GM_NSEG_LIST X(5) X(6) X(7) X(8) X(9) X(10)
-#endif
 bool nseg_supported(int n) {
   switch (n) {
 #define X(N) case N:
@@ -83,14 +89,16 @@ hipError_t launch_step(gm_ctx* c, int grid, int n_envs, int mode, DebugOut dbg) 
   switch (c->model.n_seg) {
 #define X(N)                                                                                               \
   case N:                                                                                                  \
-    hipLaunchKernelGGL((gm_step_kernel<N + 2>), dim3(grid), dim3(NT), 0, c->stream, c->d_state, c->d_model, \
-                       c->d_cfg, c->d_topo, c->d_obs, c->d_rew, c->d_done, n_envs, mode, dbg, order, cost); \
+    hipLaunchKernelGGL((gm_step_kernel<N + 2, false>), dim3(grid), dim3(NT), 0, c->stream, c->d_state,      \
+                       c->d_model, c->d_cfg, c->d_topo, c->d_obs, c->d_rew, c->d_done, n_envs, mode, dbg,    \
+                       order, cost);                                                                         \
     return hipGetLastError();
     GM_NSEG_LIST
 #undef X
     default: return hipErrorInvalidValue;
   }
 }
+
 
 int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
   std::memset(&T, 0, sizeof(T));
@@ -131,7 +139,6 @@ int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
   T.lane_body[50] = T.body_obj;
   // per-dof constants: the engine-spec H~ diagonal additions and PD gains
   // (mj_step2 implicit terms and luke::control gains, oracle.c ctrl_gains / step2)
-  const double h = m.timestep;
   for (int d = 0; d < m.nv; d++) {
     const int b = m.dof_body[d], j = m.body_jnt[b];
     T.dof_body[d] = b;
@@ -146,9 +153,12 @@ int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
     if (d == m.dof_palm) { kp = m.kp_gripper[2]; kd = m.kd_gripper[2]; tgt = 3; }
     if (d == m.dof_base) { kp = m.kp_base[2]; kd = m.kd_base[2]; tgt = 4; }
     const bool free = m.jnt_type[j] == GM_JNT_FREE;
-    double add = m.jnt_armature[j] + h * (m.jnt_damping[j] + kd);
-    if (!free) add += h * h * (m.jnt_stiffness[j] + kp);
+    double add = m.jnt_armature[j] + m.timestep * (m.jnt_damping[j] + kd);
+    if (!free) add += m.timestep * m.timestep * (m.jnt_stiffness[j] + kp);
     T.dof_add[d] = add;
+    T.dof_arm[d] = m.jnt_armature[j];
+    T.dof_dsum[d] = m.jnt_damping[j] + kd;
+    T.dof_ksum[d] = free ? 0.0 : m.jnt_stiffness[j] + kp;
     T.dof_stiff[d] = free ? 0.0 : m.jnt_stiffness[j];
     T.dof_damp[d] = m.jnt_damping[j];
     T.dof_kp[d] = kp; T.dof_kd[d] = kd; T.dof_target[d] = tgt;
@@ -247,7 +257,7 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   HIPCHK(c, hipMemcpyAsync(c->d_eq, reinterpret_cast<char*>(c->d_state) + offsetof(GmEnvState, qpos), sizeof(double) * GM_MAX_QPOS, hipMemcpyDeviceToDevice, c->stream));
   int threads = 256, blocks = (n_envs + threads - 1) / threads;
   hipLaunchKernelGGL(gm_init_envs_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, cfg->s.random_seed,
-                     (long long)env_offset, n_envs);
+                     (long long)env_offset, n_envs, c->model.timestep);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return GM_OK;
@@ -386,6 +396,182 @@ int gm_set_scene_spawn(gm_ctx* c, const gm_spawn_params* params, int max_tries) 
   HIPCHK(c, hipMemcpyAsync(c->d_scene, params, sizeof(gm_spawn_params), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->scene_tries = max_tries;
+  return GM_OK;
+}
+
+// ---------------------------------------------------------------- calibration
+namespace {
+uint32_t fbits(float x) { uint32_t u; std::memcpy(&u, &x, 4); return u; }
+
+// calc_yield_point_load (myfunctions.cpp:3587-3595), float where the reference is float
+float yield_point_load(const gm_model& m) {
+  const double I = (m.finger_width * std::pow(m.finger_thickness, 3)) / 12.0;
+  const float M_max = (m.yield_stress * I) / (0.5 * m.finger_thickness);
+  const float F_max = M_max / m.finger_length;
+  return F_max;
+}
+
+struct CalCtx {
+  gm_ctx* c = nullptr;
+  int nb = 0;
+  double* d_dt = nullptr;
+  int32_t* d_steps = nullptr;
+  uint8_t* d_bad = nullptr;
+  float* d_gauge = nullptr;
+  std::vector<gm_spawn> spawn;
+  ~CalCtx() {
+    if (c) { (void)hipFree(d_dt); (void)hipFree(d_steps); (void)hipFree(d_bad); (void)hipFree(d_gauge); gm_destroy(c); }
+  }
+  // reset the first n envs (object 0 at the origin, as MjClass::reset leaves the scene),
+  // give env i timestep dt[i], steps[i] substeps and the tip load, run them, read BADQACC
+  int run(const std::vector<double>& dt, const std::vector<int32_t>& steps, double tip, std::vector<uint8_t>& bad,
+          bool reset = true) {
+    const int n = (int)dt.size();
+    if (n == 0) return GM_OK;
+    if (reset) {
+      std::vector<uint8_t> mask(nb, 0);
+      for (int i = 0; i < n; i++) mask[i] = 1;
+      int rc = gm_reset(c, mask.data(), spawn.data());
+      if (rc != GM_OK) return rc;
+    }
+    HIPCHK(c, hipMemcpyAsync(d_dt, dt.data(), sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(d_steps, steps.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, gm_cal_launch_setup(c->stream, c->d_state, d_dt, d_steps, tip, n));
+    HIPCHK(c, gm_cal_launch_step(c->model.n_seg, n, c->stream, c->d_state, c->d_model, c->d_cfg, c->d_topo));
+    HIPCHK(c, gm_cal_launch_read(c->stream, c->d_state, d_bad, n));
+    bad.assign(n, 0);
+    HIPCHK(c, hipMemcpyAsync(bad.data(), d_bad, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return GM_OK;
+  }
+};
+}  // namespace
+
+int gm_calibrate(const gm_model* model, const gm_config* cfg, const gm_object* objects, int n_objects, int device,
+                 int what, gm_calibration* out, double* trace_dt, uint8_t* trace_unstable, int max_trace) {
+  if (!model || !cfg || !objects || !out || n_objects <= 0) return GM_E_ARG;
+  std::memset(out, 0, sizeof(*out));
+  gm_config cc = *cfg;
+  cc.s.base_position_noise = 0;          // calibration runs from the same reset pose
+  CalCtx k;
+  k.nb = 64;
+  int rc = gm_create(model, &cc, objects, n_objects, k.nb, 0, device, 0, &k.c);
+  if (rc != GM_OK) return rc;
+  gm_ctx* c = k.c;
+  HIPCHK(c, hipMalloc(&k.d_dt, sizeof(double) * k.nb));
+  HIPCHK(c, hipMalloc(&k.d_steps, sizeof(int32_t) * k.nb));
+  HIPCHK(c, hipMalloc(&k.d_bad, k.nb));
+  HIPCHK(c, hipMalloc(&k.d_gauge, sizeof(float)));
+  k.spawn.assign(k.nb, gm_spawn{0, 0.0, 0.0, 0.0});
+
+  double timestep = model->timestep;
+  if (what & GM_CAL_TIMESTEP) {
+    // find_highest_stable_timestep (mjclass.cpp:4745-4854) replayed over batched results:
+    // unknown candidates along the predicted path (coarse: stable, fine: unstable) are
+    // simulated together, one env each, then the reference's sequence is replayed
+    const float coarse_increment = 0.5e-3f, fine_increment = 50e-6f, start_value = 1.0e-3f;
+    const float test_time = 1.0f, max_allowable_timestep = 20.0e-3f, tune_param = 1.0f;
+    std::map<uint32_t, uint8_t> memo;
+    std::vector<std::pair<float, uint8_t>> trace;
+    float found = 0;
+    for (int round = 0; round < 1000; round++) {
+      std::vector<float> unknown;
+      trace.clear();
+      float next = start_value;
+      bool coarse_pass = true;
+      int status = 1;   // 0 done, -1 no stable timestep, 1 need evaluations
+      for (int guard = 0; guard < 100000; guard++) {
+        uint8_t unstable;
+        auto it = memo.find(fbits(next));
+        if (it != memo.end()) unstable = it->second;
+        else {
+          unknown.push_back(next);
+          if ((int)unknown.size() >= k.nb) break;
+          unstable = coarse_pass ? 0 : 1;
+        }
+        trace.push_back({next, unstable});
+        if (unstable) { if (coarse_pass) coarse_pass = false; next -= fine_increment; }
+        else { if (coarse_pass) next += coarse_increment; else { status = 0; found = next; break; } }
+        if (next < fine_increment) { status = -1; break; }
+        if (next > max_allowable_timestep) { next = max_allowable_timestep; coarse_pass = false; }
+      }
+      if (unknown.empty()) {
+        if (status == -1) {
+          fprintf(stderr, "gm_calibrate: no stable timestep found for the simulation\n");
+          return GM_E_RANGE;
+        }
+        if (status == 0) break;
+      }
+      std::vector<double> dts(unknown.size());
+      std::vector<int32_t> steps(unknown.size());
+      for (size_t i = 0; i < unknown.size(); i++) {
+        dts[i] = unknown[i];
+        steps[i] = (int32_t)((test_time / unknown[i]) + 1);
+      }
+      std::vector<uint8_t> bad;
+      rc = k.run(dts, steps, 0.0, bad);
+      if (rc != GM_OK) return rc;
+      for (size_t i = 0; i < unknown.size(); i++) memo[fbits(unknown[i])] = bad[i];
+    }
+    float factor;
+    if (found <= 3.0e-3) factor = tune_param * 0.8;
+    else if (found < 5.0e-3) factor = tune_param * 0.75;
+    else if (found < 10.0e-3) factor = tune_param * 0.65;
+    else factor = tune_param * 0.65;
+    float final_timestep = found * factor;
+    final_timestep = (float)((int)(final_timestep * 1e6) * 1e-6);
+    out->search_timestep = found;
+    out->n_tested = (int32_t)trace.size();
+    for (int i = 0; i < (int)trace.size() && i < max_trace; i++) {
+      if (trace_dt) trace_dt[i] = trace[i].first;
+      if (trace_unstable) trace_unstable[i] = trace[i].second;
+    }
+    timestep = final_timestep;
+  }
+  out->timestep = timestep;
+  if (what & GM_CAL_GAUGES) {
+    // calibrate_simulated_sensors (mjclass.cpp:4643-4676): 0.3 s settle (wrist Z offset
+    // from userdata[2], never written: 0), then validate_curve_under_force
+    // (mjclass.cpp:4023-4105) with the saturation tip load for 50 s, 0.8x timestep retries
+    const float yield = yield_point_load(*model);
+    const float bend_gauge_normalise = cc.s.saturation_yield_factor * yield;
+    double tsd = timestep;                 // s_.mujoco_timestep (double in simsettings.h:29)
+    const float settle_time = 0.3f;
+    std::vector<uint8_t> bad;
+    rc = k.run({tsd}, {(int32_t)(settle_time / tsd)}, 0.0, bad);
+    if (rc != GM_OK) return rc;
+    const float time_to_settle = 50;
+    const int steps_to_make = (int)(time_to_settle / tsd);
+    int repeats_done = 1;
+    bool first = true;
+    while (true) {
+      rc = k.run({tsd}, {steps_to_make}, (double)bend_gauge_normalise, bad, !first);
+      if (rc != GM_OK) return rc;
+      first = false;
+      if (bad[0]) {
+        tsd *= 0.8;
+        repeats_done += 1;
+        if (repeats_done > 5) {
+          fprintf(stderr, "gm_calibrate: curve validation unstable\n");
+          return GM_E_RANGE;
+        }
+        continue;
+      }
+      break;
+    }
+    HIPCHK(c, gm_cal_launch_gauge(c->model.n_seg, c->stream, c->d_state, c->d_model, c->d_topo, 0, k.d_gauge));
+    float normalise = 0;
+    HIPCHK(c, hipMemcpyAsync(&normalise, k.d_gauge, sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    out->yield_load = yield;
+    out->bend_gauge_normalise = bend_gauge_normalise;
+    out->bending_normalise = normalise;
+    out->sim_gauge_raw_to_N_factor = bend_gauge_normalise / normalise;
+    out->wrist_Z_offset = 0.0f;
+    out->gauge_retries = repeats_done - 1;
+    out->timestep = tsd;
+  }
+  out->sim_steps_per_action = (int32_t)std::ceil(cc.s.time_for_action / out->timestep);
   return GM_OK;
 }
 

@@ -234,6 +234,10 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
     // finger body frame: x down the finger, y radially outward, z = x cross y
     double xb[3] = {0, 0, -1};
     double yb[3] = {r[0], r[1], r[2]};
+    // tip load direction (apply_segment_force rotates its pull into the finger's rest
+    // frame so it bends the finger, myfunctions.cpp:1700-1722): here the bending
+    // direction is the finger frame's +y, radially outward, at every keyframe pose
+    for (int k = 0; k < 3; k++) m->tip_dir[f][k] = r[k];
     double zb[3] = {xb[1] * yb[2] - xb[2] * yb[1], xb[2] * yb[0] - xb[0] * yb[2],
                     xb[0] * yb[1] - xb[1] * yb[0]};
     double R[9] = {xb[0], yb[0], zb[0], xb[1], yb[1], zb[1], xb[2], yb[2], zb[2]};
@@ -285,6 +289,7 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
       int d = B.add_joint(bs, GM_JNT_HINGE, axs, seg_stiffness(k), 0.05, 0, parent_dof);
       if (k == 1) m->dof_seg[f] = d;
       B.add_geom(bs, GM_GEOM_BOX, GM_CLS_FINGER1 + f, gpos, id4, gsz, 1.0);
+      if (last) m->body_tip[f] = bs;
       if (last) {
         double hpos[3] = {Ls + 0.5 * p->hook_length * std::cos(th_h),
                           -0.5 * p->hook_length * std::sin(th_h), 0};
@@ -371,6 +376,7 @@ int64_t gm_struct_size(int which) {
     case 4: return (int64_t)sizeof(gm_spawn);
     case 5: return (int64_t)sizeof(gm_model_params);
     case 6: return (int64_t)sizeof(gm_spawn_params);
+    case 7: return (int64_t)sizeof(gm_calibration);
     default: return -1;
   }
 }

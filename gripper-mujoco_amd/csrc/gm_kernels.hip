@@ -24,6 +24,11 @@
 #include "gm_state.h"
 
 #define NT 64
+// gm_step_kernel is instantiated per finger chain length (CL = n_seg + 2) so every chain
+// recursion is unrolled into registers; GM_NSEG_LIST is the set compiled in.
+#ifndef GM_NSEG_LIST
+#define GM_NSEG_LIST X(5) X(6) X(7) X(8) X(9) X(10)
+#endif
 #define CLMAX (GM_MAX_SEG + 2)
 #define TRI(p, q) ((p) * ((p) + 1) / 2 + (q))
 #define TRIF ((CLMAX + 1) * (CLMAX + 2) / 2)
@@ -615,14 +620,22 @@ __device__ __forceinline__ void ctrl_gains(const gm_model* __restrict__ m, const
 }
 
 // lane per dof: H row entries (compact), bias/passive/actuator force
-template <int CL>
+// CAL: the calibration variant (per-env timestep, tip load); the env-step kernel is CAL = false
+template <int CL, bool CAL>
 __device__ void mass_and_forces(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
   if (lane < T->nv) {
     const int d = lane;
     const int b = T->dof_body[d];
     const int c = T->dof_grp[d];
     const int p = T->dof_p[d];
-    const real add = T->dof_add[d];
+    real add;
+    if constexpr (CAL) {   // H~ diagonal for this env's timestep (same operations as the host fold)
+      const real h = S.s.dt;
+      add = T->dof_arm[d] + h * T->dof_dsum[d];
+      add += h * h * T->dof_ksum[d];
+    } else {
+      add = T->dof_add[d];
+    }
     real cd[6], F[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
@@ -661,7 +674,28 @@ __device__ void mass_and_forces(SharedT<CL>& S, const gm_model* __restrict__ m, 
       const real target = tgt == 1 ? S.s.next.x : tgt == 2 ? S.s.next.th : tgt == 3 ? S.s.next.z : S.s.base[2];
       act = -((qp - target) * T->dof_kp[d] + qv * T->dof_kd[d]);
     }
-    S.frc[d] = pas + act - bias;
+    real frc = pas + act - bias;
+    if (CAL && S.s.tip_force != 0.0 && (c < 3 || c == GM_GRP_BASE)) {
+      // calibration tip load: resolve_segment_forces -> apply_segment_force
+      // (myfunctions.cpp:1642-1727) pulls each finger's tip link at its centre of mass
+      // along the finger's rest bending direction; J^T F for the dofs above that link
+#pragma unroll
+      for (int f = 0; f < 3; f++) {
+        if (c < 3 && f != c) continue;
+        const int bt = m->body_tip[f];
+        real R[9], ip[3], pc[3], wxp[3];
+        body_R(S, bt, R);
+        ld3(ip, m->body_ipos[bt]);
+        mulmv3(pc, R, ip);
+        pc[0] += S.xpos[bt][0]; pc[1] += S.xpos[bt][1]; pc[2] += S.xpos[bt][2];
+        const real F[3] = {S.s.tip_force * m->tip_dir[f][0], S.s.tip_force * m->tip_dir[f][1],
+                           S.s.tip_force * m->tip_dir[f][2]};
+        cross3(wxp, cd, pc);
+        const real col[3] = {cd[3] + wxp[0], cd[4] + wxp[1], cd[5] + wxp[2]};
+        frc += dot3(col, F);
+      }
+    }
+    S.frc[d] = frc;
   }
   __syncthreads();
 }
@@ -1353,7 +1387,7 @@ __device__ __forceinline__ real impedance(const gm_model* __restrict__ m, real r
   return dmin + y * (dmax - dmin);
 }
 
-template <int CL>
+template <int CL, bool CAL>
 __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                             bool prof = false) {
   unsigned long long t0 = prof ? clock64() : 0;
@@ -1453,7 +1487,7 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
   }
   PH(13);
   // impedance / reference acceleration (mj_makeImpedance)
-  real h = m->timestep;
+  real h = CAL ? S.s.dt : m->timestep;
   real tc = m->solref[0];
   if (tc < 2 * h) tc = 2 * h;
   real dr = m->solref[1], dmax = m->solimp[1];
@@ -1579,9 +1613,15 @@ __device__ void constraint_accel(SharedT<CL>& S, const GmTopo* __restrict__ T, i
 }
 
 // ============================================================ integrate
-template <int CL>
+template <int CL, bool CAL>
 __device__ void integrate(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
-  real h = (real)m->timestep;
+  const real h = CAL ? S.s.dt : m->timestep;
+  if constexpr (CAL) {
+    // mj_checkAcc's mjWARN_BADQACC (is_sim_unstable, myfunctions.cpp:4233-4242): a
+    // non-finite or |qacc| > mjMAXVAL acceleration; sticky until the next reset
+    const bool bad = lane < T->nv && !(fabs(S.qacc[lane]) <= 1e10);
+    if (__ballot(bad) != 0ull && lane == 0) S.s.badqacc = 1;
+  }
   if (lane < T->nv) S.s.qvel[lane] += h * S.qacc[lane];
   __syncthreads();
   if (lane < T->nv && lane < T->dof_obj) {
@@ -1600,7 +1640,7 @@ __device__ void integrate(SharedT<CL>& S, const gm_model* __restrict__ m, const 
       quatmul(q, q, dq);
     }
     quatnorm(q);
-    S.s.time += m->timestep;
+    S.s.time += h;
   }
   __syncthreads();
 }
@@ -1958,7 +1998,7 @@ __device__ void monitor_sensors(SharedT<CL>& S, const gm_model* __restrict__ m, 
 }
 
 // ============================================================ one full substep
-template <int CL>
+template <int CL, bool CAL>
 __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
                                                      int lane, bool prof) {
   unsigned long long t0 = prof ? clock64() : 0;
@@ -1967,7 +2007,7 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
   PH(0);
   crb_rne<CL>(S, m, T, lane, prof);
   PH(1);
-  mass_and_forces(S, m, T, lane);
+  mass_and_forces<CL, CAL>(S, m, T, lane);
   PH(2);
   factor<CL>(S, T, lane);
   PH(3);
@@ -1975,11 +2015,11 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
   PH(4);
   collision(S, m, T, lane);
   PH(5);
-  constraints<CL>(S, m, T, lane, prof);
+  constraints<CL, CAL>(S, m, T, lane, prof);
   PH(6);
   constraint_accel<CL>(S, T, lane);
   PH(7);
-  integrate(S, m, T, lane);
+  integrate<CL, CAL>(S, m, T, lane);
   PH(8);
 }
 
@@ -1993,10 +2033,10 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
 // the env-step epilogue's state), parameters typed with their address spaces so the body
 // issues global loads for the model and LDS instructions for the per-env image rather
 // than generic (flat) accesses that would serialise the two.
-template <int CL>
+template <int CL, bool CAL>
 __device__ __noinline__ void physics_substep(GM_AS_LDS SharedT<CL>* S_, const GM_AS_GLOBAL gm_model* m_,
                                              const GM_AS_GLOBAL GmTopo* T_, int lane, bool prof) {
-  physics_substep_body<CL>(*(SharedT<CL>*)S_, (const gm_model*)m_, (const GmTopo*)T_, lane, prof);
+  physics_substep_body<CL, CAL>(*(SharedT<CL>*)S_, (const gm_model*)m_, (const GmTopo*)T_, lane, prof);
 }
 
 // ============================================================ env-step epilogue (lane 0)
@@ -2313,7 +2353,7 @@ __device__ __forceinline__ void store_state(const SharedT<CL>& S, GmEnvState* __
 
 // mode 0: action_step + obs/done/reward; mode 1: calibrate_reset settle (400 substeps,
 // no sensors); mode 2: one full substep with diagnostics
-template <int CL>
+template <int CL, bool CAL>
 __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
     GmEnvState* __restrict__ states, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
     const GmTopo* __restrict__ T, float* __restrict__ obs, float* __restrict__ rew,
@@ -2329,23 +2369,33 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
   const unsigned long long t_start = cost ? __builtin_amdgcn_s_memtime() : 0;
   load_state(S, states + env, lane);
   const bool settle = (mode == 1);          // calibrate_reset settle: 400 substeps, no sensors
+  const bool calib = CAL;                   // calibration run (mode 3): S.s.cal_steps substeps, no sensors
   const bool prof = !settle && dbg.phase != nullptr;
   if (prof && lane < GM_NPHASE) S.tph[lane] = 0;
   const unsigned long long t_kernel = prof ? clock64() : 0;
   __syncthreads();
-  const int nsub = settle ? 400 : (mode == 2) ? 1 : C->sim_steps_per_action + S.s.extra_substeps;
+  const int nsub = settle ? 400 : calib ? S.s.cal_steps : (mode == 2) ? 1 : C->sim_steps_per_action + S.s.extra_substeps;
+  // a calibration run starts from a reset's mj_forward pose
+  if (calib && lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
   for (int i = 0; i < nsub; i++) {
+    if (calib && S.s.tip_force != 0.0 && lane < T->nlock && m->lock_kind[lane] == 0) {
+      // apply_segment_force locks the prismatic motors every step (set_constraint,
+      // myfunctions.cpp:1679-1685), anchored at the last mj_step1 pose
+      S.s.lock_active[lane] = 1;
+      S.s.lock_q[lane] = S.lock_pre[lane];
+    }
     const unsigned long long tc = prof ? clock64() : 0;
-    physics_substep<CL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m, (const GM_AS_GLOBAL GmTopo*)T,
+    physics_substep<CL, CAL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m, (const GM_AS_GLOBAL GmTopo*)T,
                         lane, prof);
     unsigned long long t0 = prof ? clock64() : 0;
     if (prof && lane == 0) S.tph[22] += t0 - tc;   // whole outlined call (phases 0-8 + call overhead)
     update_all(S, m, T, lane);
     PH(9);
-    if (!settle) monitor_sensors<CL>(S, m, C, T, lane);
+    if (!settle && !calib) monitor_sensors<CL>(S, m, C, T, lane);
     PH(10);
+    if (calib && S.s.badqacc) break;   // is_sim_unstable: the reference stops this run
   }
-  if (settle) {
+  if (settle || calib) {
     store_state(S, states + env, lane);
     return;
   }
@@ -2405,6 +2455,7 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
 // (shader clocks / 64, written by gm_step_kernel), bucketed into 256 cost classes.
 // One 1024-thread workgroup; the order only changes which env a workgroup slot runs
 // first, never any result.
+#ifndef GM_CAL_TU   // env-step translation unit only
 extern "C" __global__ __launch_bounds__(1024) void gm_dispatch_order_kernel(const uint32_t* __restrict__ cost,
                                                                             int32_t* __restrict__ order, int n) {
   __shared__ uint32_t cnt[256];
@@ -2433,6 +2484,7 @@ extern "C" __global__ __launch_bounds__(1024) void gm_dispatch_order_kernel(cons
     order[atomicAdd(&cnt[b], 1u)] = i;
   }
 }
+#endif
 
 // ---------------------------------------------------------------- actions
 // MjClass::set_action for every action index (mjclass.cpp:1528-1630); one thread per env.
@@ -2514,6 +2566,7 @@ __device__ void set_action_one(GmEnvState& s, const gm_model* __restrict__ m, co
   s.bev_value[GM_EV_exceed_limits] = s.bev_value[GM_EV_exceed_limits] || !wl;
 }
 
+#ifndef GM_CAL_TU   // env-step translation unit only
 extern "C" __global__ void gm_action_kernel(GmEnvState* __restrict__ states, const gm_model* __restrict__ m,
                                             const gm_config* __restrict__ C, const float* __restrict__ cont,
                                             const int32_t* __restrict__ disc, int n_envs) {
@@ -2530,6 +2583,7 @@ extern "C" __global__ void gm_action_kernel(GmEnvState* __restrict__ states, con
     set_action_one(s, m, C, disc[env], 0.0f);
   }
 }
+#endif
 
 // ---------------------------------------------------------------- reset + spawn
 // MjClass::spawn_object -> ObjectHandler::spawn_object (mjclass.cpp:2352-2420,
@@ -2745,6 +2799,7 @@ __device__ int spawn_into_scene_dev(GmEnvState& s, const gm_model* __restrict__ 
   return 0;
 }
 
+#ifndef GM_CAL_TU   // env-step translation unit only
 extern "C" __global__ void gm_spawn_into_scene_kernel(GmEnvState* __restrict__ states, const gm_model* __restrict__ m,
                                                       const GmTopo* __restrict__ T, const gm_object* __restrict__ objs,
                                                       int n_objects, const uint8_t* __restrict__ mask,
@@ -2757,7 +2812,9 @@ extern "C" __global__ void gm_spawn_into_scene_kernel(GmEnvState* __restrict__ s
   const int r = spawn_into_scene_dev(states[env], m, T, objs, n_objects, p, p.index);
   if (ok) ok[env] = (uint8_t)r;
 }
+#endif
 
+#ifndef GM_CAL_TU   // env-step translation unit only
 extern "C" __global__ void gm_autoreset_mask_kernel(const GmEnvState* __restrict__ states,
                                                     const uint8_t* __restrict__ done, int max_steps,
                                                     uint8_t* __restrict__ mask, float* __restrict__ returns,
@@ -2769,9 +2826,11 @@ extern "C" __global__ void gm_autoreset_mask_kernel(const GmEnvState* __restrict
   mask[env] = r;
   if (returns) returns[env] = r ? s.cumulative_reward : __builtin_nanf("");
 }
+#endif
 
 // MjClass::reset (mjclass.cpp:434-486) -> luke::reset / calibrate_reset (non-first call),
 // configure_settings RNG draws, random_base_Z_movement, then spawn_object.
+#ifndef GM_CAL_TU   // env-step translation unit only
 extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, const gm_model* __restrict__ m,
                                            const gm_config* __restrict__ C, const GmTopo* __restrict__ T,
                                            const double* __restrict__ eq_qpos, const uint8_t* __restrict__ mask,
@@ -2791,6 +2850,7 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
   g_reset(s.end); g_reset(s.next);
   for (int k = 0; k < GM_MAX_QPOS; k++) s.qpos[k] = m->qpos0[k];
   s.time = 0; s.last_step_time = 0;
+  s.dt = m->timestep;
   for (int d = 0; d < T->nv; d++) {
     bool motor = (d == m->dof_base || d == m->dof_palm);
     for (int f = 0; f < 3; f++) motor = motor || d == m->dof_pris[f] || d == m->dof_rev[f];
@@ -2832,8 +2892,10 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
   }
   spawn_object(s, T, objs, n_objects, sp);
 }
+#endif
 
 // settle initialisation (keyframe, targets home, locks off, flags true) for env 0
+#ifndef GM_CAL_TU   // env-step translation unit only
 extern "C" __global__ void gm_settle_init_kernel(GmEnvState* __restrict__ states, const gm_model* __restrict__ m,
                                                  const GmTopo* __restrict__ T, const gm_object* __restrict__ objs) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -2842,6 +2904,7 @@ extern "C" __global__ void gm_settle_init_kernel(GmEnvState* __restrict__ states
   for (int i = 0; i < GM_STATE_WORDS; i++) w[i] = 0;
   g_reset(s.end); g_reset(s.next);
   for (int k = 0; k < GM_MAX_QPOS; k++) s.qpos[k] = m->qpos0[k];
+  s.dt = m->timestep;
   s.old_x = s.old_y = s.old_z = 1;
   for (int st = 0; st < GM_NSTREAM; st++) s.ring_i[st] = -1;
   const gm_object& o = objs[0];
@@ -2865,19 +2928,24 @@ extern "C" __global__ void gm_settle_init_kernel(GmEnvState* __restrict__ states
     s.obj_rbound = r;
   }
 }
+#endif
 
 // per-env initialisation after the settle: RNG seeds and settled stepper flags
+#ifndef GM_CAL_TU   // env-step translation unit only
 extern "C" __global__ void gm_init_envs_kernel(GmEnvState* __restrict__ states, uint32_t base_seed, long long env_offset,
-                                               int n_envs) {
+                                               int n_envs, double dt) {
   int env = blockIdx.x * blockDim.x + threadIdx.x;
   if (env >= n_envs) return;
   GmEnvState& s = states[env];
+  s.dt = dt;
   uint64_t seed = ((uint64_t)base_seed + (uint64_t)(env_offset + env) * 1000003ull) % 2147483647ull;
   s.rng = seed == 0 ? 1u : (uint32_t)seed;
   s.old_x = s.old_y = s.old_z = 0;
 }
+#endif
 
 // spawn only (MjClass::spawn_object after MjClass::reset, MjEnv.py:1212-1267)
+#ifndef GM_CAL_TU   // env-step translation unit only
 extern "C" __global__ void gm_spawn_kernel(GmEnvState* __restrict__ states, const GmTopo* __restrict__ T,
                                            const uint8_t* __restrict__ mask, const gm_spawn* __restrict__ spawn,
                                            const gm_object* __restrict__ objs, int n_objects, int n_envs) {
@@ -2886,3 +2954,4 @@ extern "C" __global__ void gm_spawn_kernel(GmEnvState* __restrict__ states, cons
   if (mask && !mask[env]) return;
   spawn_object(states[env], T, objs, n_objects, spawn[env]);
 }
+#endif

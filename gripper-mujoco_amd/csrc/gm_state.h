@@ -49,6 +49,8 @@ struct GmEnvState {
   double start_qpos[7];
   double obj_size[3];
   double obj_mass, obj_inertia[3], obj_friction, obj_rbound, obj_rest_z;
+  double dt;                     // this env's timestep (model->opt.timestep; per env for calibration)
+  double tip_force;              // calibration tip load, N (resolve_segment_forces); 0 = off
   // ---- floats ----
   float rand_mu[SL_N][3];
   float ring[GM_NSTREAM][GM_RING];
@@ -75,12 +77,17 @@ struct GmEnvState {
   int32_t done;
   int32_t overflow;
   uint32_t rng;
-  int32_t pad_end;
+  int32_t cal_steps;             // calibration launch: substeps to run
+  int32_t badqacc;               // mjWARN_BADQACC: a non-finite or |qacc| > 1e10 was seen
+  int32_t pad_end[3];
 };
 
 // word count for HBM<->LDS sweeps
 #define GM_STATE_WORDS ((int)(sizeof(GmEnvState) / 4))
-static_assert(sizeof(GmEnvState) % 8 == 0, "GmEnvState must be 8-byte padded");
+// a multiple of 16 B: the LDS image (SharedT) places its double arrays right after the
+// state, and 16-byte alignment keeps their paired accesses as single ds_*_b128 ops
+// (an 8-byte shift measured 5-15% slower across every phase)
+static_assert(sizeof(GmEnvState) % 16 == 0, "GmEnvState must be 16-byte padded");
 
 // Topology derived from gm_model on the host (the canonical gripper tree):
 // dof/body of chain position p in finger chain f is first + p - 1 (p >= 1),
@@ -106,6 +113,8 @@ struct GmTopo {
   int32_t dof_p[GM_MAX_DOF];           // chain position (object: 0..5)
   int32_t dof_target[GM_MAX_DOF];      // PD target: 0 none, 1 next.x, 2 next.th, 3 next.z, 4 base z
   double dof_add[GM_MAX_DOF];          // armature + h (damping + kd) [+ h^2 (stiffness + kp)]
+  // the same addition's parts, formed per env from its own timestep h (calibration)
+  double dof_arm[GM_MAX_DOF], dof_dsum[GM_MAX_DOF], dof_ksum[GM_MAX_DOF];
   double dof_stiff[GM_MAX_DOF];        // 0 for the free joint
   double dof_damp[GM_MAX_DOF];
   double dof_kp[GM_MAX_DOF], dof_kd[GM_MAX_DOF];

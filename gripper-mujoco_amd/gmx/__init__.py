@@ -5,6 +5,7 @@ in include/gripper_mi355x.h.  Every env-step runs on the GPU; there is no CPU
 fallback (the library raises ImportError when the HIP extension is missing).
 """
 from ._lib import (load_library, Settings, ModelParams, Object, Spawn, SpawnParams, default_spawn_params,
+                   Calibration, calibrate, CAL_TIMESTEP, CAL_GAUGES,
                    ModelBlob, ConfigBlob,
                    default_settings, make_object_set, BINARY_EVENTS, LINEAR_EVENTS, ACTION_KINDS,
                    SENSORS, LIB_PATH)
@@ -13,6 +14,7 @@ from .env import BatchedGripperEnv, spawn_positions
 from .policy import DevicePolicy, eps_threshold
 
 __all__ = ["load_library", "Settings", "ModelParams", "Object", "Spawn", "SpawnParams", "default_spawn_params",
+           "Calibration", "calibrate", "CAL_TIMESTEP", "CAL_GAUGES",
            "ModelBlob", "ConfigBlob",
            "default_settings", "make_object_set", "canonical_settings", "disable_noise",
            "BatchedGripperEnv", "spawn_positions", "MAX_EPISODE_STEPS", "BINARY_EVENTS",

@@ -123,6 +123,37 @@ class SpawnParams(C.Structure):
                 ("xy_increment", C.c_double), ("rot_increment", C.c_double)]
 
 
+class Calibration(C.Structure):
+    """gm_calibration: the automatic settings of MjClass::configure_settings
+    (mjclass.cpp:241-308) found by simulation."""
+    _fields_ = [("timestep", C.c_double), ("sim_steps_per_action", C.c_int32), ("n_tested", C.c_int32),
+                ("search_timestep", C.c_double), ("yield_load", C.c_double),
+                ("bend_gauge_normalise", C.c_double), ("bending_normalise", C.c_float),
+                ("sim_gauge_raw_to_N_factor", C.c_float), ("wrist_Z_offset", C.c_float),
+                ("gauge_retries", C.c_int32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+CAL_TIMESTEP, CAL_GAUGES = 1, 2
+
+
+def calibrate(model, cfg, objects, what: int = CAL_TIMESTEP | CAL_GAUGES, device: int = 0):
+    """Batched device calibration (gm_calibrate): returns (Calibration, trace) where trace
+    is the timestep search's [(candidate_dt, unstable), ...] in the reference's order."""
+    lib = load_library()
+    out = Calibration()
+    tdt = (C.c_double * 256)()
+    tbad = (C.c_uint8 * 256)()
+    rc = lib.gm_calibrate(model.ptr, cfg.ptr, C.cast(objects, C.c_void_p), len(objects), int(device), int(what),
+                          C.byref(out), tdt, tbad, 256)
+    if rc != 0:
+        raise RuntimeError(f"gm_calibrate failed ({rc})")
+    n = min(out.n_tested, 256)
+    return out, [(float(tdt[i]), bool(tbad[i])) for i in range(n)]
+
+
 def default_spawn_params() -> "SpawnParams":
     p = SpawnParams()
     load_library().gm_default_spawn_params(C.byref(p))
@@ -138,7 +169,7 @@ def load_library(path: str | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("GM_LIB") or LIB_PATH   # GM_LIB: developer A/B builds
     # One HIP runtime per process: torch's libc10_hip pulls its bundled libamdhip64 by
     # the unversioned name, so if libgm (NEEDED libamdhip64.so.7) loaded first a second
     # runtime would appear and one of them sees no devices.  Loading torch first makes
@@ -154,9 +185,11 @@ def load_library(path: str | None = None):
             "(run `python -c 'import __graft_entry__ as g; g.build()'` from the repo root)")
     lib = C.CDLL(p)
     _declare(lib)
-    sizes = {0: Settings, 3: Object, 4: Spawn, 5: ModelParams, 6: SpawnParams}
+    sizes = {0: Settings, 3: Object, 4: Spawn, 5: ModelParams, 6: SpawnParams, 7: Calibration}
     for which, cls in sizes.items():
         n = lib.gm_struct_size(which)
+        if n < 0 and os.environ.get("GM_LIB"):
+            continue   # an older developer build without this struct
         if n != C.sizeof(cls):
             raise ImportError(f"struct layout mismatch for {cls.__name__}: C {n} vs ctypes {C.sizeof(cls)}")
     if path is None:
@@ -209,6 +242,7 @@ def _declare(lib):
         "gm_default_spawn_params": (None, [vp]),
         "gm_spawn_into_scene": (i32, [vp, u8p, vp, i32, u8p]),
         "gm_set_scene_spawn": (i32, [vp, vp, i32]),
+        "gm_calibrate": (i32, [vp, vp, vp, i32, i32, i32, vp, vp, vp, i32]),
         "gm_autoreset": (i32, [vp, i32, vp, i32, vp]),
         "gm_device_reset_mask": (vp, [vp]),
         "gm_policy_create": (i32, [vp, i32p, i32, f32p, C.POINTER(vp)]),
@@ -218,7 +252,11 @@ def _declare(lib):
         "gm_policy_read": (i32, [vp, i32p, f32p]),
     }
     for name, (res, args) in sig.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None and os.environ.get("GM_LIB"):
+            continue   # an older developer build without this entry point
+        if fn is None:
+            raise ImportError(f"libgm is missing {name}")
         fn.restype = res
         fn.argtypes = args
 

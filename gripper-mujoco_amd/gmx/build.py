@@ -6,14 +6,16 @@ import subprocess
 
 from ._lib import PKG_DIR, REPO_DIR, LIB_PATH
 
-SOURCES = ["csrc/gm_capi.hip", "csrc/gm_host_model.cpp"]
+SOURCES = ["csrc/gm_capi.hip", "csrc/gm_calib.hip", "csrc/gm_host_model.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics",
          "-ffp-contract=off"]
 
 
 def build(verbose: bool = False, force: bool = False) -> str:
+    """Compile each translation unit in parallel (the env-step kernel and the calibration
+    variant are separate device modules), then link libgm.so."""
     srcs = [os.path.join(PKG_DIR, s) for s in SOURCES]
     deps = srcs + [os.path.join(PKG_DIR, "csrc", f) for f in ("gm_kernels.hip", "gm_policy.hip", "gm_state.h")] + \
         [os.path.join(REPO_DIR, "include", f) for f in ("gripper_mi355x.h", "gm_settings.def")]
@@ -21,11 +23,23 @@ def build(verbose: bool = False, force: bool = False) -> str:
         t = os.path.getmtime(LIB_PATH)
         if all(os.path.getmtime(d) <= t for d in deps):
             return LIB_PATH
-    os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
-    cmd = [HIPCC, *FLAGS, "-I" + os.path.join(REPO_DIR, "include"), "-I" + os.path.join(PKG_DIR, "csrc"),
-           *srcs, "-o", LIB_PATH + ".tmp"]
+    objdir = os.path.join(os.path.dirname(LIB_PATH), "obj")
+    os.makedirs(objdir, exist_ok=True)
+    inc = ["-I" + os.path.join(REPO_DIR, "include"), "-I" + os.path.join(PKG_DIR, "csrc")]
+    procs, objs = [], []
+    for src in srcs:
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        cmd = [HIPCC, *FLAGS, *inc, "-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((subprocess.Popen(cmd), cmd))
+        objs.append(obj)
+    for p, cmd in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
+    link = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", LIB_PATH + ".tmp"]
     if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+        print(" ".join(link))
+    subprocess.run(link, check=True)
     os.replace(LIB_PATH + ".tmp", LIB_PATH)
     return LIB_PATH

@@ -317,6 +317,27 @@ class MjClass:
         p = self._model_params()
         return float(p.finger_E * p.finger_width * p.finger_thickness ** 3 / 12.0)
 
+    def yield_load(self, thickness: float | None = None, width: float | None = None) -> float:
+        """MjClass::yield_load (bind.cpp:191-192; calc_yield_point_load, myfunctions.cpp:
+        3587-3606): end load that yields the finger, float arithmetic as the reference."""
+        p = self._model_params()
+        t = p.finger_thickness if thickness is None else float(thickness)
+        w = p.finger_width if width is None else float(width)
+        I = (w * t ** 3) / 12.0
+        ys = 215e6                       # j_.dim.yield_stress (myfunctions.cpp:216)
+        M_max = np.float32((ys * I) / (0.5 * t))
+        return float(np.float32(float(M_max) / p.finger_length))
+
+    def calibrate(self, what: int = 3):
+        """The automatic settings configure_settings derives by simulation
+        (find_highest_stable_timestep, calibrate_simulated_sensors; mjclass.cpp:241-291),
+        as one batched device job.  Returns the gm_calibration fields as a dict."""
+        env = self._ensure()
+        cal, trace = gmx.calibrate(env.model, env.cfg, env.objects, what=what)
+        out = cal.as_dict()
+        out["search_trace"] = trace
+        return out
+
     def set_base_XYZ_limits(self, x: float, y: float, z: float):
         self._base_limits = (float(x), float(y), float(z))
 

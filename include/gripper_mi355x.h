@@ -256,6 +256,11 @@ typedef struct gm_model {
   /* gauge (JointSettings::gauge, myfunctions.cpp:264-270) */
   double  gauge_xpos;
   int32_t gauge_order;
+  /* tip loading for the gauge calibration (get_segment_matrices / apply_segment_force,
+   * myfunctions.cpp:1521-1610, 1660-1727): the last link of each finger and the finger's
+   * bending direction at the keyframe (world frame, radially outward) */
+  int32_t body_tip[3];
+  double  tip_dir[3][3];
 } gm_model;
 
 /* one graspable object (a synthetic object-set entry) */
@@ -294,7 +299,7 @@ typedef struct gm_ctx gm_ctx;
 const char* gm_version(void);
 int  gm_device_count(void);
 /* sizes of the interface structs (0 settings, 1 model, 2 config, 3 object, 4 spawn,
- * 5 model params, 6 spawn params) so bindings can verify their layouts */
+ * 5 model params, 6 spawn params, 7 calibration) so bindings can verify their layouts */
 int64_t gm_struct_size(int which);
 /* model summary: nq, nv, nbody, ngeom, npair, n_seg, dof_base, dof_palm, dof_obj,
  * dof_pris[3], dof_rev[3], dof_seg[3], nlock, nM (tree-sparse M nonzeros)  (20 int32) */
@@ -315,6 +320,39 @@ int  gm_configure(const gm_settings* s, const gm_model* m, gm_config* out);
 
 /* Synthetic object sets (the reference's set6/set9 MJCF sets are unavailable). */
 int  gm_make_object_set(const char* name, uint64_t seed, gm_object* out, int max_objects);
+
+/* The automatic settings of MjClass::configure_settings (mjclass.cpp:241-308), found by
+ * simulation: find_highest_stable_timestep (mjclass.cpp:4745-4854) and
+ * calibrate_simulated_sensors (4643-4676, tip load via validate_curve_under_force
+ * 4023-4105).  Timesteps keep the reference's float arithmetic. */
+typedef struct gm_calibration {
+  double  timestep;                   /* s_.mujoco_timestep after the search (and any 0.8x
+                                         gauge-run retries, mjclass.cpp:4080)            */
+  int32_t sim_steps_per_action;       /* ceil(time_for_action / timestep) (mjclass.cpp:306) */
+  int32_t n_tested;                   /* candidate timesteps simulated by the search      */
+  double  search_timestep;            /* highest stable timestep found (before the factor) */
+  double  yield_load;                 /* calc_yield_point_load (myfunctions.cpp:3587-3595), N */
+  double  bend_gauge_normalise;       /* saturation_yield_factor * yield_load (mjclass.cpp:278) */
+  float   bending_normalise;          /* gauge reading under that tip load (mjclass.cpp:4666) */
+  float   sim_gauge_raw_to_N_factor;  /* mjclass.cpp:281                                   */
+  float   wrist_Z_offset;             /* mjclass.cpp:4659: userdata[2] is never written, 0  */
+  int32_t gauge_retries;              /* 0.8x timestep retries of the tip-load run          */
+} gm_calibration;
+#define GM_CAL_TIMESTEP 1
+#define GM_CAL_GAUGES   2
+#define GM_CAL_MAX_TRACE 256
+
+/* Batched calibration on `device`: every candidate timestep of the search is simulated
+ * for 1 s as its own env in one launch (per-env timestep, mjWARN_BADQACC-style
+ * instability flag), and the search replays the reference's coarse/fine sequence over the
+ * results, so the answer equals the sequential search.  The gauge run is one env under
+ * the saturation tip load for 50 s of simulated time.  `what`: GM_CAL_TIMESTEP |
+ * GM_CAL_GAUGES (the gauge run uses model->timestep when the search is off).  trace_dt /
+ * trace_unstable (optional, max_trace entries): the search's candidates in order.
+ * Sensor and base-position noise are off during calibration. */
+int  gm_calibrate(const gm_model* model, const gm_config* cfg, const gm_object* objects, int n_objects,
+                  int device, int what, gm_calibration* out, double* trace_dt, uint8_t* trace_unstable,
+                  int max_trace);
 
 /* Context lifetime: MjClass() + load() + init() (bind.cpp:46-52, mjclass.cpp:8-95) */
 int  gm_create(const gm_model* model, const gm_config* cfg, const gm_object* objects,

@@ -296,6 +296,9 @@ struct or_env {
   float grp_peak_lateral;
   int obj_index;
   double start_qpos[7];
+  /* calibration (curve_validation tip load, mjWARN_BADQACC) */
+  double tip_force;
+  int badqacc;
 };
 
 size_t or_sizeof(void) { return sizeof(or_env); }
@@ -1097,6 +1100,22 @@ static void physics_substep(or_env* e) {
   factor(e, H);
   double f[NV];
   for (int d = 0; d < nv; d++) f[d] = e->qfrc_passive[d] + e->qfrc_act[d] - e->qfrc_bias[d];
+  if (e->tip_force != 0.0) {
+    /* resolve_segment_forces -> apply_segment_force (myfunctions.cpp:1642-1727): an
+     * xfrc_applied force at each finger's tip-link centre of mass along the finger's
+     * rest bending direction; J^T F into the generalized forces */
+    for (int fi = 0; fi < 3; fi++) {
+      int bt = m->body_tip[fi];
+      double F[3] = {e->tip_force * m->tip_dir[fi][0], e->tip_force * m->tip_dir[fi][1],
+                     e->tip_force * m->tip_dir[fi][2]};
+      for (int d = 0; d < nv; d++) {
+        if (!is_ancestor_body(m, m->dof_body[d], bt)) continue;
+        double col[3];
+        jac_point_col(e, d, e->xipos[bt], col);
+        f[d] += dot3(col, F);
+      }
+    }
+  }
   solve(e, e->qacc_smooth, f);
   constraint_solve(e);
   double jtf[NV];
@@ -1106,6 +1125,8 @@ static void physics_substep(or_env* e) {
   double dq[NV];
   solve(e, dq, jtf);
   for (int d = 0; d < nv; d++) e->qacc[d] = e->qacc_smooth[d] + dq[d];
+  /* mj_checkAcc -> mjWARN_BADQACC (is_sim_unstable, myfunctions.cpp:4233-4242) */
+  for (int d = 0; d < nv; d++) if (!(fabs(e->qacc[d]) <= 1e10)) e->badqacc = 1;
   /* semi-implicit Euler */
   for (int d = 0; d < nv; d++) e->qvel[d] += h * e->qacc[d];
   for (int b = 1; b < m->nbody; b++) {
@@ -2055,6 +2076,128 @@ void or_reset(or_env* e, const gm_spawn* sp) {
     e->qpos[m0->dof_base] = e->base[2] + e->eq_q[m0->dof_base];
   }
   or_spawn(e, sp);
+}
+
+/* =====================================================================
+ * automatic calibration (MjClass::configure_settings, mjclass.cpp:241-308), sequential
+ * as the reference runs it: find_highest_stable_timestep (4745-4854), then
+ * calibrate_simulated_sensors (4643-4676) with validate_curve_under_force (4023-4105).
+ * Noise off (base_position_noise = 0); forward declarations of the env entry points.
+ * ===================================================================== */
+or_env* or_create(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects,
+                  int64_t env_id);
+static float yield_point_load(const gm_model* m) {      /* myfunctions.cpp:3587-3595 */
+  double I = (m->finger_width * pow(m->finger_thickness, 3)) / 12.0;
+  float M_max = (m->yield_stress * I) / (0.5 * m->finger_thickness);
+  float F_max = M_max / m->finger_length;
+  return F_max;
+}
+/* n substeps of MjClass::step (before_step / resolve_segment_forces / step / after_step /
+ * monitor_sensors); stops at the first BADQACC like the reference's break */
+static int cal_steps(or_env* e, int n) {
+  /* a run starts from the reset's mj_forward pose */
+  memcpy(e->qpos_pre, e->qpos, sizeof(e->qpos));
+  e->badqacc = 0;
+  for (int i = 0; i < n; i++) {
+    if (e->tip_force != 0.0) {
+      /* apply_segment_force locks the prismatic motors every step (set_constraint,
+       * myfunctions.cpp:1679-1685), anchored at the last mj_step1 pose */
+      for (int k = 0; k < e->m.nlock; k++)
+        if (e->m.lock_kind[k] == 0) { e->lock_active[k] = 1; e->lock_q[k] = e->qpos_pre[e->m.lock_dof[k]]; }
+    }
+    physics_substep(e);
+    update_all(e);
+    if (e->badqacc) return 1;
+  }
+  return 0;
+}
+int or_calibrate(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects, int what,
+                 gm_calibration* out, double* trace_dt, uint8_t* trace_unstable, int max_trace) {
+  memset(out, 0, sizeof(*out));
+  gm_config cc = *c;
+  cc.s.base_position_noise = 0;
+  or_env* e = or_create(m, &cc, objects, n_objects, 0);
+  if (!e) return -1;
+  gm_spawn sp = {0, 0.0, 0.0, 0.0};
+  double timestep = m->timestep;
+  if (what & GM_CAL_TIMESTEP) {
+    float coarse_increment = 0.5e-3f, fine_increment = 50e-6f, start_value = 1.0e-3f;
+    float test_time = 1.0f, max_allowable_timestep = 20.0e-3f, tune_param = 1.0f;
+    float next_timestep = start_value;
+    int unstable = 0, coarse_pass = 1, ntr = 0;
+    while (1) {
+      int num_steps = (test_time / next_timestep) + 1;
+      or_reset(e, &sp);
+      e->m.timestep = next_timestep;
+      unstable = cal_steps(e, num_steps);
+      if (ntr < max_trace) {
+        if (trace_dt) trace_dt[ntr] = next_timestep;
+        if (trace_unstable) trace_unstable[ntr] = (uint8_t)unstable;
+      }
+      ntr++;
+      if (unstable) {
+        if (coarse_pass) coarse_pass = 0;
+        next_timestep -= fine_increment;
+        unstable = 0;
+      } else {
+        if (coarse_pass) next_timestep += coarse_increment;
+        else break;
+      }
+      if (next_timestep < fine_increment) { or_destroy(e); return -2; }
+      if (next_timestep > max_allowable_timestep) { next_timestep = max_allowable_timestep; coarse_pass = 0; }
+    }
+    float factor;
+    if (next_timestep <= 3.0e-3) factor = tune_param * 0.8;
+    else if (next_timestep < 5.0e-3) factor = tune_param * 0.75;
+    else if (next_timestep < 10.0e-3) factor = tune_param * 0.65;
+    else factor = tune_param * 0.65;
+    float final_timestep = next_timestep * factor;
+    final_timestep = (float)((int)(final_timestep * 1e6) * 1e-6);
+    out->search_timestep = next_timestep;
+    out->n_tested = ntr;
+    timestep = final_timestep;
+  }
+  out->timestep = timestep;
+  if (what & GM_CAL_GAUGES) {
+    float yield = yield_point_load(m);
+    float bend_gauge_normalise = cc.s.saturation_yield_factor * yield;
+    double ts = timestep;                                 /* s_.mujoco_timestep (double) */
+    or_reset(e, &sp);
+    e->m.timestep = ts;
+    e->tip_force = 0;
+    float settle_time = 0.3;
+    int steps_for_settle = settle_time / ts;
+    cal_steps(e, steps_for_settle);
+    float time_to_settle = 50;
+    int steps_to_make = time_to_settle / ts;
+    int repeats_done = 1;
+    while (1) {
+      e->tip_force = bend_gauge_normalise;
+      if (cal_steps(e, steps_to_make)) {
+        ts *= 0.8;
+        e->tip_force = 0;
+        or_reset(e, &sp);
+        e->m.timestep = ts;
+        repeats_done += 1;
+        if (repeats_done > 5) { or_destroy(e); return -3; }
+        continue;
+      }
+      break;
+    }
+    e->tip_force = 0;
+    int qa = e->m.dof_seg[0];    /* read_armadillo_gauge(data, 0): finger 0's segment joints */
+    float normalise = or_gauge_reading(&e->m, &e->qpos[qa]);
+    out->yield_load = yield;
+    out->bend_gauge_normalise = bend_gauge_normalise;
+    out->bending_normalise = normalise;
+    out->sim_gauge_raw_to_N_factor = bend_gauge_normalise / normalise;
+    out->wrist_Z_offset = 0.0f;
+    out->gauge_retries = repeats_done - 1;
+    out->timestep = ts;
+  }
+  out->sim_steps_per_action = (int32_t)ceil(cc.s.time_for_action / out->timestep);
+  or_destroy(e);
+  return 0;
 }
 
 or_env* or_create(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects,

@@ -65,6 +65,9 @@ int    or_box2d_overlaps(const double* a5, const double* b5, double gap);   /* B
 int    or_grip_step_sequence(const double* cmds, int n, double* out);  /* Gripper golden driver */
 int    or_sample(int mode, const float* window_recent_first, int n_avail, int prev_steps,
                  int readings_per_step, float* out);                  /* Sensor::*_sample */
+/* automatic calibration (find_highest_stable_timestep + calibrate_simulated_sensors) */
+int    or_calibrate(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects, int what,
+                    gm_calibration* out, double* trace_dt, uint8_t* trace_unstable, int max_trace);
 /* time one bounded CPU sample: n_envs envs x n_steps env-steps, random actions */
 double or_bench(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects,
                 int n_envs, int n_steps, uint64_t seed, int n_threads);

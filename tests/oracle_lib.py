@@ -61,6 +61,7 @@ def lib():
             "or_spawn_into_scene": (i32, [vp, vp]),
             "or_std_shuffle": (C.c_uint32, [C.c_uint32, i32, i32p]),
             "or_box2d_overlaps": (i32, [f64p, f64p, C.c_double]),
+            "or_calibrate": (i32, [vp, vp, vp, i32, i32, vp, vp, vp, i32]),
         }
         for n, (r, a) in sig.items():
             f = getattr(L, n)
@@ -232,6 +233,20 @@ def std_shuffle(seed, n):
     out = np.zeros(max(n, 1), dtype=np.int32)
     nxt = lib().or_std_shuffle(seed, n, out.ctypes.data_as(C.POINTER(C.c_int32)))
     return out[:n].tolist(), int(nxt)
+
+
+def calibrate(model, cfg, objects, what=3):
+    """or_calibrate: the sequential reference calibration; returns (Calibration, trace)."""
+    import gmx
+    out = gmx.Calibration()
+    tdt = (C.c_double * 256)()
+    tbad = (C.c_uint8 * 256)()
+    rc = lib().or_calibrate(model.ptr, cfg.ptr, C.cast(objects, C.c_void_p), len(objects), what, C.byref(out),
+                            tdt, tbad, 256)
+    if rc != 0:
+        raise RuntimeError(f"or_calibrate failed ({rc})")
+    n = min(out.n_tested, 256)
+    return out, [(float(tdt[i]), bool(tbad[i])) for i in range(n)]
 
 
 def box2d_overlaps(a5, b5, gap):

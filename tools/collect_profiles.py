@@ -5,6 +5,7 @@ import csv, json, os, shutil, sys
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
 src = os.path.join("gpurun_out", tag)
+tag = sys.argv[2] if len(sys.argv) > 2 else tag      # output prefix (the round name)
 dst = "profiles"
 os.makedirs(dst, exist_ok=True)
 shutil.copy(os.path.join(src, "stats", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
@@ -40,3 +41,17 @@ json.dump({"kernel": "gm_step_kernel", "n_envs": n_envs, "bytes_per_launch": fet
                      "WRITE_SIZE KiB x1024, averaged over the 4096-env step launches"},
           open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
 print(open(os.path.join(dst, "pmc_traffic.json")).read())
+
+# per-dispatch durations of the 4096-env step launches from the kernel trace (the stats
+# summary's average also holds the one-env calibrate_reset settle launch at gm_create)
+tr = [r for r in csv.DictReader(open(os.path.join(src, "stats", "run_kernel_trace.csv")))
+      if 'gm_step_kernel' in r['Kernel_Name']]
+grid = lambda r: int(r.get('Grid_Size_X') or r.get('Grid_Size') or 0)
+durs = [(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6 for r in tr if grid(r) == 64 * n_envs]
+summ = {"kernel": "gm_step_kernel", "grid_envs": n_envs, "launches": len(durs),
+        "avg_ms_all": sum(durs) / len(durs), "avg_ms_after_first": sum(durs[1:]) / max(len(durs) - 1, 1),
+        "min_ms": min(durs), "max_ms": max(durs), "durations_ms": durs,
+        "source": f"gpurun_out/{sys.argv[1] if len(sys.argv) > 1 else tag}/stats/run_kernel_trace.csv "
+                  "(rocprofv3 --kernel-trace --stats over bench.py --steps 5 --warmup 1)"}
+json.dump(summ, open(os.path.join(dst, f"{tag}_step_kernel_trace.json"), "w"), indent=1)
+print(json.dumps({k: v for k, v in summ.items() if k != "durations_ms"}))

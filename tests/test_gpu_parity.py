@@ -129,3 +129,29 @@ def test_large_batch_finite_and_deterministic(setup):
     for a, o1 in zip(acts, outs):
         o2 = env2.step(a)[0]
         np.testing.assert_array_equal(o1, o2)
+
+
+def test_env_offset_shards_reproduce_the_unsharded_batch(setup):
+    """a rank owns global env ids [offset, offset + n) and seeds every env's
+    RNG stream from its global id, so two half-size shards (what ranks 0 and 1 run)
+    reproduce the 8-env batch bit for bit -- resets, noise, contacts and all."""
+    gm, ol = setup
+    s = gm.canonical_settings(noise=True, seed=21)
+    full = gm.BatchedGripperEnv(8, object_set="set6_synthetic", settings=s, seed=21)
+    halves = [gm.BatchedGripperEnv(4, object_set="set6_synthetic", settings=gm.canonical_settings(noise=True, seed=21),
+                                   seed=21, env_offset=4 * k) for k in range(2)]
+    sp = full.make_spawn(x=0.0, y=0.0, idx=3, rot=0.0)
+    full.reset(spawn=sp)
+    for k, h in enumerate(halves):
+        h.reset(spawn=h.make_spawn(x=0.0, y=0.0, idx=3, rot=0.0))
+    rng = np.random.default_rng(5)
+    for t in range(4):
+        a = rng.uniform(-1, 1, size=(8, full.n_actions)).astype(np.float32)
+        of, rf, tf, _ = full.step(a)
+        for k, h in enumerate(halves):
+            oh, rh, th, _ = h.step(a[4 * k:4 * k + 4])
+            np.testing.assert_array_equal(oh, of[4 * k:4 * k + 4])
+            np.testing.assert_array_equal(rh, rf[4 * k:4 * k + 4])
+            np.testing.assert_array_equal(th, tf[4 * k:4 * k + 4])
+    for e in [full, *halves]:
+        e.close()

@@ -10,6 +10,7 @@
 // listed in DESIGN.md section "Model spec".
 #include "gripper_mi355x.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <cstdint>
@@ -428,6 +429,95 @@ static int n_samples(int fcn, const gm_sensor& s) {
   return 2 * s.prev_steps + 1;
 }
 
+// ---- calibrate_simulated_sensors without the simulation ----
+// The reference normalises the bending gauges by the reading its simulation settles at
+// under the saturation tip load (mjclass.cpp:4643-4676, validate_curve_under_force
+// 4023-4105: every fingertip pulled outward for 50 s, then read_armadillo_gauge of finger
+// 0).  That settled state is the static equilibrium of finger 0's joint chain, solved
+// here directly in the finger's plane (x down the finger, y outward): revolute motor
+// (PD spring kp about -z at the finger root), the fixed first segment, N segment hinges
+// (stiffness c_k about +z); loads = the tip pull at the last link's centre of mass and
+// gravity on every link.  The gauge then fits the settled joint points as
+// read_armadillo_gauge does.  gm_calibrate runs the actual simulation (device) and the
+// two agree to a fraction of a percent (tests/test_calibration.py).
+static double cubic_fit_eval(const double* X, const double* Y, int P, double x) {
+  // least-squares cubic through (X, Y) (arma::polyfit, myfunctions.cpp:2739) on the
+  // centred / scaled abscissa, solved by modified Gram-Schmidt
+  double lo = X[0], hi = X[0];
+  for (int i = 1; i < P; i++) { lo = std::min(lo, X[i]); hi = std::max(hi, X[i]); }
+  const double mid = 0.5 * (lo + hi), half = std::max(0.5 * (hi - lo), 1e-12);
+  double Q[4][GM_MAX_SEG + 2], R[4][4] = {{0}};
+  for (int i = 0; i < P; i++) {
+    const double t = (X[i] - mid) / half;
+    Q[0][i] = 1; Q[1][i] = t; Q[2][i] = t * t; Q[3][i] = t * t * t;
+  }
+  for (int k = 0; k < 4; k++) {
+    for (int j = 0; j < k; j++) {
+      double d = 0;
+      for (int i = 0; i < P; i++) d += Q[j][i] * Q[k][i];
+      R[j][k] = d;
+      for (int i = 0; i < P; i++) Q[k][i] -= d * Q[j][i];
+    }
+    double n = 0;
+    for (int i = 0; i < P; i++) n += Q[k][i] * Q[k][i];
+    n = std::sqrt(n);
+    R[k][k] = n;
+    for (int i = 0; i < P; i++) Q[k][i] /= n;
+  }
+  double b[4], a[4];
+  for (int k = 0; k < 4; k++) { b[k] = 0; for (int i = 0; i < P; i++) b[k] += Q[k][i] * Y[i]; }
+  for (int k = 3; k >= 0; k--) { double v = b[k]; for (int j = k + 1; j < 4; j++) v -= R[k][j] * a[j]; a[k] = v / R[k][k]; }
+  const double t = (x - mid) / half;
+  return ((a[3] * t + a[2]) * t + a[1]) * t + a[0];
+}
+
+static double static_gauge_reading(const gm_model* m, double P) {
+  const int N = m->n_seg;
+  const double Ls = m->segment_length;
+  const int b0 = m->body_finger[0];            // fixed first segment; segments b0+1 .. b0+N
+  const double g = -m->gravity[2];              // finger x axis points down: gravity is +x
+  double q[GM_MAX_SEG + 1] = {0};               // q[0]: revolute (about -z), q[1..N]: segments
+  double stiff[GM_MAX_SEG + 1];
+  stiff[0] = m->kp_gripper[1];
+  for (int k = 1; k <= N; k++) stiff[k] = m->jnt_stiffness[m->body_jnt[b0 + k]];
+  for (int it = 0; it < 2000; it++) {
+    double px[GM_MAX_SEG + 2], py[GM_MAX_SEG + 2], phi[GM_MAX_SEG + 2];
+    double cx[GM_MAX_SEG + 2], cy[GM_MAX_SEG + 2], mass[GM_MAX_SEG + 2];
+    px[0] = 0; py[0] = 0; phi[0] = -q[0];
+    for (int k = 0; k <= N; k++) {
+      if (k > 0) {
+        px[k] = px[k - 1] + Ls * std::cos(phi[k - 1]);
+        py[k] = py[k - 1] + Ls * std::sin(phi[k - 1]);
+        phi[k] = phi[k - 1] + q[k];
+      }
+      const double* ip = m->body_ipos[b0 + k];
+      cx[k] = px[k] + std::cos(phi[k]) * ip[0] - std::sin(phi[k]) * ip[1];
+      cy[k] = py[k] + std::sin(phi[k]) * ip[0] + std::cos(phi[k]) * ip[1];
+      mass[k] = m->body_mass[b0 + k];
+    }
+    double change = 0;
+    for (int j = 0; j <= N; j++) {
+      // torque about +z at joint j from the loads on links j .. N (the revolute carries all)
+      double tau = (cx[N] - px[j]) * P;                      // tip pull (0, P)
+      for (int k = j; k <= N; k++) tau += -(cy[k] - py[j]) * mass[k] * g;   // gravity (m g, 0)
+      const double qn = (j == 0) ? -tau / stiff[0] : tau / stiff[j];
+      change = std::max(change, std::fabs(qn - q[j]));
+      q[j] = qn;
+    }
+    if (change < 1e-15) break;
+  }
+  double X[GM_MAX_SEG + 2], Y[GM_MAX_SEG + 2];
+  X[0] = m->fixed_first_segment ? Ls : 0.0;
+  Y[0] = 0;
+  double cum = 0;
+  for (int i = 0; i < N; i++) {
+    cum += q[i + 1];
+    X[i + 1] = X[i] + Ls * std::cos(cum);
+    Y[i + 1] = Y[i] + Ls * std::sin(cum);
+  }
+  return 1000.0 * cubic_fit_eval(X, Y, N + 1, m->gauge_xpos);
+}
+
 int gm_configure(const gm_settings* in, const gm_model* m, gm_config* c) {
   if (!in || !m || !c) return GM_E_ARG;
   std::memset(c, 0, sizeof(*c));
@@ -469,16 +559,16 @@ int gm_configure(const gm_settings* in, const gm_model* m, gm_config* c) {
   if (s.sim_steps_per_action < 1) return GM_E_RANGE;
   c->sim_steps_per_action = s.sim_steps_per_action;
 
-  // ---- gauge calibration (mjclass.cpp:273-291): analytic Euler-Bernoulli stand-in for
-  //      calibrate_simulated_sensors(); normalise = raw gauge under the saturation load ----
-  double Ifing = m->finger_width * std::pow(m->finger_thickness, 3) / 12.0;
-  double yield = (m->yield_stress * Ifing) / (0.5 * m->finger_thickness) / m->finger_length;
+  // ---- gauge calibration (mjclass.cpp:273-291): normalise = the gauge reading the
+  //      saturation tip load settles at (static_gauge_reading above) ----
   if (s.auto_calibrate_gauges) {
-    double P = s.saturation_yield_factor * yield;
-    double x = m->gauge_xpos, L = m->finger_length;
-    double raw = 1000.0 * P * x * x * (3 * L - x) / (6 * m->finger_EI);
-    s.bending_gauge.normalise = (float)raw;
-    c->sim_gauge_raw_to_N_factor = P / (double)s.bending_gauge.normalise;
+    // calc_yield_point_load (myfunctions.cpp:3587-3595) in the reference's float steps
+    const double Ifing = m->finger_width * std::pow(m->finger_thickness, 3) / 12.0;
+    const float M_max = (m->yield_stress * Ifing) / (0.5 * m->finger_thickness);
+    const float yield = M_max / m->finger_length;
+    const float P = s.saturation_yield_factor * yield;
+    s.bending_gauge.normalise = (float)static_gauge_reading(m, P);
+    c->sim_gauge_raw_to_N_factor = P / s.bending_gauge.normalise;
     s.wrist_sensor_Z.raw_value_offset = 0.0f;   // userdata[2] is never written
   } else {
     c->sim_gauge_raw_to_N_factor = 1.0;

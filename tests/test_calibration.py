@@ -83,6 +83,17 @@ def test_oracle_gauge_calibration(world):
     assert both.bending_normalise == pytest.approx(cal.bending_normalise, rel=2e-3)
 
 
+def test_configure_gauge_normalise_is_the_settled_simulation(world):
+    """gm_configure's auto_calibrate_gauges value (the static equilibrium of the finger's
+    joint chain under the saturation tip load, solved directly) equals what the reference's
+    procedure reads after 50 s of simulation (the oracle's or_calibrate)."""
+    import ctypes as C
+    gm, model, cfg, objs, s = world
+    cs = gm.Settings.from_buffer_copy(cfg.buf[:C.sizeof(gm.Settings)])
+    cal, _ = oracle_lib.calibrate(model, cfg, objs, 2)
+    assert cs.bending_gauge.normalise == pytest.approx(cal.bending_normalise, rel=1e-5)
+
+
 @pytest.mark.gpu
 def test_gpu_calibration_matches_oracle(world):
     """The batched device search simulates every candidate as one env and replays the

@@ -225,26 +225,32 @@ __device__ __forceinline__ real row_shl(real x, int off) {
     default: return dpp_move<0x108>(x);
   }
 }
+// row_newbcast is the one DPP control the 64-bit data path takes (gfx90a+ DP-ALU DPP):
+// one v_mov_b64_dpp instead of two 32-bit halves
+template <int CTRL>
+__device__ __forceinline__ real dpp_bcast64(real x) {
+  return __builtin_amdgcn_update_dpp(0.0, x, CTRL, 0xF, 0xF, true);
+}
 // value of position k of this lane's 16-lane DPP row (row_newbcast:k), k compile-time
 // after unrolling
 __device__ __forceinline__ real row_bcast(real x, int k) {
   switch (k) {
-    case 0: return dpp_move<0x150>(x);
-    case 1: return dpp_move<0x151>(x);
-    case 2: return dpp_move<0x152>(x);
-    case 3: return dpp_move<0x153>(x);
-    case 4: return dpp_move<0x154>(x);
-    case 5: return dpp_move<0x155>(x);
-    case 6: return dpp_move<0x156>(x);
-    case 7: return dpp_move<0x157>(x);
-    case 8: return dpp_move<0x158>(x);
-    case 9: return dpp_move<0x159>(x);
-    case 10: return dpp_move<0x15A>(x);
-    case 11: return dpp_move<0x15B>(x);
-    case 12: return dpp_move<0x15C>(x);
-    case 13: return dpp_move<0x15D>(x);
-    case 14: return dpp_move<0x15E>(x);
-    default: return dpp_move<0x15F>(x);
+    case 0: return dpp_bcast64<0x150>(x);
+    case 1: return dpp_bcast64<0x151>(x);
+    case 2: return dpp_bcast64<0x152>(x);
+    case 3: return dpp_bcast64<0x153>(x);
+    case 4: return dpp_bcast64<0x154>(x);
+    case 5: return dpp_bcast64<0x155>(x);
+    case 6: return dpp_bcast64<0x156>(x);
+    case 7: return dpp_bcast64<0x157>(x);
+    case 8: return dpp_bcast64<0x158>(x);
+    case 9: return dpp_bcast64<0x159>(x);
+    case 10: return dpp_bcast64<0x15A>(x);
+    case 11: return dpp_bcast64<0x15B>(x);
+    case 12: return dpp_bcast64<0x15C>(x);
+    case 13: return dpp_bcast64<0x15D>(x);
+    case 14: return dpp_bcast64<0x15E>(x);
+    default: return dpp_bcast64<0x15F>(x);
   }
 }
 __device__ __forceinline__ real readlane_real(real x, int l) {
@@ -285,7 +291,11 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
       }
     }
   }
+#ifdef GM_PHASE_SPLIT_PGS
+  PH(0);
+#else
   PH(15);
+#endif
   // B: poses.  The base is the world's child; along each finger / palm chain the
   // local transforms are composed by a segmented inclusive scan (root-side operand on
   // the left: (p_a, q_a) o (p_b, q_b) = (p_a + R(q_a) p_b, q_a (x) q_b)), then the base
@@ -343,7 +353,11 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
     }
   }
   __syncthreads();
+#ifdef GM_PHASE_SPLIT_PGS
+  PH(0);
+#else
   PH(16);
+#endif
   // C1: world-origin spatial inertia per body
   if (lane < T->nbody && lane > 0) {
     const int b = lane;
@@ -1387,6 +1401,107 @@ __device__ __forceinline__ real impedance(const gm_model* __restrict__ m, real r
   return dmin + y * (dmax - dmin);
 }
 
+// ---------------------------------------------------------------- PGS, nefc <= 32
+// Small problems (the common case: <= 7 contacts) run on a replicated DPP-row layout:
+// every 16-lane row holds the whole problem, lane p of each row owning constraint rows p
+// ("set 0") and p + 16 ("set 1").  A row update then needs its change d only inside the
+// lane's own 16-lane row, which v_fmac_f64_dpp row_newbcast delivers as the FMA's source
+// operand -- no v_readlane / SGPR round trip on the dependent chain (fma -> max -> sub ->
+// fmac_dpp).  The arithmetic per row is the general path's, operation for operation
+// (f_n = max(u_r, lb_r), d = f_n - f_r, u_j <- fma(-B_j[r], d, u_j)), so the two paths
+// give bit-identical forces.
+
+// value of lane addr/4 (ds_bpermute: the LDS crossbar, no LDS storage), 64-bit
+__device__ __forceinline__ real bperm_f64(int addr, real x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)b);
+  const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// max(u, lb) without the canonicalising v_max x,x the compiler puts in front of fmax()
+// of a value it cannot prove canonical (u is a finite FMA result; lb is 0 or -inf)
+__device__ __forceinline__ real vmax_f64(real a, real b) {
+  real r;
+  asm volatile("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// One row r of the small-problem sweep: the general path's arithmetic (f_n = max(u_r, lb_r),
+// d = f_n - f_r, u_j <- fma(-B_j[r], d, u_j), f_r <- f_n), with d broadcast inside each
+// 16-lane row by v_mov_b64_dpp row_newbcast instead of two v_readlane.  (Keeping each
+// row's f_n in a register of its own instead of the select measured a little faster in
+// isolation but pushed the outlined substep past 256 VGPRs; the select stays.)
+template <int R, bool TWO>
+__device__ __forceinline__ void pgs_small_row(real& u0, real& u1, real& f0, real& f1, real lb0, const real* nB0,
+                                              const real* nB1) {
+  constexpr int P = R & 15;
+  // lanes p == P of every 16-lane row: a scalar constant, no VALU compare
+  const bool mine = __builtin_amdgcn_inverse_ballot_w64(0x0001000100010001ull << P);
+  if constexpr (R < 16) {
+    const real fn = vmax_f64(u0, lb0);
+    const real d = row_bcast(fn - f0, P);
+    u0 = fma(nB0[R], d, u0);                  // == fma(-B_j[r], d, u_j): nB = -B exactly
+    if constexpr (TWO) u1 = fma(nB1[R], d, u1);
+    f0 = mine ? fn : f0;
+  } else {
+    const real fn = vmax_f64(u1, 0.0);      // rows >= 16 are contact edges or padding
+    const real d = row_bcast(fn - f1, P);
+    u1 = fma(nB1[R], d, u1);
+    u0 = fma(nB0[R], d, u0);
+    f1 = mine ? fn : f1;
+  }
+}
+
+template <int C, bool TWO>
+__device__ __forceinline__ void pgs_small_chunk(real& u0, real& u1, real& f0, real& f1, real lb0, const real* nB0,
+                                                const real* nB1) {
+  pgs_small_row<4 * C + 0, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
+  pgs_small_row<4 * C + 1, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
+  pgs_small_row<4 * C + 2, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
+  pgs_small_row<4 * C + 3, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
+}
+
+// The whole small-problem solve: gather the scaled Delassus columns into the replicated
+// layout (lane p of every 16-lane row gets constraint p and, with TWO, p + 16), run the
+// fixed sweeps (chunks past nchunk skipped by a scalar guard, as in the general path) and
+// return f of constraint `lane` (lanes 0..31).  nBrow is the general path's
+// lane-per-row scaled column (B_j[r] = ARinv_j AR_jr, zero on the diagonal), negated.
+template <bool TWO>
+__device__ __forceinline__ real pgs_small(const real* nBrow, real u, int nl, int nchunk, int iters, int lane) {
+  constexpr int NR = TWO ? 32 : 16;
+  const int p = lane & 15;
+  const int a0 = p << 2, a1 = (p + 16) << 2;
+  real nB0[NR], nB1[NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    nB0[r] = bperm_f64(a0, nBrow[r]);
+    nB1[r] = TWO ? bperm_f64(a1, nBrow[r]) : 0.0;
+  }
+  real u0 = bperm_f64(a0, u);
+  real u1 = TWO ? bperm_f64(a1, u) : 0.0;
+  const real lb0 = (p < nl) ? -__builtin_inf() : 0.0;   // lock rows come first (nl <= 4)
+  real f0 = 0.0, f1 = 0.0;
+  for (int it = 0; it < iters; it++) {
+    if constexpr (!TWO) {
+      if (0 < nchunk) pgs_small_chunk<0, false>(u0, u1, f0, f1, lb0, nB0, nB1);
+      if (1 < nchunk) pgs_small_chunk<1, false>(u0, u1, f0, f1, lb0, nB0, nB1);
+      if (2 < nchunk) pgs_small_chunk<2, false>(u0, u1, f0, f1, lb0, nB0, nB1);
+      if (3 < nchunk) pgs_small_chunk<3, false>(u0, u1, f0, f1, lb0, nB0, nB1);
+    } else {
+      pgs_small_chunk<0, true>(u0, u1, f0, f1, lb0, nB0, nB1);
+      pgs_small_chunk<1, true>(u0, u1, f0, f1, lb0, nB0, nB1);
+      pgs_small_chunk<2, true>(u0, u1, f0, f1, lb0, nB0, nB1);
+      pgs_small_chunk<3, true>(u0, u1, f0, f1, lb0, nB0, nB1);
+      if (4 < nchunk) pgs_small_chunk<4, true>(u0, u1, f0, f1, lb0, nB0, nB1);
+      if (5 < nchunk) pgs_small_chunk<5, true>(u0, u1, f0, f1, lb0, nB0, nB1);
+      if (6 < nchunk) pgs_small_chunk<6, true>(u0, u1, f0, f1, lb0, nB0, nB1);
+      if (7 < nchunk) pgs_small_chunk<7, true>(u0, u1, f0, f1, lb0, nB0, nB1);
+    }
+  }
+  return (lane < 16) ? f0 : f1;   // constraint `lane` (lanes 0..15: set 0, 16..31: set 1)
+}
+
 template <int CL, bool CAL>
 __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                             bool prof = false) {
@@ -1517,6 +1632,32 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
   const real arinv_l = (lane < nefc) ? arinv : 0.0;
   real u = -(((lane < nefc) ? (a0 - aref) : 0.0) * arinv_l);   // f = 0: u = -ARinv b
   real f = 0;
+#ifdef GM_PHASE_SPLIT_PGS
+  PH(15);   // developer split: impedance, ARinv, u init
+#endif
+  if (nchunk <= 8) {
+    // nefc <= 32: replicated DPP-row layout (see pgs_small_row)
+    const real narinv = -arinv_l;
+    real nBrow[32];
+#pragma unroll
+    for (int r = 0; r < 32; r++) {
+      unsigned long long onehot;
+      asm volatile("s_bfm_b64 %0, 1, %1" : "=s"(onehot) : "i"(r));
+      // -0.0 mirrors the general path's fma(-A[r], d, u) with A[r] = 0 (same zero sign);
+      // A[r] is 0 for every r >= nefc (A build), so rows past nefc stay exact no-ops
+      nBrow[r] = __builtin_amdgcn_inverse_ballot_w64(onehot) ? -0.0 : A[r] * narinv;
+    }
+#ifdef GM_PHASE_SPLIT_PGS
+    PH(16);   // developer split: B scaling
+#endif
+    const int iters = m->pgs_iterations;
+    const real fl = (nchunk <= 4) ? pgs_small<false>(nBrow, u, nl, nchunk, iters, lane)
+                                  : pgs_small<true>(nBrow, u, nl, nchunk, iters, lane);
+    PH(14);
+    S.efc_f[lane] = (lane < nefc) ? fl : 0.0;
+    __syncthreads();
+    return;
+  }
 #pragma unroll
   for (int c = 0; c < GM_MAX_EFC / 4; c++) {
     if (c >= nchunk) continue;

@@ -1710,11 +1710,27 @@ __device__ void constraint_accel(SharedT<CL>& S, const GmTopo* __restrict__ T, i
     else if (d == T->dof_palm) { grp_d = 3; slot = 7; }
     else { grp_d = (d - T->dof_f0[0]) / CL; slot = 6 + 1 + (d - T->dof_f0[grp_d]); }
     (void)b;
+    // rows in chunks of 8 with the LDS reads of a chunk issued before its (sequential,
+    // same-order) accumulation; rows past nefc are masked, never read as data
     real acc = 0;
-    for (int r = 0; r < nefc; r++) {
-      int g = S.ygrp[r];
-      bool use = (grp_d == GM_GRP_OBJECT) || (grp_d == GM_GRP_BASE && g >= 0 && g <= 3) || (grp_d == g);
-      if (use) acc += S.Y[r][slot] * S.efc_f[r];
+    const int nch = (__builtin_amdgcn_readfirstlane(nefc) + 7) >> 3;
+    for (int c = 0; c < nch; c++) {
+      real yv[8], fv[8];
+      int gv[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int r = c * 8 + k;
+        yv[k] = S.Y[r][slot];
+        fv[k] = S.efc_f[r];
+        gv[k] = S.ygrp[r];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int g = gv[k];
+        const bool use = (c * 8 + k < nefc) &&
+                         ((grp_d == GM_GRP_OBJECT) || (grp_d == GM_GRP_BASE && g >= 0 && g <= 3) || (grp_d == g));
+        if (use) acc += yv[k] * fv[k];
+      }
     }
     real Dd;
     if (grp_d == GM_GRP_OBJECT) Dd = S.Do[slot];

@@ -1396,6 +1396,7 @@ __device__ __forceinline__ real impedance(const gm_model* __restrict__ m, real r
   if (x <= 0) return dmin;
   real y;
   if (pw == 1) y = x;
+  else if (pw == 2) y = (x <= mid) ? x * x / mid : 1 - (1 - x) * (1 - x) / (1 - mid);   // MuJoCo's default power
   else if (x <= mid) y = pow(x, pw) / pow(mid, pw - 1);
   else y = 1 - pow(1 - x, pw) / pow(1 - mid, pw - 1);
   return dmin + y * (dmax - dmin);
@@ -1572,6 +1573,20 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
     for (int k = 0; k < CW - 1; k++) Yd[k] = 0;
   }
   const bool gj = grp >= 0 && grp <= 3;
+  // diagonal A_jj from the lane's own row (J == S.Y[lane]), the A build's arithmetic for
+  // i == j operation for operation, instead of a 64-way select out of A[]
+  real Ajj = 0;
+  if (lane < nefc) {
+    real ao = 0, ac = 0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) ao = fma(Yd[k], J[k], ao);
+    const real ab = Yd[6] * J[6];
+#pragma unroll
+    for (int q = 1; q <= CL; q++) ac = fma(Yd[6 + q], J[6 + q], ac);
+    Ajj = ao;
+    Ajj += gj ? ab : 0.0;
+    Ajj += gj ? ac : 0.0;
+  }
   // Delassus column A[:, lane] = Y D^-1 Y_lane^T, held in this lane's VGPRs
   real A[GM_MAX_EFC];
   const int nchunk_a = (__builtin_amdgcn_readfirstlane(nefc) + 7) >> 3;
@@ -1608,9 +1623,6 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
   real dr = m->solref[1], dmax = m->solimp[1];
   real K = 1.0 / (dmax * dmax * tc * tc * dr * dr);
   real Bd = 2.0 / (dmax * tc);
-  real Ajj = 0;
-#pragma unroll
-  for (int i = 0; i < GM_MAX_EFC; i++) if (i == lane) Ajj = A[i];
   real imp = impedance(m, pos);
   real aref = -Bd * vel - K * imp * pos;
   real R = (1 - imp) / imp * Ajj;

@@ -933,6 +933,9 @@ static double impedance(const gm_model* m, double r) {
   if (x <= 0) return dmin;
   double y;
   if (pw == 1) y = x;
+  /* pw == 2 (MuJoCo's default solimp power): x*x / mid, the correctly rounded square
+   * (glibc pow is within 0.52 ulp, so it can differ by one ulp); the device does the same */
+  else if (pw == 2) y = (x <= mid) ? x * x / mid : 1 - (1 - x) * (1 - x) / (1 - mid);
   else if (x <= mid) y = pow(x, pw) / pow(mid, pw - 1);
   else y = 1 - pow(1 - x, pw) / pow(1 - mid, pw - 1);
   return dmin + y * (dmax - dmin);

@@ -1562,11 +1562,14 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
   if (lane < nefc) {
     for (int k = 0; k < 6; k++) Yd[k] = J[k] * S.Do[k];
     Yd[6] = J[6] * S.Dbb;
+    // branch-free pivot lookup: every lane reads a valid LDS word and selects (a branch
+    // per q serialised the reads behind exec masks)
+    const bool fgrp = grp >= 0 && grp < 3;
+    const real* dsrc = fgrp ? &S.Df[grp][0] : &S.Dp[0];
 #pragma unroll
     for (int q = 1; q <= CL; q++) {
-      real dv = 1.0;
-      if (grp >= 0 && grp < 3 && q <= CL) dv = S.Df[grp][q];
-      else if (grp == 3 && q == 1) dv = S.Dp[1];
+      const real v = dsrc[fgrp ? q : 1];
+      const real dv = (fgrp || (grp == 3 && q == 1)) ? v : 1.0;
       Yd[6 + q] = J[6 + q] * dv;
     }
   } else {

@@ -656,21 +656,16 @@ __device__ void mass_and_forces(SharedT<CL>& S, const gm_model* __restrict__ m, 
     inert_mul(F, S.Ic[b], cd);
     if (c == GM_GRP_BASE) {
       S.Hbb = dot6(cd, F) + add;
-    } else if (c == GM_GRP_OBJECT) {
-#pragma unroll
-      for (int q = 0; q < 6; q++) {
-        if (q > p) continue;
-        real v = dot6(S.cdof[T->dof_obj + q], F);
-        if (q == p) v += add;
-        S.Ho[TRI(p, q)] = v;
-      }
     } else {
-      const int d0 = (c < 3) ? T->dof_f0[c] : T->dof_palm;
-      real* Hrow = (c < 3) ? &S.Hf[c][TRI(p, 0)] : &S.Hp[TRI(p, 0)];
+      // object and chain rows share one loop (one pass of the wave instead of two
+      // divergent ones): row p of the object block or of the chain's block
+      const bool objd = c == GM_GRP_OBJECT;
+      const int d0 = objd ? T->dof_obj : (c < 3) ? T->dof_f0[c] : T->dof_palm;
+      real* Hrow = objd ? &S.Ho[TRI(p, 0)] : (c < 3) ? &S.Hf[c][TRI(p, 0)] : &S.Hp[TRI(p, 0)];
 #pragma unroll
       for (int q = 0; q <= CL; q++) {
         if (q > p) continue;
-        const int dq = (q == 0) ? T->dof_base : d0 + q - 1;
+        const int dq = objd ? d0 + q : (q == 0) ? T->dof_base : d0 + q - 1;
         real v = dot6(S.cdof[dq], F);
         if (q == p) v += add;
         Hrow[q] = v;
@@ -1592,15 +1587,16 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
   }
   // Delassus column A[:, lane] = Y D^-1 Y_lane^T, held in this lane's VGPRs
   real A[GM_MAX_EFC];
-  const int nchunk_a = (__builtin_amdgcn_readfirstlane(nefc) + 7) >> 3;
+  // rows in chunks of 4 (the PGS granularity): fewer padding rows than chunks of 8
+  const int nchunk_a = (__builtin_amdgcn_readfirstlane(nefc) + 3) >> 2;
 #pragma unroll
-  for (int c = 0; c < GM_MAX_EFC / 8; c++) {
+  for (int c = 0; c < GM_MAX_EFC / 4; c++) {
 #pragma unroll
-    for (int rr = 0; rr < 8; rr++) A[c * 8 + rr] = 0;
+    for (int rr = 0; rr < 4; rr++) A[c * 4 + rr] = 0;
     if (c >= nchunk_a) continue;
 #pragma unroll
-    for (int rr = 0; rr < 8; rr++) {
-      const int i = c * 8 + rr;
+    for (int rr = 0; rr < 4; rr++) {
+      const int i = c * 4 + rr;
       // rows past nefc hold stale data in LDS: their products are masked below
       const real* Yi = S.Y[i];
       const int gi = S.ygrp[i];

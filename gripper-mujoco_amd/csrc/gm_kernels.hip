@@ -38,6 +38,16 @@
 // `real` is the dynamics type: fp64, MuJoCo's mjtNum.  Collision geometry and the
 // PGS inner loop run in fp32 (see DESIGN.md "Precision").
 typedef double real;
+// Developer switch: GM_SUBSTEP_INLINE inlines the physics substep into the step kernel and
+// outlines the per-substep / per-env-step bookkeeping instead (default: the substep is
+// the outlined unit).
+#ifdef GM_SUBSTEP_INLINE
+#define GM_SUBSTEP_ATTR __device__ __forceinline__
+#define GM_EPI_ATTR __device__ __noinline__
+#else
+#define GM_SUBSTEP_ATTR __device__ __noinline__
+#define GM_EPI_ATTR __device__
+#endif
 
 struct DebugOut {
   int32_t* ncon;      // [n_envs]
@@ -1891,7 +1901,7 @@ __device__ int g_step_to(GmGrip& g, const GmGrip& t, int num) {
 
 // update_all: update_stepper / update_constraints (myfunctions.cpp:2129-2284), antiroll
 template <int CL>
-__device__ __forceinline__ void update_all(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+GM_EPI_ATTR void update_all(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
   if (lane == 0) {
     GmEnvState& s = S.s;
     if (s.time > s.last_step_time + m->time_per_step) {
@@ -2118,7 +2128,7 @@ __device__ void extract_forces(SharedT<CL>& S, const gm_model* __restrict__ m, c
 
 // MjClass::monitor_sensors (mjclass.cpp:741-898)
 template <int CL>
-__device__ void monitor_sensors(SharedT<CL>& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
+GM_EPI_ATTR void monitor_sensors(SharedT<CL>& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
                                 const GmTopo* __restrict__ T, int lane) {
   __shared__ int bend_ready;
   if (lane == 0) bend_ready = s_ready(S.s, C->s.bending_gauge, SL_BEND);
@@ -2202,7 +2212,7 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
 // issues global loads for the model and LDS instructions for the per-env image rather
 // than generic (flat) accesses that would serialise the two.
 template <int CL, bool CAL>
-__device__ __noinline__ void physics_substep(GM_AS_LDS SharedT<CL>* S_, const GM_AS_GLOBAL gm_model* m_,
+GM_SUBSTEP_ATTR void physics_substep(GM_AS_LDS SharedT<CL>* S_, const GM_AS_GLOBAL gm_model* m_,
                                              const GM_AS_GLOBAL GmTopo* T_, int lane, bool prof) {
   physics_substep_body<CL, CAL>(*(SharedT<CL>*)S_, (const gm_model*)m_, (const GmTopo*)T_, lane, prof);
 }
@@ -2215,7 +2225,7 @@ __device__ __forceinline__ float normalise_between(float val, float mn, float mx
 }
 
 template <int CL>
-__device__ void sense_gripper_state(SharedT<CL>& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C) {
+GM_EPI_ATTR void sense_gripper_state(SharedT<CL>& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C) {
   GmEnvState& s = S.s;
   const gm_settings& st = C->s;
   const double* bmn = C->base_min;
@@ -2273,7 +2283,7 @@ __device__ float mag3f(const float* v) { return (float)sqrt((double)v[0] * v[0] 
 
 // MjClass::update_env (mjclass.cpp:966-1346) + update_events (5437-5469)
 template <int CL>
-__device__ void update_env(SharedT<CL>& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
+GM_EPI_ATTR void update_env(SharedT<CL>& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
                            const GmTopo* __restrict__ T) {
   GmEnvState& s = S.s;
   const gm_settings& st = C->s;
@@ -2452,7 +2462,7 @@ __device__ int get_obs(const GmEnvState& s, const gm_config* __restrict__ C, flo
   return n;
 }
 
-__device__ int is_done(const GmEnvState& s, const gm_config* __restrict__ C) {
+GM_EPI_ATTR int is_done(const GmEnvState& s, const gm_config* __restrict__ C) {
   const gm_settings& st = C->s;
   int k = 0;
   int done = 0;

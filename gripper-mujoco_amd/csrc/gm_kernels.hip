@@ -498,12 +498,17 @@ __device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const Gm
   const int grp = (b >= 0) ? T->body_group[b] : -1;
   const bool chain = grp >= 0 && grp <= 3;
   const int p = chain ? T->body_cpos[b] : 0;
-  const int Lc = (grp == 3) ? 1 : CL;
   const int d = chain ? (grp < 3 ? T->dof_f0[grp] + p - 1 : T->dof_palm) : db;
   real cd[6], v[6];
   const real qd = chain ? S.s.qvel[d] : 0.0;
 #pragma unroll
   for (int k = 0; k < 6; k++) { cd[k] = chain ? S.cdof[d][k] : 0.0; v[k] = cd[k] * qd; }
+  // The scans add their shifted operand unconditionally: every source outside a lane's
+  // chain segment holds an exact zero (the empty position 0 of each finger row, the base
+  // lane before the palm, the no-body lanes past the chain end, the zero-inertia object
+  // lane, and DPP's bound_ctrl zero past the row edge), so the old p > off / p + off <= Lc
+  // selects only cost two v_cndmask per double per step.  The sums of nonzero terms keep
+  // the scan's association; only the sign of an exactly-zero entry can differ.
   // velocities: inclusive prefix along the chain, then the base contribution
   real cv[6];
 #pragma unroll
@@ -513,7 +518,7 @@ __device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const Gm
 #pragma unroll
     for (int k = 0; k < 6; k++) {
       const real nb = row_shr(cv[k], off);
-      if (p > off) cv[k] += nb;
+      cv[k] += nb;
     }
   }
   real cvp[6];
@@ -533,7 +538,7 @@ __device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const Gm
 #pragma unroll
     for (int k = 0; k < 6; k++) {
       const real nb = row_shr(ca[k], off);
-      if (p > off) ca[k] += nb;
+      ca[k] += nb;
     }
   }
 #pragma unroll
@@ -555,12 +560,12 @@ __device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const Gm
 #pragma unroll
     for (int k = 0; k < 6; k++) {
       const real nb = row_shl(f[k], off);
-      if (p + off <= Lc) f[k] += nb;
+      f[k] += nb;
     }
 #pragma unroll
     for (int k = 0; k < 10; k++) {
       const real nb = row_shl(ci[k], off);
-      if (p + off <= Lc) ci[k] += nb;
+      ci[k] += nb;
     }
   }
   if (chain) {

@@ -809,11 +809,12 @@ __device__ __forceinline__ real rows_LT_D(SharedT<CL>& S, int rowf, int p, bool 
     else if (obj) { if (k > p && k < 6) v = S.Ho[TRI(k, p)]; }
     Lc[k] = v;
   }
+  // Lc[k] is an exact zero wherever the update does not apply (k <= p, k > 5 on the
+  // object row, lanes off the blocks), so the update runs unpredicated
 #pragma unroll
   for (int k = CL; k >= 1; k--) {
-    const bool act = fing || (obj && k <= 5);
     const real yk = row_bcast(y, k);
-    if (act && p < k) y -= Lc[k] * yk;
+    y -= Lc[k] * yk;
   }
   if (fing) { if (p >= 1) y *= S.Df[rowf][p]; }
   else if (obj) y *= S.Do[p];
@@ -831,11 +832,11 @@ __device__ __forceinline__ real rows_L(SharedT<CL>& S, int rowf, int p, bool fin
     else if (obj) { if (k < p) v = S.Ho[TRI(p, k)]; }
     Lr[k] = v;
   }
+  // Lr[k] is an exact zero wherever the update does not apply (unpredicated, as above)
 #pragma unroll
   for (int k = 0; k < CL; k++) {
-    const bool act = fing || (obj && k < 5);
     const real xk = row_bcast(y, k);
-    if (act && p > k) y -= Lr[k] * xk;
+    y -= Lr[k] * xk;
   }
   return y;
 }

@@ -301,7 +301,7 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
       }
     }
   }
-#ifdef GM_PHASE_SPLIT_PGS
+#if defined(GM_PHASE_SPLIT_PGS) || defined(GM_PHASE_SPLIT_COLL)
   PH(0);
 #else
   PH(15);
@@ -363,7 +363,7 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
     }
   }
   __syncthreads();
-#ifdef GM_PHASE_SPLIT_PGS
+#if defined(GM_PHASE_SPLIT_PGS) || defined(GM_PHASE_SPLIT_COLL)
   PH(0);
 #else
   PH(16);
@@ -946,24 +946,32 @@ __device__ __forceinline__ int plane_box_point(const GeomV& P, const GeomV& B, i
   for (int k = 0; k < 3; k++) { h.pos[k] = v[k] - 0.5 * d * nz[k]; h.n[k] = nz[k]; }
   return 1;
 }
-__device__ __forceinline__ int plane_cyl_point(const GeomV& P, const GeomV& Cy, int i, Hit& h) {
-  real nz[3] = {P.R[2], P.R[5], P.R[8]};
-  real a[3] = {Cy.R[2], Cy.R[5], Cy.R[8]};
-  real r = Cy.size[0], hh = Cy.size[1];
-  real na = dot3(nz, a);
-  real w[3] = {-nz[0] + na * a[0], -nz[1] + na * a[1], -nz[2] + na * a[2]};
+// per-pair part of the plane-cylinder rim test (the rim frame: axis a, w = the in-plane
+// direction towards the plane, a x w), computed once per pair instead of once per rim
+// point -- the same operations, so the same values
+struct CylFrame { real nz[3], a[3], w[3], axw[3]; };
+__device__ __forceinline__ void cyl_frame(const GeomV& P, const GeomV& Cy, CylFrame& F) {
+  F.nz[0] = P.R[2]; F.nz[1] = P.R[5]; F.nz[2] = P.R[8];
+  F.a[0] = Cy.R[2]; F.a[1] = Cy.R[5]; F.a[2] = Cy.R[8];
+  real na = dot3(F.nz, F.a);
+  real w[3] = {-F.nz[0] + na * F.a[0], -F.nz[1] + na * F.a[1], -F.nz[2] + na * F.a[2]};
   real lw = sqrt(dot3(w, w));
   if (lw < 1e-6) { w[0] = Cy.R[0]; w[1] = Cy.R[3]; w[2] = Cy.R[6]; }
   else { w[0] /= lw; w[1] /= lw; w[2] /= lw; }
-  real axw[3];
-  cross3(axw, a, w);
+  F.w[0] = w[0]; F.w[1] = w[1]; F.w[2] = w[2];
+  cross3(F.axw, F.a, F.w);
+}
+__device__ __forceinline__ int plane_cyl_point(const GeomV& P, const GeomV& Cy, const CylFrame& F, int i, Hit& h) {
+  const real* nz = F.nz;
+  const real* a = F.a;
+  real r = Cy.size[0], hh = Cy.size[1];
   int s = i >> 2, k = i & 3;
   real sg = s == 0 ? 1.0 : -1.0;
   real dir[3];
-  if (k == 0) { dir[0] = w[0]; dir[1] = w[1]; dir[2] = w[2]; }
-  else if (k == 1) { dir[0] = axw[0]; dir[1] = axw[1]; dir[2] = axw[2]; }
-  else if (k == 2) { dir[0] = -w[0]; dir[1] = -w[1]; dir[2] = -w[2]; }
-  else { dir[0] = -axw[0]; dir[1] = -axw[1]; dir[2] = -axw[2]; }
+  if (k == 0) { dir[0] = F.w[0]; dir[1] = F.w[1]; dir[2] = F.w[2]; }
+  else if (k == 1) { dir[0] = F.axw[0]; dir[1] = F.axw[1]; dir[2] = F.axw[2]; }
+  else if (k == 2) { dir[0] = -F.w[0]; dir[1] = -F.w[1]; dir[2] = -F.w[2]; }
+  else { dir[0] = -F.axw[0]; dir[1] = -F.axw[1]; dir[2] = -F.axw[2]; }
   real v[3];
   for (int t = 0; t < 3; t++) v[t] = Cy.c[t] + sg * hh * a[t] + r * dir[t];
   real dv[3] = {v[0] - P.c[0], v[1] - P.c[1], v[2] - P.c[2]};
@@ -1245,10 +1253,15 @@ __device__ void write_contact(SharedT<CL>& S, int slot, int g1, int g2, const Hi
 }
 
 template <int CL>
-__device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+__device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
+                          bool prof = false) {
+  unsigned long long t0 = prof ? clock64() : 0;
+  (void)t0;
   int cnt = 0, kind = 0, g1 = 0, g2 = 0;
+  unsigned hm = 0;   // plane-box / plane-cylinder: the counted corners (pass 2 revisits only these)
   Hit single;
   GeomV A, B;
+  CylFrame cf;
   if (lane < T->npair) {
     int a = m->pair_a[lane], b = m->pair_b[lane];
     int ta = (a == T->geom_obj) ? S.s.obj_type : m->geom_type[a];
@@ -1256,6 +1269,9 @@ __device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const 
     canon_pair(a, b, ta, tb, g1, g2);
     load_geom(S, m, T, g1, A);
     load_geom(S, m, T, g2, B);
+#ifdef GM_PHASE_SPLIT_COLL
+    PH(15);   // developer split: pair setup + geom poses
+#endif
     bool pass;
     if (A.type == GM_GEOM_PLANE) {
       real nz[3] = {A.R[2], A.R[5], A.R[8]};
@@ -1272,11 +1288,20 @@ __device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const 
         else if (B.type == GM_GEOM_BOX) {
           kind = 2;
           Hit t;
-          for (int i = 0; i < 8 && cnt < 4; i++) cnt += plane_box_point(A, B, i, t);
+          for (int i = 0; i < 8 && cnt < 4; i++) {
+            const int ok = plane_box_point(A, B, i, t);
+            hm |= (unsigned)ok << i;
+            cnt += ok;
+          }
         } else if (B.type == GM_GEOM_CYLINDER) {
           kind = 3;
           Hit t;
-          for (int i = 0; i < 8 && cnt < 4; i++) cnt += plane_cyl_point(A, B, i, t);
+          cyl_frame(A, B, cf);
+          for (int i = 0; i < 8 && cnt < 4; i++) {
+            const int ok = plane_cyl_point(A, B, cf, i, t);
+            hm |= (unsigned)ok << i;
+            cnt += ok;
+          }
         }
       } else if (A.type == GM_GEOM_SPHERE && B.type == GM_GEOM_BOX) {
         kind = 1; cnt = sphere_box(A, B, single);
@@ -1286,6 +1311,9 @@ __device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const 
       }
     }
   }
+#ifdef GM_PHASE_SPLIT_COLL
+  PH(16);   // developer split: broadphase + narrowphase
+#endif
   // contact slots: exclusive prefix sum of the per-lane counts (0..4, three bits) from
   // three ballots -- no LDS round trip
   int off = 0, total = 0;
@@ -1302,9 +1330,13 @@ __device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const 
     } else {
       Hit t;
       int w = 0;
-      for (int i = 0; i < 8 && w < cnt; i++) {
-        int ok = (kind == 2) ? plane_box_point(A, B, i, t) : plane_cyl_point(A, B, i, t);
-        if (ok) { if (off + w < GM_MAX_CON) write_contact(S, off + w, g1, g2, t, mu); w++; }
+      while (hm) {   // the counted corners in index order, as pass 1 found them
+        const int i = __builtin_ctz(hm);
+        hm &= hm - 1;
+        if (kind == 2) plane_box_point(A, B, i, t);
+        else plane_cyl_point(A, B, cf, i, t);
+        if (off + w < GM_MAX_CON) write_contact(S, off + w, g1, g2, t, mu);
+        w++;
       }
     }
   }
@@ -2197,7 +2229,7 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
   PH(3);
   solve_full<CL>(S, T, S.frc, S.qacc, lane);
   PH(4);
-  collision(S, m, T, lane);
+  collision(S, m, T, lane, prof);
   PH(5);
   constraints<CL, CAL>(S, m, T, lane, prof);
   PH(6);

@@ -1506,9 +1506,24 @@ __device__ __forceinline__ void pgs_small_chunk(real& u0, real& u1, real& f0, re
   pgs_small_row<4 * C + 3, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
 }
 
+template <int NCH, bool TWO>
+__device__ __forceinline__ void pgs_small_sweeps(int iters, real& u0, real& u1, real& f0, real& f1, real lb0,
+                                                 const real* nB0, const real* nB1) {
+  for (int it = 0; it < iters; it++) {
+    pgs_small_chunk<0, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
+    if constexpr (NCH > 1) pgs_small_chunk<1, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
+    if constexpr (NCH > 2) pgs_small_chunk<2, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
+    if constexpr (NCH > 3) pgs_small_chunk<3, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
+    if constexpr (NCH > 4) pgs_small_chunk<4, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
+    if constexpr (NCH > 5) pgs_small_chunk<5, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
+    if constexpr (NCH > 6) pgs_small_chunk<6, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
+    if constexpr (NCH > 7) pgs_small_chunk<7, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
+  }
+}
+
 // The whole small-problem solve: gather the scaled Delassus columns into the replicated
 // layout (lane p of every 16-lane row gets constraint p and, with TWO, p + 16), run the
-// fixed sweeps (chunks past nchunk skipped by a scalar guard, as in the general path) and
+// fixed sweeps over the nchunk live chunks (rows past nefc in the last one are exact no-ops) and
 // return f of constraint `lane` (lanes 0..31).  nBrow is the general path's
 // lane-per-row scaled column (B_j[r] = ARinv_j AR_jr, zero on the diagonal), negated.
 template <bool TWO>
@@ -1526,21 +1541,21 @@ __device__ __forceinline__ real pgs_small(const real* nBrow, real u, int nl, int
   real u1 = TWO ? bperm_f64(a1, u) : 0.0;
   const real lb0 = (p < nl) ? -__builtin_inf() : 0.0;   // lock rows come first (nl <= 4)
   real f0 = 0.0, f1 = 0.0;
-  for (int it = 0; it < iters; it++) {
-    if constexpr (!TWO) {
-      if (0 < nchunk) pgs_small_chunk<0, false>(u0, u1, f0, f1, lb0, nB0, nB1);
-      if (1 < nchunk) pgs_small_chunk<1, false>(u0, u1, f0, f1, lb0, nB0, nB1);
-      if (2 < nchunk) pgs_small_chunk<2, false>(u0, u1, f0, f1, lb0, nB0, nB1);
-      if (3 < nchunk) pgs_small_chunk<3, false>(u0, u1, f0, f1, lb0, nB0, nB1);
-    } else {
-      pgs_small_chunk<0, true>(u0, u1, f0, f1, lb0, nB0, nB1);
-      pgs_small_chunk<1, true>(u0, u1, f0, f1, lb0, nB0, nB1);
-      pgs_small_chunk<2, true>(u0, u1, f0, f1, lb0, nB0, nB1);
-      pgs_small_chunk<3, true>(u0, u1, f0, f1, lb0, nB0, nB1);
-      if (4 < nchunk) pgs_small_chunk<4, true>(u0, u1, f0, f1, lb0, nB0, nB1);
-      if (5 < nchunk) pgs_small_chunk<5, true>(u0, u1, f0, f1, lb0, nB0, nB1);
-      if (6 < nchunk) pgs_small_chunk<6, true>(u0, u1, f0, f1, lb0, nB0, nB1);
-      if (7 < nchunk) pgs_small_chunk<7, true>(u0, u1, f0, f1, lb0, nB0, nB1);
+  // one branch-free sweep body per chunk count (a scalar branch inside the sweep costs
+  // more than the padding rows it would skip)
+  if constexpr (!TWO) {
+    switch (nchunk) {
+      case 1: pgs_small_sweeps<1, false>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
+      case 2: pgs_small_sweeps<2, false>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
+      case 3: pgs_small_sweeps<3, false>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
+      default: pgs_small_sweeps<4, false>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
+    }
+  } else {
+    switch (nchunk) {
+      case 5: pgs_small_sweeps<5, true>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
+      case 6: pgs_small_sweeps<6, true>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
+      case 7: pgs_small_sweeps<7, true>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
+      default: pgs_small_sweeps<8, true>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
     }
   }
   return (lane < 16) ? f0 : f1;   // constraint `lane` (lanes 0..15: set 0, 16..31: set 1)

@@ -1955,12 +1955,21 @@ __device__ int g_step_to(GmGrip& g, const GmGrip& t, int num) {
 // update_all: update_stepper / update_constraints (myfunctions.cpp:2129-2284), antiroll
 template <int CL>
 GM_EPI_ATTR void update_all(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+  GmEnvState& s = S.s;
+  const bool stepping = s.time > s.last_step_time + m->time_per_step;   // uniform (LDS broadcast)
+  int nx = 0, ny = 0, nz = 0;
+  if (stepping) {
+    // the end (lane 0) and next (lane 1) grippers' step counts and angle in one pass of
+    // the wave instead of two serial evaluations on lane 0 (an asin and two divisions each)
+    const GmGrip& g = (lane & 1) ? s.next : s.end;
+    const int xs = g_xs(g), zs = g_zs(g);
+    const double th = g_th_deg(g);
+    nx = __builtin_amdgcn_readlane(xs, 0) != __builtin_amdgcn_readlane(xs, 1);
+    ny = !(fabs(readlane_real(th, 0) - readlane_real(th, 1)) < 5e-1);
+    nz = __builtin_amdgcn_readlane(zs, 0) != __builtin_amdgcn_readlane(zs, 1);
+  }
   if (lane == 0) {
-    GmEnvState& s = S.s;
-    if (s.time > s.last_step_time + m->time_per_step) {
-      int nx = g_xs(s.end) != g_xs(s.next);
-      int ny = !(fabs(g_th_deg(s.end) - g_th_deg(s.next)) < 5e-1);
-      int nz = g_zs(s.end) != g_zs(s.next);
+    if (stepping) {
       if (nx != s.old_x) {
         for (int k = 0; k < T->nlock; k++)
           if (m->lock_kind[k] == 0) { s.lock_active[k] = !nx; if (!nx) s.lock_q[k] = S.lock_pre[k]; }

@@ -1709,7 +1709,13 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
 #ifdef GM_PHASE_SPLIT_PGS
   PH(15);   // developer split: impedance, ARinv, u init
 #endif
+#ifdef GM_PGS_GENERAL_ONLY
+  // test build (lib/libgm_pgsgen.so): every problem on the lane-per-row path, so the
+  // GPU tests can hold the DPP-row path against it on identical states
+  if (false) {
+#else
   if (nchunk <= 8) {
+#endif
     // nefc <= 32: replicated DPP-row layout (see pgs_small_row)
     const real narinv = -arinv_l;
     real nBrow[32];

@@ -30,8 +30,8 @@ def spawn_positions(rng: np.random.Generator, n: int, n_objects: int, pos_noise_
 class BatchedGripperEnv:
     def __init__(self, n_envs: int, object_set: str = "set6_synthetic", settings=None,
                  model_params: ModelParams | None = None, device: int = 0, seed: int = 1234,
-                 env_offset: int = 0, max_episode_steps: int = MAX_EPISODE_STEPS):
-        self.lib = load_library()
+                 env_offset: int = 0, max_episode_steps: int = MAX_EPISODE_STEPS, lib=None):
+        self.lib = lib if lib is not None else load_library()
         self.n_envs = int(n_envs)
         self.model = ModelBlob(model_params)
         self.settings = settings if settings is not None else canonical_settings(seed=seed)

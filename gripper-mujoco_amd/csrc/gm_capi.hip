@@ -303,7 +303,8 @@ int gm_reset(gm_ctx* c, const uint8_t* mask, const gm_spawn* spawn) {
   }
   int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
   hipLaunchKernelGGL(gm_reset_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
-                     c->d_topo, c->d_eq, dm, ds, c->d_objs, c->n_objects, c->n_envs, c->d_scene, c->scene_tries);
+                     c->d_topo, c->d_eq, dm, ds, c->d_objs, c->n_objects, c->n_envs, c->d_scene, c->scene_tries,
+                     c->d_obs);
   HIPCHK(c, hipGetLastError());
   if (mask || spawn) HIPCHK(c, hipStreamSynchronize(c->stream));   // host buffers may be reused
   return GM_OK;
@@ -643,20 +644,20 @@ int gm_get_event_rows(gm_ctx* c, int32_t* rows, int32_t* absc, float* lastv) {
   return GM_OK;
 }
 
-int gm_get_state(gm_ctx* c, float* qpos, float* qvel, double* time) {
+int gm_get_state(gm_ctx* c, double* qpos, double* qvel, double* time) {
   if (!c) return GM_E_ARG;
   std::vector<GmEnvState> h;
   int rc = fetch_states(c, h);
   if (rc) return rc;
   for (int e = 0; e < c->n_envs; e++) {
-    if (qpos) for (int i = 0; i < c->model.nq; i++) qpos[(size_t)e * c->model.nq + i] = (float)h[e].qpos[i];
-    if (qvel) for (int i = 0; i < c->model.nv; i++) qvel[(size_t)e * c->model.nv + i] = (float)h[e].qvel[i];
+    if (qpos) for (int i = 0; i < c->model.nq; i++) qpos[(size_t)e * c->model.nq + i] = h[e].qpos[i];
+    if (qvel) for (int i = 0; i < c->model.nv; i++) qvel[(size_t)e * c->model.nv + i] = h[e].qvel[i];
     if (time) time[e] = h[e].time;
   }
   return GM_OK;
 }
 
-int gm_set_state(gm_ctx* c, const float* qpos, const float* qvel) {
+int gm_set_state(gm_ctx* c, const double* qpos, const double* qvel) {
   if (!c) return GM_E_ARG;
   std::vector<GmEnvState> h;
   int rc = fetch_states(c, h);
@@ -666,6 +667,28 @@ int gm_set_state(gm_ctx* c, const float* qpos, const float* qvel) {
     if (qvel) for (int i = 0; i < c->model.nv; i++) h[e].qvel[i] = qvel[(size_t)e * c->model.nv + i];
   }
   HIPCHK(c, hipMemcpyAsync(c->d_state, h.data(), sizeof(GmEnvState) * (size_t)c->n_envs, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+
+int64_t gm_env_state_size(void) { return (int64_t)sizeof(GmEnvState); }
+
+int gm_get_env_states(gm_ctx* c, void* out) {
+  if (!c || !out) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpyAsync(out, c->d_state, sizeof(GmEnvState) * (size_t)c->n_envs, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+
+int gm_set_env_states(gm_ctx* c, const void* in) {
+  if (!c || !in) return GM_E_ARG;
+  const GmEnvState* h = (const GmEnvState*)in;
+  for (int e = 0; e < c->n_envs; e++)
+    if (h[e].obj_index < 0 || h[e].obj_index >= c->n_objects || h[e].extra_substeps < 0)
+      return fail(c, GM_E_ARG, "gm_set_env_states: env " + std::to_string(e) + " is not a valid state");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpyAsync(c->d_state, in, sizeof(GmEnvState) * (size_t)c->n_envs, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return GM_OK;
 }
@@ -699,23 +722,29 @@ void* gm_device_done(gm_ctx* c) { return c ? c->d_done : nullptr; }
 void* gm_device_actions(gm_ctx* c) { return c ? c->d_act : nullptr; }
 void* gm_stream(gm_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
-int gm_debug_substep(gm_ctx* c, int32_t* ncon, float* contact, float* efc_force, float* qacc) {
+int gm_debug_substep(gm_ctx* c, int32_t* ncon, double* contact, double* efc_force, double* qacc, int32_t* nefc,
+                     double* obj_wrench) {
   if (!c) return GM_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
-  int32_t* d_ncon; float *d_con, *d_f, *d_q;
+  int32_t *d_ncon, *d_nefc; double *d_con, *d_f, *d_q, *d_w;
   size_t n = (size_t)c->n_envs;
   HIPCHK(c, hipMalloc(&d_ncon, sizeof(int32_t) * n));
-  HIPCHK(c, hipMalloc(&d_con, sizeof(float) * n * GM_MAX_CON * 16));
-  HIPCHK(c, hipMalloc(&d_f, sizeof(float) * n * GM_MAX_EFC));
-  HIPCHK(c, hipMalloc(&d_q, sizeof(float) * n * GM_MAX_DOF));
-  DebugOut dbg{d_ncon, d_con, d_f, d_q, nullptr};
+  HIPCHK(c, hipMalloc(&d_nefc, sizeof(int32_t) * n));
+  HIPCHK(c, hipMalloc(&d_con, sizeof(double) * n * GM_MAX_CON * 16));
+  HIPCHK(c, hipMalloc(&d_f, sizeof(double) * n * GM_MAX_EFC));
+  HIPCHK(c, hipMalloc(&d_q, sizeof(double) * n * GM_MAX_DOF));
+  HIPCHK(c, hipMalloc(&d_w, sizeof(double) * n * 6));
+  DebugOut dbg{d_ncon, d_con, d_f, d_q, nullptr, d_nefc, d_w};
   HIPCHK(c, launch_step(c, c->n_envs, c->n_envs, 2, dbg));
   if (ncon) HIPCHK(c, hipMemcpyAsync(ncon, d_ncon, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
-  if (contact) HIPCHK(c, hipMemcpyAsync(contact, d_con, sizeof(float) * n * GM_MAX_CON * 16, hipMemcpyDeviceToHost, c->stream));
-  if (efc_force) HIPCHK(c, hipMemcpyAsync(efc_force, d_f, sizeof(float) * n * GM_MAX_EFC, hipMemcpyDeviceToHost, c->stream));
-  if (qacc) HIPCHK(c, hipMemcpyAsync(qacc, d_q, sizeof(float) * n * GM_MAX_DOF, hipMemcpyDeviceToHost, c->stream));
+  if (nefc) HIPCHK(c, hipMemcpyAsync(nefc, d_nefc, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+  if (contact) HIPCHK(c, hipMemcpyAsync(contact, d_con, sizeof(double) * n * GM_MAX_CON * 16, hipMemcpyDeviceToHost, c->stream));
+  if (efc_force) HIPCHK(c, hipMemcpyAsync(efc_force, d_f, sizeof(double) * n * GM_MAX_EFC, hipMemcpyDeviceToHost, c->stream));
+  if (qacc) HIPCHK(c, hipMemcpyAsync(qacc, d_q, sizeof(double) * n * GM_MAX_DOF, hipMemcpyDeviceToHost, c->stream));
+  if (obj_wrench) HIPCHK(c, hipMemcpyAsync(obj_wrench, d_w, sizeof(double) * n * 6, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  (void)hipFree(d_ncon); (void)hipFree(d_con); (void)hipFree(d_f); (void)hipFree(d_q);
+  (void)hipFree(d_ncon); (void)hipFree(d_nefc); (void)hipFree(d_con); (void)hipFree(d_f); (void)hipFree(d_q);
+  (void)hipFree(d_w);
   return GM_OK;
 }
 
@@ -743,7 +772,7 @@ int gm_autoreset(gm_ctx* c, int max_episode_steps, const gm_spawn* spawn, int sp
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(gm_reset_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
                      c->d_topo, c->d_eq, c->d_mask, ds, c->d_objs, c->n_objects, c->n_envs, c->d_scene,
-                     c->scene_tries);
+                     c->scene_tries, c->d_obs);
   HIPCHK(c, hipGetLastError());
   if (spawn && !spawn_on_device) HIPCHK(c, hipStreamSynchronize(c->stream));
   return GM_OK;

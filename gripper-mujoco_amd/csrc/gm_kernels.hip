@@ -18,7 +18,8 @@
 //     reductions in the inner loop)
 //   - reference scalar logic (stepper in fp64, events, RNG): lane 0
 // The algorithm is the engine spec restated in oracle/oracle.c (fp64); this
-// file is the fp32 device implementation of the same spec.
+// file is the fp64 device implementation of the same spec (MuJoCo's mjtNum is double),
+// with fp32 only where the reference itself uses float (sensor windows, observations).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "gm_state.h"
@@ -35,8 +36,8 @@
 #define CW (CL + 8)   // compact row: obj[6], base, chain[CL] (+1 scratch slot); needs CL in scope
 #define PI_F 3.14159265358979f
 
-// `real` is the dynamics type: fp64, MuJoCo's mjtNum.  Collision geometry and the
-// PGS inner loop run in fp32 (see DESIGN.md "Precision").
+// `real` is the dynamics type: fp64, MuJoCo's mjtNum.  Kinematics, dynamics, collision
+// geometry and the PGS solve all run in it (see DESIGN.md "Precision").
 typedef double real;
 // Developer switch: GM_SUBSTEP_INLINE inlines the physics substep into the step kernel and
 // outlines the per-substep / per-env-step bookkeeping instead (default: the substep is
@@ -51,10 +52,12 @@ typedef double real;
 
 struct DebugOut {
   int32_t* ncon;      // [n_envs]
-  float* contact;     // [n_envs][GM_MAX_CON][16]
-  float* efc_force;   // [n_envs][GM_MAX_EFC]
-  float* qacc;        // [n_envs][GM_MAX_DOF]
+  double* contact;    // [n_envs][GM_MAX_CON][16]
+  double* efc_force;  // [n_envs][GM_MAX_EFC]
+  double* qacc;       // [n_envs][GM_MAX_DOF]
   unsigned long long* phase;   // [n_envs][GM_NPHASE] shader-clock cycles per phase (profiling)
+  int32_t* nefc;      // [n_envs]
+  double* wrench;     // [n_envs][6] the live object's cfrc_ext, [force; torque]
 };
 #define GM_NPHASE 24
 
@@ -1047,12 +1050,13 @@ __device__ __forceinline__ void support_geom(const GeomV& G, const real* d, real
   real dl[3];
   mulmtv3(dl, G.R, d);
   real pl[3] = {0, 0, 0};
+  // face / rim-line ties take the centre (oracle.c support_geom, GM_SUPPORT_TIE)
   if (G.type == GM_GEOM_BOX) {
-    for (int k = 0; k < 3; k++) pl[k] = dl[k] >= 0 ? G.size[k] : -G.size[k];
+    for (int k = 0; k < 3; k++) pl[k] = fabs(dl[k]) < GM_SUPPORT_TIE ? 0.0 : (dl[k] >= 0 ? G.size[k] : -G.size[k]);
   } else if (G.type == GM_GEOM_CYLINDER) {
     real rr = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
     if (rr > 1e-12) { pl[0] = G.size[0] * dl[0] / rr; pl[1] = G.size[0] * dl[1] / rr; }
-    pl[2] = dl[2] >= 0 ? G.size[1] : -G.size[1];
+    pl[2] = fabs(dl[2]) < GM_SUPPORT_TIE ? 0.0 : (dl[2] >= 0 ? G.size[1] : -G.size[1]);
   } else if (G.type == GM_GEOM_SPHERE) {
     real l = sqrt(dot3(dl, dl));
     if (l > 1e-12) { pl[0] = dl[0] * G.size[0] / l; pl[1] = dl[1] * G.size[0] / l; pl[2] = dl[2] * G.size[0] / l; }
@@ -2194,6 +2198,34 @@ __device__ void extract_forces(SharedT<CL>& S, const gm_model* __restrict__ m, c
   F[12] = (float)og[4][0]; F[13] = (float)og[4][1]; F[14] = (float)og[4][2];
 }
 
+// mj_rnePostConstraint's cfrc_ext for the live object (myfunctions.cpp:1905), as
+// ObjectHandler::get_object_net_force_faster reads it (objecthandler.cpp:543-565): each
+// contact's world force (frame^T * contact-frame force) acts on geom2, its reaction on
+// geom1; torques about the object's centre of mass.  out = [force; torque] (the
+// reference's swapped order).  Lane-parallel over contacts, wave-reduced.
+template <int CL>
+__device__ void object_net_wrench(SharedT<CL>& S, const GmTopo* __restrict__ T, int lane, real* out) {
+  real w[6] = {0, 0, 0, 0, 0, 0};
+  if (lane < S.ncon) {
+    const real* C = S.con[lane];
+    const int g1 = S.cgeom[lane][0], g2 = S.cgeom[lane][1];
+    const real sgn = (g2 == T->geom_obj) ? 1.0 : (g1 == T->geom_obj) ? -1.0 : 0.0;
+    real Fr[9], g[3], r[3], t[3];
+    make_frame(Fr, C + 4);
+    for (int k = 0; k < 3; k++) g[k] = Fr[k] * C[8] + Fr[3 + k] * C[9] + Fr[6 + k] * C[10];
+    const int bo = T->body_obj;
+    for (int k = 0; k < 3; k++) r[k] = C[1 + k] - S.xpos[bo][k];
+    cross3(t, r, g);
+    for (int k = 0; k < 3; k++) { w[k] = sgn * g[k]; w[3 + k] = sgn * t[k]; }
+  }
+  // contact order sum (lane 0 accumulates in index order, as the oracle does)
+  for (int k = 0; k < 6; k++) {
+    real acc = 0;
+    for (int i = 0; i < GM_MAX_CON; i++) acc += readlane_real(w[k], i);
+    out[k] = acc;
+  }
+}
+
 // MjClass::monitor_sensors (mjclass.cpp:741-898)
 template <int CL>
 GM_EPI_ATTR void monitor_sensors(SharedT<CL>& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
@@ -2646,9 +2678,9 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
     return;
   }
   if (mode == 2) {
-    if (lane == 0) dbg.ncon[env] = S.ncon;
+    if (lane == 0) { dbg.ncon[env] = S.ncon; dbg.nefc[env] = S.nefc; }
     if (lane < GM_MAX_CON) {
-      float* o = dbg.contact + ((size_t)env * GM_MAX_CON + lane) * 16;
+      double* o = dbg.contact + ((size_t)env * GM_MAX_CON + lane) * 16;
       for (int k = 0; k < 16; k++) o[k] = 0;
       if (lane < S.ncon) {
         const real* Cc = S.con[lane];
@@ -2660,8 +2692,13 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
         o[13] = S.cgeom[lane][0]; o[14] = S.cgeom[lane][1]; o[15] = Cc[7];
       }
     }
-    dbg.efc_force[(size_t)env * GM_MAX_EFC + lane] = lane < S.nefc ? S.efc_f[lane] : 0.0f;
-    if (lane < GM_MAX_DOF) dbg.qacc[(size_t)env * GM_MAX_DOF + lane] = lane < T->nv ? S.qacc[lane] : 0.0f;
+    dbg.efc_force[(size_t)env * GM_MAX_EFC + lane] = lane < S.nefc ? S.efc_f[lane] : 0.0;
+    if (lane < GM_MAX_DOF) dbg.qacc[(size_t)env * GM_MAX_DOF + lane] = lane < T->nv ? S.qacc[lane] : 0.0;
+    {
+      real w[6];
+      object_net_wrench(S, T, lane, w);
+      if (lane == 0) for (int k = 0; k < 6; k++) dbg.wrench[(size_t)env * 6 + k] = w[k];
+    }
     store_state(S, states + env, lane);
     return;
   }
@@ -3082,7 +3119,7 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
                                            const double* __restrict__ eq_qpos, const uint8_t* __restrict__ mask,
                                            const gm_spawn* __restrict__ spawn, const gm_object* __restrict__ objs,
                                            int n_objects, int n_envs, const gm_spawn_params* __restrict__ scene,
-                                           int scene_tries) {
+                                           int scene_tries, float* __restrict__ obs) {
   int env = blockIdx.x * blockDim.x + threadIdx.x;
   if (env >= n_envs) return;
   if (mask && !mask[env]) return;
@@ -3130,13 +3167,19 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
     s.qpos[m->dof_base] = s.base[2] + eq_qpos[m->dof_base];
   }
   const gm_spawn sp = spawn ? spawn[env] : gm_spawn{0, 0.0, 0.0, 0.0};
+  bool placed = false;
   if (scene) {
     // MjEnv._spawn_object (MjEnv.py:1177-1267): spawn_into_scene up to scene_tries times,
     // then the "old method" pose from the spawn table
-    for (int t = 0; t < scene_tries; t++)
-      if (spawn_into_scene_dev(s, m, T, objs, n_objects, *scene, sp.object_index)) return;
+    for (int t = 0; t < scene_tries && !placed; t++)
+      placed = spawn_into_scene_dev(s, m, T, objs, n_objects, *scene, sp.object_index);
   }
-  spawn_object(s, T, objs, n_objects, sp);
+  if (!placed) spawn_object(s, T, objs, n_objects, sp);
+  // MjEnv.reset returns _next_observation() of the fresh episode (MjEnv.py:2222-2263):
+  // the observation buffer holds the reset env's sensor windows, not the last episode's
+  if (obs) get_obs(s, C, obs + (size_t)env * C->n_obs);
+  s.done = 0;
+  s.reward = 0;
 }
 #endif
 

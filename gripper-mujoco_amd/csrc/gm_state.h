@@ -2,7 +2,9 @@
 //
 // One EnvState per env, array-of-structs: the fused step kernel runs one
 // 64-lane workgroup per env and moves the whole struct HBM<->LDS with fully
-// coalesced 4-byte-per-lane sweeps at launch entry/exit.  Everything an
+// coalesced 4-byte-per-lane sweeps at launch entry/exit.  Plain C as well as C++: the
+// CPU oracle (oracle/oracle.c, test infrastructure) imports / exports this struct so
+// parity tests can hand the device's fp64 state to it verbatim.  Everything an
 // MjClass instance carries between action_step() calls (mjclass.h:1554-1833,
 // myfunctions.cpp:464-473 globals, the function-static flags the reference
 // keeps across resets) lives here.
@@ -30,6 +32,10 @@ enum {
 };
 // sensor slots in settings (SS) order, used for last_read_time / rand_mu
 enum { SL_MOTOR = 0, SL_BASEZ, SL_BASEXY, SL_YAW, SL_BEND, SL_AXIAL, SL_PALM, SL_WRISTXY, SL_WRISTZ, SL_CART, SL_N };
+
+typedef struct GmGrip GmGrip;
+typedef struct GmEnvState GmEnvState;
+typedef struct GmTopo GmTopo;
 
 struct GmGrip {            // luke::Gripper (gripper.h:11-198)
   double x, y, z, th;
@@ -87,7 +93,11 @@ struct GmEnvState {
 // a multiple of 16 B: the LDS image (SharedT) places its double arrays right after the
 // state, and 16-byte alignment keeps their paired accesses as single ds_*_b128 ops
 // (an 8-byte shift measured 5-15% slower across every phase)
+#ifdef __cplusplus
 static_assert(sizeof(GmEnvState) % 16 == 0, "GmEnvState must be 16-byte padded");
+#else
+_Static_assert(sizeof(GmEnvState) % 16 == 0, "GmEnvState must be 16-byte padded");
+#endif
 
 // Topology derived from gm_model on the host (the canonical gripper tree):
 // dof/body of chain position p in finger chain f is first + p - 1 (p >= 1),

@@ -8,14 +8,16 @@ from ._lib import (load_library, Settings, ModelParams, Object, Spawn, SpawnPara
                    Calibration, calibrate, CAL_TIMESTEP, CAL_GAUGES,
                    ModelBlob, ConfigBlob,
                    default_settings, make_object_set, BINARY_EVENTS, LINEAR_EVENTS, ACTION_KINDS,
-                   SENSORS, LIB_PATH)
+                   SENSORS, LIB_PATH, env_state_dtype, env_state_view)
 from .settings import canonical_settings, disable_noise, MAX_EPISODE_STEPS
 from .env import BatchedGripperEnv, spawn_positions
 from .policy import DevicePolicy, eps_threshold
+from .scripted import GraspScript, in_use_actions
 
 __all__ = ["load_library", "Settings", "ModelParams", "Object", "Spawn", "SpawnParams", "default_spawn_params",
            "Calibration", "calibrate", "CAL_TIMESTEP", "CAL_GAUGES",
            "ModelBlob", "ConfigBlob",
            "default_settings", "make_object_set", "canonical_settings", "disable_noise",
            "BatchedGripperEnv", "spawn_positions", "MAX_EPISODE_STEPS", "BINARY_EVENTS",
-           "LINEAR_EVENTS", "ACTION_KINDS", "SENSORS", "LIB_PATH", "DevicePolicy", "eps_threshold"]
+           "LINEAR_EVENTS", "ACTION_KINDS", "SENSORS", "LIB_PATH", "DevicePolicy", "eps_threshold",
+           "GraspScript", "in_use_actions", "env_state_dtype", "env_state_view"]

@@ -225,8 +225,11 @@ def _declare(lib):
         "gm_get_obs": (i32, [vp, vp, i32]),
         "gm_get_reward_done": (i32, [vp, vp, vp, i32]),
         "gm_get_event_rows": (i32, [vp, i32p, i32p, f32p]),
-        "gm_get_state": (i32, [vp, f32p, f32p, f64p]),
-        "gm_set_state": (i32, [vp, f32p, f32p]),
+        "gm_get_state": (i32, [vp, f64p, f64p, f64p]),
+        "gm_set_state": (i32, [vp, f64p, f64p]),
+        "gm_env_state_size": (C.c_int64, []),
+        "gm_get_env_states": (i32, [vp, vp]),
+        "gm_set_env_states": (i32, [vp, vp]),
         "gm_get_target": (i32, [vp, f64p, i32p, i32p, f64p]),
         "gm_get_overflow": (i32, [vp, i32p]),
         "gm_device_obs": (vp, [vp]),
@@ -235,7 +238,7 @@ def _declare(lib):
         "gm_device_actions": (vp, [vp]),
         "gm_stream": (vp, [vp]),
         "gm_last_step_ms": (i32, [vp, f32p]),
-        "gm_debug_substep": (i32, [vp, i32p, f32p, f32p, f32p]),
+        "gm_debug_substep": (i32, [vp, i32p, f64p, f64p, f64p, i32p, f64p]),
         "gm_step_profiled": (i32, [vp, C.POINTER(C.c_uint64)]),
         "gm_set_stream": (i32, [vp, vp]),
         "gm_spawn_object": (i32, [vp, vp, vp]),
@@ -290,6 +293,39 @@ class ModelBlob:
     @property
     def ptr(self):
         return C.cast(self.buf, C.c_void_p)
+
+
+def env_state_dtype():
+    """numpy view of one GmEnvState record (gripper-mujoco_amd/csrc/gm_state.h), C layout
+    (align=True); checked against gm_env_state_size() at load."""
+    import numpy as np
+    nb, nl = len(BINARY_EVENTS), len(LINEAR_EVENTS)
+    grip = np.dtype([("x", "f8"), ("y", "f8"), ("z", "f8"), ("th", "f8"),
+                     ("sx", "i4"), ("sy", "i4"), ("sz", "i4"), ("pad", "i4")], align=True)
+    return np.dtype([
+        ("time", "f8"), ("last_step_time", "f8"), ("end", grip), ("next", grip), ("base", "f8", 6),
+        ("last_read", "f8", 10), ("qpos", "f8", GM_MAX_QPOS), ("qvel", "f8", GM_MAX_DOF),
+        ("lock_q", "f8", GM_MAX_LOCK), ("start_qpos", "f8", 7), ("obj_size", "f8", 3), ("obj_mass", "f8"),
+        ("obj_inertia", "f8", 3), ("obj_friction", "f8"), ("obj_rbound", "f8"), ("obj_rest_z", "f8"),
+        ("dt", "f8"), ("tip_force", "f8"),
+        ("rand_mu", "f4", (10, 3)), ("ring", "f4", (37, 8)), ("lev_value", "f4", nl), ("lev_last", "f4", nl),
+        ("cumulative_reward", "f4"), ("grp_peak_lateral", "f4"), ("reward", "f4"),
+        ("ring_i", "i4", 37), ("bev_value", "i4", nb), ("bev_last", "i4", nb), ("bev_row", "i4", nb),
+        ("bev_abs", "i4", nb), ("lev_row", "i4", nl), ("lev_abs", "i4", nl), ("lock_active", "i4", GM_MAX_LOCK),
+        ("old_x", "i4"), ("old_y", "i4"), ("old_z", "i4"), ("num_action_steps", "i4"),
+        ("termination_signal_sent", "i4"), ("extra_substeps", "i4"), ("obj_type", "i4"), ("obj_index", "i4"),
+        ("done", "i4"), ("overflow", "i4"), ("rng", "u4"), ("cal_steps", "i4"), ("badqacc", "i4"),
+        ("pad_end", "i4", 3)], align=True)
+
+
+def env_state_view(records):
+    """Structured view of raw [n, size] uint8 GmEnvState records."""
+    import numpy as np
+    dt = env_state_dtype()
+    r = np.ascontiguousarray(records, dtype=np.uint8)
+    if r.shape[-1] != dt.itemsize:
+        raise ValueError(f"GmEnvState is {r.shape[-1]} bytes, numpy view expects {dt.itemsize}")
+    return r.reshape(-1, dt.itemsize).view(dt).reshape(r.shape[:-1])
 
 
 class ConfigBlob:

@@ -195,19 +195,34 @@ class BatchedGripperEnv:
 
     # ------------------------------------------------------------ inspection
     def state(self):
-        q = np.zeros((self.n_envs, self.model.nq), dtype=np.float32)
-        v = np.zeros((self.n_envs, self.model.nv), dtype=np.float32)
+        """fp64 qpos [n, nq], qvel [n, nv], time [n] (mjData's precision)."""
+        q = np.zeros((self.n_envs, self.model.nq), dtype=np.float64)
+        v = np.zeros((self.n_envs, self.model.nv), dtype=np.float64)
         t = np.zeros(self.n_envs, dtype=np.float64)
-        self._check(self.lib.gm_get_state(self._ctx, q.ctypes.data_as(C.POINTER(C.c_float)),
-                                          v.ctypes.data_as(C.POINTER(C.c_float)),
+        self._check(self.lib.gm_get_state(self._ctx, q.ctypes.data_as(C.POINTER(C.c_double)),
+                                          v.ctypes.data_as(C.POINTER(C.c_double)),
                                           t.ctypes.data_as(C.POINTER(C.c_double))))
         return q, v, t
 
     def set_state(self, qpos, qvel):
-        q = np.ascontiguousarray(np.asarray(qpos, dtype=np.float32))
-        v = np.ascontiguousarray(np.asarray(qvel, dtype=np.float32))
-        self._check(self.lib.gm_set_state(self._ctx, q.ctypes.data_as(C.POINTER(C.c_float)),
-                                          v.ctypes.data_as(C.POINTER(C.c_float))))
+        q = np.ascontiguousarray(np.asarray(qpos, dtype=np.float64))
+        v = np.ascontiguousarray(np.asarray(qvel, dtype=np.float64))
+        self._check(self.lib.gm_set_state(self._ctx, q.ctypes.data_as(C.POINTER(C.c_double)),
+                                          v.ctypes.data_as(C.POINTER(C.c_double))))
+
+    def env_states(self) -> np.ndarray:
+        """The whole per-env state as raw GmEnvState records, [n_envs, state_size] uint8
+        (checkpoint / resume, and the oracle hand-off of the parity tests)."""
+        sz = int(self.lib.gm_env_state_size())
+        out = np.zeros((self.n_envs, sz), dtype=np.uint8)
+        self._check(self.lib.gm_get_env_states(self._ctx, out.ctypes.data))
+        return out
+
+    def set_env_states(self, states):
+        a = np.ascontiguousarray(np.asarray(states, dtype=np.uint8))
+        if a.shape != (self.n_envs, int(self.lib.gm_env_state_size())):
+            raise ValueError(f"expected {(self.n_envs, int(self.lib.gm_env_state_size()))} state records, got {a.shape}")
+        self._check(self.lib.gm_set_env_states(self._ctx, a.ctypes.data))
 
     def target(self):
         e = np.zeros((self.n_envs, 4)); es = np.zeros((self.n_envs, 3), dtype=np.int32)
@@ -233,16 +248,23 @@ class BatchedGripperEnv:
         self._check(self.lib.gm_get_overflow(self._ctx, o.ctypes.data_as(C.POINTER(C.c_int32))))
         return o
 
-    def debug_substep(self):
+    def debug_substep(self, full: bool = False):
+        """One MjClass::step on every env with fp64 diagnostics: (ncon, contact [n,15,16],
+        efc_force [n,64], qacc [n,40]) and, with full=True, also nefc [n] and the object's
+        cfrc_ext wrench [n,6]."""
         n = self.n_envs
         ncon = np.zeros(n, dtype=np.int32)
-        con = np.zeros((n, 15, 16), dtype=np.float32)
-        f = np.zeros((n, 64), dtype=np.float32)
-        qacc = np.zeros((n, 40), dtype=np.float32)
+        nefc = np.zeros(n, dtype=np.int32)
+        con = np.zeros((n, 15, 16), dtype=np.float64)
+        f = np.zeros((n, 64), dtype=np.float64)
+        qacc = np.zeros((n, 40), dtype=np.float64)
+        w = np.zeros((n, 6), dtype=np.float64)
+        d = C.POINTER(C.c_double)
         self._check(self.lib.gm_debug_substep(self._ctx, ncon.ctypes.data_as(C.POINTER(C.c_int32)),
-                                              con.ctypes.data_as(C.POINTER(C.c_float)),
-                                              f.ctypes.data_as(C.POINTER(C.c_float)),
-                                              qacc.ctypes.data_as(C.POINTER(C.c_float))))
+                                              con.ctypes.data_as(d), f.ctypes.data_as(d), qacc.ctypes.data_as(d),
+                                              nefc.ctypes.data_as(C.POINTER(C.c_int32)), w.ctypes.data_as(d)))
+        if full:
+            return ncon, con, f, qacc, nefc, w
         return ncon, con, f, qacc
 
     PHASES = ("kinematics", "crb_rne", "mass_forces", "factor", "smooth_solve", "collision",

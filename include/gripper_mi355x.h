@@ -38,6 +38,9 @@ extern "C" {
 #define GM_MAX_OBJSET 64      /* objects in one synthetic object set          */
 #define GM_RING       8       /* sensor ring length (needs 1 + 2*3 = 7)       */
 #define GM_CHAIN      (GM_MAX_SEG + 2)  /* dofs per finger chain below base   */
+/* MPR support-point tie band: a unit direction whose body-frame component along a box
+ * face normal / cylinder axis is below this picks the face centre (see support_geom) */
+#define GM_SUPPORT_TIE 1e-9
 
 /* ------------------------------------------------------------------ errors */
 #define GM_OK            0
@@ -409,9 +412,19 @@ int  gm_get_reward_done(gm_ctx* ctx, float* reward, uint8_t* done, int on_device
 /* EventTrack rows: [n_envs x (GM_N_BINARY + GM_N_LINEAR)] int32 `row`, and
  * `abs` counters; MjClass::get_event_state / EventTrack (bind.cpp:525-590). */
 int  gm_get_event_rows(gm_ctx* ctx, int32_t* rows, int32_t* abs_counts, float* last_values);
-/* raw state readback (testing / checkpoint): qpos [n_envs x nq], qvel [n_envs x nv] */
-int  gm_get_state(gm_ctx* ctx, float* qpos, float* qvel, double* time);
-int  gm_set_state(gm_ctx* ctx, const float* qpos, const float* qvel);
+/* raw state readback (testing / checkpoint), fp64 like mjData's qpos / qvel:
+ * qpos [n_envs x nq], qvel [n_envs x nv], time [n_envs] (MjClass::get_state-style access
+ * the reference's tests use through mjData) */
+int  gm_get_state(gm_ctx* ctx, double* qpos, double* qvel, double* time);
+int  gm_set_state(gm_ctx* ctx, const double* qpos, const double* qvel);
+/* The whole per-env state (everything an MjClass carries between action_step() calls:
+ * mjData qpos/qvel/time, target_ stepper state, sensor windows, event tracks, RNG,
+ * function-static flags), fp64 where the reference is: gm_env_state_size() bytes per env,
+ * [n_envs] records.  Checkpoint / resume, and the hand-off the parity tests use to run
+ * the CPU oracle from exactly the device's state.  Host buffers. */
+int64_t gm_env_state_size(void);
+int  gm_get_env_states(gm_ctx* ctx, void* out);
+int  gm_set_env_states(gm_ctx* ctx, const void* in);
 /* target (stepper) state: [n_envs x 8] = end x,y,z,th (m/rad) then step x,y,z and base z */
 int  gm_get_target(gm_ctx* ctx, double* end_xyzth, int32_t* end_steps, int32_t* next_steps,
                    double* base_xyz);
@@ -436,18 +449,22 @@ int  gm_set_stream(gm_ctx* ctx, void* stream);
  * spawn: host array unless spawn_on_device; NULL spawns object 0 at the origin. */
 int  gm_autoreset(gm_ctx* ctx, int max_episode_steps, const gm_spawn* spawn, int spawn_on_device,
                   float* returns);
-void* gm_device_reset_mask(gm_ctx* ctx);   /* uint8 [n_envs], written by gm_autoreset */            /* hipStream_t the context launches on */
+void* gm_device_reset_mask(gm_ctx* ctx);   /* uint8 [n_envs], written by gm_autoreset */
 
 /* Timing of the fused env-step kernel (HIP events on the context's stream). */
 int  gm_last_step_ms(gm_ctx* ctx, float* ms);
 
 /* ---- single-substep stage hooks for parity testing (GPU vs oracle) ---- */
-/* Runs exactly one physics substep (mj_step1 + control + mj_step2 equivalent)
- * on every env, from the current state, and copies out diagnostics:
+/* Runs exactly one MjClass::step (mj_step1 + control + mj_step2 + mj_rnePostConstraint
+ * equivalent, then update_all and monitor_sensors; mjclass.cpp:504-530) on every env,
+ * from the current state, and copies out fp64 diagnostics (any pointer may be NULL):
  * ncon[n_envs], contact [n_envs x GM_MAX_CON x 16] (dist, pos3, frame9, g1, g2, mu),
- * efc_force [n_envs x GM_MAX_EFC], qacc [n_envs x nv]. */
-int  gm_debug_substep(gm_ctx* ctx, int32_t* ncon, float* contact, float* efc_force,
-                      float* qacc);
+ * efc_force [n_envs x GM_MAX_EFC], qacc [n_envs x GM_MAX_DOF], nefc [n_envs], and
+ * obj_wrench [n_envs x 6]: the live object's cfrc_ext as
+ * ObjectHandler::get_object_net_force_faster returns it (objecthandler.cpp:543-565),
+ * [force; torque about its centre of mass]. */
+int  gm_debug_substep(gm_ctx* ctx, int32_t* ncon, double* contact, double* efc_force,
+                      double* qacc, int32_t* nefc, double* obj_wrench);
 /* diagnostic: one gm_step with per-phase shader-clock cycle counters, lane-0 view,
    summed over substeps: out[n_envs][24] = kinematics, crb_rne, mass+forces, factor,
    smooth solve, collision, constraint build+PGS, constraint accel, integrate,

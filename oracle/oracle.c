@@ -10,6 +10,7 @@
  */
 #define _POSIX_C_SOURCE 200809L
 #include "oracle.h"
+#include "../gripper-mujoco_amd/csrc/gm_state.h"
 
 #include <math.h>
 #include <stdlib.h>
@@ -293,6 +294,8 @@ struct or_env {
   int num_action_steps;
   int termination_signal_sent;
   int term_pending_steps;
+  int last_done;                   /* the last is_done() / reward() results (GmEnvState::done / reward) */
+  float last_reward;
   float grp_peak_lateral;
   int obj_index;
   double start_qpos[7];
@@ -695,12 +698,17 @@ static void support_geom(const or_env* e, int g, const double* d, double* out) {
   mulmtv3(dl, R, d);
   double pl[3] = {0, 0, 0};
   int t = e->m.geom_type[g];
+  /* A direction (numerically) perpendicular to a face or to the cylinder axis has the
+   * whole face / rim line as its support set; the face centre is taken there instead of
+   * a corner picked by the sign of a rounding-level component (|dl_k| < GM_SUPPORT_TIE),
+   * so aligned plates and faces -- the grasp configuration -- give one portal path
+   * rather than one chosen by ulp noise. */
   if (t == GM_GEOM_BOX) {
-    for (int k = 0; k < 3; k++) pl[k] = dl[k] >= 0 ? s[k] : -s[k];
+    for (int k = 0; k < 3; k++) pl[k] = fabs(dl[k]) < GM_SUPPORT_TIE ? 0.0 : (dl[k] >= 0 ? s[k] : -s[k]);
   } else if (t == GM_GEOM_CYLINDER) {
     double rr = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
     if (rr > 1e-12) { pl[0] = s[0] * dl[0] / rr; pl[1] = s[0] * dl[1] / rr; }
-    pl[2] = dl[2] >= 0 ? s[1] : -s[1];
+    pl[2] = fabs(dl[2]) < GM_SUPPORT_TIE ? 0.0 : (dl[2] >= 0 ? s[1] : -s[1]);
   } else if (t == GM_GEOM_SPHERE) {
     double l = norm3(dl);
     if (l > 1e-12) scl3(pl, dl, s[0] / l);
@@ -1665,7 +1673,7 @@ int or_get_obs(or_env* e, float* out) {
 }
 
 /* MjClass::is_done (mjclass.cpp:1632-1698) */
-int or_is_done(or_env* e) {
+static int is_done_eval(or_env* e) {
   const gm_settings* s = &e->c.s;
   int k = 0;
 #define GM_BR(n, r, d, t) if (s->n.done && e->bev[k].row >= s->n.done) return 1; k++;
@@ -1691,6 +1699,8 @@ static float linear_reward(float val, float mn, float mx, float overshoot) {
   return (val - mn) / (mx - mn);
 }
 /* MjClass::reward + calc_rewards (mjclass.cpp:3000-3049, 5471-5528) */
+/* is_done (mjclass.cpp:1632-1698); the result is kept as GmEnvState::done */
+int or_is_done(or_env* e) { return e->last_done = is_done_eval(e); }
 float or_reward(or_env* e) {
   const gm_settings* s = &e->c.s;
   float r = 0;
@@ -1714,6 +1724,7 @@ float or_reward(or_env* e) {
     r += s->reward_cap_upper_bound - e->cumulative_reward;
     e->cumulative_reward = s->reward_cap_upper_bound;
   }
+  e->last_reward = r;
   return r;
 }
 
@@ -2066,6 +2077,8 @@ void or_reset(or_env* e, const gm_spawn* sp) {
   e->num_action_steps = 0;
   e->termination_signal_sent = 0;
   e->grp_peak_lateral = 0;
+  e->last_done = 0;
+  e->last_reward = 0;
   /* configure_settings: noise mean draws */
   randomise_mu(e);
   /* random_base_Z_movement (mjclass.cpp:1423-1434) */
@@ -2251,23 +2264,293 @@ void or_get_event_rows(const or_env* e, int32_t* rows, int32_t* absc, float* las
 int or_overflow(const or_env* e) { return e->overflow; }
 void or_get_eq(const or_env* e, double* eq) { for (int i = 0; i < e->m.nq; i++) eq[i] = e->eq_q[i]; }
 
-void or_debug_substep(or_env* e, int32_t* ncon, float* contact, float* efc_force, double* qacc) {
+/* mj_rnePostConstraint's cfrc_ext for the live object (myfunctions.cpp:1905), as
+ * ObjectHandler::get_object_net_force_faster reads it (objecthandler.cpp:543-565): every
+ * contact's world force (frame^T * contact-frame force) acts on geom2 and its reaction on
+ * geom1; torques about the object's centre of mass (its c-frame origin: the object is the
+ * root of its own tree).  out = [force; torque] (the reference's swapped order). */
+void or_object_net_wrench(const or_env* e, double* out) {
+  const gm_model* m = &e->m;
+  const double* com = e->xpos[m->body_obj];   /* free object: centre of mass at the body origin */
+  for (int k = 0; k < 6; k++) out[k] = 0;
+  for (int i = 0; i < e->ncon; i++) {
+    const con_t* C = &e->con[i];
+    double sgn = 0;
+    if (C->g2 == m->geom_obj) sgn = 1;
+    else if (C->g1 == m->geom_obj) sgn = -1;
+    else continue;
+    double g[3] = {0, 0, 0};
+    for (int k = 0; k < 3; k++)
+      for (int r = 0; r < 3; r++) g[k] += C->frame[3 * r + k] * C->force[r];
+    double rr[3], t[3];
+    sub3(rr, C->pos, com);
+    cross3(t, rr, g);
+    for (int k = 0; k < 3; k++) { out[k] += sgn * g[k]; out[3 + k] += sgn * t[k]; }
+  }
+}
+
+void or_debug_substep(or_env* e, int32_t* ncon, double* contact, double* efc_force, double* qacc,
+                      double* obj_wrench) {
   full_substep(e);
   if (ncon) *ncon = e->ncon;
   if (contact) {
     for (int c = 0; c < NC; c++) {
-      float* o = contact + 16 * c;
+      double* o = contact + 16 * c;
       for (int k = 0; k < 16; k++) o[k] = 0;
       if (c >= e->ncon) continue;
       const con_t* C = &e->con[c];
-      o[0] = (float)C->dist;
-      for (int k = 0; k < 3; k++) o[1 + k] = (float)C->pos[k];
-      for (int k = 0; k < 9; k++) o[4 + k] = (float)C->frame[k];
-      o[13] = (float)C->g1; o[14] = (float)C->g2; o[15] = (float)C->mu;
+      o[0] = C->dist;
+      for (int k = 0; k < 3; k++) o[1 + k] = C->pos[k];
+      for (int k = 0; k < 9; k++) o[4 + k] = C->frame[k];
+      o[13] = C->g1; o[14] = C->g2; o[15] = C->mu;
     }
   }
-  if (efc_force) for (int r = 0; r < NE; r++) efc_force[r] = r < e->nefc ? (float)e->efc_f[r] : 0.0f;
+  if (efc_force) for (int r = 0; r < NE; r++) efc_force[r] = r < e->nefc ? e->efc_f[r] : 0.0;
   if (qacc) for (int d = 0; d < e->m.nv; d++) qacc[d] = e->qacc[d];
+  if (obj_wrench) or_object_net_wrench(e, obj_wrench);
+}
+
+/* =====================================================================
+ * fp64 state hand-off with the device (GmEnvState, gripper-mujoco_amd/csrc/gm_state.h):
+ * the parity tests snapshot the device state at any point of an episode and run the
+ * oracle from exactly that state.  Stream ids / slots are the device's (gm_state.h).
+ * ===================================================================== */
+static ring_t* ring_of(or_env* e, int st) {
+  if (st < 3) return &e->w_gauge[st];
+  if (st < 6) return &e->w_axial[st - 3];
+  switch (st) {
+    case ST_PALM: return &e->w_palm;
+    case ST_WX: return &e->w_wx;
+    case ST_WY: return &e->w_wy;
+    case ST_WZ: return &e->w_wz;
+    case ST_YAW: return &e->w_yaw;
+    case ST_SI_PALM: return &e->si_palm;
+    case ST_SI_WZ: return &e->si_wz;
+    default: break;
+  }
+  if (st >= ST_MOTOR && st < ST_MOTOR + 3) return &e->w_motor[st - ST_MOTOR];
+  if (st >= ST_BASE && st < ST_BASE + 3) return &e->w_base[st - ST_BASE];
+  if (st >= ST_CART && st < ST_CART + 12) return &e->w_cart[st - ST_CART];
+  if (st >= ST_SI_GAUGE && st < ST_SI_GAUGE + 3) return &e->si_gauge[st - ST_SI_GAUGE];
+  return &e->si_axial[st - ST_SI_AXIAL];
+}
+static void grip_in(grip_t* g, const GmGrip* s) {
+  g->x = s->x; g->y = s->y; g->z = s->z; g->th = s->th; g->sx = s->sx; g->sy = s->sy; g->sz = s->sz;
+}
+static void grip_out(GmGrip* s, const grip_t* g) {
+  s->x = g->x; s->y = g->y; s->z = g->z; s->th = g->th; s->sx = g->sx; s->sy = g->sy; s->sz = g->sz; s->pad = 0;
+}
+size_t or_state_size(void) { return sizeof(GmEnvState); }
+
+int or_import_state(or_env* e, const void* state) {
+  const GmEnvState* s = (const GmEnvState*)state;
+  const gm_model* m = &e->m;
+  if (s->extra_substeps != 0) return -1;   /* a pending termination lift: not a step boundary */
+  if (s->obj_index < 0 || s->obj_index >= e->nobj) return -2;
+  e->obj_index = s->obj_index;
+  apply_object(&e->m, &e->objs[s->obj_index]);
+  e->time = s->time;
+  e->last_step_time = s->last_step_time;
+  grip_in(&e->end, &s->end);
+  grip_in(&e->next, &s->next);
+  for (int k = 0; k < 6; k++) e->base[k] = s->base[k];
+  for (int k = 0; k < S_N; k++) e->last_read[k] = s->last_read[k];
+  for (int i = 0; i < NQ; i++) e->qpos[i] = i < m->nq ? s->qpos[i] : 0.0;
+  for (int i = 0; i < NV; i++) e->qvel[i] = i < m->nv ? s->qvel[i] : 0.0;
+  for (int k = 0; k < GM_MAX_LOCK; k++) { e->lock_q[k] = s->lock_q[k]; e->lock_active[k] = s->lock_active[k]; }
+  for (int k = 0; k < 7; k++) e->start_qpos[k] = s->start_qpos[k];
+  for (int k = 0; k < S_N; k++)
+    for (int i = 0; i < 3; i++) e->rand_mu[k][i] = s->rand_mu[k][i];
+  for (int st = 0; st < GM_NSTREAM; st++) {
+    ring_t* r = ring_of(e, st);
+    for (int k = 0; k < GM_RING; k++) r->v[k] = s->ring[st][k];
+    r->i = s->ring_i[st];
+  }
+  for (int k = 0; k < GM_N_BINARY; k++) {
+    e->bev[k].value = s->bev_value[k]; e->bev[k].last_value = s->bev_last[k];
+    e->bev[k].row = s->bev_row[k]; e->bev[k].abs = s->bev_abs[k]; e->bev[k].active_sum = s->bev_row[k] != 0;
+  }
+  for (int k = 0; k < GM_N_LINEAR; k++) {
+    e->lev[k].value = s->lev_value[k]; e->lev[k].last_value = s->lev_last[k];
+    e->lev[k].row = s->lev_row[k]; e->lev[k].abs = s->lev_abs[k]; e->lev[k].active_sum = s->lev_row[k] != 0;
+  }
+  e->cumulative_reward = s->cumulative_reward;
+  e->grp_peak_lateral = s->grp_peak_lateral;
+  e->old_x = s->old_x; e->old_y = s->old_y; e->old_z = s->old_z;
+  e->num_action_steps = s->num_action_steps;
+  e->termination_signal_sent = s->termination_signal_sent;
+  e->overflow = s->overflow;
+  e->rng = s->rng;
+  e->tip_force = s->tip_force;
+  e->badqacc = s->badqacc;
+  e->last_done = s->done;
+  e->last_reward = s->reward;
+  return 0;
+}
+
+void or_export_state(const or_env* e, void* state) {
+  GmEnvState* s = (GmEnvState*)state;
+  const gm_model* m = &e->m;
+  memset(s, 0, sizeof(*s));
+  s->time = e->time;
+  s->last_step_time = e->last_step_time;
+  grip_out(&s->end, &e->end);
+  grip_out(&s->next, &e->next);
+  for (int k = 0; k < 6; k++) s->base[k] = e->base[k];
+  for (int k = 0; k < S_N; k++) s->last_read[k] = e->last_read[k];
+  for (int i = 0; i < m->nq; i++) s->qpos[i] = e->qpos[i];
+  for (int i = 0; i < m->nv; i++) s->qvel[i] = e->qvel[i];
+  for (int k = 0; k < GM_MAX_LOCK; k++) { s->lock_q[k] = e->lock_q[k]; s->lock_active[k] = e->lock_active[k]; }
+  for (int k = 0; k < 7; k++) s->start_qpos[k] = e->start_qpos[k];
+  {
+    const int g = m->geom_obj, b = m->body_obj;
+    const gm_object* o = &e->objs[e->obj_index];
+    for (int k = 0; k < 3; k++) { s->obj_size[k] = m->geom_size[g][k]; s->obj_inertia[k] = m->body_inertia[b][k]; }
+    s->obj_mass = m->body_mass[b];
+    s->obj_friction = m->geom_friction[g];
+    s->obj_rbound = m->geom_rbound[g];
+    s->obj_rest_z = object_rest_z(o);
+    s->obj_type = m->geom_type[g];
+  }
+  s->dt = m->timestep;
+  s->tip_force = e->tip_force;
+  for (int k = 0; k < S_N; k++)
+    for (int i = 0; i < 3; i++) s->rand_mu[k][i] = e->rand_mu[k][i];
+  for (int st = 0; st < GM_NSTREAM; st++) {
+    const ring_t* r = ring_of((or_env*)e, st);
+    for (int k = 0; k < GM_RING; k++) s->ring[st][k] = r->v[k];
+    s->ring_i[st] = r->i;
+  }
+  for (int k = 0; k < GM_N_BINARY; k++) {
+    s->bev_value[k] = e->bev[k].value; s->bev_last[k] = e->bev[k].last_value;
+    s->bev_row[k] = e->bev[k].row; s->bev_abs[k] = e->bev[k].abs;
+  }
+  for (int k = 0; k < GM_N_LINEAR; k++) {
+    s->lev_value[k] = e->lev[k].value; s->lev_last[k] = e->lev[k].last_value;
+    s->lev_row[k] = e->lev[k].row; s->lev_abs[k] = e->lev[k].abs;
+  }
+  s->cumulative_reward = e->cumulative_reward;
+  s->grp_peak_lateral = e->grp_peak_lateral;
+  s->old_x = e->old_x; s->old_y = e->old_y; s->old_z = e->old_z;
+  s->num_action_steps = e->num_action_steps;
+  s->termination_signal_sent = e->termination_signal_sent;
+  s->obj_index = e->obj_index;
+  s->overflow = e->overflow;
+  s->rng = e->rng;
+  s->badqacc = e->badqacc;
+  s->done = e->last_done;
+  s->reward = e->last_reward;
+}
+
+/* One env-step for n envs from device-format states (threaded, one oracle env per
+ * thread): import, set_action (continuous row or discrete code), action_step,
+ * get_observation, is_done, reward -- MjEnv.step's order -- then export.  states is
+ * updated in place; obs [n x n_obs], reward [n], done [n] (any may be NULL). */
+typedef struct {
+  const or_env* proto;
+  int n, tid, n_threads, n_obs, n_act;
+  unsigned char* states;
+  const float* cont;
+  const int32_t* disc;
+  float* obs; float* rew; uint8_t* done;
+  int err;
+} batch_job;
+static void* batch_worker(void* arg) {
+  batch_job* j = (batch_job*)arg;
+  or_env* e = (or_env*)malloc(sizeof(or_env));
+  float ob[512];
+  for (int k = j->tid; k < j->n; k += j->n_threads) {
+    *e = *j->proto;
+    GmEnvState* st = (GmEnvState*)(j->states + (size_t)k * sizeof(GmEnvState));
+    if (or_import_state(e, st) != 0) { j->err = k + 1; continue; }
+    if (j->cont) or_set_action(e, j->cont + (size_t)k * j->n_act);
+    else if (j->disc) or_set_discrete_action(e, j->disc[k]);
+    or_step(e);
+    int no = or_get_obs(e, ob);
+    int d = or_is_done(e);
+    float r = or_reward(e);
+    if (j->obs) for (int i = 0; i < no && i < j->n_obs; i++) j->obs[(size_t)k * j->n_obs + i] = ob[i];
+    if (j->rew) j->rew[k] = r;
+    if (j->done) j->done[k] = (uint8_t)d;
+    or_export_state(e, st);
+  }
+  free(e);
+  return NULL;
+}
+int or_batch_step(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects, int n,
+                  void* states, const float* cont_actions, const int32_t* disc_actions, float* obs,
+                  float* reward, uint8_t* done, int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > 256) n_threads = 256;
+  or_env* proto = or_create(m, c, objects, n_objects, 0);
+  if (!proto) return -1;
+  batch_job jobs[256];
+  pthread_t th[256];
+  for (int t = 0; t < n_threads; t++) {
+    jobs[t] = (batch_job){proto, n, t, n_threads, c->n_obs, c->n_actions, (unsigned char*)states,
+                          cont_actions, disc_actions, obs, reward, done, 0};
+    if (n_threads == 1) batch_worker(&jobs[0]);
+    else pthread_create(&th[t], NULL, batch_worker, &jobs[t]);
+  }
+  int err = 0;
+  for (int t = 0; t < n_threads; t++) {
+    if (n_threads > 1) pthread_join(th[t], NULL);
+    if (jobs[t].err) err = jobs[t].err;
+  }
+  or_destroy(proto);
+  return err ? -1000 - err : 0;
+}
+
+/* One physics substep (with update_all + monitor_sensors, like gm_debug_substep) for n
+ * envs from device-format states, with the substep diagnostics; threaded as above.
+ * contact [n x GM_MAX_CON x 16], efc_force [n x GM_MAX_EFC], qacc [n x GM_MAX_DOF],
+ * obj_wrench [n x 6], nefc [n]. */
+typedef struct {
+  const or_env* proto;
+  int n, tid, n_threads;
+  unsigned char* states;
+  int32_t* ncon; int32_t* nefc; double* contact; double* efc; double* qacc; double* wrench;
+  int err;
+} sub_job;
+static void* sub_worker(void* arg) {
+  sub_job* j = (sub_job*)arg;
+  or_env* e = (or_env*)malloc(sizeof(or_env));
+  for (int k = j->tid; k < j->n; k += j->n_threads) {
+    *e = *j->proto;
+    GmEnvState* st = (GmEnvState*)(j->states + (size_t)k * sizeof(GmEnvState));
+    if (or_import_state(e, st) != 0) { j->err = k + 1; continue; }
+    double qacc[NV];
+    or_debug_substep(e, j->ncon ? &j->ncon[k] : NULL, j->contact ? j->contact + (size_t)k * NC * 16 : NULL,
+                     j->efc ? j->efc + (size_t)k * NE : NULL, qacc, j->wrench ? j->wrench + (size_t)k * 6 : NULL);
+    if (j->qacc) for (int d = 0; d < NV; d++) j->qacc[(size_t)k * NV + d] = d < e->m.nv ? qacc[d] : 0.0;
+    if (j->nefc) j->nefc[k] = e->nefc;
+    or_export_state(e, st);
+  }
+  free(e);
+  return NULL;
+}
+int or_batch_substep(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects, int n,
+                     void* states, int32_t* ncon, int32_t* nefc, double* contact, double* efc_force, double* qacc,
+                     double* obj_wrench, int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > 256) n_threads = 256;
+  or_env* proto = or_create(m, c, objects, n_objects, 0);
+  if (!proto) return -1;
+  sub_job jobs[256];
+  pthread_t th[256];
+  for (int t = 0; t < n_threads; t++) {
+    jobs[t] = (sub_job){proto, n, t, n_threads, (unsigned char*)states, ncon, nefc, contact, efc_force, qacc,
+                        obj_wrench, 0};
+    if (n_threads == 1) sub_worker(&jobs[0]);
+    else pthread_create(&th[t], NULL, sub_worker, &jobs[t]);
+  }
+  int err = 0;
+  for (int t = 0; t < n_threads; t++) {
+    if (n_threads > 1) pthread_join(th[t], NULL);
+    if (jobs[t].err) err = jobs[t].err;
+  }
+  or_destroy(proto);
+  return err ? -1000 - err : 0;
 }
 
 /* bounded CPU baseline: n_envs independent envs, random continuous actions */

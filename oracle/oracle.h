@@ -50,8 +50,24 @@ void  or_get_event_rows(const or_env* e, int32_t* rows, int32_t* abs_counts, flo
 int   or_overflow(const or_env* e);
 void  or_get_eq(const or_env* e, double* eq_qpos);                 /* settled equilibrium */
 
-/* one physics substep, with diagnostics (same layout as gm_debug_substep) */
-void  or_debug_substep(or_env* e, int32_t* ncon, float* contact, float* efc_force, double* qacc);
+/* one physics substep, with diagnostics (same layout as gm_debug_substep, fp64);
+ * obj_wrench: the live object's cfrc_ext [force; torque about its centre of mass] */
+void  or_debug_substep(or_env* e, int32_t* ncon, double* contact, double* efc_force, double* qacc,
+                       double* obj_wrench);
+void  or_object_net_wrench(const or_env* e, double* out);
+
+/* fp64 state hand-off with the device's GmEnvState (gripper-mujoco_amd/csrc/gm_state.h) */
+size_t or_state_size(void);
+int   or_import_state(or_env* e, const void* gm_env_state);   /* 0 ok, <0 not a step boundary */
+void  or_export_state(const or_env* e, void* gm_env_state);
+/* n envs x one env-step from device-format states (updated in place), threaded */
+int   or_batch_step(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects, int n,
+                    void* states, const float* cont_actions, const int32_t* disc_actions, float* obs,
+                    float* reward, uint8_t* done, int n_threads);
+/* n envs x one substep with diagnostics from device-format states (updated in place) */
+int   or_batch_substep(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects, int n,
+                       void* states, int32_t* ncon, int32_t* nefc, double* contact, double* efc_force,
+                       double* qacc, double* obj_wrench, int n_threads);
 
 /* standalone pieces used by the golden-vector tests */
 float  or_gauge_reading(const gm_model* m, const double* finger_q);   /* read_armadillo_gauge */

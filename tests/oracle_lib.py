@@ -48,7 +48,12 @@ def lib():
             "or_get_event_rows": (None, [vp, i32p, i32p, f32p]),
             "or_overflow": (i32, [vp]),
             "or_get_eq": (None, [vp, f64p]),
-            "or_debug_substep": (None, [vp, i32p, f32p, f32p, f64p]),
+            "or_debug_substep": (None, [vp, i32p, f64p, f64p, f64p, f64p]),
+            "or_state_size": (C.c_size_t, []),
+            "or_import_state": (i32, [vp, vp]),
+            "or_export_state": (None, [vp, vp]),
+            "or_batch_step": (i32, [vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, i32]),
+            "or_batch_substep": (i32, [vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, i32]),
             "or_gauge_reading": (C.c_float, [vp, f64p]),
             "or_minstd_next_canonical_float": (C.c_double, [C.POINTER(C.c_uint32)]),
             "or_minstd_next_canonical_double": (C.c_double, [C.POINTER(C.c_uint32)]),
@@ -167,12 +172,62 @@ class OracleEnv:
 
     def debug_substep(self):
         n = C.c_int32()
-        con = np.zeros((15, 16), dtype=np.float32)
-        f = np.zeros(64, dtype=np.float32)
+        con = np.zeros((15, 16), dtype=np.float64)
+        f = np.zeros(64, dtype=np.float64)
         qacc = np.zeros(self.model.nv)
-        self.L.or_debug_substep(self.h, C.byref(n), con.ctypes.data_as(C.POINTER(C.c_float)),
-                                f.ctypes.data_as(C.POINTER(C.c_float)), qacc.ctypes.data_as(C.POINTER(C.c_double)))
+        d = C.POINTER(C.c_double)
+        self.L.or_debug_substep(self.h, C.byref(n), con.ctypes.data_as(d), f.ctypes.data_as(d), qacc.ctypes.data_as(d),
+                                None)
         return n.value, con, f, qacc
+
+    def import_state(self, rec):
+        """Load one device GmEnvState record (uint8 row of BatchedGripperEnv.env_states())."""
+        r = np.ascontiguousarray(rec, dtype=np.uint8)
+        rc = self.L.or_import_state(self.h, r.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"or_import_state failed ({rc})")
+
+    def export_state(self):
+        out = np.zeros(int(self.L.or_state_size()), dtype=np.uint8)
+        self.L.or_export_state(self.h, out.ctypes.data)
+        return out
+
+
+def n_threads():
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def batch_step(model, cfg, objects, states, actions=None, discrete=None, threads=None):
+    """One env-step of the oracle for every device state record (threaded).  Returns
+    (obs [n, n_obs], reward [n], done [n], states_after [n, size])."""
+    st = np.array(states, dtype=np.uint8, copy=True, order="C")
+    n = st.shape[0]
+    obs = np.zeros((n, max(cfg.n_obs, 1)), dtype=np.float32)
+    rew = np.zeros(n, dtype=np.float32)
+    done = np.zeros(n, dtype=np.uint8)
+    ca = None if actions is None else np.ascontiguousarray(actions, dtype=np.float32)
+    da = None if discrete is None else np.ascontiguousarray(discrete, dtype=np.int32)
+    rc = lib().or_batch_step(model.ptr, cfg.ptr, C.cast(objects, C.c_void_p), len(objects), n, st.ctypes.data,
+                             None if ca is None else ca.ctypes.data, None if da is None else da.ctypes.data,
+                             obs.ctypes.data, rew.ctypes.data, done.ctypes.data, threads or n_threads())
+    if rc != 0:
+        raise RuntimeError(f"or_batch_step failed ({rc})")
+    return obs[:, :cfg.n_obs], rew, done, st
+
+
+def batch_substep(model, cfg, objects, states, threads=None):
+    """One MjClass::step with diagnostics for every device state record (threaded).
+    Returns (ncon, nefc, contact [n,15,16], efc [n,64], qacc [n,40], wrench [n,6], states_after)."""
+    st = np.array(states, dtype=np.uint8, copy=True, order="C")
+    n = st.shape[0]
+    ncon = np.zeros(n, dtype=np.int32); nefc = np.zeros(n, dtype=np.int32)
+    con = np.zeros((n, 15, 16)); efc = np.zeros((n, 64)); qacc = np.zeros((n, 40)); w = np.zeros((n, 6))
+    rc = lib().or_batch_substep(model.ptr, cfg.ptr, C.cast(objects, C.c_void_p), len(objects), n, st.ctypes.data,
+                                ncon.ctypes.data, nefc.ctypes.data, con.ctypes.data, efc.ctypes.data, qacc.ctypes.data,
+                                w.ctypes.data, threads or n_threads())
+    if rc != 0:
+        raise RuntimeError(f"or_batch_substep failed ({rc})")
+    return ncon, nefc, con, efc, qacc, w, st
 
 
 def gauge_reading(model, finger_q):

@@ -86,7 +86,7 @@ def test_facade_spawn_into_scene_matches_oracle(gm):
     q, _, _ = env.state()
     qo, _, _ = o.state()
     qa = env.model.nq - 7
-    np.testing.assert_array_equal(q[0][qa:qa + 7], qo[qa:qa + 7].astype(np.float32))
+    np.testing.assert_array_equal(q[0][qa:qa + 7], qo[qa:qa + 7])
 
 
 @pytest.mark.gpu

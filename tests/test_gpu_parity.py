@@ -2,10 +2,11 @@
 
 Tolerances: observations max rel-err <= 1e-4 over entries with
 |ref| >= 1e-3 and abs-err <= 1e-4 elsewhere; stepper step counts, event rows and
-done flags bit-exact.  fp32 device physics vs fp64 oracle diverges chaotically
-once contacts slip, so contact-rich comparisons are short-horizon (single
-substep / single env-step from an identical state); contact-free rollouts are
-compared over whole episodes.
+done flags bit-exact.  Device and oracle are both fp64 (FMA contraction off) but
+associate some sums differently (segmented scans, tree-sparse factor), so contact-rich
+trajectories separate at the ulp level and are compared per env-step from identical
+states (tests/test_grasp_parity.py hands the whole device state to the oracle);
+contact-free rollouts are compared over whole episodes.
 """
 import numpy as np
 import pytest
@@ -70,10 +71,14 @@ def test_single_substep_parity(setup):
     for e, o in enumerate(ors):
         n_o, con_o, f_o, qacc_o = o.debug_substep()
         assert ncon[e] == n_o
-        # contact pair indexing bit-exact; geometry to fp32 tolerance
+        # contact pair indexing bit-exact; geometry, constraint forces and accelerations
+        # at the fp64 rounding level (identical fp64 start state on both sides)
         np.testing.assert_array_equal(con[e, :n_o, 13:15], con_o[:n_o, 13:15])
-        np.testing.assert_allclose(con[e, :n_o, 0:13], con_o[:n_o, 0:13], rtol=1e-3, atol=2e-6)
-        np.testing.assert_allclose(qacc[e, :env.model.nv], qacc_o, rtol=2e-3, atol=2e-3 * np.abs(qacc_o).max())
+        np.testing.assert_allclose(con[e, :n_o, 0:13], con_o[:n_o, 0:13], rtol=0, atol=1e-12)
+        fs = max(1.0, float(np.abs(f_o).max()))
+        np.testing.assert_allclose(f[e] / fs, f_o / fs, rtol=0, atol=1e-10)
+        qs = max(1.0, float(np.abs(qacc_o).max()))
+        np.testing.assert_allclose(qacc[e, :env.model.nv] / qs, qacc_o / qs, rtol=0, atol=1e-10)
 
 
 def test_contact_free_rollout_parity(setup):
@@ -109,7 +114,7 @@ def test_contact_rich_one_step_parity(setup):
     obs, rew, term, trunc = env.step(a)
     for e, o in enumerate(ors):
         obs_o, r_o, d_o = o.step(a[e])
-        ok, er, ea = obs_close(obs[e], obs_o, rtol=1e-3, atol=1e-3)
+        ok, er, ea = obs_close(obs[e], obs_o)     # the north-star bound, 1e-4
         assert ok, (e, er, ea)
 
 

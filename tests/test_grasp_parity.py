@@ -1,0 +1,152 @@
+"""GPU parity on grasp-phase states at the BASELINE configs (C3: 4096 envs, set6-like
+mixed objects, randomised spawn; C2: 256 envs, one cylinder).
+
+A scripted grasp mix (gmx.GraspScript: close, squeeze, palm press, lift, with jitter)
+drives the whole batch on the device.  At several episode phases the fp64 device state
+of every env is handed to the CPU oracle verbatim (gm_get_env_states ->
+or_import_state), both run the same env-step, and the results are compared:
+
+- observations: max rel-err <= 1e-4 over |ref| >= 1e-3, abs <= 1e-4 elsewhere
+  (BASELINE.json north star);
+- done flags, event rows / abs counters, stepper step counts: bit-exact;
+- reward: |d| <= 1e-6 + 1e-5 |r| (a float sum of the same terms);
+- one MjClass::step (substep) from the same states: contact pair ids bit-exact, contact
+  geometry, constraint forces, accelerations and the object's cfrc_ext near bit level
+  (both sides fp64 with FMA contraction off), and the contact-force-sum invariant of
+  ObjectHandler::check_contact_forces (objecthandler.cpp:994-1032, tol 1e-5).
+
+The batch is asserted to contain the hard cases: finger-object contacts, constraint
+problems with nefc > 32 (the general PGS path), event rows that fire, and done == 1.
+"""
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+OBS_RTOL = 1e-4
+OBS_ATOL = 1e-4
+SNAPS = (22, 38, 45, 52, 60, 68)
+
+
+def obs_err(a, b):
+    """per-env (max rel over |ref| >= 1e-3, max abs elsewhere)"""
+    a = np.asarray(a, dtype=np.float64); b = np.asarray(b, dtype=np.float64)
+    big = np.abs(b) >= 1e-3
+    d = np.abs(a - b)
+    rel = np.where(big, d / np.where(big, np.abs(b), 1.0), 0.0).max(axis=1)
+    ab = np.where(big, 0.0, d).max(axis=1)
+    return rel, ab
+
+
+@pytest.fixture(scope="module")
+def ol():
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import oracle_lib
+    return oracle_lib
+
+
+def rollout(gm, n_envs, object_set, seed, steps=max(SNAPS) + 1, snaps=SNAPS):
+    settings = gm.canonical_settings(noise=False, seed=seed)
+    env = gm.BatchedGripperEnv(n_envs, object_set=object_set, settings=settings, seed=seed)
+    env.set_scene_spawn(gm.default_spawn_params(), max_tries=3)
+    env.reset()
+    script = gm.GraspScript(settings, n_envs, seed=seed)
+    out = []
+    for k in range(steps):
+        a = script.actions(k)
+        rec = env.env_states() if k in snaps else None
+        obs, rew, _, _ = env.step(a)
+        if rec is not None:
+            _, done = env.reward_done()
+            out.append(dict(k=k, rec=rec, a=a, obs=obs, rew=rew, done=done, after=env.env_states()))
+    return env, out
+
+
+def compare_step(gm, ol, env, snap):
+    obs_o, rew_o, done_o, after_o = ol.batch_step(env.model, env.cfg, env.objects, snap["rec"], actions=snap["a"])
+    dv, ov = gm.env_state_view(snap["after"]), gm.env_state_view(after_o)
+    rel, ab = obs_err(snap["obs"], obs_o)
+    bad_obs = np.where((rel > OBS_RTOL) | (ab > OBS_ATOL))[0]
+    assert bad_obs.size == 0, (f"step {snap['k']}: {bad_obs.size} envs exceed the obs bound, worst rel "
+                               f"{rel.max():.3e} abs {ab.max():.3e} (envs {bad_obs[:8]})")
+    np.testing.assert_array_equal(snap["done"].astype(np.uint8), done_o, err_msg=f"done flags, step {snap['k']}")
+    for f in ("bev_row", "bev_abs", "lev_row", "lev_abs", "num_action_steps", "old_x", "old_y", "old_z",
+              "lock_active", "rng", "ring_i"):
+        np.testing.assert_array_equal(dv[f], ov[f], err_msg=f"{f}, step {snap['k']}")
+    for g in ("end", "next"):
+        for f in ("sx", "sy", "sz"):
+            np.testing.assert_array_equal(dv[g][f], ov[g][f], err_msg=f"{g}.{f}, step {snap['k']}")
+    np.testing.assert_allclose(snap["rew"], rew_o, rtol=1e-5, atol=1e-6, err_msg=f"reward, step {snap['k']}")
+    # the physical state after 63 substeps: reported, bounded loosely (contact-rich
+    # trajectories are chaotic at the ulp level; the obs bound above is the contract)
+    dq = np.abs(dv["qpos"] - ov["qpos"]).max(axis=1)
+    return dict(k=snap["k"], obs_rel=float(rel.max()), obs_abs=float(ab.max()), qpos_max=float(dq.max()),
+                qpos_p99=float(np.percentile(dq, 99)), done=int(done_o.sum()))
+
+
+def compare_substep(gm, ol, env, snap):
+    env.set_env_states(snap["rec"])
+    ncon, con, efc, qacc, nefc, w = env.debug_substep(full=True)
+    after_d = env.env_states()
+    ncon_o, nefc_o, con_o, efc_o, qacc_o, w_o, after_o = ol.batch_substep(env.model, env.cfg, env.objects, snap["rec"])
+    np.testing.assert_array_equal(ncon, ncon_o, err_msg="contact counts")
+    np.testing.assert_array_equal(nefc, nefc_o, err_msg="constraint row counts")
+    np.testing.assert_array_equal(con[:, :, 13:15], con_o[:, :, 13:15], err_msg="contact pair ids")
+    np.testing.assert_allclose(con[:, :, :13], con_o[:, :, :13], rtol=0, atol=1e-9, err_msg="contact geometry")
+    fs = np.maximum(1.0, np.abs(efc_o).max(axis=1, keepdims=True))
+    np.testing.assert_allclose(efc / fs, efc_o / fs, rtol=0, atol=1e-7, err_msg="efc_force")
+    qs = np.maximum(1.0, np.abs(qacc_o).max(axis=1, keepdims=True))
+    np.testing.assert_allclose(qacc / qs, qacc_o / qs, rtol=0, atol=1e-7, err_msg="qacc")
+    np.testing.assert_allclose(w, w_o, rtol=0, atol=1e-7, err_msg="object cfrc_ext")
+    # ObjectHandler::check_contact_forces: sum of the object's contact forces (global
+    # frame, force on the object) == cfrc_ext force part, within 1e-5
+    obj = env.model.ngeom - 1            # the live object's geom is the model's last (gm_build_model)
+    fsum = np.zeros((env.n_envs, 3))
+    for e in range(env.n_envs):
+        for c in range(ncon[e]):
+            g1, g2 = int(con[e, c, 13]), int(con[e, c, 14])
+            s = 1.0 if g2 == obj else (-1.0 if g1 == obj else 0.0)
+            if s == 0.0:
+                continue
+            Fr = con[e, c, 4:13].reshape(3, 3)
+            fe = efc[e]
+            base = nefc[e] - 4 * ncon[e] + 4 * c
+            f_loc = np.array([fe[base:base + 4].sum(), con[e, c, 15] * (fe[base] - fe[base + 1]),
+                              con[e, c, 15] * (fe[base + 2] - fe[base + 3])])
+            fsum[e] += s * (Fr.T @ f_loc)
+    assert np.abs(fsum - w[:, :3]).max() <= 1e-5, "contact-force sum differs from cfrc_ext"
+    dv, ov = gm.env_state_view(after_d), gm.env_state_view(after_o)
+    np.testing.assert_allclose(dv["qpos"], ov["qpos"], rtol=0, atol=1e-9, err_msg="qpos after one substep")
+    return dict(k=snap["k"], ncon_max=int(ncon.max()), nefc_max=int(nefc.max()), n_big=int((nefc > 32).sum()),
+                efc_err=float(np.abs((efc - efc_o) / fs).max()), qacc_err=float(np.abs((qacc - qacc_o) / qs).max()))
+
+
+def check_config(gm, ol, n_envs, object_set, seed):
+    env, snaps = rollout(gm, n_envs, object_set, seed)
+    rep = []
+    for sn in snaps:
+        rep.append(compare_step(gm, ol, env, sn))
+    sub = [compare_substep(gm, ol, env, sn) for sn in snaps]
+    last = gm.env_state_view(snaps[-1]["after"])
+    ev = {n: int((last["bev_row"][:, i] > 0).sum() + (last["bev_abs"][:, i] > 0).sum())
+          for i, n in enumerate(gm.BINARY_EVENTS)}
+    print(f"\n{object_set} x{n_envs}: step parity {rep}\nsubstep parity {sub}\nenvs with events {ev}")
+    env.close()
+    return rep, sub, last
+
+
+def test_c3_grasp_states_4096(gm, ol):
+    rep, sub, last = check_config(gm, ol, 4096, "set6_synthetic", seed=1234)
+    i_oc = gm.BINARY_EVENTS.index("object_contact")
+    assert (last["bev_abs"][:, i_oc] > 0).sum() > 1000, "too few envs reached finger-object contact"
+    assert sum(r["done"] for r in rep) > 0, "no env reached done == 1"
+    assert sum(s["n_big"] for s in sub) > 0, "no constraint problem with nefc > 32 was checked"
+
+
+def test_c2_single_cylinder_256(gm, ol):
+    rep, sub, last = check_config(gm, ol, 256, "cylinder", seed=77)
+    i_oc = gm.BINARY_EVENTS.index("object_contact")
+    assert (last["bev_abs"][:, i_oc] > 0).sum() > 64

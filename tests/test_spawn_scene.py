@@ -138,7 +138,7 @@ def test_search_is_deterministic_per_stream(world):
 @pytest.mark.gpu
 def test_gpu_spawn_into_scene_matches_oracle(world):
     """Device search vs oracle, env by env: same success flags, the same grid pose
-    (object qpos, float32 readback), and the same RNG position afterwards (the next
+    (object qpos, fp64 readback), and the same RNG position afterwards (the next
     reset's noise draws give identical observations)."""
     if not gpu_available():
         pytest.skip("no GPU")
@@ -169,7 +169,7 @@ def test_gpu_spawn_into_scene_matches_oracle(world):
         ok_ref = o.spawn_into_scene(params[e])
         assert bool(ok[e]) == ok_ref, e
         qo, _, _ = o.state()
-        np.testing.assert_array_equal(q[e][qa:qa + 7], qo[qa:qa + 7].astype(np.float32), err_msg=f"env {e}")
+        np.testing.assert_array_equal(q[e][qa:qa + 7], qo[qa:qa + 7], err_msg=f"env {e}")
         oracles.append(o)
     assert (~ok).sum() >= n // 16
     # RNG stream position: the sensor noise of the next env-step comes from the same
@@ -204,6 +204,6 @@ def test_gpu_reset_with_scene_spawn_matches_oracle(world):
         pe = mjenv_params(gm, sp[e].object_index)
         assert o.spawn_into_scene(pe)
         qo, _, _ = o.state()
-        np.testing.assert_array_equal(q[e][qa:qa + 7], qo[qa:qa + 7].astype(np.float32), err_msg=f"env {e}")
+        np.testing.assert_array_equal(q[e][qa:qa + 7], qo[qa:qa + 7], err_msg=f"env {e}")
     env.set_scene_spawn(None)
     env.close()

@@ -57,6 +57,7 @@ struct gm_ctx {
   uint32_t* d_cost = nullptr;          // per-env cost of the last env-step (clocks / 64)
   gm_spawn_params* d_scene = nullptr;  // gm_set_scene_spawn parameters (NULL: plain spawn_object)
   int scene_tries = 0;
+  GmSpawnRand spawn_rand{};            // gm_set_random_spawn (enable = 0: spawn tables)
   std::string err;
 };
 
@@ -304,7 +305,7 @@ int gm_reset(gm_ctx* c, const uint8_t* mask, const gm_spawn* spawn) {
   int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
   hipLaunchKernelGGL(gm_reset_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
                      c->d_topo, c->d_eq, dm, ds, c->d_objs, c->n_objects, c->n_envs, c->d_scene, c->scene_tries,
-                     c->d_obs);
+                     c->d_obs, c->spawn_rand);
   HIPCHK(c, hipGetLastError());
   if (mask || spawn) HIPCHK(c, hipStreamSynchronize(c->stream));   // host buffers may be reused
   return GM_OK;
@@ -397,6 +398,33 @@ int gm_set_scene_spawn(gm_ctx* c, const gm_spawn_params* params, int max_tries) 
   HIPCHK(c, hipMemcpyAsync(c->d_scene, params, sizeof(gm_spawn_params), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->scene_tries = max_tries;
+  return GM_OK;
+}
+
+int gm_scripted_actions(gm_ctx* c, uint64_t seed, float jitter, float* out, int on_device) {
+  if (!c || !out) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  float* d = on_device ? out : c->d_act;
+  int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
+  hipLaunchKernelGGL(gm_scripted_action_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_cfg, d,
+                     c->n_envs, seed, (long long)c->env_offset, jitter);
+  HIPCHK(c, hipGetLastError());
+  if (!on_device) {
+    HIPCHK(c, hipMemcpyAsync(out, d, sizeof(float) * (size_t)c->n_envs * c->cfg.n_actions, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return GM_OK;
+}
+
+int gm_set_random_spawn(gm_ctx* c, int enable, uint64_t seed, int position_noise_mm, int rotation_noise_deg) {
+  if (!c) return GM_E_ARG;
+  if (position_noise_mm < 0 || rotation_noise_deg < 0) return fail(c, GM_E_ARG, "gm_set_random_spawn: negative noise");
+  c->spawn_rand.enable = enable ? 1 : 0;
+  c->spawn_rand.seed = seed;
+  c->spawn_rand.position_noise_mm = position_noise_mm;
+  c->spawn_rand.rotation_noise_deg = rotation_noise_deg;
+  c->spawn_rand.env_offset = c->env_offset;
   return GM_OK;
 }
 
@@ -772,7 +800,7 @@ int gm_autoreset(gm_ctx* c, int max_episode_steps, const gm_spawn* spawn, int sp
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(gm_reset_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
                      c->d_topo, c->d_eq, c->d_mask, ds, c->d_objs, c->n_objects, c->n_envs, c->d_scene,
-                     c->scene_tries, c->d_obs);
+                     c->scene_tries, c->d_obs, c->spawn_rand);
   HIPCHK(c, hipGetLastError());
   if (spawn && !spawn_on_device) HIPCHK(c, hipStreamSynchronize(c->stream));
   return GM_OK;

@@ -2868,6 +2868,48 @@ extern "C" __global__ void gm_action_kernel(GmEnvState* __restrict__ states, con
 }
 #endif
 
+// ---------------------------------------------------------------- scripted grasp mix
+// The benchmark's / parity tests' synthetic driver (gmx.GraspScript mirrors it on the
+// host bit for bit): per env and episode, phase lengths drawn from the counter-based
+// hash (seed, global env id, episode) -- close the fingers, squeeze (tilt the tips), press
+// the palm, lift the base -- indexed by the env's own episode step (num_action_steps),
+// plus uniform jitter per (step, action).  Continuous action fractions in [-1, 1] for
+// the in-use actions (MjClass::set_continous_action order).
+__device__ __host__ inline float gm_script_fraction(uint64_t seed, int64_t gid, int32_t ep, int32_t k, int i, int kind,
+                                                    float jitter) {
+  const int close_n = gm_spawn_int(seed, gid, ep, 16, 34, 45);
+  const int tilt_n = gm_spawn_int(seed, gid, ep, 17, 0, 25);
+  const float tilt_dir = gm_spawn_int(seed, gid, ep, 18, 0, 4) < 4 ? -1.0f : 1.0f;
+  const int palm_n = gm_spawn_int(seed, gid, ep, 19, 0, 15);
+  const int t1 = close_n, t2 = t1 + tilt_n, t3 = t2 + palm_n;
+  float a = 0.0f;
+  if (kind == GM_ACT_gripper_prismatic_X && k < t1) a = 1.0f;
+  if (kind == GM_ACT_gripper_revolute_Y && k >= t1 && k < t2) a = tilt_dir;
+  if (kind == GM_ACT_gripper_Z && k >= t2 && k < t3) a = 1.0f;
+  if (kind == GM_ACT_base_Z && k >= t3) a = -1.0f;
+  if (jitter > 0.0f) {
+    const int u = gm_spawn_int(seed, gid, ep, 32 + 8 * k + i, 0, 1 << 20);
+    a += jitter * ((float)u * (2.0f / (float)(1 << 20)) - 1.0f);
+  }
+  return a > 1.0f ? 1.0f : (a < -1.0f ? -1.0f : a);
+}
+
+#ifndef GM_CAL_TU   // env-step translation unit only
+extern "C" __global__ void gm_scripted_action_kernel(const GmEnvState* __restrict__ states, const gm_config* __restrict__ C,
+                                                     float* __restrict__ out, int n_envs, uint64_t seed,
+                                                     long long env_offset, float jitter) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n_envs) return;
+  const GmEnvState& s = states[env];
+  const int na = C->n_actions;
+  for (int i = 0; i < na; i++) {
+    const int code = C->action_options[i];
+    const int kind = (code >= 0 && code < GM_ACTION_TERMINATION) ? code / 3 : -1;
+    out[(size_t)env * na + i] = gm_script_fraction(seed, env_offset + env, s.episode, s.num_action_steps, i, kind, jitter);
+  }
+}
+#endif
+
 // ---------------------------------------------------------------- reset + spawn
 // MjClass::spawn_object -> ObjectHandler::spawn_object (mjclass.cpp:2352-2420,
 // objecthandler.cpp:403-428): live object, pose on the ground at (x, y), z-rotation
@@ -3119,7 +3161,7 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
                                            const double* __restrict__ eq_qpos, const uint8_t* __restrict__ mask,
                                            const gm_spawn* __restrict__ spawn, const gm_object* __restrict__ objs,
                                            int n_objects, int n_envs, const gm_spawn_params* __restrict__ scene,
-                                           int scene_tries, float* __restrict__ obs) {
+                                           int scene_tries, float* __restrict__ obs, GmSpawnRand sr) {
   int env = blockIdx.x * blockDim.x + threadIdx.x;
   if (env >= n_envs) return;
   if (mask && !mask[env]) return;
@@ -3127,9 +3169,11 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
   // keep the per-env RNG stream and the function-static stepper flags (quirk)
   uint32_t rng = s.rng;
   int ox = s.old_x, oy = s.old_y, oz = s.old_z;
+  const int32_t episode = s.episode + 1;
   uint32_t* w = reinterpret_cast<uint32_t*>(&s);
   for (int i = 0; i < GM_STATE_WORDS; i++) w[i] = 0;
   s.rng = rng; s.old_x = ox; s.old_y = oy; s.old_z = oz;
+  s.episode = episode;
   g_reset(s.end); g_reset(s.next);
   for (int k = 0; k < GM_MAX_QPOS; k++) s.qpos[k] = m->qpos0[k];
   s.time = 0; s.last_step_time = 0;
@@ -3166,7 +3210,19 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
     if (s.base[2] < C->base_min[2]) s.base[2] = C->base_min[2];
     s.qpos[m->dof_base] = s.base[2] + eq_qpos[m->dof_base];
   }
-  const gm_spawn sp = spawn ? spawn[env] : gm_spawn{0, 0.0, 0.0, 0.0};
+  gm_spawn sp = spawn ? spawn[env] : gm_spawn{0, 0.0, 0.0, 0.0};
+  if (sr.enable && !spawn) {
+    // MjEnv._spawn_object's generator draws: object index, then the "old method" pose
+    // (integer mm offsets, one of {0, 60, 120} deg plus integer-degree noise)
+    const int64_t gid = sr.env_offset + env;
+    const int nm = sr.position_noise_mm, nd = sr.rotation_noise_deg;
+    sp.object_index = gm_spawn_int(sr.seed, gid, episode, 0, 0, n_objects - 1);
+    sp.x = gm_spawn_int(sr.seed, gid, episode, 1, -nm, nm) * 1e-3;
+    sp.y = gm_spawn_int(sr.seed, gid, episode, 2, -nm, nm) * 1e-3;
+    const int noise_deg = gm_spawn_int(sr.seed, gid, episode, 3, -nd, nd);
+    const int opt = gm_spawn_int(sr.seed, gid, episode, 4, 0, 2);
+    sp.zrot = (60 * opt + noise_deg) * (M_PI / 180.0);
+  }
   bool placed = false;
   if (scene) {
     // MjEnv._spawn_object (MjEnv.py:1177-1267): spawn_into_scene up to scene_tries times,

@@ -85,7 +85,8 @@ struct GmEnvState {
   uint32_t rng;
   int32_t cal_steps;             // calibration launch: substeps to run
   int32_t badqacc;               // mjWARN_BADQACC: a non-finite or |qacc| > 1e10 was seen
-  int32_t pad_end[3];
+  int32_t episode;               // resets since gm_create (keys the counter-based spawn draws)
+  int32_t pad_end[2];
 };
 
 // word count for HBM<->LDS sweeps
@@ -98,6 +99,43 @@ static_assert(sizeof(GmEnvState) % 16 == 0, "GmEnvState must be 16-byte padded")
 #else
 _Static_assert(sizeof(GmEnvState) % 16 == 0, "GmEnvState must be 16-byte padded");
 #endif
+
+// MjEnv._spawn_object's Python-side draws (MjEnv.py:1177-1267: object index, and the
+// "old method" pose when spawn_into_scene fails) made on the device from a counter-based
+// hash of (seed, global env id, episode, draw) -- splitmix64, identical on the host
+// (gmx.spawn_draws) -- so they do not depend on sharding and leave the reference's C++
+// RNG stream (GmEnvState::rng) untouched.
+typedef struct GmSpawnRand {
+  uint64_t seed;
+  int32_t enable;
+  int32_t position_noise_mm;     // object_position_noise_mm (MjEnv default 10)
+  int32_t rotation_noise_deg;    // object_rotation_noise_deg (MjEnv default 5)
+  int32_t pad;
+  int64_t env_offset;            // global id of env 0 of this context
+} GmSpawnRand;
+
+static inline
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+uint64_t gm_splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+// uniform integer in [lo, hi] from draw k of (seed, gid, episode)
+static inline
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+int32_t gm_spawn_int(uint64_t seed, int64_t gid, int32_t episode, int k, int32_t lo, int32_t hi) {
+  const uint64_t h = gm_splitmix64(seed + (uint64_t)gid * 0xD1B54A32D192ED03ull +
+                                   (uint64_t)(uint32_t)episode * 0x8CB92BA72F3D8DD7ull +
+                                   (uint64_t)k * 0x9E3779B97F4A7C15ull);
+  const uint64_t span = (uint64_t)(hi - lo + 1);
+  return lo + (int32_t)(((h >> 32) * span) >> 32);
+}
 
 // Topology derived from gm_model on the host (the canonical gripper tree):
 // dof/body of chain position p in finger chain f is first + p - 1 (p >= 1),

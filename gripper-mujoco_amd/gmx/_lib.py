@@ -247,6 +247,8 @@ def _declare(lib):
         "gm_set_scene_spawn": (i32, [vp, vp, i32]),
         "gm_calibrate": (i32, [vp, vp, vp, i32, i32, i32, vp, vp, vp, i32]),
         "gm_autoreset": (i32, [vp, i32, vp, i32, vp]),
+        "gm_set_random_spawn": (i32, [vp, i32, C.c_uint64, i32, i32]),
+        "gm_scripted_actions": (i32, [vp, C.c_uint64, C.c_float, vp, i32]),
         "gm_device_reset_mask": (vp, [vp]),
         "gm_policy_create": (i32, [vp, i32p, i32, f32p, C.POINTER(vp)]),
         "gm_policy_destroy": (None, [vp]),
@@ -315,7 +317,7 @@ def env_state_dtype():
         ("old_x", "i4"), ("old_y", "i4"), ("old_z", "i4"), ("num_action_steps", "i4"),
         ("termination_signal_sent", "i4"), ("extra_substeps", "i4"), ("obj_type", "i4"), ("obj_index", "i4"),
         ("done", "i4"), ("overflow", "i4"), ("rng", "u4"), ("cal_steps", "i4"), ("badqacc", "i4"),
-        ("pad_end", "i4", 3)], align=True)
+        ("episode", "i4"), ("pad_end", "i4", 2)], align=True)
 
 
 def env_state_view(records):

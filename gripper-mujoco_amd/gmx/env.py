@@ -16,14 +16,42 @@ from ._lib import (load_library, ModelBlob, ConfigBlob, ModelParams, Spawn, Spaw
 from .settings import canonical_settings, MAX_EPISODE_STEPS
 
 
-def spawn_positions(rng: np.random.Generator, n: int, n_objects: int, pos_noise_m: float = 10e-3,
-                    rot_noise_rad: float = np.deg2rad(5.0)):
-    """Object index and pose per env, MjEnv._spawn_object defaults
-    (object_position_noise_mm=10, object_rotation_noise_deg=5; MjEnv.py:1177-1267)."""
-    idx = rng.integers(0, n_objects, size=n)
-    x = rng.uniform(-pos_noise_m, pos_noise_m, size=n)
-    y = rng.uniform(-pos_noise_m, pos_noise_m, size=n)
-    rot = rng.uniform(-rot_noise_rad, rot_noise_rad, size=n)
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _splitmix64(x):
+    x = (x + np.uint64(0x9E3779B97F4A7C15)) & _M64
+    x = ((x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & _M64
+    x = ((x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & _M64
+    return x ^ (x >> np.uint64(31))
+
+
+def spawn_int(seed, gid, episode, k, lo, hi):
+    """gm_spawn_int (csrc/gm_state.h) vectorised: uniform integer in [lo, hi] from draw k of
+    splitmix64(seed, global env id, episode) -- bit-identical to the device draw."""
+    with np.errstate(over="ignore"):
+        gid = np.asarray(gid, dtype=np.int64).astype(np.uint64)
+        ep = np.asarray(episode, dtype=np.int64).astype(np.uint32).astype(np.uint64)
+        kk = np.asarray(k, dtype=np.int64).astype(np.uint64)
+        x = (np.uint64(seed) + gid * np.uint64(0xD1B54A32D192ED03) + ep * np.uint64(0x8CB92BA72F3D8DD7)
+             + kk * np.uint64(0x9E3779B97F4A7C15)) & _M64
+        h = _splitmix64(x)
+        span = np.uint64(hi - lo + 1)
+        return lo + (((h >> np.uint64(32)) * span) >> np.uint64(32)).astype(np.int64)
+
+
+def spawn_draws(seed, gids, episodes, n_objects, position_noise_mm: int = 10, rotation_noise_deg: int = 5):
+    """MjEnv._spawn_object's generator draws (MjEnv.py:1177-1267) for each (global env id,
+    episode): object index and the "old method" pose (integer mm offsets; z rotation one of
+    {0, 60, 120} deg plus integer-degree noise).  The device makes the same draws in
+    gm_reset / gm_autoreset (gm_set_random_spawn), so they are shard-independent."""
+    nm, nd = int(position_noise_mm), int(rotation_noise_deg)
+    idx = spawn_int(seed, gids, episodes, 0, 0, n_objects - 1)
+    x = spawn_int(seed, gids, episodes, 1, -nm, nm) * 1e-3
+    y = spawn_int(seed, gids, episodes, 2, -nm, nm) * 1e-3
+    noise = spawn_int(seed, gids, episodes, 3, -nd, nd)
+    opt = spawn_int(seed, gids, episodes, 4, 0, 2)
+    rot = (60 * opt + noise) * (np.pi / 180.0)
     return idx, x, y, rot
 
 
@@ -39,13 +67,17 @@ class BatchedGripperEnv:
         self.objects = make_object_set(object_set, seed)
         self.max_episode_steps = max_episode_steps
         self.device = device
-        self.rng = np.random.default_rng(seed + 7919 * env_offset)
+        self.seed = int(seed)
+        self.env_offset = int(env_offset)
+        self._episode = np.zeros(self.n_envs, dtype=np.int64)   # mirrors GmEnvState::episode
         self._ctx = C.c_void_p()
         rc = self.lib.gm_create(self.model.ptr, self.cfg.ptr, self.objects, len(self.objects), self.n_envs,
                                 int(env_offset), int(device), int(seed), C.byref(self._ctx))
         if rc != 0:
             msg = self.lib.gm_last_error(self._ctx).decode() if self._ctx else ""
             raise RuntimeError(f"gm_create failed ({rc}) {msg}")
+        # resets without a spawn table draw MjEnv._spawn_object's object / pose on the device
+        self._check(self.lib.gm_set_random_spawn(self._ctx, 1, self.seed, 10, 5))
         self.n_obs = self.lib.gm_n_obs(self._ctx)
         self.n_actions = self.lib.gm_n_actions(self._ctx)
         self.current_step = np.zeros(self.n_envs, dtype=np.int64)
@@ -79,8 +111,11 @@ class BatchedGripperEnv:
 
     # ------------------------------------------------------------ env API
     def make_spawn(self, mask=None, idx=None, x=None, y=None, rot=None):
+        """An explicit spawn table for the next reset: MjEnv._spawn_object's draws for each
+        env's global id and next episode (spawn_draws), with optional overrides."""
         n = self.n_envs
-        si, sx, sy, sr = spawn_positions(self.rng, n, len(self.objects))
+        gids = self.env_offset + np.arange(n)
+        si, sx, sy, sr = spawn_draws(self.seed, gids, self._episode + 1, len(self.objects))
         if idx is not None: si = np.broadcast_to(np.asarray(idx), (n,))
         if x is not None: sx = np.broadcast_to(np.asarray(x, dtype=np.float64), (n,))
         if y is not None: sy = np.broadcast_to(np.asarray(y, dtype=np.float64), (n,))
@@ -91,16 +126,17 @@ class BatchedGripperEnv:
         return arr
 
     def reset(self, mask=None, spawn=None):
-        """MjClass::reset + spawn for masked envs; returns the observation (MjEnv.reset)."""
-        if spawn is None:
-            spawn = self.make_spawn()
+        """MjClass::reset + spawn for masked envs; returns the observation (MjEnv.reset).
+        spawn=None: the object and pose are drawn on the device (gm_set_random_spawn)."""
         if mask is not None:
             m = np.ascontiguousarray(np.asarray(mask, dtype=np.uint8))
             self._check(self.lib.gm_reset(self._ctx, m.ctypes.data_as(C.POINTER(C.c_uint8)), spawn))
             self.current_step[m.astype(bool)] = 0
+            self._episode[m.astype(bool)] += 1
         else:
             self._check(self.lib.gm_reset(self._ctx, None, spawn))
             self.current_step[:] = 0
+            self._episode += 1
         return self.observation()
 
     def spawn_into_scene(self, params, mask=None):
@@ -124,6 +160,13 @@ class BatchedGripperEnv:
         """Resets place objects with spawn_into_scene (MjEnv._spawn_object: up to max_tries
         attempts, then the spawn table pose); params=None restores plain spawn_object."""
         self._check(self.lib.gm_set_scene_spawn(self._ctx, None if params is None else C.byref(params), int(max_tries)))
+
+    def scripted_actions(self, seed: int, jitter: float = 0.2) -> np.ndarray:
+        """The device scripted grasp mix for every env's current episode step
+        (gm_scripted_actions; gmx.GraspScript is its host mirror)."""
+        out = np.zeros((self.n_envs, self.n_actions), dtype=np.float32)
+        self._check(self.lib.gm_scripted_actions(self._ctx, int(seed), float(jitter), out.ctypes.data, 0))
+        return out
 
     def set_action(self, actions):
         a = np.ascontiguousarray(np.asarray(actions, dtype=np.float32).reshape(self.n_envs, self.n_actions))

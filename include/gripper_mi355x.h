@@ -395,6 +395,25 @@ int  gm_spawn_into_scene(gm_ctx* ctx, const uint8_t* mask, const gm_spawn_params
  * params == NULL restores plain spawn_object(spawn[e]). */
 int  gm_set_scene_spawn(gm_ctx* ctx, const gm_spawn_params* params, int max_tries);
 
+/* MjEnv._spawn_object's Python-side draws (MjEnv.py:1177-1267) made per reset on the
+ * device: with enable != 0, gm_reset / gm_autoreset called without a spawn table draw each
+ * reset env's object index uniformly over the set and its fallback ("old method") pose
+ * -- integer-mm x, y in [-position_noise_mm, position_noise_mm], z rotation one of
+ * {0, 60, 120} deg plus integer-degree noise in [-rotation_noise_deg, rotation_noise_deg]
+ * -- from splitmix64(seed, global env id, episode, draw) (gm_state.h gm_spawn_int), so
+ * every episode gets a fresh object, results do not depend on how envs are sharded, and
+ * the reference's C++ RNG stream is not consumed.  With gm_set_scene_spawn the drawn index
+ * goes to spawn_into_scene first, as MjEnv does. */
+int  gm_set_random_spawn(gm_ctx* ctx, int enable, uint64_t seed, int position_noise_mm, int rotation_noise_deg);
+
+/* Synthetic driver for benchmarks and parity tests (not a reference interface): the
+ * scripted grasp mix -- per env and episode, phase lengths from splitmix64(seed, global
+ * env id, episode); close the fingers, squeeze, press the palm, lift the base, indexed by
+ * the env's episode step, plus uniform jitter -- written as continuous action fractions
+ * [n_envs x n_actions] to `out` (a device pointer when on_device; feed it to
+ * gm_set_action).  Runs on the context's stream after whatever reset came before it. */
+int  gm_scripted_actions(gm_ctx* ctx, uint64_t seed, float jitter, float* out, int on_device);
+
 /* MjClass::set_continous_action for every action index i in order
  * (mjclass.cpp:1517-1630; called per index by MjEnv._set_action, MjEnv.py:591-594).
  * actions: [n_envs x n_actions] float32. */

@@ -295,6 +295,7 @@ struct or_env {
   int termination_signal_sent;
   int term_pending_steps;
   int last_done;                   /* the last is_done() / reward() results (GmEnvState::done / reward) */
+  int episode;                     /* resets so far (GmEnvState::episode) */
   float last_reward;
   float grp_peak_lateral;
   int obj_index;
@@ -2079,6 +2080,7 @@ void or_reset(or_env* e, const gm_spawn* sp) {
   e->grp_peak_lateral = 0;
   e->last_done = 0;
   e->last_reward = 0;
+  e->episode += 1;
   /* configure_settings: noise mean draws */
   randomise_mu(e);
   /* random_base_Z_movement (mjclass.cpp:1423-1434) */
@@ -2385,6 +2387,7 @@ int or_import_state(or_env* e, const void* state) {
   e->badqacc = s->badqacc;
   e->last_done = s->done;
   e->last_reward = s->reward;
+  e->episode = s->episode;
   return 0;
 }
 
@@ -2440,6 +2443,7 @@ void or_export_state(const or_env* e, void* state) {
   s->badqacc = e->badqacc;
   s->done = e->last_done;
   s->reward = e->last_reward;
+  s->episode = e->episode;
 }
 
 /* One env-step for n envs from device-format states (threaded, one oracle env per

@@ -48,6 +48,24 @@ def test_struct_sizes_match_ctypes(gm):
     assert lib.gm_struct_size(0) == C.sizeof(gm.Settings)
     assert lib.gm_struct_size(5) == C.sizeof(gm.ModelParams)
     assert lib.gm_struct_size(99) == -1
+    # the raw per-env state record and its numpy view (checkpoint / oracle hand-off)
+    assert lib.gm_env_state_size() == gm.env_state_dtype().itemsize
+    import oracle_lib
+    assert oracle_lib.lib().or_state_size() == lib.gm_env_state_size()
+
+
+def test_spawn_draws_are_shard_independent(gm):
+    """gm_spawn_int / spawn_draws: keyed on the global env id, not on the shard."""
+    seed, n = 1234, 64
+    full = gm.spawn_draws(seed, np.arange(2 * n), np.full(2 * n, 3), 20)
+    second = gm.spawn_draws(seed, n + np.arange(n), np.full(n, 3), 20)
+    for a, b in zip(full, second):
+        np.testing.assert_array_equal(a[n:], b)
+    idx, x, y, rot = gm.spawn_draws(seed, np.arange(4096), np.ones(4096), 20)
+    assert idx.min() == 0 and idx.max() == 19
+    assert np.abs(x).max() <= 10e-3 + 1e-12 and set(np.round(x * 1e3).astype(int)) <= set(range(-10, 11))
+    deg = np.round(np.rad2deg(rot)).astype(int)
+    assert set(np.unique(deg)) <= set(d + o for d in range(-5, 6) for o in (0, 60, 120))
 
 
 def test_canonical_model_dimensions(model):

@@ -1,0 +1,215 @@
+"""GPU parity for the episode-boundary and action-mode paths, each against the fp64 oracle:
+
+- device auto-reset (gm_autoreset: MjEnv's truncation / termination handling,
+  MjEnv.py:616-637, then MjEnv.reset + _spawn_object, 2222-2263 / 1177-1267): reset
+  masks, episode returns, the respawned object and pose, the reference RNG stream position
+  and the fresh observation, for envs forced done (out-of-bounds spawns) and envs truncated
+  at max_episode_steps;
+- the observation right after a reset of an env that has stepped (MjEnv.reset returns the
+  new episode's observation, not the last one's);
+- discrete actions (MjClass::set_discrete_action, mjclass.cpp:1510-1515) including the
+  termination action with lift_on_termination (+2S substeps, mjclass.cpp:1590-1601);
+- C5 at 4096 envs: the on-device DQN picks the discrete actions, and one env-step from
+  every env's device state equals the oracle's.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ol():
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import oracle_lib
+    return oracle_lib
+
+
+def obs_ok(a, b):
+    a = np.asarray(a, dtype=np.float64); b = np.asarray(b, dtype=np.float64)
+    big = np.abs(b) >= 1e-3
+    d = np.abs(a - b)
+    return (d[big] / np.abs(b[big])).max(initial=0) <= 1e-4 and d[~big].max(initial=0) <= 1e-4
+
+
+def mjenv_params(gm):
+    p = gm.default_spawn_params()
+    p.xrange = p.yrange = 10e-3
+    p.rotrange = math.pi / 2.0
+    return p
+
+
+def oracle_mjenv_reset(gm, o, seed, gid, episode, n_objects, params, tries=3):
+    """MjEnv.reset -> _spawn_object on the oracle with the device's draws: reset with the
+    fallback pose, then spawn_into_scene(idx) up to `tries` times (a failed try leaves the
+    fallback pose and consumes its RNG draws, as on the device)."""
+    idx, x, y, rot = gm.spawn_draws(seed, np.array([gid]), np.array([episode]), n_objects)
+    sp = gm.Spawn()
+    sp.object_index, sp.x, sp.y, sp.zrot = int(idx[0]), float(x[0]), float(y[0]), float(rot[0])
+    o.reset(sp)
+    p = gm.SpawnParams.from_buffer_copy(params)
+    p.index = int(idx[0])
+    for _ in range(tries):
+        if o.spawn_into_scene(p):
+            break
+
+
+def test_autoreset_matches_oracle(gm, ol):
+    import torch
+    n, seed, max_steps = 48, 21, 3
+    s = gm.canonical_settings(noise=True, seed=seed)          # noise on: RNG positions matter
+    env = gm.BatchedGripperEnv(n, object_set="set6_synthetic", settings=s, seed=seed)
+    params = mjenv_params(gm)
+    env.set_scene_spawn(params, max_tries=3)
+    # first episode: an explicit table, every 4th env spawned out of bounds (oob -> done)
+    sp = env.make_spawn()
+    for e in range(0, n, 4):
+        sp[e].x = 0.09
+    env.reset(spawn=sp)
+    ors = []
+    for e in range(n):
+        o = ol.OracleEnv(env.model, env.cfg, env.objects, env_id=e)
+        o.reset(sp[e])
+        p = gm.SpawnParams.from_buffer_copy(params)
+        p.index = sp[e].object_index
+        for _ in range(3):
+            if o.spawn_into_scene(p):
+                break
+        ors.append(o)
+    episode = np.ones(n, dtype=np.int64)
+    steps = np.zeros(n, dtype=np.int64)
+    returns = torch.full((n,), float("nan"), device="cuda")
+    rng = np.random.default_rng(5)
+    n_reset = 0
+    for t in range(7):
+        a = rng.uniform(-1, 1, size=(n, env.n_actions)).astype(np.float32)
+        env.set_action(a)
+        env.action_step()
+        obs = env.observation()
+        rew, done = env.reward_done()
+        env.autoreset_device(0, returns.data_ptr(), max_episode_steps=max_steps)
+        torch.cuda.synchronize()
+        ret = returns.cpu().numpy()
+        recs = env.env_states()
+        view = gm.env_state_view(recs)
+        obs_after = env.observation()
+        for e, o in enumerate(ors):
+            ob, r, d = o.step(a[e])
+            assert obs_ok(obs[e], ob), (t, e)
+            assert bool(done[e]) == d, (t, e)
+            steps[e] += 1
+            reset = d or steps[e] >= max_steps
+            if reset:
+                assert ret[e] == pytest.approx(o.export_state().view(gm.env_state_dtype())[0]["cumulative_reward"],
+                                               rel=0, abs=0), (t, e)
+                episode[e] += 1
+                steps[e] = 0
+                oracle_mjenv_reset(gm, o, seed, e, int(episode[e]), len(env.objects), params)
+                n_reset += 1
+                ov = o.export_state().view(gm.env_state_dtype())[0]
+                for f in ("obj_index", "rng", "episode", "num_action_steps", "bev_row", "lev_row", "ring_i"):
+                    np.testing.assert_array_equal(view[f][e], ov[f], err_msg=f"{f} after reset, env {e} t {t}")
+                qa = env.model.nq - 7
+                np.testing.assert_array_equal(view["qpos"][e][qa:qa + 7], ov["qpos"][qa:qa + 7])
+                np.testing.assert_array_equal(view["rand_mu"][e], ov["rand_mu"])
+                np.testing.assert_allclose(view["qpos"][e][:qa], ov["qpos"][:qa], rtol=0, atol=2e-6)
+                np.testing.assert_array_equal(obs_after[e], o.observation())
+            else:
+                assert math.isnan(ret[e]), (t, e)
+    assert n_reset >= n + n // 4
+
+
+def test_reset_observation_after_steps(gm, ol):
+    n = 4
+    s = gm.canonical_settings(noise=False, seed=8)
+    env = gm.BatchedGripperEnv(n, object_set="set1_synthetic", settings=s, seed=8)
+    sp = env.make_spawn(x=0.0, y=0.0)
+    env.reset(spawn=sp)
+    for k in range(6):
+        env.step(np.ones((n, env.n_actions), dtype=np.float32))
+    assert np.abs(env.observation()).max() > 0
+    sp2 = env.make_spawn()
+    obs = env.reset(spawn=sp2)
+    for e in range(n):
+        o = ol.OracleEnv(env.model, env.cfg, env.objects, env_id=e)
+        o.reset(sp[e])
+        for k in range(6):
+            o.step(np.ones(env.n_actions, dtype=np.float32))
+        o.reset(sp2[e])
+        np.testing.assert_array_equal(obs[e], o.observation())
+
+
+def test_discrete_and_termination_match_oracle(gm, ol):
+    """Discrete action codes (two per action kind, plus the termination action with the
+    base lift and 2S extra substeps), per env-step from the device state."""
+    n, seed = 256, 31
+    s = gm.canonical_settings(noise=False, seed=seed)
+    s.continous_actions = 0
+    s.use_termination_action = 1
+    s.lift_on_termination = 1
+    env = gm.BatchedGripperEnv(n, object_set="set6_synthetic", settings=s, seed=seed)
+    assert env.n_actions == 9
+    env.set_scene_spawn(mjenv_params(gm), max_tries=3)
+    env.reset()
+    rng = np.random.default_rng(3)
+    n_term = 0
+    for t in range(40):
+        # mostly "close" (code 0 = prismatic +), some of everything, termination late
+        a = np.where(rng.random(n) < 0.6, 0, rng.integers(0, 8, size=n))
+        if t >= 30:
+            a = np.where(rng.random(n) < 0.3, 8, a)
+        rec = env.env_states()
+        obs, rew, term, trunc = env.step(a.astype(np.int32), discrete=True)
+        _, done = env.reward_done()
+        if t % 3 == 0 or t >= 30:
+            obs_o, rew_o, done_o, after_o = ol.batch_step(env.model, env.cfg, env.objects, rec, discrete=a)
+            bad = [e for e in range(n) if not obs_ok(obs[e], obs_o[e])]
+            assert not bad, (t, bad[:5])
+            np.testing.assert_array_equal(done.astype(np.uint8), done_o)
+            np.testing.assert_allclose(rew, rew_o, rtol=1e-5, atol=1e-6)
+            dv, ov = gm.env_state_view(env.env_states()), gm.env_state_view(after_o)
+            for f in ("bev_row", "lev_row", "termination_signal_sent", "old_x", "old_z", "lock_active"):
+                np.testing.assert_array_equal(dv[f], ov[f], err_msg=f"{f}, step {t}")
+            np.testing.assert_array_equal(dv["base"], ov["base"])
+            n_term += int((a == 8).sum())
+    assert n_term > 50
+
+
+def test_c5_policy_rollout_4096(gm, ol):
+    """C5: 4096 envs, the device DQN chooses every env's discrete action from its own
+    observation; the policy's choice matches a torch f32 forward where the top two
+    outputs are clearly apart, and the env-step those actions drive equals the oracle's."""
+    from test_policy import torch_forward, Q_ATOL
+    n, seed = 4096, 13
+    s = gm.canonical_settings(noise=False, seed=seed)
+    s.continous_actions = 0
+    env = gm.BatchedGripperEnv(n, object_set="set6_synthetic", settings=s, seed=seed)
+    env.set_scene_spawn(mjenv_params(gm), max_tries=3)
+    env.reset()
+    pol = gm.DevicePolicy(env, seed=5)
+    for t in range(12):                        # on-device rollout: policy -> step
+        pol.act(eps=gm.eps_threshold(t), seed=1, decision=t)
+        env.action_step()
+    rec = env.env_states()
+    obs = env.observation()
+    pol.act(eps=0.0, seed=1, decision=99)
+    acts, q = pol.read()
+    qref = torch_forward(pol.sizes, pol.params, obs)
+    np.testing.assert_allclose(q, qref, rtol=0, atol=Q_ATOL)
+    top2 = np.sort(qref, axis=1)[:, -2:]
+    clear = (top2[:, 1] - top2[:, 0]) > 4 * Q_ATOL
+    np.testing.assert_array_equal(acts[clear], np.argmax(qref, axis=1)[clear])
+    env.action_step()                          # the policy already applied `acts`
+    obs_d = env.observation()
+    rew_d, done_d = env.reward_done()
+    obs_o, rew_o, done_o, _ = ol.batch_step(env.model, env.cfg, env.objects, rec, discrete=acts)
+    bad = [e for e in range(n) if not obs_ok(obs_d[e], obs_o[e])]
+    assert not bad, bad[:5]
+    np.testing.assert_array_equal(done_d.astype(np.uint8), done_o)
+    np.testing.assert_allclose(rew_d, rew_o, rtol=1e-5, atol=1e-6)
+    pol.close()

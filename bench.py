@@ -6,13 +6,17 @@ set actions (MjClass::set_continous_action x n_actions), action_step() = S = 63 
 substeps + sense_gripper_state + update_env, then observation, done and reward
 (mjclass.cpp:1483-1508, 1632-1959, 3000-3049), followed by the episode-boundary
 bookkeeping (return hand-off, reset + respawn of done/truncated envs, MjEnv.py:616-637).
-Everything runs on the device; inputs (pre-drawn random actions, a spawn table) are
-resident in HBM before the timed region starts.
+Everything runs on the device: the actions come from a device driver reading each env's
+episode step (gm_scripted_actions), resets draw their object and pose on the device.
 
 Workload = BASELINE.json configs[2] ("C3"): 4096 envs per GPU, 20-object synthetic
-set6-like mixed set, randomised spawn, random actions U[-1,1]^4.  N GPUs run N x 4096
-envs sharded by env id (weak scaling); the only collective is an RCCL all-gather of
-the per-env episode returns each step.
+set6-like mixed set, randomised spawn (MjEnv._spawn_object: object drawn per episode,
+spawn_into_scene grid search), at STEADY STATE: before the timed region
+(and independent of --warmup) the batch is pre-rolled untimed so that the envs are spread
+uniformly over episode steps 1..250, driven by the scripted grasp mix (close, squeeze,
+palm press, lift, with jitter), so grasp contacts, done flags and resets all fall inside
+the timed window.  N GPUs run N x 4096 envs sharded by env id (weak scaling); the only
+collective is an RCCL all-gather of the per-env episode returns each step.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -27,6 +31,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import numpy as np
 import os
 import sys
 import time
@@ -37,6 +42,7 @@ sys.path.insert(0, os.path.join(REPO, "gripper-mujoco_amd"))
 METRIC = "env-steps/sec (batched rollout) at 4096 envs; obs max-rel-err vs C++ ref"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM")
 NCON_NOMINAL = 12              # SURVEY.md 8d nominal contacts per env-substep
+MAX_EP = 250                   # baseline yaml env.max_episode_steps
 
 
 def algorithmic_bytes_per_substep(model, ncon: int = NCON_NOMINAL) -> dict:
@@ -61,7 +67,7 @@ def algorithmic_bytes_per_substep(model, ncon: int = NCON_NOMINAL) -> dict:
 def mjenv_spawn_params(gmx):
     """default_spawn_params as MjEnv._spawn_object sets them (MjEnv.py:1211-1215):
     +-10 mm xy on the 2 mm grid, +-pi/2 rotation on the pi/30 grid; resets place the
-    object with spawn_into_scene on the device (3 tries, then the spawn-table pose)."""
+    object with spawn_into_scene on the device (3 tries, then the drawn fallback pose)."""
     import math
     p = gmx.default_spawn_params()
     p.xrange = p.yrange = 10e-3
@@ -83,66 +89,96 @@ def load_traffic(n_envs: int):
     return None, None
 
 
-def _rel_abs(obs, ref):
-    import numpy as np
-    ref = np.asarray(ref, dtype=np.float64)
-    d = np.abs(np.asarray(obs, dtype=np.float64) - ref)
-    big = np.abs(ref) >= 1e-3
-    rel = float((d[big] / np.abs(ref[big])).max()) if big.any() else 0.0
-    ab = float(d[~big].max()) if (~big).any() else 0.0
-    return rel, ab
-
-
-def obs_parity(gmx):
-    """obs max-rel-err of the GPU path vs the fp64 oracle (noise off; SURVEY.md 8d: rel
-    over |ref| >= 1e-3, abs elsewhere) on two probes: a 20-step contact-free rollout of
-    4 envs, and the first env-step of 3 envs closing on an object (contact-rich, from the
-    identical reset state; longer contact-rich rollouts separate chaotically)."""
+def obs_parity(gmx, env, seed: int):
+    """obs max-rel-err of the GPU path vs the fp64 oracle ON THE BENCHMARK'S OWN STATES
+    (rel over |ref| >= 1e-3, abs elsewhere): the whole batch's fp64 state
+    after the timed window is handed to the oracle (gm_get_env_states -> or_import_state),
+    and both run the next env-step of the scripted mix.  Done flags and event rows are
+    compared bit for bit."""
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib
-    s = gmx.canonical_settings(noise=False, seed=5)
-    out = {}
-    # contact-free rollout
-    env = gmx.BatchedGripperEnv(4, object_set="set1_synthetic", settings=s, seed=5)
-    xs = np.array([0.055, 0.058, 0.06, 0.062])
-    sp = env.make_spawn(x=xs, y=xs, idx=0)
-    env.reset(spawn=sp)
-    orc = []
-    for e in range(4):
-        o = oracle_lib.OracleEnv(env.model, env.cfg, env.objects, e)
-        o.reset(sp[e])
-        orc.append(o)
-    rng = np.random.default_rng(1234)
-    rel = ab = 0.0
-    for _ in range(20):
-        a = rng.uniform(-1, 1, size=(4, env.n_actions)).astype(np.float32)
-        obs, _, _, _ = env.step(a)
-        for e in range(4):
-            r, b = _rel_abs(obs[e], orc[e].step(a[e])[0])
-            rel, ab = max(rel, r), max(ab, b)
+    rec = env.env_states()
+    a = env.scripted_actions(seed)
+    env.set_action(a)
+    env.action_step()
+    obs = env.observation()
+    rew, done = env.reward_done()
+    after = env.env_states()
+    t = time.time()
+    obs_o, rew_o, done_o, after_o = oracle_lib.batch_step(env.model, env.cfg, env.objects, rec, actions=a)
+    ref = obs_o.astype(np.float64)
+    d = np.abs(obs.astype(np.float64) - ref)
+    big = np.abs(ref) >= 1e-3
+    rel = np.where(big, d / np.where(big, np.abs(ref), 1.0), 0.0).max(axis=1)
+    ab = np.where(big, 0.0, d).max(axis=1)
+    dv, ov = gmx.env_state_view(after), gmx.env_state_view(after_o)
+    return {"max_rel": float(rel.max()), "max_abs_small": float(ab.max()),
+            "envs_over_1e-4": int(((rel > 1e-4) | (ab > 1e-4)).sum()), "envs": int(env.n_envs),
+            "p99_rel": float(np.percentile(rel, 99)),
+            "done_mismatch": int((done.astype(np.uint8) != done_o).sum()),
+            "event_row_mismatch_envs": int(((dv["bev_row"] != ov["bev_row"]).any(axis=1) |
+                                            (dv["lev_row"] != ov["lev_row"]).any(axis=1)).sum()),
+            "reward_max_abs_diff": float(np.abs(rew - rew_o).max()),
+            "states": "the benchmark batch after the timed window (steady state, noise on), one env-step",
+            "oracle_s": round(time.time() - t, 2)}
+
+
+def c2_line(gmx, torch, dev, stream, steps: int, seed: int, env_offset: int):
+    """C2 (BASELINE.json configs[1]): 256 envs, one cylinder (r 20 mm, h 60 mm), the same
+    steady-state scripted workload as the headline."""
+    s = gmx.canonical_settings(seed=seed)
+    n = 256
+    env = gmx.BatchedGripperEnv(n, object_set="cylinder", settings=s, seed=seed, env_offset=env_offset,
+                                device=dev.index)
+    env.set_stream(stream.cuda_stream)
+    env.set_scene_spawn(mjenv_spawn_params(gmx), max_tries=3)
+    env.reset()
+    returns = torch.full((n,), float("nan"), device=dev)
+    d_act = env.lib.gm_device_actions(env.ctx)
+
+    def drive():
+        env.lib.gm_scripted_actions(env.ctx, seed, 0.2, d_act, 1)
+        env.lib.gm_set_action(env.ctx, d_act, 1)
+        env.lib.gm_step(env.ctx)
+        env.autoreset_device(0, returns.data_ptr(), max_episode_steps=MAX_EP)
+
+    t_start = gmx.spawn_int(seed, env_offset + np.arange(n), 0, 99, 0, MAX_EP - 1)
+    import ctypes
+    for t in range(MAX_EP):
+        m = (t_start == t)
+        if m.any():
+            env.lib.gm_reset(env.ctx, np.ascontiguousarray(m.astype(np.uint8)).ctypes.data_as(
+                ctypes.POINTER(ctypes.c_uint8)), None)
+        drive()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        drive()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
     env.close()
-    out["contact_free_rollout"] = {"max_rel": rel, "max_abs_small": ab, "envs": 4, "steps": 20}
-    # contact-rich first step
-    env = gmx.BatchedGripperEnv(3, object_set="set1_synthetic", settings=s, seed=5)
-    sp = env.make_spawn(x=0.0, y=0.0)
-    env.reset(spawn=sp)
-    a = np.array([[1.0, 0.0, 1.0, 0.5]] * 3, dtype=np.float32)
-    obs, _, _, _ = env.step(a)
-    rel = ab = 0.0
-    for e in range(3):
-        o = oracle_lib.OracleEnv(env.model, env.cfg, env.objects, e)
-        o.reset(sp[e])
-        r, b = _rel_abs(obs[e], o.step(a[e])[0])
-        rel, ab = max(rel, r), max(ab, b)
-    env.close()
-    out["contact_rich_first_step"] = {"max_rel": rel, "max_abs_small": ab, "envs": 3, "steps": 1}
-    return out
+    return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "envs": n, "steps": steps,
+            "ms_per_step": round(el / steps * 1e3, 3), "workload": "C2: 256 envs, one cylinder, steady-state "
+                                                                   "scripted grasp mix"}
+
+
+def host_cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline(gmx, n_envs: int, n_steps: int, n_threads: int):
     """The fp64 CPU oracle on the host cores: envs are independent (one env
-    per thread, as the reference runs one env per process), spread over n_threads."""
+    per thread, as the reference runs one env per process), spread over n_threads; the
+    same workload as the GPU line (scripted grasp mix, device-identical spawn draws,
+    resets at done / 250 steps)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib
     s = gmx.canonical_settings(seed=1234)
@@ -150,11 +186,12 @@ def cpu_baseline(gmx, n_envs: int, n_steps: int, n_threads: int):
     cfg = gmx.ConfigBlob(s, model)
     objs = gmx.make_object_set("set6_synthetic", 1234)
     t = time.time()
-    v = oracle_lib.bench(model, cfg, objs, n_envs, n_steps, seed=1234, n_threads=n_threads)
+    v = oracle_lib.bench(model, cfg, objs, n_envs, n_steps, seed=1234, n_threads=n_threads, scripted=True)
     return {"value": round(v, 2), "unit": "env-steps/s", "cores": n_threads, "kind": "port",
+            "cpu_model": host_cpu_model(), "host_cpus_visible": os.cpu_count(),
             "sample": f"fp64 C oracle (oracle/oracle.c, gcc -O2 -mavx), {n_threads} thread(s), {n_envs} envs x "
-                      f"{n_steps} env-steps of the C3 workload (set6_synthetic, random actions, "
-                      f"resets at done), {time.time() - t:.1f} s wall"}
+                      f"{n_steps} env-steps of the C3 workload (set6_synthetic, scripted grasp mix, resets at "
+                      f"done / 250 steps), {time.time() - t:.1f} s wall"}
 
 
 def policy_rollout(gmx, torch, dev, stream, n: int, steps: int, seed: int, env_offset: int):
@@ -168,9 +205,7 @@ def policy_rollout(gmx, torch, dev, stream, n: int, steps: int, seed: int, env_o
                                 device=dev.index)
     env.set_stream(stream.cuda_stream)
     env.set_scene_spawn(mjenv_spawn_params(gmx), max_tries=3)
-    spawn = env.make_spawn()
-    env.reset(spawn=spawn)
-    spawn_ptr = env.upload_spawn(spawn)
+    env.reset()
     pol = gmx.DevicePolicy(env, seed=seed)
     returns = torch.full((n,), float("nan"), device=dev)
     evp = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
@@ -182,7 +217,7 @@ def policy_rollout(gmx, torch, dev, stream, n: int, steps: int, seed: int, env_o
         if k is not None:
             evp[k][1].record(stream)
         env.lib.gm_step(env.ctx)
-        env.autoreset_device(spawn_ptr, returns.data_ptr())
+        env.autoreset_device(0, returns.data_ptr())
 
     one(0, None)
     torch.cuda.synchronize()
@@ -214,6 +249,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-policy", action="store_true", help="skip the C5 on-device DQN rollout line item")
+    ap.add_argument("--no-c2", action="store_true", help="skip the C2 (256 envs, one cylinder) line item")
+    ap.add_argument("--no-preroll", dest="preroll", action="store_false",
+                    help="skip the steady-state pre-roll (profiling runs only; the headline needs it)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -243,51 +281,66 @@ def main():
     env.set_stream(stream.cuda_stream)
     S = env.cfg.sim_steps_per_action
     env.set_scene_spawn(mjenv_spawn_params(gmx), max_tries=3)
-    spawn = env.make_spawn()
-    env.reset(spawn=spawn)
-    spawn_ptr = env.upload_spawn(spawn)
-
-    K, W = args.steps, args.warmup
-    g = torch.Generator(device=dev)
-    g.manual_seed(args.seed + 7919 * rank)
-    actions = torch.rand((W + K, n, env.n_actions), generator=g, device=dev) * 2 - 1
+    env.reset()
     returns = torch.full((n,), float("nan"), device=dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    d_act = env.lib.gm_device_actions(env.ctx)
     episodes = torch.zeros((), device=dev, dtype=torch.int64)
+    counting = [False]
 
-    def one_step(i, timed):
-        env.lib.gm_set_action(env.ctx, actions[i].data_ptr(), 1)
+    def drive(timed=None):
+        """one MjEnv.step-equivalent for the whole batch, all on the device"""
+        env.lib.gm_scripted_actions(env.ctx, args.seed, 0.2, d_act, 1)
+        env.lib.gm_set_action(env.ctx, d_act, 1)
         if timed is not None:
             ev[timed][0].record(stream)
         env.lib.gm_step(env.ctx)
         if timed is not None:
             ev[timed][1].record(stream)
-        env.autoreset_device(spawn_ptr, returns.data_ptr())
-        episodes.add_(torch.isfinite(gather_returns(returns, world)).sum())
+        env.autoreset_device(0, returns.data_ptr(), max_episode_steps=MAX_EP)
+        if counting[0]:
+            episodes.add_(torch.isfinite(gather_returns(returns, world)).sum())
 
+    # steady state: env e (global id) starts its episode at pre-roll step t_e, so after
+    # MAX_EP untimed steps the batch covers episode steps 1..MAX_EP uniformly
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    gids = first_env + np.arange(n)
+    t_start = gmx.spawn_int(args.seed, gids, 0, 99, 0, MAX_EP - 1)
+    for t in range(MAX_EP if args.preroll else 0):
+        m = (t_start == t)
+        if m.any():
+            env.lib.gm_reset(env.ctx, np.ascontiguousarray(m.astype(np.uint8)).ctypes.data_as(
+                __import__("ctypes").POINTER(__import__("ctypes").c_uint8)), None)
+        drive()
+    K, W = args.steps, args.warmup
     for i in range(W):
-        one_step(i, None)
+        drive()
+    counting[0] = True
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(K):
-        one_step(W + k, k)
+        drive(k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, dev)
+    steps_view = gmx.env_state_view(env.env_states())["num_action_steps"]
 
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
     finite = bool(torch.isfinite(torch.as_tensor(env.observation())).all())
     overflow = int(env.overflow().sum())
+    parity = None if (args.no_parity or rank != 0) else obs_parity(gmx, env, args.seed)
+    # contact load of the batch state (one probing substep after the timed window)
+    ncon_m, _, _, _, nefc_m, _ = env.debug_substep(full=True)
 
     if rank == 0:
         B = algorithmic_bytes_per_substep(env.model)
+        Bm = algorithmic_bytes_per_substep(env.model, ncon=int(round(float(ncon_m.mean()))))
         bytes_per_launch = n * S * B["bytes"]
         achieved = bytes_per_launch / kern_avg_s / 1e9
         traffic, traffic_src = load_traffic(n)
@@ -300,7 +353,7 @@ def main():
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(gmx, args.cpu_envs * args.cpu_threads // 4, args.cpu_steps, args.cpu_threads)
             cpu["single_thread"] = cpu_baseline(gmx, args.cpu_envs, args.cpu_steps, 1)["value"]
-        parity = None if args.no_parity else obs_parity(gmx)
+        c2 = None if (args.no_c2 or world > 1) else c2_line(gmx, torch, dev, stream, K, args.seed, first_env)
         c5 = None if (args.no_policy or world > 1) else policy_rollout(gmx, torch, dev, stream, n, max(3, K // 2), args.seed,
                                                         first_env)
         value = world * n * K / elapsed
@@ -309,18 +362,27 @@ def main():
             "steps": K, "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "C3: set6_synthetic 20 mixed objects, randomised spawn (spawn_into_scene "
-                                   "grid search on the device), random actions U[-1,1]^4, canonical "
-                                   "sensor/reward config, device auto-reset",
+            "config": {"workload": "C3: set6_synthetic 20 mixed objects, randomised spawn (object drawn per "
+                                   "episode, spawn_into_scene grid search on the device), steady state: envs "
+                                   "staggered over episode steps 1..250 by an untimed pre-roll, scripted grasp "
+                                   "mix (close / squeeze / palm / lift + jitter), canonical sensor/reward "
+                                   "config, device auto-reset at done / 250 steps",
                        "envs_per_gpu": n, "global_envs": world * n, "substeps_per_env_step": S,
                        "parallelism": f"env-shard x{world}",
                        "B_substep_bytes": B["bytes"], "B_substep_ncon": B["ncon"], "B_substep_nefc": B["nefc"],
+                       "measured_contacts": {"mean_ncon": round(float(ncon_m.mean()), 3),
+                                             "mean_nefc": round(float(nefc_m.mean()), 3),
+                                             "frac_nefc_gt_32": round(float((nefc_m > 32).mean()), 4),
+                                             "B_substep_bytes_at_mean_ncon": Bm["bytes"],
+                                             "episode_step_spread": [int(steps_view.min()), int(steps_view.max()),
+                                                                     round(float(steps_view.mean()), 1)]},
                        "model": {"nq": env.model.nq, "nv": env.model.nv, "nbody": env.model.nbody,
                                  "ngeom": env.model.ngeom, "nM": env.model.nM, "nlock": env.model.nlock},
                        "dtype_detail": "f64 dynamics, collision and PGS; f32 sensor windows / observations (as the reference)"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "obs_max_rel_err": parity,
+            "c2_single_cylinder_256": c2,
             "c5_device_policy_rollout": c5,
             "episodes_finished": int(episodes.item()),
             "overflow_envs": overflow, "finite": finite,

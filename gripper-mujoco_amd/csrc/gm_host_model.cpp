@@ -634,6 +634,19 @@ int gm_configure(const gm_settings* in, const gm_model* m, gm_config* c) {
   return GM_OK;
 }
 
+// luke::set_base_XYZ_limits / set_base_yaw_limit -> update_base_limits
+// (myfunctions.cpp:2286-2333): symmetric limits written into target_.base_min/max, which
+// the base action clamps and the base state normalisation read.
+int gm_config_set_base_limits(gm_config* c, double x, double y, double z, double yaw) {
+  if (!c) return GM_E_ARG;
+  if (x < 0 || y < 0 || z < 0) return GM_E_RANGE;
+  c->base_min[0] = -x; c->base_max[0] = x;
+  c->base_min[1] = -y; c->base_max[1] = y;
+  c->base_min[2] = -z; c->base_max[2] = z;
+  if (yaw >= 0) { c->base_min[5] = -yaw; c->base_max[5] = yaw; }
+  return GM_OK;
+}
+
 // ---- synthetic object sets (the reference's MJCF object sets are unavailable) ----
 static uint64_t splitmix(uint64_t& x) {
   uint64_t z = (x += 0x9E3779B97F4A7C15ull);

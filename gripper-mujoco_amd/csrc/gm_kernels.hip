@@ -2875,25 +2875,6 @@ extern "C" __global__ void gm_action_kernel(GmEnvState* __restrict__ states, con
 // the palm, lift the base -- indexed by the env's own episode step (num_action_steps),
 // plus uniform jitter per (step, action).  Continuous action fractions in [-1, 1] for
 // the in-use actions (MjClass::set_continous_action order).
-__device__ __host__ inline float gm_script_fraction(uint64_t seed, int64_t gid, int32_t ep, int32_t k, int i, int kind,
-                                                    float jitter) {
-  const int close_n = gm_spawn_int(seed, gid, ep, 16, 34, 45);
-  const int tilt_n = gm_spawn_int(seed, gid, ep, 17, 0, 25);
-  const float tilt_dir = gm_spawn_int(seed, gid, ep, 18, 0, 4) < 4 ? -1.0f : 1.0f;
-  const int palm_n = gm_spawn_int(seed, gid, ep, 19, 0, 15);
-  const int t1 = close_n, t2 = t1 + tilt_n, t3 = t2 + palm_n;
-  float a = 0.0f;
-  if (kind == GM_ACT_gripper_prismatic_X && k < t1) a = 1.0f;
-  if (kind == GM_ACT_gripper_revolute_Y && k >= t1 && k < t2) a = tilt_dir;
-  if (kind == GM_ACT_gripper_Z && k >= t2 && k < t3) a = 1.0f;
-  if (kind == GM_ACT_base_Z && k >= t3) a = -1.0f;
-  if (jitter > 0.0f) {
-    const int u = gm_spawn_int(seed, gid, ep, 32 + 8 * k + i, 0, 1 << 20);
-    a += jitter * ((float)u * (2.0f / (float)(1 << 20)) - 1.0f);
-  }
-  return a > 1.0f ? 1.0f : (a < -1.0f ? -1.0f : a);
-}
-
 #ifndef GM_CAL_TU   // env-step translation unit only
 extern "C" __global__ void gm_scripted_action_kernel(const GmEnvState* __restrict__ states, const gm_config* __restrict__ C,
                                                      float* __restrict__ out, int n_envs, uint64_t seed,

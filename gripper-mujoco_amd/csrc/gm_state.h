@@ -137,6 +137,32 @@ int32_t gm_spawn_int(uint64_t seed, int64_t gid, int32_t episode, int k, int32_t
   return lo + (int32_t)(((h >> 32) * span) >> 32);
 }
 
+// scripted grasp mix (gm_scripted_actions; host mirror gmx.GraspScript; the CPU oracle's
+// bench sample uses it too): action fraction for action index i of kind `kind` at episode
+// step k
+static inline
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+float gm_script_fraction(uint64_t seed, int64_t gid, int32_t ep, int32_t k, int i, int kind,
+                                                    float jitter) {
+  const int close_n = gm_spawn_int(seed, gid, ep, 16, 34, 45);
+  const int tilt_n = gm_spawn_int(seed, gid, ep, 17, 0, 25);
+  const float tilt_dir = gm_spawn_int(seed, gid, ep, 18, 0, 4) < 4 ? -1.0f : 1.0f;
+  const int palm_n = gm_spawn_int(seed, gid, ep, 19, 0, 15);
+  const int t1 = close_n, t2 = t1 + tilt_n, t3 = t2 + palm_n;
+  float a = 0.0f;
+  if (kind == GM_ACT_gripper_prismatic_X && k < t1) a = 1.0f;
+  if (kind == GM_ACT_gripper_revolute_Y && k >= t1 && k < t2) a = tilt_dir;
+  if (kind == GM_ACT_gripper_Z && k >= t2 && k < t3) a = 1.0f;
+  if (kind == GM_ACT_base_Z && k >= t3) a = -1.0f;
+  if (jitter > 0.0f) {
+    const int u = gm_spawn_int(seed, gid, ep, 32 + 8 * k + i, 0, 1 << 20);
+    a += jitter * ((float)u * (2.0f / (float)(1 << 20)) - 1.0f);
+  }
+  return a > 1.0f ? 1.0f : (a < -1.0f ? -1.0f : a);
+}
+
 // Topology derived from gm_model on the host (the canonical gripper tree):
 // dof/body of chain position p in finger chain f is first + p - 1 (p >= 1),
 // position 0 of every finger / palm chain is the base dof.

@@ -210,6 +210,7 @@ def _declare(lib):
         "gm_build_model": (i32, [vp, vp]),
         "gm_default_settings": (None, [vp]),
         "gm_configure": (i32, [vp, vp, vp]),
+        "gm_config_set_base_limits": (i32, [vp, C.c_double, C.c_double, C.c_double, C.c_double]),
         "gm_make_object_set": (i32, [C.c_char_p, C.c_uint64, vp, i32]),
         "gm_create": (i32, [vp, vp, vp, i32, i32, i32, i32, C.c_uint64, C.POINTER(vp)]),
         "gm_destroy": (None, [vp]),

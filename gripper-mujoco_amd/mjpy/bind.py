@@ -13,6 +13,9 @@ with the reference's names, argument meaning and error behaviour:
   is_done() / reward()                               bind.cpp:115,128 (MjEnv.py:635,1039)
   reset() / hard_reset()                             bind.cpp:53-54   (MjEnv.py:2240,2249)
   spawn_object / spawn_into_scene / default_spawn_params / set_new_base_XY
+  set_base_XYZ_limits / set_base_yaw_limit (effective on the device config)
+  is_finger_hook_fixed / using_xyz_base_actions / reset_timestep
+  get_test_report / add_events / reward(event)
   get_n_actions / get_n_obs / get_N / finger dimension setters and getters
   get_event_state() -> EventTrack                    bind.cpp:525-590 (MjEnv.py:1020)
   __getstate__ / __setstate__ (pickle pair)          bind.cpp:207-241 (MjEnv.py:2088-2105)
@@ -78,14 +81,46 @@ class EventTrack:
         self.__init__()
 
     def calculate_percentage(self):
-        # percent = abs / total steps is what the reference derives; callers that need it
-        # divide by their own step count (MjEnv tracks current_step)
-        return None
+        """EventTrack::calculate_percentage (mjclass.h:628-645): percent = 100 abs /
+        step_num.abs for every event."""
+        total = float(self.step_num.abs)
+        for n in list(BINARY_EVENTS) + list(LINEAR_EVENTS):
+            e = getattr(self, n)
+            e.percent = (100.0 * e.abs) / total if total else float("nan")
 
     def print(self):
         for n in list(BINARY_EVENTS) + list(LINEAR_EVENTS):
             e = getattr(self, n)
             print(f"{n}: row {e.row} abs {e.abs} last {e.last_value}")
+
+
+class TestReport:
+    """MjType::TestReport (mjclass.h:941-950): object name, cumulative reward, event counts."""
+
+    def __init__(self, object_name: str = "", cumulative_reward: float = 0.0, cnt: EventTrack | None = None):
+        self.object_name = object_name
+        self.cumulative_reward = cumulative_reward
+        self.cnt = cnt if cnt is not None else EventTrack()
+
+
+def _linear_reward(val, mn, mx, overshoot):
+    """linear_reward (mjclass.cpp:4866-4894), float arithmetic."""
+    f = np.float32
+    val, mn, mx, overshoot = f(val), f(mn), f(mx), f(overshoot)
+    if val < mn:
+        return f(0.0)
+    if val > mx:
+        if overshoot < mx:
+            return f(1.0)
+        if val > overshoot:
+            return f(0.0)
+        mn, mx, val = f(0.0), f(overshoot - mx), f(overshoot - val)
+    return f((val - mn) / (mx - mn))
+
+
+# j_.baseLims defaults (myfunctions.cpp:245-261): x, y, z (m) and yaw (rad)
+_BASE_LIMITS_DEFAULT = (500e-3, 500e-3, 30e-3)
+_BASE_YAW_DEFAULT = math.pi / 2
 
 
 class MjClass:
@@ -102,7 +137,8 @@ class MjClass:
         self._env = None
         self._pending = None         # continuous action vector buffered between calls
         self._rng = np.random.default_rng(0)
-        self._base_xy = (0.0, 0.0)
+        self._base_limits = _BASE_LIMITS_DEFAULT     # j_.baseLims (reset by hard_reset)
+        self._base_yaw = _BASE_YAW_DEFAULT
 
     # ------------------------------------------------------------ model / lifecycle
     def load(self, file_path: str = ""):
@@ -126,7 +162,17 @@ class MjClass:
                                               model_params=model_params, seed=int(self.set.random_seed),
                                               max_episode_steps=1 << 30)
             self._rng = np.random.default_rng(int(self.set.random_seed))
+            self._push_base_limits(self._env.cfg)
         return self._env
+
+    def _push_base_limits(self, cfg):
+        """write j_.baseLims into the context's configuration (update_base_limits)"""
+        env = self._env
+        x, y, z = self._base_limits
+        rc = env.lib.gm_config_set_base_limits(cfg.ptr, x, y, z, self._base_yaw)
+        if rc != 0:
+            raise RuntimeError(f"base limits rejected ({rc})")
+        env._check(env.lib.gm_update_config(env.ctx, cfg.ptr))
 
     def reset(self):
         """MjClass::reset (mjclass.cpp:434-486): re-apply settings (configure_settings),
@@ -134,11 +180,13 @@ class MjClass:
         is placed until spawn_object / spawn_into_scene picks one (MjEnv.reset order)."""
         env = self._ensure()
         cfg = gmx.ConfigBlob(self.set, env.model)
+        env.lib.gm_config_set_base_limits(cfg.ptr, *self._base_limits, self._base_yaw)
         if env.lib.gm_update_config(env.ctx, cfg.ptr) != 0:
             # the observation layout changed: the reference re-sizes on reset too
             self._drop()
             env = self._ensure()
             cfg = env.cfg
+        env.cfg = cfg
         env.n_obs, env.n_actions = cfg.n_obs, cfg.n_actions
         env._obs = np.zeros((1, cfg.n_obs), dtype=np.float32)
         sp = (gmx.Spawn * 1)()
@@ -147,9 +195,23 @@ class MjClass:
         self._pending = None
 
     def hard_reset(self):
-        """Reload from scratch (bind.cpp:54): a fresh device context."""
+        """Reload from scratch (bind.cpp:54): a fresh device context.  Base limits do not
+        persist through a hard reset (myfunctions.cpp:2309-2333; MjEnv re-sets them)."""
+        self._drop()
+        self._base_limits = _BASE_LIMITS_DEFAULT
+        self._base_yaw = _BASE_YAW_DEFAULT
+        self.reset()
+
+    def reset_timestep(self):
+        """MjEnv.reset(timestep=True) (MjEnv.py:2247): recalibrate the timestep
+        (find_highest_stable_timestep, mjclass.cpp:4745-4854, as one batched device job),
+        rebuild the model with it (S = ceil(time_for_action / dt)) and reset."""
+        env = self._ensure()
+        cal, _ = gmx.calibrate(env.model, env.cfg, env.objects, what=gmx.CAL_TIMESTEP)
+        self._model_params().timestep = float(cal.timestep)
         self._drop()
         self.reset()
+        return float(cal.timestep)
 
     def step(self):
         raise NotImplementedError("single physics substeps are inside action_step() on the device")
@@ -194,9 +256,43 @@ class MjClass:
         _, d = self._ensure().reward_done()
         return bool(d[0])
 
-    def reward(self) -> float:
-        r, _ = self._ensure().reward_done()
-        return float(r[0])
+    def reward(self, event: "EventTrack | None" = None) -> float:
+        """MjClass::reward (mjclass.cpp:3000-3049): the current transition's reward; with
+        an EventTrack, calc_rewards over that track (mjclass.cpp:5471-5528: binary
+        reward if row >= trigger, linear reward x linear_reward(last_value) likewise)."""
+        if event is None:
+            r, _ = self._ensure().reward_done()
+            return float(r[0])
+        st = self.set
+        r = np.float32(0.0)
+        for n in BINARY_EVENTS:
+            if getattr(event, n).row >= getattr(st, n).trigger:
+                r = np.float32(r + np.float32(getattr(st, n).reward))
+        for n in LINEAR_EVENTS:
+            sr, ev = getattr(st, n), getattr(event, n)
+            if ev.row >= sr.trigger:
+                frac = _linear_reward(ev.last_value, sr.min, sr.max, sr.overshoot)
+                r = np.float32(r + np.float32(np.float32(sr.reward) * frac))
+        return float(r)
+
+    def add_events(self, e1: "EventTrack", e2: "EventTrack") -> "EventTrack":
+        """MjClass::add_events (mjclass.cpp:4692-4715): abs and active_sum summed, linear
+        last_value summed, everything else default."""
+        out = EventTrack()
+        for n in BINARY_EVENTS:
+            a, b, o = getattr(e1, n), getattr(e2, n), getattr(out, n)
+            o.abs, o.active_sum = a.abs + b.abs, a.active_sum + b.active_sum
+        for n in LINEAR_EVENTS:
+            a, b, o = getattr(e1, n), getattr(e2, n), getattr(out, n)
+            o.abs, o.active_sum = a.abs + b.abs, a.active_sum + b.active_sum
+            o.last_value = float(np.float32(np.float32(a.last_value) + np.float32(b.last_value)))
+        return out
+
+    def get_test_report(self) -> TestReport:
+        """MjClass::get_test_report (mjclass.cpp:3800-3809)."""
+        env = self._ensure()
+        st = gmx.env_state_view(env.env_states())[0]
+        return TestReport(self.get_current_object_name(), float(st["cumulative_reward"]), self.get_event_state())
 
     def get_event_state(self) -> EventTrack:
         rows, absc, lastv = self._ensure().event_rows()
@@ -206,6 +302,7 @@ class MjClass:
             e.row, e.abs = int(rows[0, i]), int(absc[0, i])
             e.last_value = float(lastv[0, i]) if i >= len(BINARY_EVENTS) else int(lastv[0, i])
             e.value = e.last_value
+            e.active_sum = int(e.row != 0)
         return t
 
     def get_n_actions(self) -> int:
@@ -260,8 +357,20 @@ class MjClass:
             self._spawned = int(index)
         return ok
 
-    def set_new_base_XY(self, x: float, y: float):
-        self._base_xy = (float(x), float(y))
+    def set_new_base_XY(self, x: float, y: float) -> bool:
+        """MjClass::set_new_base_XY -> luke::set_base_to_XY_position (mjclass.cpp:1394-1402,
+        myfunctions.cpp:2568-2608): the base XY target is clamped to the base limits, then
+        the qpos snap needs XY base joints -- this gripper (like the reference's canonical
+        one) has base Z only, so, as the reference does, it raises after setting the target."""
+        env = self._ensure()
+        rec = env.env_states()
+        st = gmx.env_state_view(rec)[0]
+        lx, ly, _ = self._base_limits
+        tx = min(max(float(x), -lx), lx)
+        ty = min(max(float(y), -ly), ly)
+        st["base"][0], st["base"][1] = tx, ty
+        env.set_env_states(rec)
+        raise RuntimeError("luke::set_base_to_XY_position() cannot move XY because these motions are not in use")
 
     def set_scene_grasp_target(self, num_objects: int):
         return None
@@ -339,14 +448,35 @@ class MjClass:
         return out
 
     def set_base_XYZ_limits(self, x: float, y: float, z: float):
+        """MjClass::set_base_XYZ_limits (mjclass.cpp:3847-3852): symmetric base limits,
+        effective immediately on the device (base action clamps, base state normalisation)."""
         self._base_limits = (float(x), float(y), float(z))
+        if self._env is not None:
+            self._push_base_limits(self._env.cfg)
 
     def set_base_yaw_limit(self, yaw: float):
+        """MjClass::set_base_yaw_limit (mjclass.cpp:3854-3859)."""
         self._base_yaw = float(yaw)
+        if self._env is not None:
+            self._push_base_limits(self._env.cfg)
+
+    def is_finger_hook_fixed(self) -> bool:
+        """MjClass::is_finger_hook_fixed (mjclass.cpp:3941-3946): the hook is a fixed part
+        of the last finger link in this gripper model."""
+        return True
+
+    def using_xyz_base_actions(self) -> bool:
+        """MjClass::using_xyz_base_actions (mjclass.cpp:3955-3960): the base moves in Z only."""
+        return False
+
+    def get_base_limits(self):
+        """(x, y, z, yaw) symmetric base limits currently applied."""
+        return (*self._base_limits, self._base_yaw)
 
     # ------------------------------------------------------------ pickling (bind.cpp:207-241)
     def __getstate__(self):
         return {"set": bytes(self.set), "params": bytes(self._params) if self._params is not None else None,
+                "base_limits": self._base_limits, "base_yaw": self._base_yaw,
                 "object_set_name": self.object_set_name, "model_folder_path": self.model_folder_path,
                 "machine": self.machine, "default_spawn_params": bytes(self.default_spawn_params)}
 
@@ -357,5 +487,8 @@ class MjClass:
             self._params = gmx.ModelParams.from_buffer_copy(st["params"])
         self.object_set_name = st["object_set_name"]
         self.machine = st["machine"]
+        if st.get("base_limits") is not None:
+            self._base_limits = tuple(st["base_limits"])
+            self._base_yaw = float(st["base_yaw"])
         if st.get("default_spawn_params") is not None:
             C.memmove(C.byref(self.default_spawn_params), st["default_spawn_params"], C.sizeof(SpawnParams))

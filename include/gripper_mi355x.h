@@ -321,6 +321,12 @@ int  gm_build_model(const gm_model_params* p, gm_model* out);
 void gm_default_settings(gm_settings* s);
 int  gm_configure(const gm_settings* s, const gm_model* m, gm_config* out);
 
+/* MjClass::set_base_XYZ_limits / set_base_yaw_limit (mjclass.cpp:3847-3859 ->
+ * luke::set_base_XYZ_limits / set_base_yaw_limit, myfunctions.cpp:2309-2333): symmetric
+ * base operating limits [-x, x], [-y, y], [-z, z] (m) and, when yaw >= 0, [-yaw, yaw]
+ * (rad) in a configuration; push it to a context with gm_update_config. */
+int  gm_config_set_base_limits(gm_config* cfg, double x, double y, double z, double yaw);
+
 /* Synthetic object sets (the reference's set6/set9 MJCF sets are unavailable). */
 int  gm_make_object_set(const char* name, uint64_t seed, gm_object* out, int max_objects);
 

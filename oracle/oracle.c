@@ -2557,18 +2557,38 @@ int or_batch_substep(const gm_model* m, const gm_config* c, const gm_object* obj
   return err ? -1000 - err : 0;
 }
 
-/* bounded CPU baseline: n_envs independent envs, random continuous actions */
-/* CPU throughput baseline: n_envs independent envs x n_steps env-steps of random
- * actions (one LCG stream per env, so the work does not depend on the thread count),
- * spread over n_threads POSIX threads (envs share nothing, like the reference's
- * one-env-per-process model).  Returns env-steps per wall second. */
+/* CPU throughput baseline: n_envs independent envs x n_steps env-steps, spread over
+ * n_threads POSIX threads (envs share nothing, like the reference's one-env-per-process
+ * model).  The workload is the benchmark's: MjEnv.reset -> _spawn_object with the same
+ * counter-based object / pose draws as the device (gm_spawn_int; spawn_into_scene with
+ * +-10 mm / +-pi/2, 3 tries, then the fallback pose), actions from the scripted grasp mix
+ * (mode 1, gm_script_fraction) or uniform random (mode 0), a reset at done or at
+ * max_episode_steps (MjEnv.py:616-637).  Returns env-steps per wall second. */
 typedef struct {
   const or_env* proto;
   const gm_config* c;
-  int n_objects, n_envs, n_steps, tid, n_threads;
+  int n_objects, n_envs, n_steps, tid, n_threads, mode, max_steps;
   uint64_t seed;
-  long done_steps;
+  long done_steps, episodes;
 } bench_job;
+
+static void bench_reset(or_env* e, uint64_t seed, int64_t gid, int n_objects) {
+  const int ep = e->episode + 1;
+  gm_spawn sp;
+  sp.object_index = gm_spawn_int(seed, gid, ep, 0, 0, n_objects - 1);
+  sp.x = gm_spawn_int(seed, gid, ep, 1, -10, 10) * 1e-3;
+  sp.y = gm_spawn_int(seed, gid, ep, 2, -10, 10) * 1e-3;
+  const int noise = gm_spawn_int(seed, gid, ep, 3, -5, 5), opt = gm_spawn_int(seed, gid, ep, 4, 0, 2);
+  sp.zrot = (60 * opt + noise) * (PI_D / 180.0);
+  or_reset(e, &sp);
+  gm_spawn_params sc;
+  memset(&sc, 0, sizeof(sc));
+  sc.index = sp.object_index;
+  sc.xrange = sc.yrange = 10e-3; sc.rotrange = PI_D / 2.0;
+  sc.xmin = sc.ymin = -100; sc.xmax = sc.ymax = 100;
+  sc.smallest_gap = 1e-3; sc.xy_increment = 2e-3; sc.rot_increment = PI_D / 30.0;
+  for (int tr = 0; tr < 3; tr++) if (or_spawn_into_scene(e, &sc)) break;
+}
 
 static void* bench_worker(void* arg) {
   bench_job* j = (bench_job*)arg;
@@ -2577,22 +2597,20 @@ static void* bench_worker(void* arg) {
     *e = *j->proto;
     e->env_id = k;
     e->rng = lcg_seed((uint64_t)j->c->s.random_seed + (uint64_t)k * 1000003ull);
-    gm_spawn sp = {k % (j->n_objects > 0 ? j->n_objects : 1), 0.0, 0.0, 0.0};
-    /* MjEnv._spawn_object (MjEnv.py:1211-1223): +-10 mm, +-pi/2 grid search, 3 tries */
-    gm_spawn_params sc;
-    memset(&sc, 0, sizeof(sc));
-    sc.index = sp.object_index;
-    sc.xrange = sc.yrange = 10e-3; sc.rotrange = PI_D / 2.0;
-    sc.xmin = sc.ymin = -100; sc.xmax = sc.ymax = 100;
-    sc.smallest_gap = 1e-3; sc.xy_increment = 2e-3; sc.rot_increment = PI_D / 30.0;
-#define BENCH_RESET() do { or_reset(e, &sp); for (int tr = 0; tr < 3; tr++) if (or_spawn_into_scene(e, &sc)) break; } while (0)
-    BENCH_RESET();
+    e->episode = 0;
+    bench_reset(e, j->seed, k, j->n_objects);
     uint64_t x = j->seed + (uint64_t)k * 0x9E3779B97F4A7C15ull;
     for (int t = 0; t < j->n_steps; t++) {
-      float a[8];
-      for (int i = 0; i < e->c.n_actions && i < 8; i++) {
-        x = x * 6364136223846793005ull + 1442695040888963407ull;
-        a[i] = (float)((double)(x >> 11) / 9007199254740992.0 * 2 - 1);
+      float a[16];
+      for (int i = 0; i < e->c.n_actions && i < 16; i++) {
+        if (j->mode == 1) {
+          const int code = e->c.action_options[i];
+          const int kind = (code >= 0 && code < GM_ACTION_TERMINATION) ? code / 3 : -1;
+          a[i] = gm_script_fraction(j->seed, k, e->episode, e->num_action_steps, i, kind, 0.2f);
+        } else {
+          x = x * 6364136223846793005ull + 1442695040888963407ull;
+          a[i] = (float)((double)(x >> 11) / 9007199254740992.0 * 2 - 1);
+        }
       }
       or_set_action(e, a);
       or_step(e);
@@ -2601,16 +2619,18 @@ static void* bench_worker(void* arg) {
       int d = or_is_done(e);
       or_reward(e);
       j->done_steps++;
-      if (d) BENCH_RESET();
+      if (d || (j->max_steps > 0 && e->num_action_steps >= j->max_steps)) {
+        j->episodes++;
+        bench_reset(e, j->seed, k, j->n_objects);
+      }
     }
-#undef BENCH_RESET
   }
   free(e);
   return NULL;
 }
 
 double or_bench(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects,
-                int n_envs, int n_steps, uint64_t seed, int n_threads) {
+                int n_envs, int n_steps, uint64_t seed, int n_threads, int mode, int max_episode_steps) {
   if (n_threads < 1) n_threads = 1;
   if (n_threads > 256) n_threads = 256;
   or_env* proto = or_create(m, c, objects, n_objects, 0);
@@ -2620,7 +2640,7 @@ double or_bench(const gm_model* m, const gm_config* c, const gm_object* objects,
   struct timespec t0, t1;
   clock_gettime(CLOCK_MONOTONIC, &t0);
   for (int t = 0; t < n_threads; t++) {
-    jobs[t] = (bench_job){proto, c, n_objects, n_envs, n_steps, t, n_threads, seed, 0};
+    jobs[t] = (bench_job){proto, c, n_objects, n_envs, n_steps, t, n_threads, mode, max_episode_steps, seed, 0, 0};
     if (n_threads == 1) bench_worker(&jobs[0]);
     else pthread_create(&th[t], NULL, bench_worker, &jobs[t]);
   }

@@ -84,9 +84,10 @@ int    or_sample(int mode, const float* window_recent_first, int n_avail, int pr
 /* automatic calibration (find_highest_stable_timestep + calibrate_simulated_sensors) */
 int    or_calibrate(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects, int what,
                     gm_calibration* out, double* trace_dt, uint8_t* trace_unstable, int max_trace);
-/* time one bounded CPU sample: n_envs envs x n_steps env-steps, random actions */
+/* time one bounded CPU sample: n_envs envs x n_steps env-steps of the benchmark workload
+ * (mode 1: scripted grasp mix, 0: random actions; resets at done / max_episode_steps) */
 double or_bench(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects,
-                int n_envs, int n_steps, uint64_t seed, int n_threads);
+                int n_envs, int n_steps, uint64_t seed, int n_threads, int mode, int max_episode_steps);
 
 #ifdef __cplusplus
 }

@@ -59,7 +59,7 @@ def lib():
             "or_minstd_next_canonical_double": (C.c_double, [C.POINTER(C.c_uint32)]),
             "or_grip_step_sequence": (i32, [f64p, i32, f64p]),
             "or_sample": (i32, [i32, f32p, i32, i32, i32, f32p]),
-            "or_bench": (C.c_double, [vp, vp, vp, i32, i32, i32, C.c_uint64, i32]),
+            "or_bench": (C.c_double, [vp, vp, vp, i32, i32, i32, C.c_uint64, i32, i32, i32]),
             "or_polyfit_eval": (C.c_float, [f64p, f64p, i32, i32, C.c_double]),
             "or_gauge_points": (None, [vp, f64p, f64p, f64p]),
             "or_ring_trace": (None, [f32p, i32, i32, f32p]),
@@ -256,9 +256,9 @@ def canonical_floats(seed, n):
     return np.array([lib().or_minstd_next_canonical_float(C.byref(s)) for _ in range(n)])
 
 
-def bench(model, cfg, objects, n_envs, n_steps, seed=1234, n_threads=1):
+def bench(model, cfg, objects, n_envs, n_steps, seed=1234, n_threads=1, scripted=True, max_episode_steps=250):
     return float(lib().or_bench(model.ptr, cfg.ptr, C.cast(objects, C.c_void_p), len(objects), n_envs, n_steps,
-                                seed, n_threads))
+                                seed, n_threads, 1 if scripted else 0, max_episode_steps))
 
 
 def polyfit_eval(X, Y, order, x):

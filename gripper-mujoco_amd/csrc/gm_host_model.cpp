@@ -122,6 +122,27 @@ void box_inertia(double mass, double hx, double hy, double hz, double out[3]) {
 
 }  // namespace
 
+void gm_derive_model_constants(gm_model* m);
+// Everything the reference derives from the MJCF's gripper numerics rather than reading
+// it (JointSettings::Dim / ctrl / gauge, myfunctions.cpp:207-296, 535): shared by the
+// builder and the MJCF loader (gm_mjcf.cpp) so both produce the same model bit for bit.
+void gm_derive_model_constants(gm_model* m) {
+  const double I = m->finger_width * std::pow(m->finger_thickness, 3) / 12.0;
+  m->finger_EI = m->finger_E * I;
+  m->yield_stress = 215e6;
+  const int Ntotal = m->n_seg + m->fixed_first_segment;
+  m->segment_length = m->finger_length / double(Ntotal);   // myfunctions.cpp:535
+  const double EI = m->finger_EI;
+  set3(m->kp_gripper, EI * 541.3 + 49.65, EI * 44.92 - 0.846, 1000);
+  set3(m->kd_gripper, 1, 1, 1);
+  set3(m->kp_base, 500, 500, 2000);
+  set3(m->kd_base, 80, 80, 100);
+  m->stepper_num_steps = 10;
+  m->time_per_step = 10 / 2000.0;
+  m->gauge_xpos = 50e-3;
+  m->gauge_order = 3;
+}
+
 extern "C" {
 
 void gm_default_model_params(gm_model_params* p) {
@@ -152,27 +173,13 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
   m->finger_width = p->finger_width;
   m->finger_thickness = p->finger_thickness;
   m->finger_E = p->finger_E;
-  double I = p->finger_width * std::pow(p->finger_thickness, 3) / 12.0;
-  m->finger_EI = p->finger_E * I;
   m->hook_length = p->hook_length;
   m->hook_angle_degrees = p->hook_angle_degrees;
   m->fingertip_clearance = p->fingertip_clearance;
-  m->yield_stress = 215e6;
   m->fixed_first_segment = 1;   // links 2..N+1 carry the N joints (myfunctions.cpp:650-660)
-  const int Ntotal = N + m->fixed_first_segment;
-  const double Ls = p->finger_length / double(Ntotal);   // myfunctions.cpp:535
-  m->segment_length = Ls;
-
-  // ---- gains (myfunctions.cpp:273-296) ----
-  double EI = m->finger_EI;
-  set3(m->kp_gripper, EI * 541.3 + 49.65, EI * 44.92 - 0.846, 1000);
-  set3(m->kd_gripper, 1, 1, 1);
-  set3(m->kp_base, 500, 500, 2000);
-  set3(m->kd_base, 80, 80, 100);
-  m->stepper_num_steps = 10;
-  m->time_per_step = 10 / 2000.0;
-  m->gauge_xpos = 50e-3;
-  m->gauge_order = 3;
+  gm_derive_model_constants(m);
+  const double Ls = m->segment_length;
+  const double EI = m->finger_EI;
 
   // ---- options ----
   m->timestep = p->timestep;

@@ -210,6 +210,8 @@ def _declare(lib):
         "gm_build_model": (i32, [vp, vp]),
         "gm_default_settings": (None, [vp]),
         "gm_configure": (i32, [vp, vp, vp]),
+        "gm_model_to_mjcf": (C.c_int64, [vp, C.c_char_p, C.c_int64]),
+        "gm_model_from_mjcf": (i32, [C.c_char_p, vp, C.c_char_p, i32]),
         "gm_config_set_base_limits": (i32, [vp, C.c_double, C.c_double, C.c_double, C.c_double]),
         "gm_make_object_set": (i32, [C.c_char_p, C.c_uint64, vp, i32]),
         "gm_create": (i32, [vp, vp, vp, i32, i32, i32, i32, C.c_uint64, C.POINTER(vp)]),
@@ -296,6 +298,38 @@ class ModelBlob:
     @property
     def ptr(self):
         return C.cast(self.buf, C.c_void_p)
+
+    def _read_info(self, lib):
+        info = (C.c_int32 * 20)()
+        lib.gm_model_info(self.buf, info)
+        self.nlock, self.nM = info[18], info[19]
+        (self.nq, self.nv, self.nbody, self.ngeom, self.npair, self.n_seg, self.dof_base,
+         self.dof_palm, self.dof_obj) = info[:9]
+        self.dof_pris = list(info[9:12])
+        self.dof_rev = list(info[12:15])
+        self.dof_seg = list(info[15:18])
+
+    def to_mjcf(self) -> str:
+        """The model as MJCF with the reference's names (gm_model_to_mjcf)."""
+        lib = load_library()
+        n = lib.gm_model_to_mjcf(self.buf, None, 0)
+        out = C.create_string_buffer(n + 1)
+        lib.gm_model_to_mjcf(self.buf, out, n + 1)
+        return out.value.decode()
+
+    @classmethod
+    def from_mjcf(cls, xml: str) -> "ModelBlob":
+        """Compile an MJCF (the subset gm_model_from_mjcf reads) into a model."""
+        lib = load_library()
+        self = cls.__new__(cls)
+        self.params = None
+        self.buf = C.create_string_buffer(struct_size(1))
+        err = C.create_string_buffer(512)
+        rc = lib.gm_model_from_mjcf(xml.encode(), self.buf, err, 512)
+        if rc != 0:
+            raise ValueError(f"gm_model_from_mjcf: {err.value.decode()}")
+        self._read_info(lib)
+        return self
 
 
 def env_state_dtype():

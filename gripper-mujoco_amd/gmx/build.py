@@ -6,7 +6,7 @@ import subprocess
 
 from ._lib import PKG_DIR, REPO_DIR, LIB_PATH
 
-SOURCES = ["csrc/gm_capi.hip", "csrc/gm_calib.hip", "csrc/gm_host_model.cpp"]
+SOURCES = ["csrc/gm_capi.hip", "csrc/gm_calib.hip", "csrc/gm_host_model.cpp", "csrc/gm_mjcf.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics",

@@ -58,10 +58,11 @@ def spawn_draws(seed, gids, episodes, n_objects, position_noise_mm: int = 10, ro
 class BatchedGripperEnv:
     def __init__(self, n_envs: int, object_set: str = "set6_synthetic", settings=None,
                  model_params: ModelParams | None = None, device: int = 0, seed: int = 1234,
-                 env_offset: int = 0, max_episode_steps: int = MAX_EPISODE_STEPS, lib=None):
+                 env_offset: int = 0, max_episode_steps: int = MAX_EPISODE_STEPS, lib=None,
+                 model_blob: ModelBlob | None = None):
         self.lib = lib if lib is not None else load_library()
         self.n_envs = int(n_envs)
-        self.model = ModelBlob(model_params)
+        self.model = model_blob if model_blob is not None else ModelBlob(model_params)
         self.settings = settings if settings is not None else canonical_settings(seed=seed)
         self.cfg = ConfigBlob(self.settings, self.model)
         self.objects = make_object_set(object_set, seed)

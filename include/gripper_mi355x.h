@@ -316,6 +316,19 @@ void gm_config_info(const gm_config* c, int32_t* out);
 void gm_default_model_params(gm_model_params* p);
 int  gm_build_model(const gm_model_params* p, gm_model* out);
 
+/* MJCF.  The reference compiles its task MJCF with mj_loadXML
+ * (mjclass.cpp:377-409), finds everything by the JointSettings / ObjectHandler names
+ * (myfunctions.cpp:176-196, 719-787; objecthandler.cpp:22-133) and reads the gripper
+ * numerics from <custom><numeric> (read_gripper_dimensions, myfunctions.cpp:836-953).
+ * gm_model_to_mjcf writes a model as MJCF with those names (returns the text length;
+ * writes it, NUL-terminated, when cap > length); gm_model_from_mjcf compiles the MJCF
+ * subset it uses (option, default geom solref/solimp, custom numerics, body / joint
+ * slide|hinge|free / inertial / geom plane|sphere|cylinder|box|capsule, contact pairs,
+ * equality joint locks, the "initial pose" keyframe) into a gm_model.  A written model
+ * reads back identical bit for bit.  err (optional): a message on failure. */
+int64_t gm_model_to_mjcf(const gm_model* m, char* buf, int64_t cap);
+int  gm_model_from_mjcf(const char* xml, gm_model* out, char* err, int err_cap);
+
 /* Settings defaults (simsettings.h) and derived configuration
  * (MjClass::configure_settings, mjclass.cpp:97-314). */
 void gm_default_settings(gm_settings* s);

@@ -38,11 +38,13 @@ def pair(gm):
     return envs
 
 
-def test_dpp_row_pgs_matches_general_path(pair):
+def test_dpp_row_pgs_matches_general_path(pair, gm):
     dflt, gen = pair
-    rng = np.random.default_rng(3)
-    for t in range(4):
-        a = rng.uniform(-1, 1, size=(N_ENVS, dflt.n_actions)).astype(np.float32)
+    # the scripted grasp mix drives the batch into finger / object contact, so problems
+    # of every size class occur; every env-step's outputs must agree exactly
+    script = gm.GraspScript(dflt.settings, N_ENVS, seed=11)
+    for t in range(48):
+        a = script.actions(t)
         od, rd, _, _ = dflt.step(a)
         og, rg, _, _ = gen.step(a)
         np.testing.assert_array_equal(od, og)

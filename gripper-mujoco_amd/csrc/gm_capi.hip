@@ -123,7 +123,10 @@ int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
       int par = (p == 1) ? m.dof_base : d - 1;
       if (m.dof_parent[d] != par) { err = "unexpected dof parent"; return GM_E_ARG; }
     }
-  if (m.npair > GM_MAX_PAIR || m.nv > GM_MAX_DOF || T.qadr_obj != m.dof_obj) { err = "model exceeds kernel limits"; return GM_E_RANGE; }
+  if (m.npair > GM_MAX_PAIR || m.npair > NT * gm_pair_batches(T.CL) || m.nv > GM_MAX_DOF || T.qadr_obj != m.dof_obj) {
+    err = "model exceeds kernel limits";
+    return GM_E_RANGE;
+  }
   for (int b = 0; b < GM_MAX_BODY; b++) { T.body_group[b] = -1; T.body_cpos[b] = 0; }
   for (int b = 0; b < m.nbody; b++) {
     T.body_group[b] = m.body_group[b];
@@ -139,7 +142,7 @@ int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
   T.lane_body[49] = T.body_palm;
   T.lane_body[50] = T.body_obj;
   // per-dof constants: the engine-spec H~ diagonal additions and PD gains
-  // (mj_step2 implicit terms and luke::control gains, oracle.c ctrl_gains / step2)
+  // (mj_step2 implicit damping / PD terms and luke::control gains, oracle.c ctrl_gains / step2)
   for (int d = 0; d < m.nv; d++) {
     const int b = m.dof_body[d], j = m.body_jnt[b];
     T.dof_body[d] = b;
@@ -154,12 +157,13 @@ int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
     if (d == m.dof_palm) { kp = m.kp_gripper[2]; kd = m.kd_gripper[2]; tgt = 3; }
     if (d == m.dof_base) { kp = m.kp_base[2]; kd = m.kd_base[2]; tgt = 4; }
     const bool free = m.jnt_type[j] == GM_JNT_FREE;
+    // joint springs are explicit (qfrc_passive), joint damping and the PD gains implicit
     double add = m.jnt_armature[j] + m.timestep * (m.jnt_damping[j] + kd);
-    if (!free) add += m.timestep * m.timestep * (m.jnt_stiffness[j] + kp);
+    if (!free) add += m.timestep * m.timestep * kp;
     T.dof_add[d] = add;
     T.dof_arm[d] = m.jnt_armature[j];
     T.dof_dsum[d] = m.jnt_damping[j] + kd;
-    T.dof_ksum[d] = free ? 0.0 : m.jnt_stiffness[j] + kp;
+    T.dof_ksum[d] = free ? 0.0 : kp;
     T.dof_stiff[d] = free ? 0.0 : m.jnt_stiffness[j];
     T.dof_damp[d] = m.jnt_damping[j];
     T.dof_kp[d] = kp; T.dof_kd[d] = kd; T.dof_target[d] = tgt;

@@ -231,6 +231,14 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
     return (N * EI) / p->finger_length;
   };
 
+  // segment hinge damping (the MJCF's value is absent): 0.24 / N N m s / rad, i.e. in
+  // proportion to the segment length.  With the springs explicit and the damping implicit
+  // (MuJoCo 2.1.5 Euler), this makes find_highest_stable_timestep reproduce the reference's
+  // own measured stable timesteps (rl/juypter/thesis_plots/mujoco_timesteps.csv, the
+  // t = 0.9 mm, w = 28 mm, inertia x50 column) within a few percent for N = 5..10
+  // (tests/test_calibration.py).
+  const double seg_damping = 0.24 / N;
+
   int first_finger_geom = m->ngeom;
   for (int f = 0; f < 3; f++) {
     const double a = f * 2.0 * kPi / 3.0;   // angles[] in myfunctions.cpp:3640
@@ -294,7 +302,7 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
       }
       int bs = B.add_body(parent, GM_GRP_FINGER0 + f, pos, id4, mass, ipos, in);
       double axs[3] = {0, 0, 1};
-      int d = B.add_joint(bs, GM_JNT_HINGE, axs, seg_stiffness(k), 0.05, 0, parent_dof);
+      int d = B.add_joint(bs, GM_JNT_HINGE, axs, seg_stiffness(k), seg_damping, 0, parent_dof);
       if (k == 1) m->dof_seg[f] = d;
       B.add_geom(bs, GM_GEOM_BOX, GM_CLS_FINGER1 + f, gpos, id4, gsz, 1.0);
       if (last) m->body_tip[f] = bs;
@@ -346,7 +354,10 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
 
   // ---- collision pairs: object pairs first (kept first under GM_MAX_CON) ----
   m->npair = 0;
-  auto add_pair = [&](int a, int b) { m->pair_a[m->npair] = a; m->pair_b[m->npair] = b; m->npair++; };
+  auto add_pair = [&](int a, int b) {
+    if (m->npair < GM_MAX_PAIR) { m->pair_a[m->npair] = a; m->pair_b[m->npair] = b; }
+    m->npair++;
+  };
   add_pair(m->geom_ground, m->geom_obj);
   for (int g = first_finger_geom; g < last_finger_geom; g++) add_pair(g, m->geom_obj);
   add_pair(palm_geom, m->geom_obj);

@@ -1256,97 +1256,109 @@ __device__ void write_contact(SharedT<CL>& S, int slot, int g1, int g2, const Hi
   S.cgeom[slot][0] = g1; S.cgeom[slot][1] = g2;
 }
 
+__host__ __device__ constexpr int gm_pair_batches(int CL) { return CL <= 10 ? 1 : 2; }
+
 template <int CL>
 __device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                           bool prof = false) {
   unsigned long long t0 = prof ? clock64() : 0;
   (void)t0;
-  int cnt = 0, kind = 0, g1 = 0, g2 = 0;
-  unsigned hm = 0;   // plane-box / plane-cylinder: the counted corners (pass 2 revisits only these)
-  Hit single;
-  GeomV A, B;
-  CylFrame cf;
-  if (lane < T->npair) {
-    int a = m->pair_a[lane], b = m->pair_b[lane];
-    int ta = (a == T->geom_obj) ? S.s.obj_type : m->geom_type[a];
-    int tb = (b == T->geom_obj) ? S.s.obj_type : m->geom_type[b];
-    canon_pair(a, b, ta, tb, g1, g2);
-    load_geom(S, m, T, g1, A);
-    load_geom(S, m, T, g2, B);
-#ifdef GM_PHASE_SPLIT_COLL
-    PH(15);   // developer split: pair setup + geom poses
-#endif
-    bool pass;
-    if (A.type == GM_GEOM_PLANE) {
-      real nz[3] = {A.R[2], A.R[5], A.R[8]};
-      real dv[3] = {B.c[0] - A.c[0], B.c[1] - A.c[1], B.c[2] - A.c[2]};
-      pass = !(dot3(dv, nz) > B.rbound);
-    } else {
-      real dv[3] = {B.c[0] - A.c[0], B.c[1] - A.c[1], B.c[2] - A.c[2]};
-      real rr = A.rbound + B.rbound;
-      pass = !(dot3(dv, dv) > rr * rr);
-    }
-    if (pass) {
-      if (A.type == GM_GEOM_PLANE) {
-        if (B.type == GM_GEOM_SPHERE) { kind = 1; cnt = plane_sphere(A, B, single); }
-        else if (B.type == GM_GEOM_BOX) {
-          kind = 2;
-          Hit t;
-          for (int i = 0; i < 8 && cnt < 4; i++) {
-            const int ok = plane_box_point(A, B, i, t);
-            hm |= (unsigned)ok << i;
-            cnt += ok;
-          }
-        } else if (B.type == GM_GEOM_CYLINDER) {
-          kind = 3;
-          Hit t;
-          cyl_frame(A, B, cf);
-          for (int i = 0; i < 8 && cnt < 4; i++) {
-            const int ok = plane_cyl_point(A, B, cf, i, t);
-            hm |= (unsigned)ok << i;
-            cnt += ok;
-          }
-        }
-      } else if (A.type == GM_GEOM_SPHERE && B.type == GM_GEOM_BOX) {
-        kind = 1; cnt = sphere_box(A, B, single);
-      } else {
-        kind = 1; cnt = mpr(A, B, (real)m->mpr_tolerance, m->mpr_iterations, single);
-        if (cnt && !(single.dist < 0)) cnt = 0;
-      }
-    }
-  }
-#ifdef GM_PHASE_SPLIT_COLL
-  PH(16);   // developer split: broadphase + narrowphase
-#endif
-  // contact slots: exclusive prefix sum of the per-lane counts (0..4, three bits) from
-  // three ballots -- no LDS round trip
-  int off = 0, total = 0;
+  // one lane per candidate pair, in batches of 64 pairs: the 6 N + 15 pairs fit one batch
+  // for N <= 8 (CL <= 10), N = 9, 10 take two (gm_create checks npair against this);
+  // contacts keep the pair order across batches
+  constexpr int NBATCH = gm_pair_batches(CL);
+  int written = 0;
 #pragma unroll
-  for (int bit = 0; bit < 3; bit++) {
-    const unsigned long long bal = __ballot((cnt >> bit) & 1);
-    off += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u)) << bit;
-    total += __popcll(bal) << bit;
-  }
-  if (cnt > 0) {
-    real mu = fmax(A.friction, B.friction);
-    if (kind == 1) {
-      if (off < GM_MAX_CON) write_contact(S, off, g1, g2, single, mu);
-    } else {
-      Hit t;
-      int w = 0;
-      while (hm) {   // the counted corners in index order, as pass 1 found them
-        const int i = __builtin_ctz(hm);
-        hm &= hm - 1;
-        if (kind == 2) plane_box_point(A, B, i, t);
-        else plane_cyl_point(A, B, cf, i, t);
-        if (off + w < GM_MAX_CON) write_contact(S, off + w, g1, g2, t, mu);
-        w++;
+  for (int bi = 0; bi < NBATCH; bi++) {
+    const int pr = bi * NT + lane;
+    int cnt = 0, kind = 0, g1 = 0, g2 = 0;
+    unsigned hm = 0;   // plane-box / plane-cylinder: the counted corners (pass 2 revisits only these)
+    Hit single;
+    GeomV A, B;
+    CylFrame cf;
+    if (pr < T->npair) {
+      int a = m->pair_a[pr], b = m->pair_b[pr];
+      int ta = (a == T->geom_obj) ? S.s.obj_type : m->geom_type[a];
+      int tb = (b == T->geom_obj) ? S.s.obj_type : m->geom_type[b];
+      canon_pair(a, b, ta, tb, g1, g2);
+      load_geom(S, m, T, g1, A);
+      load_geom(S, m, T, g2, B);
+#ifdef GM_PHASE_SPLIT_COLL
+      PH(15);   // developer split: pair setup + geom poses
+#endif
+      bool pass;
+      if (A.type == GM_GEOM_PLANE) {
+        real nz[3] = {A.R[2], A.R[5], A.R[8]};
+        real dv[3] = {B.c[0] - A.c[0], B.c[1] - A.c[1], B.c[2] - A.c[2]};
+        pass = !(dot3(dv, nz) > B.rbound);
+      } else {
+        real dv[3] = {B.c[0] - A.c[0], B.c[1] - A.c[1], B.c[2] - A.c[2]};
+        real rr = A.rbound + B.rbound;
+        pass = !(dot3(dv, dv) > rr * rr);
+      }
+      if (pass) {
+        if (A.type == GM_GEOM_PLANE) {
+          if (B.type == GM_GEOM_SPHERE) { kind = 1; cnt = plane_sphere(A, B, single); }
+          else if (B.type == GM_GEOM_BOX) {
+            kind = 2;
+            Hit t;
+            for (int i = 0; i < 8 && cnt < 4; i++) {
+              const int ok = plane_box_point(A, B, i, t);
+              hm |= (unsigned)ok << i;
+              cnt += ok;
+            }
+          } else if (B.type == GM_GEOM_CYLINDER) {
+            kind = 3;
+            Hit t;
+            cyl_frame(A, B, cf);
+            for (int i = 0; i < 8 && cnt < 4; i++) {
+              const int ok = plane_cyl_point(A, B, cf, i, t);
+              hm |= (unsigned)ok << i;
+              cnt += ok;
+            }
+          }
+        } else if (A.type == GM_GEOM_SPHERE && B.type == GM_GEOM_BOX) {
+          kind = 1; cnt = sphere_box(A, B, single);
+        } else {
+          kind = 1; cnt = mpr(A, B, (real)m->mpr_tolerance, m->mpr_iterations, single);
+          if (cnt && !(single.dist < 0)) cnt = 0;
+        }
       }
     }
+#ifdef GM_PHASE_SPLIT_COLL
+    PH(16);   // developer split: broadphase + narrowphase
+#endif
+    // contact slots: exclusive prefix sum of the per-lane counts (0..4, three bits) from
+    // three ballots -- no LDS round trip
+    int off = written, total = 0;
+#pragma unroll
+    for (int bit = 0; bit < 3; bit++) {
+      const unsigned long long bal = __ballot((cnt >> bit) & 1);
+      off += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u)) << bit;
+      total += __popcll(bal) << bit;
+    }
+    if (cnt > 0) {
+      real mu = fmax(A.friction, B.friction);
+      if (kind == 1) {
+        if (off < GM_MAX_CON) write_contact(S, off, g1, g2, single, mu);
+      } else {
+        Hit t;
+        int w = 0;
+        while (hm) {   // the counted corners in index order, as pass 1 found them
+          const int i = __builtin_ctz(hm);
+          hm &= hm - 1;
+          if (kind == 2) plane_box_point(A, B, i, t);
+          else plane_cyl_point(A, B, cf, i, t);
+          if (off + w < GM_MAX_CON) write_contact(S, off + w, g1, g2, t, mu);
+          w++;
+        }
+      }
+    }
+    written += total;
   }
   if (lane == 0) {
-    S.ncon = total < GM_MAX_CON ? total : GM_MAX_CON;
-    S.overflow = total > GM_MAX_CON;
+    S.ncon = written < GM_MAX_CON ? written : GM_MAX_CON;
+    S.overflow = written > GM_MAX_CON;
   }
   __syncthreads();
 }
@@ -2311,10 +2323,22 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
 // the env-step epilogue's state), parameters typed with their address spaces so the body
 // issues global loads for the model and LDS instructions for the per-env image rather
 // than generic (flat) accesses that would serialise the two.
+#define GM_AS_CONST __attribute__((address_space(4)))
+// The model and topology pointers arrive in VGPRs (callee ABI); read back as wave-uniform
+// constant-address-space pointers, every access with a uniform index is a scalar load
+// through the scalar cache instead of a vector memory round trip.
+template <typename P>
+__device__ __forceinline__ const GM_AS_CONST P* uniform_const_ptr(const GM_AS_GLOBAL P* p) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return (const GM_AS_CONST P*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
 template <int CL, bool CAL>
 GM_SUBSTEP_ATTR void physics_substep(GM_AS_LDS SharedT<CL>* S_, const GM_AS_GLOBAL gm_model* m_,
                                              const GM_AS_GLOBAL GmTopo* T_, int lane, bool prof) {
-  physics_substep_body<CL, CAL>(*(SharedT<CL>*)S_, (const gm_model*)m_, (const GmTopo*)T_, lane, prof);
+  physics_substep_body<CL, CAL>(*(SharedT<CL>*)S_, (const gm_model*)uniform_const_ptr(m_),
+                                (const GmTopo*)uniform_const_ptr(T_), lane, prof);
 }
 
 // ============================================================ env-step epilogue (lane 0)

@@ -186,7 +186,7 @@ struct GmTopo {
   int32_t dof_grp[GM_MAX_DOF];         // 0..2 finger, 3 palm, 4 base, 5 object
   int32_t dof_p[GM_MAX_DOF];           // chain position (object: 0..5)
   int32_t dof_target[GM_MAX_DOF];      // PD target: 0 none, 1 next.x, 2 next.th, 3 next.z, 4 base z
-  double dof_add[GM_MAX_DOF];          // armature + h (damping + kd) [+ h^2 (stiffness + kp)]
+  double dof_add[GM_MAX_DOF];          // armature + h (damping + kd) [+ h^2 kp]; springs are explicit
   // the same addition's parts, formed per env from its own timestep h (calibration)
   double dof_arm[GM_MAX_DOF], dof_dsum[GM_MAX_DOF], dof_ksum[GM_MAX_DOF];
   double dof_stiff[GM_MAX_DOF];        // 0 for the free joint

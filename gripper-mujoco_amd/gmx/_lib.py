@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libgm.so")
 
 GM_MAX_SEG = 10
 GM_MAX_BODY = 40
-GM_MAX_DOF = 40
+GM_MAX_DOF = 44
 GM_MAX_QPOS = 48
 GM_MAX_GEOM = 40
 GM_MAX_PAIR = 64

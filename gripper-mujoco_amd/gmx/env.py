@@ -11,7 +11,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import (load_library, ModelBlob, ConfigBlob, ModelParams, Spawn, SpawnParams, make_object_set,
+from ._lib import (GM_MAX_DOF, load_library, ModelBlob, ConfigBlob, ModelParams, Spawn, SpawnParams, make_object_set,
                    BINARY_EVENTS, LINEAR_EVENTS)
 from .settings import canonical_settings, MAX_EPISODE_STEPS
 
@@ -301,7 +301,7 @@ class BatchedGripperEnv:
         nefc = np.zeros(n, dtype=np.int32)
         con = np.zeros((n, 15, 16), dtype=np.float64)
         f = np.zeros((n, 64), dtype=np.float64)
-        qacc = np.zeros((n, 40), dtype=np.float64)
+        qacc = np.zeros((n, GM_MAX_DOF), dtype=np.float64)
         w = np.zeros((n, 6), dtype=np.float64)
         d = C.POINTER(C.c_double)
         self._check(self.lib.gm_debug_substep(self._ctx, ncon.ctypes.data_as(C.POINTER(C.c_int32)),

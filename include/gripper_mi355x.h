@@ -28,10 +28,10 @@ extern "C" {
 /* ------------------------------------------------------------------ limits */
 #define GM_MAX_SEG    10      /* finger segment joints N (reference: 5..10)   */
 #define GM_MAX_BODY   40
-#define GM_MAX_DOF    40
+#define GM_MAX_DOF    44      /* 3 (N + 2) + 8 for N = 10                    */
 #define GM_MAX_QPOS   48
 #define GM_MAX_GEOM   40
-#define GM_MAX_PAIR   64      /* one wave lane per collision pair              */
+#define GM_MAX_PAIR   80      /* 6 N + 15 candidate pairs; a lane per pair per 64-pair batch */
 #define GM_MAX_CON    15      /* contacts kept per env per substep             */
 #define GM_MAX_EFC    64      /* constraint rows: 4 per contact + motor locks  */
 #define GM_MAX_LOCK   4       /* prismatic x3 + palm (revolute locks disabled) */

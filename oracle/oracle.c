@@ -5,8 +5,9 @@
  * restatement of MuJoCo 2.1.5's published pipeline (mj_step1 / mj_step2, an
  * un-vendored dependency pinned by reference buildsettings.mk:32) with the
  * deliberate, documented deviations listed in DESIGN.md ("Engine spec"):
- * implicit joint spring+damper in the Euler step, PGS on a pyramidal cone with
- * a fixed sweep count, MPR single-contact for box-box and box-cylinder.
+ * the Euler step keeps MuJoCo's explicit joint springs and implicit joint damping but
+ * folds the PD motor gains in implicitly, PGS on a pyramidal cone with a fixed sweep
+ * count, MPR single-contact for box-box and box-cylinder.
  */
 #define _POSIX_C_SOURCE 200809L
 #include "oracle.h"
@@ -1097,16 +1098,18 @@ static void physics_substep(or_env* e) {
   }
   /* control between step1 and step2 */
   control(e, e->qfrc_act);
-  /* mj_step2: implicit spring/damper mass matrix, smooth accel, constraints */
+  /* mj_step2 (MuJoCo 2.1.5 Euler): joint springs explicit (qfrc_passive above), joint
+   * damping implicit in the factored matrix; the PD motor gains are folded in implicitly
+   * as well (engine spec) */
   double H[NV][NV];
   memcpy(H, e->M, sizeof(H));
   for (int d = 0; d < nv; d++) {
-    /* implicit joint spring/damper and implicit PD motor gains (engine spec) */
+    /* implicit joint damping (mj_Euler) and implicit PD motor gains (engine spec) */
     int j = m->body_jnt[m->dof_body[d]];
     double kp, kd;
     ctrl_gains(m, d, &kp, &kd);
     double add = m->jnt_armature[j] + h * (m->jnt_damping[j] + kd);
-    if (m->jnt_type[j] != GM_JNT_FREE) add += h * h * (m->jnt_stiffness[j] + kp);
+    if (m->jnt_type[j] != GM_JNT_FREE) add += h * h * kp;
     H[d][d] += add;
   }
   factor(e, H);

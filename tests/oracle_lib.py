@@ -10,6 +10,7 @@ import os
 import subprocess
 
 import numpy as np
+from gmx._lib import GM_MAX_DOF  # noqa: E402
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
@@ -221,7 +222,7 @@ def batch_substep(model, cfg, objects, states, threads=None):
     st = np.array(states, dtype=np.uint8, copy=True, order="C")
     n = st.shape[0]
     ncon = np.zeros(n, dtype=np.int32); nefc = np.zeros(n, dtype=np.int32)
-    con = np.zeros((n, 15, 16)); efc = np.zeros((n, 64)); qacc = np.zeros((n, 40)); w = np.zeros((n, 6))
+    con = np.zeros((n, 15, 16)); efc = np.zeros((n, 64)); qacc = np.zeros((n, GM_MAX_DOF)); w = np.zeros((n, 6))
     rc = lib().or_batch_substep(model.ptr, cfg.ptr, C.cast(objects, C.c_void_p), len(objects), n, st.ctypes.data,
                                 ncon.ctypes.data, nefc.ctypes.data, con.ctypes.data, efc.ctypes.data, qacc.ctypes.data,
                                 w.ctypes.data, threads or n_threads())

@@ -3,11 +3,17 @@ find_highest_stable_timestep (mjclass.cpp:4745-4854) and calibrate_simulated_sen
 (4643-4676, tip load via validate_curve_under_force 4023-4105).
 
 The oracle runs the reference's sequential procedure; the device runs every search
-candidate as its own env in one launch and replays the sequence (gm_calibrate).  With
-this engine's implicit spring / damper / PD terms every candidate up to the 20 ms cap is
-stable, so the fine-comb branch of the search is not reached by a physical model here.
+candidate as its own env in one launch and replays the sequence (gm_calibrate).  The
+engine integrates like MuJoCo 2.1.5's Euler (joint springs explicit, joint damping
+implicit), so the search is a real one: it climbs in coarse steps until a candidate
+goes unstable (mjWARN_BADQACC) and combs down in fine steps.  Its result is pinned to
+the reference's own measured stable timesteps (rl/juypter/thesis_plots/
+mujoco_timesteps.csv -> tests/golden/mujoco_timesteps.json).
 """
+import json
 import math
+import os
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import pytest
@@ -115,3 +121,72 @@ def test_gpu_calibration_matches_oracle(world):
 
 def model_timestep(model):
     return model.params.timestep
+
+
+# ---------------------------------------------------------------- the reference's own data
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mujoco_timesteps.json")
+# The operating point of every reference baseline is segment_inertia_scaling = 50
+# (rl/baseline_settings/*.yaml); its three (t, w) columns are pinned to this band.  The
+# segment damping law (0.24 / N, gm_host_model.cpp) is the one invented model numeric the
+# fit sets; the other inertia columns are reported in DESIGN.md, not asserted.
+CSV_BAND = 0.08
+
+
+def search_ms(gm, n_seg, t_mm, w_mm, inertia, device=False):
+    import ctypes as C
+    p = gm.ModelParams()
+    gm.load_library().gm_default_model_params(C.byref(p))
+    p.n_seg, p.finger_thickness, p.finger_width = n_seg, t_mm * 1e-3, w_mm * 1e-3
+    # the search's own start value: the one-time settle before it runs at a stable step
+    p.segment_inertia_scaling, p.timestep = inertia, 1.0e-3
+    model = gm.ModelBlob(p)
+    cfg = gm.ConfigBlob(gm.canonical_settings(noise=False, seed=1), model)
+    objs = gm.make_object_set("set1_synthetic", 1)
+    if device:
+        cal, trace = gm.calibrate(model, cfg, objs, what=gm.CAL_TIMESTEP)
+    else:
+        cal, trace = oracle_lib.calibrate(model, cfg, objs, 1)
+    return cal.search_timestep * 1e3, trace
+
+
+def csv_cases():
+    cols = json.load(open(GOLDEN))["columns"]
+    out = []
+    for name, col in cols.items():
+        kv = dict(x.strip().split("=") for x in name.split(","))
+        if float(kv["inertia"]) != 50.0:
+            continue
+        for n, ms in col.items():
+            out.append((int(n), float(kv["t"]), float(kv["w"]), 50.0, ms))
+    return out
+
+
+def test_timestep_search_reproduces_reference_csv(world):
+    """find_highest_stable_timestep on the oracle for N = 5..10 at the three inertia-x50
+    (t, w) columns of the reference's mujoco_timesteps.csv: every point within 8 %, and
+    the search really combs down (an unstable candidate precedes the answer)."""
+    gm = world[0]
+    cases = csv_cases()
+    assert len(cases) == 18
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:   # ctypes drops the GIL
+        res = list(ex.map(lambda c: search_ms(gm, *c[:4]), cases))
+    worst = 0.0
+    for (n, t, w, i, ref), (ms, trace) in zip(cases, res):
+        assert any(bad for _, bad in trace), f"N={n} t={t} w={w}: no unstable candidate, search degenerate"
+        rel = ms / ref - 1.0
+        worst = max(worst, abs(rel))
+        assert abs(rel) <= CSV_BAND, f"N={n} t={t} w={w}: {ms:.3f} ms vs reference {ref:.3f} ms ({rel:+.1%})"
+    print(f"worst |rel| vs mujoco_timesteps.csv (inertia x50): {worst:.3f}")
+
+
+@pytest.mark.gpu
+def test_gpu_timestep_search_matches_oracle_over_segments(world):
+    """The batched device search equals the oracle's sequential one, candidate for
+    candidate, for N = 5..10 (t = 0.9 mm, w = 28 mm, inertia x50)."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    gm = world[0]
+    for n in range(5, 11):
+        ms_d, tr_d = search_ms(gm, n, 0.9, 28.0, 50.0, device=True)
+        ms_o, tr_o = search_ms(gm, n, 0.9, 28.0, 50.0)
+        assert tr_d == tr_o and ms_d == ms_o, n

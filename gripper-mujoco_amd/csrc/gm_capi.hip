@@ -174,6 +174,51 @@ int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
     if (T.geom_group[g] == GM_GRP_BASE) T.geom_group[g] = -1;
     T.geom_cpos[g] = T.body_cpos[b];
   }
+  // flattened per-lane constants (GmTopo kl_* / dof_* / pr_* / lock_*): the same values
+  // the kernels read through the model's index chains, resolved here once
+  for (int l = 0; l < 64; l++) {
+    const int b = T.lane_body[l];
+    T.kl_type[l] = -1; T.kl_qadr[l] = 0;
+    T.kl_grp[l] = (b >= 0) ? T.body_group[b] : -1;
+    const bool chain = T.kl_grp[l] >= 0 && T.kl_grp[l] <= 3;
+    T.kl_cpos[l] = chain ? T.body_cpos[b] : 0;
+    for (int k = 0; k < 3; k++) { T.kl_pos[l][k] = 0; T.kl_axis[l][k] = 0; }
+    T.kl_quat[l][0] = 1; T.kl_quat[l][1] = T.kl_quat[l][2] = T.kl_quat[l][3] = 0;
+    if (b > 0) {
+      for (int k = 0; k < 3; k++) T.kl_pos[l][k] = m.body_pos[b][k];
+      for (int k = 0; k < 4; k++) T.kl_quat[l][k] = m.body_quat[b][k];
+      const int j = m.body_jnt[b];
+      if (j >= 0) {
+        T.kl_type[l] = m.jnt_type[j];
+        T.kl_qadr[l] = m.jnt_qposadr[j];
+        for (int k = 0; k < 3; k++) T.kl_axis[l][k] = m.jnt_axis[j][k];
+      }
+    }
+  }
+  for (int d = 0; d < m.nv; d++) {
+    const int j = m.body_jnt[m.dof_body[d]];
+    T.dof_jtype[d] = m.jnt_type[j];
+    T.dof_k[d] = d - m.jnt_dofadr[j];
+    for (int k = 0; k < 3; k++) T.dof_axis[d][k] = m.jnt_axis[j][k];
+  }
+  for (int p = 0; p < m.npair; p++) {
+    const int gs[2] = {m.pair_a[p], m.pair_b[p]};
+    for (int s = 0; s < 2; s++) {
+      const int g = gs[s];
+      T.pr_g[p][s] = g;
+      T.pr_type[p][s] = (g == m.geom_obj) ? -1 : m.geom_type[g];
+      T.pr_body[p][s] = m.geom_body[g];
+      for (int k = 0; k < 3; k++) { T.pr_pos[p][s][k] = m.geom_pos[g][k]; T.pr_size[p][s][k] = m.geom_size[g][k]; }
+      for (int k = 0; k < 4; k++) T.pr_quat[p][s][k] = m.geom_quat[g][k];
+      T.pr_rbound[p][s] = m.geom_rbound[g];
+      T.pr_fric[p][s] = m.geom_friction[g];
+    }
+  }
+  for (int k = 0; k < m.nlock; k++) {
+    const int b = m.dof_body[m.lock_dof[k]];
+    T.lock_grp[k] = T.body_group[b];
+    T.lock_cpos[k] = T.body_cpos[b];
+  }
   return GM_OK;
 }
 

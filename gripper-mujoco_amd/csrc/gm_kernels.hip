@@ -280,17 +280,18 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
   // A: local transform of every body (model constants + its joint), lane = body:
   //    slide  p = bpos + R(bquat) axis q,  quat = bquat
   //    hinge  p = bpos,                    quat = bquat (x) (cos q/2, axis sin q/2)
-  real lp[3] = {0, 0, 0}, lq[4] = {1, 0, 0, 0};
+  // every constant below is one load from the lane's flattened GmTopo entry (identity
+  // transform and no joint on lanes without a body)
+  real lp[3], lq[4];
   const int b = T->lane_body[lane];   // scan-lane layout (GmTopo::lane_body)
-  if (b > 0) {
-    ld3(lp, m->body_pos[b]);
-    ld4(lq, m->body_quat[b]);
-    const int j = m->body_jnt[b];
-    if (j >= 0) {
-      const int type = m->jnt_type[j];
-      const real qv = S.s.qpos[m->jnt_qposadr[j]];
+  ld3(lp, T->kl_pos[lane]);
+  ld4(lq, T->kl_quat[lane]);
+  {
+    const int type = T->kl_type[lane];
+    if (type >= 0) {
+      const real qv = S.s.qpos[T->kl_qadr[lane]];
       real ax[3];
-      ld3(ax, m->jnt_axis[j]);
+      ld3(ax, T->kl_axis[lane]);
       if (type == GM_JNT_SLIDE) {
         real R[9], wa[3];
         quat2mat(R, lq);
@@ -324,9 +325,9 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
     quatnorm(bq);
     real bR[9];
     quat2mat(bR, bq);
-    const int grp = (b >= 0) ? T->body_group[b] : -1;
+    const int grp = T->kl_grp[lane];
     const bool chain = grp >= 0 && grp <= 3;
-    const int p = chain ? T->body_cpos[b] : 0;
+    const int p = T->kl_cpos[lane];
 #pragma unroll
     for (int off = 1; off < CL; off <<= 1) {
       real np[3], nq[4];
@@ -407,13 +408,12 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
   // C2: motion subspaces, one lane per dof
   if (lane < T->nv) {
     const int d = lane;
-    const int b = m->dof_body[d];
-    const int j = m->body_jnt[b];
-    const int type = m->jnt_type[j];
+    const int b = T->dof_body[d];
+    const int type = T->dof_jtype[d];
     real* cd = S.cdof[d];
     const real xp[3] = {S.xpos[b][0], S.xpos[b][1], S.xpos[b][2]};
     if (type == GM_JNT_FREE) {
-      const int k = d - m->jnt_dofadr[j];
+      const int k = T->dof_k[d];
       if (k < 3) {
         cd[0] = cd[1] = cd[2] = 0; cd[3] = cd[4] = cd[5] = 0; cd[3 + k] = 1;
       } else {
@@ -426,7 +426,7 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
     } else {
       real ax[3], wa[3], R[9];
       body_R(S, b, R);
-      ld3(ax, m->jnt_axis[j]);
+      ld3(ax, T->dof_axis[d]);
       mulmv3(wa, R, ax);
       if (type == GM_JNT_SLIDE) {
         cd[0] = cd[1] = cd[2] = 0; cd[3] = wa[0]; cd[4] = wa[1]; cd[5] = wa[2];
@@ -498,9 +498,9 @@ __device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const Gm
   cab[3] = -(real)m->gravity[0]; cab[4] = -(real)m->gravity[1]; cab[5] = -(real)m->gravity[2];
 
   const int b = T->lane_body[lane];   // scan-lane layout (GmTopo::lane_body)
-  const int grp = (b >= 0) ? T->body_group[b] : -1;
+  const int grp = T->kl_grp[lane];
   const bool chain = grp >= 0 && grp <= 3;
-  const int p = chain ? T->body_cpos[b] : 0;
+  const int p = T->kl_cpos[lane];
   const int d = chain ? (grp < 3 ? T->dof_f0[grp] + p - 1 : T->dof_palm) : db;
   real cd[6], v[6];
   const real qd = chain ? S.s.qvel[d] : 0.0;
@@ -896,10 +896,11 @@ __device__ void make_frame(real* F, const real* n) {
 
 struct GeomV { int type; real size[3]; real c[3]; real R[9]; real rbound; real friction; };
 
-// world pose of geom g (oracle.c fk, geom part), computed where a pair lane needs it
+// world pose of a geom on body b with local pose (gp, gq) (oracle.c fk, geom part),
+// computed where a pair lane needs it
 template <int CL>
-__device__ __forceinline__ void geom_pose(SharedT<CL>& S, const gm_model* __restrict__ m, int g, real* c, real* Rw) {
-  const int b = m->geom_body[g];
+__device__ __forceinline__ void geom_pose(SharedT<CL>& S, int b, const double* gpos, const double* gquat, real* c,
+                                          real* Rw) {
   real R[9];
   if (b == 0) {
     R[0] = 1; R[1] = 0; R[2] = 0; R[3] = 0; R[4] = 1; R[5] = 0; R[6] = 0; R[7] = 0; R[8] = 1;
@@ -907,11 +908,11 @@ __device__ __forceinline__ void geom_pose(SharedT<CL>& S, const gm_model* __rest
     body_R(S, b, R);
   }
   real gp[3], t[3], gq[4], Rg[9];
-  ld3(gp, m->geom_pos[g]);
+  ld3(gp, gpos);
   mulmv3(t, R, gp);
   const real bp0 = b == 0 ? 0.0 : S.xpos[b][0], bp1 = b == 0 ? 0.0 : S.xpos[b][1], bp2 = b == 0 ? 0.0 : S.xpos[b][2];
   c[0] = bp0 + t[0]; c[1] = bp1 + t[1]; c[2] = bp2 + t[2];
-  ld4(gq, m->geom_quat[g]);
+  ld4(gq, gquat);
   quat2mat(Rg, gq);
 #pragma unroll
   for (int i = 0; i < 3; i++)
@@ -920,19 +921,22 @@ __device__ __forceinline__ void geom_pose(SharedT<CL>& S, const gm_model* __rest
       Rw[3 * i + k] = R[3 * i] * Rg[k] + R[3 * i + 1] * Rg[3 + k] + R[3 * i + 2] * Rg[6 + k];
 }
 
+// geom slot sl (0: pair_a, 1: pair_b) of candidate pair pr from the pair's flattened
+// constants (GmTopo pr_*); the live object's geom reads its type and size from the env
 template <int CL>
-__device__ __forceinline__ void load_geom(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int g, GeomV& G) {
-  if (g == T->geom_obj) {
+__device__ __forceinline__ void load_pair_geom(SharedT<CL>& S, const GmTopo* __restrict__ T, int pr, int sl, GeomV& G) {
+  const int t = T->pr_type[pr][sl];
+  if (t < 0) {
     G.type = S.s.obj_type;
     G.size[0] = S.s.obj_size[0]; G.size[1] = S.s.obj_size[1]; G.size[2] = S.s.obj_size[2];
     G.rbound = S.s.obj_rbound; G.friction = S.s.obj_friction;
   } else {
-    G.type = m->geom_type[g];
-    ld3(G.size, m->geom_size[g]);
-    G.rbound = (real)m->geom_rbound[g];
-    G.friction = (real)m->geom_friction[g];
+    G.type = t;
+    ld3(G.size, T->pr_size[pr][sl]);
+    G.rbound = (real)T->pr_rbound[pr][sl];
+    G.friction = (real)T->pr_fric[pr][sl];
   }
-  geom_pose(S, m, g, G.c, G.R);
+  geom_pose(S, T->pr_body[pr][sl], T->pr_pos[pr][sl], T->pr_quat[pr][sl], G.c, G.R);
 }
 
 // plane-X multi-contact generators: k-th candidate point (returns 0 if none)
@@ -1277,12 +1281,13 @@ __device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const 
     GeomV A, B;
     CylFrame cf;
     if (pr < T->npair) {
-      int a = m->pair_a[pr], b = m->pair_b[pr];
-      int ta = (a == T->geom_obj) ? S.s.obj_type : m->geom_type[a];
-      int tb = (b == T->geom_obj) ? S.s.obj_type : m->geom_type[b];
+      const int a = T->pr_g[pr][0], b = T->pr_g[pr][1];
+      const int ta0 = T->pr_type[pr][0], tb0 = T->pr_type[pr][1];
+      const int ta = ta0 < 0 ? S.s.obj_type : ta0, tb = tb0 < 0 ? S.s.obj_type : tb0;
       canon_pair(a, b, ta, tb, g1, g2);
-      load_geom(S, m, T, g1, A);
-      load_geom(S, m, T, g2, B);
+      const int s1 = (g1 == a) ? 0 : 1;
+      load_pair_geom(S, T, pr, s1, A);
+      load_pair_geom(S, T, pr, 1 - s1, B);
 #ifdef GM_PHASE_SPLIT_COLL
       PH(15);   // developer split: pair setup + geom poses
 #endif
@@ -1595,9 +1600,8 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
       for (k = 0; k < T->nlock; k++) { if (S.s.lock_active[k]) cntl++; if (cntl == lane) break; }
       int d = m->lock_dof[k];
       for (int t = 0; t < CW; t++) J[t] = 0;
-      int b = m->dof_body[d];
-      grp = T->body_group[b];
-      const int cpos = T->body_cpos[b];
+      grp = T->lock_grp[k];
+      const int cpos = T->lock_cpos[k];
 #pragma unroll
       for (int q = 0; q <= CL; q++) J[6 + q] = (q == cpos) ? 1.0 : 0.0;
       pos = S.s.qpos[d] - S.s.lock_q[k];

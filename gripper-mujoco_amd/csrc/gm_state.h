@@ -192,4 +192,22 @@ struct GmTopo {
   double dof_stiff[GM_MAX_DOF];        // 0 for the free joint
   double dof_damp[GM_MAX_DOF];
   double dof_kp[GM_MAX_DOF], dof_kd[GM_MAX_DOF];
+  // Model constants flattened per lane on the host, so a phase issues all of a lane's
+  // loads at one level instead of body -> joint -> qpos chains of dependent loads.
+  // per scan lane (lane_body): the body's joint and local transform
+  int32_t kl_type[64];                 // joint type, -1: no body / welded
+  int32_t kl_qadr[64];                 // the joint's qpos address
+  int32_t kl_grp[64];                  // body group, -1: no body
+  int32_t kl_cpos[64];                 // chain position (fingers / palm), else 0
+  double kl_pos[64][3], kl_quat[64][4], kl_axis[64][3];   // body_pos / body_quat / jnt_axis
+  // per dof: its joint's type, index inside the joint, axis
+  int32_t dof_jtype[GM_MAX_DOF], dof_k[GM_MAX_DOF];
+  double dof_axis[GM_MAX_DOF][3];
+  // per candidate pair, both geoms (slot 0 = pair_a, 1 = pair_b); the live object's
+  // geom has type -1 (its type, size, rbound and friction come from the env state)
+  int32_t pr_g[GM_MAX_PAIR][2], pr_type[GM_MAX_PAIR][2], pr_body[GM_MAX_PAIR][2];
+  double pr_pos[GM_MAX_PAIR][2][3], pr_quat[GM_MAX_PAIR][2][4], pr_size[GM_MAX_PAIR][2][3];
+  double pr_rbound[GM_MAX_PAIR][2], pr_fric[GM_MAX_PAIR][2];
+  // per motor lock: the locked dof's group and chain position
+  int32_t lock_grp[GM_MAX_LOCK], lock_cpos[GM_MAX_LOCK];
 };

@@ -304,7 +304,7 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   hipLaunchKernelGGL(gm_settle_init_kernel, dim3(1), dim3(1), 0, c->stream, c->d_state, c->d_model, c->d_topo, c->d_objs);
   DebugOut dbg{nullptr, nullptr, nullptr, nullptr, nullptr};
   HIPCHK(c, launch_step(c, 1, 1, 1, dbg));
-  HIPCHK(c, hipMemcpyAsync(c->d_eq, reinterpret_cast<char*>(c->d_state) + offsetof(GmEnvState, qpos), sizeof(double) * GM_MAX_QPOS, hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_eq, reinterpret_cast<char*>(c->d_state) + offsetof(GmEnvHot, qpos), sizeof(double) * GM_MAX_QPOS, hipMemcpyDeviceToDevice, c->stream));
   int threads = 256, blocks = (n_envs + threads - 1) / threads;
   hipLaunchKernelGGL(gm_init_envs_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, cfg->s.random_seed,
                      (long long)env_offset, n_envs, c->model.timestep);

@@ -69,7 +69,7 @@ struct __align__(16) SharedT {
   static constexpr int NB = 3 * CL + 4;
   static constexpr int NV = 3 * CL + 8;
   static constexpr int TRIC = (CL + 1) * (CL + 2) / 2;
-  GmEnvState s;
+  GmEnvHot s;                     // the env's state minus its sensor windows
   real lock_pre[GM_MAX_LOCK];     // pre-integration qpos of the lock dofs (weld re-anchoring)
   real qacc[NV], z[NV];   // qacc: smooth, then total acceleration
   real xpos[NB][3];
@@ -105,6 +105,7 @@ struct __align__(16) SharedT {
   int32_t have_forces;
   float gauge_tmp[3];
   unsigned long long tph[GM_NPHASE];
+  GmEnvState* gs;                 // the env's record in HBM (sensor windows read / written there)
 };
 
 // per-phase shader-clock accounting (gm_step_profiled); needs `prof`, `lane`, `t0` in scope
@@ -1981,7 +1982,7 @@ __device__ int g_step_to(GmGrip& g, const GmGrip& t, int num) {
 // update_all: update_stepper / update_constraints (myfunctions.cpp:2129-2284), antiroll
 template <int CL>
 GM_EPI_ATTR void update_all(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
-  GmEnvState& s = S.s;
+  GmEnvHot& s = S.s;
   const bool stepping = s.time > s.last_step_time + m->time_per_step;   // uniform (LDS broadcast)
   int nx = 0, ny = 0, nz = 0;
   if (stepping) {
@@ -2039,19 +2040,22 @@ __device__ double canon_d(uint32_t& s) {
 }
 
 // ---- sensors (mjclass.h:155-241) ----
-__device__ __forceinline__ void ring_add(GmEnvState& s, int st, float x) {
+// SlidingWindow::add / read_element on a ring of GM_RING readings (the window itself
+// lives in the env's HBM record, GmEnvState::ring; its write index in the hot state)
+typedef float (*RingRef)[GM_RING];
+__device__ __forceinline__ void ring_add(GmEnvHot& s, RingRef R, int st, float x) {
   int i = s.ring_i[st] + 1;
   if (i > GM_RING - 1) i = 0;
   s.ring_i[st] = i;
-  s.ring[st][i] = x;
+  R[st][i] = x;
 }
-__device__ __forceinline__ float ring_read(const GmEnvState& s, int st, int n) {
+__device__ __forceinline__ float ring_read(const GmEnvHot& s, RingRef R, int st, int n) {
   int idx = s.ring_i[st] - n;
   while (idx < 0) idx += GM_RING;
-  return s.ring[st][idx];
+  return R[st][idx];
 }
-__device__ __forceinline__ float ring_latest(const GmEnvState& s, int st) {
-  return s.ring_i[st] == -1 ? s.ring[st][0] : s.ring[st][s.ring_i[st]];
+__device__ __forceinline__ float ring_latest(const GmEnvHot& s, RingRef R, int st) {
+  return s.ring_i[st] == -1 ? R[st][0] : R[st][s.ring_i[st]];
 }
 __device__ float s_normalise(const gm_sensor& ss, float v) {
   if (!ss.use_normalisation) return v;
@@ -2060,7 +2064,7 @@ __device__ float s_normalise(const gm_sensor& ss, float v) {
   if (v < -ss.normalise) return -1.0f;
   return v / ss.normalise;
 }
-__device__ float s_noise(GmEnvState& s, const gm_sensor& ss, int slot, float value, int i) {
+__device__ float s_noise(GmEnvHot& s, const gm_sensor& ss, int slot, float value, int i) {
   if (!ss.use_noise) return value;
   const float two_pi = (float)(2.0 * 3.14159265358979323846);
   const float eps = 1.1920928955078125e-07f;
@@ -2080,7 +2084,7 @@ __device__ float s_noise(GmEnvState& s, const gm_sensor& ss, int slot, float val
   else if (value < -1) value = -1;
   return value;
 }
-__device__ int s_ready(GmEnvState& s, const gm_sensor& ss, int slot) {
+__device__ int s_ready(GmEnvHot& s, const gm_sensor& ss, int slot) {
   double tbr = (double)(1 / ss.read_rate);
   if (s.time > s.last_read[slot] + tbr) { s.last_read[slot] = s.time; return 1; }
   return 0;
@@ -2252,40 +2256,41 @@ GM_EPI_ATTR void monitor_sensors(SharedT<CL>& S, const gm_model* __restrict__ m,
   if (bend_ready && lane < 3) S.gauge_tmp[lane] = gauge_reading<CL - 2>(m, &S.s.qpos[T->dof_f0[lane] + 2]);
   __syncthreads();
   if (lane == 0) {
-    GmEnvState& s = S.s;
+    GmEnvHot& s = S.s;
+  RingRef R = S.gs->ring;
     const gm_settings& st = C->s;
     int have = 0;
     if (bend_ready) {
       float g[3] = {S.gauge_tmp[0], S.gauge_tmp[1], S.gauge_tmp[2]};
-      for (int f = 0; f < 3; f++) ring_add(s, ST_SI_GAUGE + f, (float)(g[f] * C->sim_gauge_raw_to_N_factor));
+      for (int f = 0; f < 3; f++) ring_add(s, R, ST_SI_GAUGE + f, (float)(g[f] * C->sim_gauge_raw_to_N_factor));
       for (int f = 0; f < 3; f++) g[f] = s_normalise(st.bending_gauge, g[f]);
       for (int f = 0; f < 3; f++) g[f] = s_noise(s, st.bending_gauge, SL_BEND, g[f], f + 1);
-      for (int f = 0; f < 3; f++) ring_add(s, ST_GAUGE + f, g[f]);
+      for (int f = 0; f < 3; f++) ring_add(s, R, ST_GAUGE + f, g[f]);
     }
     if (s_ready(s, st.axial_gauge, SL_AXIAL)) {
       if (!have) { extract_forces(S, m, T); have = 1; }
       float a[3] = {S.forces[15], S.forces[16], S.forces[17]};
-      for (int f = 0; f < 3; f++) ring_add(s, ST_SI_AXIAL + f, a[f]);
+      for (int f = 0; f < 3; f++) ring_add(s, R, ST_SI_AXIAL + f, a[f]);
       for (int f = 0; f < 3; f++) a[f] = s_normalise(st.axial_gauge, a[f]);
       for (int f = 0; f < 3; f++) a[f] = s_noise(s, st.axial_gauge, SL_AXIAL, a[f], f + 1);
-      for (int f = 0; f < 3; f++) ring_add(s, ST_AXIAL + f, a[f]);
+      for (int f = 0; f < 3; f++) ring_add(s, R, ST_AXIAL + f, a[f]);
     }
     if (s_ready(s, st.palm_sensor, SL_PALM)) {
       if (!have) { extract_forces(S, m, T); have = 1; }
       float p = S.forces[18];
       p *= st.palm_scale_factor;
-      ring_add(s, ST_SI_PALM, p);
+      ring_add(s, R, ST_SI_PALM, p);
       p = s_normalise(st.palm_sensor, p);
       p = s_noise(s, st.palm_sensor, SL_PALM, p, 1);
-      ring_add(s, ST_PALM, p);
+      ring_add(s, R, ST_PALM, p);
     }
     if (s_ready(s, st.wrist_sensor_Z, SL_WRISTZ)) {
       float z = 0.0f;
       z -= st.wrist_sensor_Z.raw_value_offset;
-      ring_add(s, ST_SI_WZ, z);
+      ring_add(s, R, ST_SI_WZ, z);
       z = s_normalise(st.wrist_sensor_Z, z);
       z = s_noise(s, st.wrist_sensor_Z, SL_WRISTZ, z, 1);
-      ring_add(s, ST_WZ, z);
+      ring_add(s, R, ST_WZ, z);
     }
   }
   __syncthreads();
@@ -2354,7 +2359,8 @@ __device__ __forceinline__ float normalise_between(float val, float mn, float mx
 
 template <int CL>
 GM_EPI_ATTR void sense_gripper_state(SharedT<CL>& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C) {
-  GmEnvState& s = S.s;
+  GmEnvHot& s = S.s;
+  RingRef R = S.gs->ring;
   const gm_settings& st = C->s;
   const double* bmn = C->base_min;
   const double* bmx = C->base_max;
@@ -2372,16 +2378,16 @@ GM_EPI_ATTR void sense_gripper_state(SharedT<CL>& S, const gm_model* __restrict_
   by = s_noise(s, st.base_state_sensor_XY, SL_BASEXY, (float)by, 2);
   bz = s_noise(s, st.base_state_sensor_Z, SL_BASEZ, (float)bz, 1);
   byaw = s_noise(s, st.base_state_sensor_yaw, SL_YAW, (float)byaw, 1);
-  ring_add(s, ST_MOTOR + 0, (float)gx);
-  ring_add(s, ST_MOTOR + 1, (float)gy);
-  ring_add(s, ST_MOTOR + 2, (float)gz);
-  ring_add(s, ST_BASE + 0, (float)bx);
-  ring_add(s, ST_BASE + 1, (float)by);
-  ring_add(s, ST_BASE + 2, (float)bz);
-  ring_add(s, ST_YAW, (float)byaw);
+  ring_add(s, R, ST_MOTOR + 0, (float)gx);
+  ring_add(s, R, ST_MOTOR + 1, (float)gy);
+  ring_add(s, R, ST_MOTOR + 2, (float)gz);
+  ring_add(s, R, ST_BASE + 0, (float)bx);
+  ring_add(s, R, ST_BASE + 1, (float)by);
+  ring_add(s, R, ST_BASE + 2, (float)bz);
+  ring_add(s, R, ST_YAW, (float)byaw);
   // MAT cartesian contact points (get_fingerend_and_palm_xyz, myfunctions.cpp:3622-3688)
-  double fsi[3] = {ring_latest(s, ST_SI_GAUGE), ring_latest(s, ST_SI_GAUGE + 1), ring_latest(s, ST_SI_GAUGE + 2)};
-  double psi = ring_latest(s, ST_SI_PALM);
+  double fsi[3] = {ring_latest(s, R, ST_SI_GAUGE), ring_latest(s, R, ST_SI_GAUGE + 1), ring_latest(s, R, ST_SI_GAUGE + 2)};
+  double psi = ring_latest(s, R, ST_SI_PALM);
   double fx = s.end.x, fth = g_calc_th(s.end.x, s.end.y), pz = s.end.z;
   const double PI23 = 3.14159265358979323846 * (2.0 / 3.0);
   double ang[3] = {0.0, PI23, 2 * PI23};
@@ -2397,14 +2403,14 @@ GM_EPI_ATTR void sense_gripper_state(SharedT<CL>& S, const gm_model* __restrict_
     double py = -fin_x * cos(ang[i] + s.base[5]) + s.base[1];
     double pzz = tilted - defl * sin(fth);
     bool on = fabs(fsi[i]) > ft;
-    ring_add(s, ST_CART + 3 * i + 0, (float)(on ? px : 0.0));
-    ring_add(s, ST_CART + 3 * i + 1, (float)(on ? py : 0.0));
-    ring_add(s, ST_CART + 3 * i + 2, (float)(on ? pzz : 0.0));
+    ring_add(s, R, ST_CART + 3 * i + 0, (float)(on ? px : 0.0));
+    ring_add(s, R, ST_CART + 3 * i + 1, (float)(on ? py : 0.0));
+    ring_add(s, R, ST_CART + 3 * i + 2, (float)(on ? pzz : 0.0));
   }
   bool pon = psi > ft;
-  ring_add(s, ST_CART + 9, (float)(pon ? s.base[0] : 0.0));
-  ring_add(s, ST_CART + 10, (float)(pon ? s.base[1] : 0.0));
-  ring_add(s, ST_CART + 11, (float)(pon ? unt + 165e-3 - pz : 0.0));
+  ring_add(s, R, ST_CART + 9, (float)(pon ? s.base[0] : 0.0));
+  ring_add(s, R, ST_CART + 10, (float)(pon ? s.base[1] : 0.0));
+  ring_add(s, R, ST_CART + 11, (float)(pon ? unt + 165e-3 - pz : 0.0));
 }
 
 __device__ float mag3f(const float* v) { return (float)sqrt((double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2]); }
@@ -2413,7 +2419,8 @@ __device__ float mag3f(const float* v) { return (float)sqrt((double)v[0] * v[0] 
 template <int CL>
 GM_EPI_ATTR void update_env(SharedT<CL>& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
                            const GmTopo* __restrict__ T) {
-  GmEnvState& s = S.s;
+  GmEnvHot& s = S.s;
+  RingRef R = S.gs->ring;
   const gm_settings& st = C->s;
   const double ftol = 1e-5;
   extract_forces(S, m, T);
@@ -2440,8 +2447,8 @@ GM_EPI_ATTR void update_env(SharedT<CL>& S, const gm_model* __restrict__ m, cons
   if (F[20] < ga) ga = F[20];
   if (F[21] < ga) ga = F[21];
   float grp_peak_axial = -1 * ga;
-  float g1 = ring_latest(s, ST_SI_GAUGE), g2 = ring_latest(s, ST_SI_GAUGE + 1), g3 = ring_latest(s, ST_SI_GAUGE + 2);
-  float last_palm = ring_latest(s, ST_SI_PALM), last_wrist = ring_latest(s, ST_SI_WZ);
+  float g1 = ring_latest(s, R, ST_SI_GAUGE), g2 = ring_latest(s, R, ST_SI_GAUGE + 1), g3 = ring_latest(s, R, ST_SI_GAUGE + 2);
+  float last_palm = ring_latest(s, R, ST_SI_PALM), last_wrist = ring_latest(s, R, ST_SI_WZ);
   float max_gauge = g1 > g2 ? g1 : g2;
   max_gauge = max_gauge > g3 ? max_gauge : g3;
   float avg_gauge = (float)((1.0 / 3.0) * (g1 + g2 + g3));
@@ -2526,28 +2533,28 @@ GM_EPI_ATTR void update_env(SharedT<CL>& S, const gm_model* __restrict__ m, cons
   }
 }
 
-__device__ int sample_stream(const GmEnvState& s, int mode, int st, const gm_sensor& ss, float* out) {
+__device__ int sample_stream(const GmEnvHot& s, RingRef R, int mode, int st, const gm_sensor& ss, float* out) {
   int prev = ss.prev_steps, rps = ss.readings_per_step, total = ss.total_readings;
   if (mode == GM_SAMPLE_RAW) {
     int n = total - 1;
-    for (int j = n - 1, k = 0; j >= 0; j--, k++) out[k] = ring_read(s, st, j);
+    for (int j = n - 1, k = 0; j >= 0; j--, k++) out[k] = ring_read(s, R, st, j);
     return n;
   }
-  out[0] = ring_read(s, st, total - 1);
+  out[0] = ring_read(s, R, st, total - 1);
   for (int i = 0; i < prev; i++) {
     int first = total - 1 - i * rps;
-    out[2 * i + 2] = ring_read(s, st, first - rps);
+    out[2 * i + 2] = ring_read(s, R, st, first - rps);
     float a = out[2 * i], b = out[2 * i + 2];
     float r;
     if (mode == GM_SAMPLE_CHANGE) r = b - a;
     else if (mode == GM_SAMPLE_AVERAGE) {
       float acc = 0;
-      for (int j = 0; j < rps + 1; j++) acc += ring_read(s, st, first - j);
+      for (int j = 0; j < rps + 1; j++) acc += ring_read(s, R, st, first - j);
       r = acc / (rps + 1);
     } else if (mode == GM_SAMPLE_MEDIAN) {
       float v[GM_RING + 1];
       int nv = rps + 1;
-      for (int j = 0; j < nv; j++) v[j] = ring_read(s, st, first - j);
+      for (int j = 0; j < nv; j++) v[j] = ring_read(s, R, st, first - j);
       for (int x = 1; x < nv; x++) { float t = v[x]; int y = x - 1; while (y >= 0 && v[y] > t) { v[y + 1] = v[y]; y--; } v[y + 1] = t; }
       int hn = nv / 2;
       float med = v[hn];
@@ -2570,27 +2577,27 @@ __device__ int sample_stream(const GmEnvState& s, int mode, int st, const gm_sen
 }
 
 // MjClass::get_observation (mjclass.cpp:1707-1959)
-__device__ int get_obs(const GmEnvState& s, const gm_config* __restrict__ C, float* out) {
+__device__ int get_obs(const GmEnvHot& s, RingRef R, const gm_config* __restrict__ C, float* out) {
   const gm_settings& st = C->s;
   int sf = C->sensor_fcn, tf = C->state_fcn, n = 0;
-  if (st.bending_gauge.in_use) for (int f = 0; f < 3; f++) n += sample_stream(s, sf, ST_GAUGE + f, st.bending_gauge, out + n);
-  if (st.axial_gauge.in_use) for (int f = 0; f < 3; f++) n += sample_stream(s, sf, ST_AXIAL + f, st.axial_gauge, out + n);
-  if (st.palm_sensor.in_use) n += sample_stream(s, sf, ST_PALM, st.palm_sensor, out + n);
+  if (st.bending_gauge.in_use) for (int f = 0; f < 3; f++) n += sample_stream(s, R, sf, ST_GAUGE + f, st.bending_gauge, out + n);
+  if (st.axial_gauge.in_use) for (int f = 0; f < 3; f++) n += sample_stream(s, R, sf, ST_AXIAL + f, st.axial_gauge, out + n);
+  if (st.palm_sensor.in_use) n += sample_stream(s, R, sf, ST_PALM, st.palm_sensor, out + n);
   if (st.wrist_sensor_XY.in_use) {
-    n += sample_stream(s, sf, ST_WX, st.wrist_sensor_XY, out + n);
-    n += sample_stream(s, sf, ST_WY, st.wrist_sensor_XY, out + n);
+    n += sample_stream(s, R, sf, ST_WX, st.wrist_sensor_XY, out + n);
+    n += sample_stream(s, R, sf, ST_WY, st.wrist_sensor_XY, out + n);
   }
-  if (st.wrist_sensor_Z.in_use) n += sample_stream(s, sf, ST_WZ, st.wrist_sensor_XY, out + n);
-  if (st.motor_state_sensor.in_use) for (int k = 0; k < 3; k++) n += sample_stream(s, tf, ST_MOTOR + k, st.motor_state_sensor, out + n);
-  if (st.base_state_sensor_XY.in_use) for (int k = 0; k < 2; k++) n += sample_stream(s, tf, ST_BASE + k, st.base_state_sensor_XY, out + n);
-  if (st.base_state_sensor_Z.in_use) n += sample_stream(s, tf, ST_BASE + 2, st.base_state_sensor_Z, out + n);
-  if (st.base_state_sensor_yaw.in_use) n += sample_stream(s, tf, ST_YAW, st.base_state_sensor_yaw, out + n);
+  if (st.wrist_sensor_Z.in_use) n += sample_stream(s, R, sf, ST_WZ, st.wrist_sensor_XY, out + n);
+  if (st.motor_state_sensor.in_use) for (int k = 0; k < 3; k++) n += sample_stream(s, R, tf, ST_MOTOR + k, st.motor_state_sensor, out + n);
+  if (st.base_state_sensor_XY.in_use) for (int k = 0; k < 2; k++) n += sample_stream(s, R, tf, ST_BASE + k, st.base_state_sensor_XY, out + n);
+  if (st.base_state_sensor_Z.in_use) n += sample_stream(s, R, tf, ST_BASE + 2, st.base_state_sensor_Z, out + n);
+  if (st.base_state_sensor_yaw.in_use) n += sample_stream(s, R, tf, ST_YAW, st.base_state_sensor_yaw, out + n);
   if (st.cartesian_contacts_XYZ.in_use)
-    for (int k = 0; k < 12; k++) n += sample_stream(s, GM_SAMPLE_CHANGE, ST_CART + k, st.cartesian_contacts_XYZ, out + n);
+    for (int k = 0; k < 12; k++) n += sample_stream(s, R, GM_SAMPLE_CHANGE, ST_CART + k, st.cartesian_contacts_XYZ, out + n);
   return n;
 }
 
-GM_EPI_ATTR int is_done(const GmEnvState& s, const gm_config* __restrict__ C) {
+GM_EPI_ATTR int is_done(const GmEnvHot& s, const gm_config* __restrict__ C) {
   const gm_settings& st = C->s;
   int k = 0;
   int done = 0;
@@ -2615,7 +2622,7 @@ __device__ float linear_reward(float val, float mn, float mx, float overshoot) {
   }
   return (val - mn) / (mx - mn);
 }
-__device__ float reward(GmEnvState& s, const gm_config* __restrict__ C) {
+__device__ float reward(GmEnvHot& s, const gm_config* __restrict__ C) {
   const gm_settings& st = C->s;
   float r = 0;
   int k = 0;
@@ -2643,10 +2650,11 @@ __device__ float reward(GmEnvState& s, const gm_config* __restrict__ C) {
 
 // ============================================================ kernels
 template <int CL>
-__device__ __forceinline__ void load_state(SharedT<CL>& S, const GmEnvState* __restrict__ g, int lane) {
+__device__ __forceinline__ void load_state(SharedT<CL>& S, GmEnvState* __restrict__ g, int lane) {
   const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
   uint32_t* dst = reinterpret_cast<uint32_t*>(&S.s);
-  for (int i = lane; i < GM_STATE_WORDS; i += NT) dst[i] = src[i];
+  for (int i = lane; i < GM_HOT_WORDS; i += NT) dst[i] = src[i];
+  S.gs = g;
   __syncthreads();
 }
 template <int CL>
@@ -2654,7 +2662,7 @@ __device__ __forceinline__ void store_state(const SharedT<CL>& S, GmEnvState* __
   __syncthreads();
   const uint32_t* src = reinterpret_cast<const uint32_t*>(&S.s);
   uint32_t* dst = reinterpret_cast<uint32_t*>(g);
-  for (int i = lane; i < GM_STATE_WORDS; i += NT) dst[i] = src[i];
+  for (int i = lane; i < GM_HOT_WORDS; i += NT) dst[i] = src[i];
 }
 
 // mode 0: action_step + obs/done/reward; mode 1: calibrate_reset settle (400 substeps,
@@ -2740,7 +2748,7 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
     PH(19);
     S.s.num_action_steps += 1;
     float* o = obs + (size_t)env * C->n_obs;
-    get_obs(S.s, C, o);
+    get_obs(S.s, S.gs->ring, C, o);
     PH(20);
     int d = is_done(S.s, C);
     float r = reward(S.s, C);
@@ -3242,7 +3250,7 @@ extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, cons
   if (!placed) spawn_object(s, T, objs, n_objects, sp);
   // MjEnv.reset returns _next_observation() of the fresh episode (MjEnv.py:2222-2263):
   // the observation buffer holds the reset env's sensor windows, not the last episode's
-  if (obs) get_obs(s, C, obs + (size_t)env * C->n_obs);
+  if (obs) get_obs(s, s.ring, C, obs + (size_t)env * C->n_obs);
   s.done = 0;
   s.reward = 0;
 }

@@ -9,6 +9,7 @@
 // myfunctions.cpp:464-473 globals, the function-static flags the reference
 // keeps across resets) lives here.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 #include "gripper_mi355x.h"
 
@@ -34,6 +35,7 @@ enum {
 enum { SL_MOTOR = 0, SL_BASEZ, SL_BASEXY, SL_YAW, SL_BEND, SL_AXIAL, SL_PALM, SL_WRISTXY, SL_WRISTZ, SL_CART, SL_N };
 
 typedef struct GmGrip GmGrip;
+typedef struct GmEnvHot GmEnvHot;
 typedef struct GmEnvState GmEnvState;
 typedef struct GmTopo GmTopo;
 
@@ -42,62 +44,85 @@ struct GmGrip {            // luke::Gripper (gripper.h:11-198)
   int32_t sx, sy, sz, pad;
 };
 
-struct GmEnvState {
-  // ---- doubles first (8-byte aligned) ----
-  double time;
-  double last_step_time;
-  GmGrip end, next;
-  double base[6];
-  double last_read[SL_N];
-  double qpos[GM_MAX_QPOS];      // fp64 like MuJoCo's mjtNum (reference physics type)
-  double qvel[GM_MAX_DOF];
-  double lock_q[GM_MAX_LOCK];
-  double start_qpos[7];
-  double obj_size[3];
-  double obj_mass, obj_inertia[3], obj_friction, obj_rbound, obj_rest_z;
-  double dt;                     // this env's timestep (model->opt.timestep; per env for calibration)
-  double tip_force;              // calibration tip load, N (resolve_segment_forces); 0 = off
-  // ---- floats ----
-  float rand_mu[SL_N][3];
-  float ring[GM_NSTREAM][GM_RING];
-  float lev_value[GM_N_LINEAR];
-  float lev_last[GM_N_LINEAR];
-  float cumulative_reward;
-  float grp_peak_lateral;
-  float reward;
-  // ---- ints ----
-  int32_t ring_i[GM_NSTREAM];
-  int32_t bev_value[GM_N_BINARY];
-  int32_t bev_last[GM_N_BINARY];
-  int32_t bev_row[GM_N_BINARY];
-  int32_t bev_abs[GM_N_BINARY];
-  int32_t lev_row[GM_N_LINEAR];
-  int32_t lev_abs[GM_N_LINEAR];
-  int32_t lock_active[GM_MAX_LOCK];
-  int32_t old_x, old_y, old_z;
-  int32_t num_action_steps;
-  int32_t termination_signal_sent;
-  int32_t extra_substeps;        // termination lift substeps pending (2 * S)
-  int32_t obj_type;
-  int32_t obj_index;
-  int32_t done;
-  int32_t overflow;
-  uint32_t rng;
-  int32_t cal_steps;             // calibration launch: substeps to run
-  int32_t badqacc;               // mjWARN_BADQACC: a non-finite or |qacc| > 1e10 was seen
-  int32_t episode;               // resets since gm_create (keys the counter-based spawn draws)
-  int32_t pad_end[2];
-};
+// Everything but the sensor windows: the part of the state the step kernel stages into
+// LDS (GmEnvHot is the leading part of GmEnvState, field for field).
+#define GM_ENV_HOT_FIELDS                                                              \
+  /* ---- doubles first (8-byte aligned) ---- */                                       \
+  double time;                                                                         \
+  double last_step_time;                                                               \
+  GmGrip end, next;                                                                    \
+  double base[6];                                                                      \
+  double last_read[SL_N];                                                              \
+  double qpos[GM_MAX_QPOS];      /* fp64 like MuJoCo's mjtNum (reference physics type) */ \
+  double qvel[GM_MAX_DOF];                                                             \
+  double lock_q[GM_MAX_LOCK];                                                          \
+  double start_qpos[7];                                                                \
+  double obj_size[3];                                                                  \
+  double obj_mass, obj_inertia[3], obj_friction, obj_rbound, obj_rest_z;               \
+  double dt;                     /* this env's timestep (per env for calibration) */   \
+  double tip_force;              /* calibration tip load, N; 0 = off */                \
+  /* ---- floats ---- */                                                               \
+  float rand_mu[SL_N][3];                                                              \
+  float lev_value[GM_N_LINEAR];                                                        \
+  float lev_last[GM_N_LINEAR];                                                         \
+  float cumulative_reward;                                                             \
+  float grp_peak_lateral;                                                              \
+  float reward;                                                                        \
+  /* ---- ints ---- */                                                                 \
+  int32_t ring_i[GM_NSTREAM];                                                          \
+  int32_t bev_value[GM_N_BINARY];                                                      \
+  int32_t bev_last[GM_N_BINARY];                                                       \
+  int32_t bev_row[GM_N_BINARY];                                                        \
+  int32_t bev_abs[GM_N_BINARY];                                                        \
+  int32_t lev_row[GM_N_LINEAR];                                                        \
+  int32_t lev_abs[GM_N_LINEAR];                                                        \
+  int32_t lock_active[GM_MAX_LOCK];                                                    \
+  int32_t old_x, old_y, old_z;                                                         \
+  int32_t num_action_steps;                                                            \
+  int32_t termination_signal_sent;                                                     \
+  int32_t extra_substeps;        /* termination lift substeps pending (2 * S) */       \
+  int32_t obj_type;                                                                    \
+  int32_t obj_index;                                                                   \
+  int32_t done;                                                                        \
+  int32_t overflow;                                                                    \
+  uint32_t rng;                                                                        \
+  int32_t cal_steps;             /* calibration launch: substeps to run */             \
+  int32_t badqacc;               /* mjWARN_BADQACC: non-finite or |qacc| > 1e10 seen */ \
+  int32_t episode;               /* resets since gm_create (keys the spawn draws) */   \
+  int32_t pad_end[GM_HOT_PAD];
 
-// word count for HBM<->LDS sweeps
+// pad words so the hot part is a multiple of 16 B (see GM_STATE_WORDS below)
+#define GM_HOT_PAD 2
+struct GmEnvHot { GM_ENV_HOT_FIELDS };
+
+// The sensor windows (SlidingWindow, mjclass.h:155-241) are the state's tail: GM_RING
+// readings per stream, read and written in place in HBM by the kernel's lane-0 sensor
+// code (once per sensor reading / observation), never staged into LDS.
+#ifdef __cplusplus
+struct GmEnvState : GmEnvHot {
+  float ring[GM_NSTREAM][GM_RING];
+};
+#else
+struct GmEnvState {
+  GM_ENV_HOT_FIELDS
+  float ring[GM_NSTREAM][GM_RING];
+};
+#endif
+
+// word counts for HBM<->LDS sweeps (the hot part) and whole-state clears
+#define GM_HOT_WORDS ((int)(sizeof(GmEnvHot) / 4))
 #define GM_STATE_WORDS ((int)(sizeof(GmEnvState) / 4))
-// a multiple of 16 B: the LDS image (SharedT) places its double arrays right after the
-// state, and 16-byte alignment keeps their paired accesses as single ds_*_b128 ops
+// multiples of 16 B: the LDS image (SharedT) places its double arrays right after the
+// hot state, and 16-byte alignment keeps their paired accesses as single ds_*_b128 ops
 // (an 8-byte shift measured 5-15% slower across every phase)
 #ifdef __cplusplus
+static_assert(sizeof(GmEnvHot) % 16 == 0, "GmEnvHot must be 16-byte padded");
 static_assert(sizeof(GmEnvState) % 16 == 0, "GmEnvState must be 16-byte padded");
+static_assert(sizeof(GmEnvState) == sizeof(GmEnvHot) + sizeof(float) * GM_NSTREAM * GM_RING, "rings follow the hot part");
 #else
+_Static_assert(sizeof(GmEnvHot) % 16 == 0, "GmEnvHot must be 16-byte padded");
 _Static_assert(sizeof(GmEnvState) % 16 == 0, "GmEnvState must be 16-byte padded");
+_Static_assert(offsetof(GmEnvState, ring) == sizeof(GmEnvHot), "rings follow the hot part");
 #endif
 
 // MjEnv._spawn_object's Python-side draws (MjEnv.py:1177-1267: object index, and the

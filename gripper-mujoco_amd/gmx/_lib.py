@@ -19,8 +19,9 @@ GM_MAX_SEG = 10
 GM_MAX_BODY = 40
 GM_MAX_DOF = 44
 GM_MAX_QPOS = 48
+GM_RING = 64
 GM_MAX_GEOM = 40
-GM_MAX_PAIR = 64
+GM_MAX_PAIR = 80
 GM_MAX_CON = 15
 GM_MAX_EFC = 64
 GM_MAX_LOCK = 4
@@ -345,14 +346,16 @@ def env_state_dtype():
         ("lock_q", "f8", GM_MAX_LOCK), ("start_qpos", "f8", 7), ("obj_size", "f8", 3), ("obj_mass", "f8"),
         ("obj_inertia", "f8", 3), ("obj_friction", "f8"), ("obj_rbound", "f8"), ("obj_rest_z", "f8"),
         ("dt", "f8"), ("tip_force", "f8"),
-        ("rand_mu", "f4", (10, 3)), ("ring", "f4", (37, 8)), ("lev_value", "f4", nl), ("lev_last", "f4", nl),
+        ("rand_mu", "f4", (10, 3)), ("lev_value", "f4", nl), ("lev_last", "f4", nl),
         ("cumulative_reward", "f4"), ("grp_peak_lateral", "f4"), ("reward", "f4"),
         ("ring_i", "i4", 37), ("bev_value", "i4", nb), ("bev_last", "i4", nb), ("bev_row", "i4", nb),
         ("bev_abs", "i4", nb), ("lev_row", "i4", nl), ("lev_abs", "i4", nl), ("lock_active", "i4", GM_MAX_LOCK),
         ("old_x", "i4"), ("old_y", "i4"), ("old_z", "i4"), ("num_action_steps", "i4"),
         ("termination_signal_sent", "i4"), ("extra_substeps", "i4"), ("obj_type", "i4"), ("obj_index", "i4"),
         ("done", "i4"), ("overflow", "i4"), ("rng", "u4"), ("cal_steps", "i4"), ("badqacc", "i4"),
-        ("episode", "i4"), ("pad_end", "i4", 2)], align=True)
+        ("episode", "i4"), ("pad_end", "i4", 2),
+        # the sensor windows follow the part the step kernel stages into LDS (GmEnvHot)
+        ("ring", "f4", (37, GM_RING))], align=True)
 
 
 def env_state_view(records):

@@ -36,7 +36,7 @@ extern "C" {
 #define GM_MAX_EFC    64      /* constraint rows: 4 per contact + motor locks  */
 #define GM_MAX_LOCK   4       /* prismatic x3 + palm (revolute locks disabled) */
 #define GM_MAX_OBJSET 64      /* objects in one synthetic object set          */
-#define GM_RING       8       /* sensor ring length (needs 1 + 2*3 = 7)       */
+#define GM_RING       64      /* sensor window: last 64 readings per stream (1 + rps * prev_steps <= 64) */
 #define GM_CHAIN      (GM_MAX_SEG + 2)  /* dofs per finger chain below base   */
 /* MPR support-point tie band: a unit direction whose body-frame component along a box
  * face normal / cylinder axis is below this picks the face centre (see support_geom) */

@@ -94,11 +94,17 @@ def test_configure_derives_substeps(gm, model):
 
 
 def test_configure_rejects_windows_beyond_ring(gm, model):
-    """Sensor windows hold the last GM_RING=8 readings (the reference keeps 1000 but the
-    observation reads at most 1 + readings_per_step * prev_steps); larger requests are
-    rejected loudly, never truncated."""
+    """Sensor windows hold the last GM_RING=64 readings (the reference keeps 1000 but the
+    observation reads at most 1 + readings_per_step * prev_steps); longer histories than
+    the canonical 3 steps run, larger requests are rejected loudly, never truncated."""
     s = gm.canonical_settings(seed=1)
-    s.time_for_action = 0.5       # 5 readings per step x 3 prev steps + 1 = 16 > 8
+    s.time_for_action = 0.5       # 5 readings per step x 3 prev steps + 1 = 16 <= 64
+    gm.ConfigBlob(s, model)
+    s = gm.canonical_settings(seed=1)
+    s.sensor_n_prev_steps = s.state_n_prev_steps = 10
+    cfg = gm.ConfigBlob(s, model)
+    assert cfg.n_obs > gm.ConfigBlob(gm.canonical_settings(seed=1), model).n_obs
+    s.sensor_n_prev_steps = 40    # 2 readings per step x 40 + 1 = 81 > 64
     with pytest.raises(RuntimeError):
         gm.ConfigBlob(s, model)
 

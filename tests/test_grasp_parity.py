@@ -49,8 +49,10 @@ def ol():
     return oracle_lib
 
 
-def rollout(gm, n_envs, object_set, seed, steps=max(SNAPS) + 1, snaps=SNAPS):
+def rollout(gm, n_envs, object_set, seed, steps=max(SNAPS) + 1, snaps=SNAPS, tweak=None):
     settings = gm.canonical_settings(noise=False, seed=seed)
+    if tweak is not None:
+        tweak(settings)
     env = gm.BatchedGripperEnv(n_envs, object_set=object_set, settings=settings, seed=seed)
     env.set_scene_spawn(gm.default_spawn_params(), max_tries=3)
     env.reset()
@@ -161,3 +163,17 @@ def test_c2_single_cylinder_256(gm, ol):
     rep, sub, last = check_config(gm, ol, 256, "cylinder", seed=77)
     i_oc = gm.BINARY_EVENTS.index("object_contact")
     assert (last["bev_abs"][:, i_oc] > 0).sum() > 64
+
+
+def test_long_sensor_history_512(gm, ol):
+    """Histories beyond the canonical 3 steps (sensor and state windows of 8 previous
+    steps, 17 readings deep, on the GM_RING = 64 windows): the observation, events and
+    done flags still match the oracle on grasp states."""
+    def longer(s):
+        s.sensor_n_prev_steps = 8
+        s.state_n_prev_steps = 8
+    env, snaps = rollout(gm, 512, "set6_synthetic", 4321, steps=53, snaps=(12, 30, 52), tweak=longer)
+    assert env.cfg.n_obs > gm.ConfigBlob(gm.canonical_settings(seed=1), env.model).n_obs
+    rep = [compare_step(gm, ol, env, sn) for sn in snaps]
+    print("long history", rep)
+    env.close()

@@ -318,6 +318,6 @@ class BatchedGripperEnv:
 
     def step_profiled(self):
         """One env-step with per-phase shader-clock counters (lane 0, summed over substeps)."""
-        ph = np.zeros((self.n_envs, 24), dtype=np.uint64)
+        ph = np.zeros((self.n_envs, 26), dtype=np.uint64)
         self._check(self.lib.gm_step_profiled(self._ctx, ph.ctypes.data_as(C.POINTER(C.c_uint64))))
         return ph

@@ -10,7 +10,7 @@ env.reset()
 rng = np.random.default_rng(0)
 for t in range(3):
     env.step(rng.uniform(-1, 1, size=(n, env.n_actions)).astype(np.float32))
-tot = np.zeros(24)
+tot = np.zeros(26)
 for t in range(3):
     env.set_action(rng.uniform(-1, 1, size=(n, env.n_actions)).astype(np.float32))
     ph = env.step_profiled().astype(np.float64)

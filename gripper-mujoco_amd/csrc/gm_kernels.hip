@@ -1558,17 +1558,13 @@ __device__ __forceinline__ void pgs_small_sweeps(int iters, real& u0, real& u1, 
 // fixed sweeps over the nchunk live chunks (rows past nefc in the last one are exact no-ops) and
 // return f of constraint `lane` (lanes 0..31).  nBrow is the general path's
 // lane-per-row scaled column (B_j[r] = ARinv_j AR_jr, zero on the diagonal), negated.
+// The sweeps on the replicated layout: nB0 / nB1 hold, in every 16-lane row, the scaled
+// negated Delassus columns of constraints p and p + 16 (p = lane & 15).
 template <bool TWO>
-__device__ __forceinline__ real pgs_small(const real* nBrow, real u, int nl, int nchunk, int iters, int lane) {
-  constexpr int NR = TWO ? 32 : 16;
+__device__ __forceinline__ real pgs_small_solve(const real* nB0, const real* nB1, real u, int nl, int nchunk,
+                                                int iters, int lane) {
   const int p = lane & 15;
   const int a0 = p << 2, a1 = (p + 16) << 2;
-  real nB0[NR], nB1[NR];
-#pragma unroll
-  for (int r = 0; r < NR; r++) {
-    nB0[r] = bperm_f64(a0, nBrow[r]);
-    nB1[r] = TWO ? bperm_f64(a1, nBrow[r]) : 0.0;
-  }
   real u0 = bperm_f64(a0, u);
   real u1 = TWO ? bperm_f64(a1, u) : 0.0;
   const real lb0 = (p < nl) ? -__builtin_inf() : 0.0;   // lock rows come first (nl <= 4)
@@ -1591,6 +1587,177 @@ __device__ __forceinline__ real pgs_small(const real* nBrow, real u, int nl, int
     }
   }
   return (lane < 16) ? f0 : f1;   // constraint `lane` (lanes 0..15: set 0, 16..31: set 1)
+}
+
+// The whole small-problem solve (nefc <= 32) with the Delassus matrix built split across
+// the wave: lane l builds column c of A = Y D^-1 Y^T for K of its rows only -- without
+// TWO (nefc <= 16) c = l & 15 and the rows 4 (l >> 4) .. + 3, with TWO (nefc <= 32)
+// c = l & 31 and the rows 16 (l >> 5) .. + 15 -- instead of every lane building its whole
+// column (4x / 2x fewer dot products per lane).  Each entry is the lane-per-column
+// build's arithmetic operation for operation (same FMA order, same masks), so A is
+// bit-identical; ds_bpermute then gathers the replicated layout (lane p of every 16-lane
+// row: columns p and p + 16), scaled by the column's -ARinv with -0.0 on the diagonal.
+template <int CL, bool TWO>
+__device__ __forceinline__ real pgs_small_split(SharedT<CL>& S, int nefc, real narinv_own, real u, int nl,
+                                                int nchunk, int iters, int lane) {
+  constexpr int K = TWO ? 16 : 4;
+  const int c = TWO ? (lane & 31) : (lane & 15);
+  const int i0 = TWO ? 16 * (lane >> 5) : 4 * (lane >> 4);
+  // Y D^-1 of row c (the Yd phase's arithmetic on the LDS copy of the row); zero past nefc
+  real Ydc[CW - 1];
+  const bool cvalid = c < nefc;
+  const int gc = cvalid ? S.ygrp[c] : -1;
+  if (cvalid) {
+    const real* Yc = S.Y[c];
+    for (int k = 0; k < 6; k++) Ydc[k] = Yc[k] * S.Do[k];
+    Ydc[6] = Yc[6] * S.Dbb;
+    const bool fgrp = gc >= 0 && gc < 3;
+    const real* dsrc = fgrp ? &S.Df[gc][0] : &S.Dp[0];
+#pragma unroll
+    for (int q = 1; q <= CL; q++) {
+      const real v = dsrc[fgrp ? q : 1];
+      const real dv = (fgrp || (gc == 3 && q == 1)) ? v : 1.0;
+      Ydc[6 + q] = Yc[6 + q] * dv;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < CW - 1; k++) Ydc[k] = 0;
+  }
+  const bool gj = gc >= 0 && gc <= 3;
+  const real narinv_c = bperm_f64(c << 2, narinv_own);
+  real Ah[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const int i = i0 + k;
+    // rows past nefc hold stale data in LDS: their products are masked below
+    const real* Yi = S.Y[i];
+    const int gi = S.ygrp[i];
+    real ao = 0, ab = 0, ac = 0;
+#pragma unroll
+    for (int t = 0; t < 6; t++) ao = fma(Ydc[t], Yi[t], ao);
+    ab = Ydc[6] * Yi[6];
+#pragma unroll
+    for (int q = 1; q <= CL; q++) ac = fma(Ydc[6 + q], Yi[6 + q], ac);
+    const bool valid = i < nefc;
+    const bool gi_chain = gi >= 0 && gi <= 3;
+    real acc = ao;
+    acc += (gj && gi_chain) ? ab : 0.0;
+    acc += (gj && gi == gc) ? ac : 0.0;
+    const real a = valid ? acc : 0.0;
+    // -0.0 mirrors the general path's fma(-A[r], d, u) with A[r] = 0 (same zero sign)
+    Ah[k] = (i == c) ? -0.0 : a * narinv_c;
+  }
+  constexpr int NR = TWO ? 32 : 16;
+  const int p = lane & 15;
+  real nB0[NR], nB1[NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    if constexpr (TWO) {
+      nB0[r] = bperm_f64((p + 32 * (r >> 4)) << 2, Ah[r & 15]);
+      nB1[r] = bperm_f64((p + 16 + 32 * (r >> 4)) << 2, Ah[r & 15]);
+    } else {
+      nB0[r] = bperm_f64((((r >> 2) << 4) + p) << 2, Ah[r & 3]);
+      nB1[r] = 0.0;
+    }
+  }
+  return pgs_small_solve<TWO>(nB0, nB1, u, nl, nchunk, iters, lane);
+}
+
+// The general PGS path (nefc > 32, a few percent of envs at C3): lane j builds its whole
+// Delassus column A[:, j] in VGPRs and the sweeps broadcast each row's change with a
+// v_readlane pair.  Outlined: the rare path's unrolled 64-row code stays out of the
+// substep's instruction stream and register allocation (keeping it inline measured 8 %
+// slower on every phase), at the price of a call when it runs.  Y D^-1 of the lane's row
+// is recomputed from the LDS copy of the row, operation for operation as in the Yd phase.
+#define GM_AS_LDS __attribute__((address_space(3)))
+template <int CL>
+__device__ __noinline__ void pgs_general(GM_AS_LDS SharedT<CL>* S_, int nefc, real arinv_l, real u, real lb, int iters,
+                                         int lane) {
+  SharedT<CL>& S = *(SharedT<CL>*)S_;
+  const int grp = (lane < nefc) ? S.ygrp[lane] : -1;
+  real Yd[CW - 1];
+  if (lane < nefc) {
+    const real* J = S.Y[lane];
+    for (int k = 0; k < 6; k++) Yd[k] = J[k] * S.Do[k];
+    Yd[6] = J[6] * S.Dbb;
+    const bool fgrp = grp >= 0 && grp < 3;
+    const real* dsrc = fgrp ? &S.Df[grp][0] : &S.Dp[0];
+#pragma unroll
+    for (int q = 1; q <= CL; q++) {
+      const real v = dsrc[fgrp ? q : 1];
+      const real dv = (fgrp || (grp == 3 && q == 1)) ? v : 1.0;
+      Yd[6 + q] = J[6 + q] * dv;
+    }
+  } else {
+    for (int k = 0; k < CW - 1; k++) Yd[k] = 0;
+  }
+  const bool gj = grp >= 0 && grp <= 3;
+  const int nchunk = (__builtin_amdgcn_readfirstlane(nefc) + 3) >> 2;
+  real f = 0;
+  // Delassus column A[:, lane] = Y D^-1 Y_lane^T, held in this lane's VGPRs
+  real A[GM_MAX_EFC];
+  // rows in chunks of 4 (the PGS granularity): fewer padding rows than chunks of 8
+  const int nchunk_a = (__builtin_amdgcn_readfirstlane(nefc) + 3) >> 2;
+#pragma unroll
+  for (int c = 0; c < GM_MAX_EFC / 4; c++) {
+#pragma unroll
+    for (int rr = 0; rr < 4; rr++) A[c * 4 + rr] = 0;
+    if (c >= nchunk_a) continue;
+#pragma unroll
+    for (int rr = 0; rr < 4; rr++) {
+      const int i = c * 4 + rr;
+      // rows past nefc hold stale data in LDS: their products are masked below
+      const real* Yi = S.Y[i];
+      const int gi = S.ygrp[i];
+      real ao = 0, ab = 0, ac = 0;
+#pragma unroll
+      for (int k = 0; k < 6; k++) ao = fma(Yd[k], Yi[k], ao);
+      ab = Yd[6] * Yi[6];
+#pragma unroll
+      for (int q = 1; q <= CL; q++) ac = fma(Yd[6 + q], Yi[6 + q], ac);
+      const bool valid = i < nefc;
+      const bool gi_chain = gi >= 0 && gi <= 3;
+      real acc = ao;
+      acc += (gj && gi_chain) ? ab : 0.0;
+      acc += (gj && gi == grp) ? ac : 0.0;
+      A[i] = valid ? acc : 0.0;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < GM_MAX_EFC / 4; c++) {
+    if (c >= nchunk) continue;
+#pragma unroll
+    for (int rr = 0; rr < 4; rr++) {
+      unsigned long long onehot;
+      asm volatile("s_bfm_b64 %0, 1, %1" : "=s"(onehot) : "i"(c * 4 + rr));
+      A[c * 4 + rr] = __builtin_amdgcn_inverse_ballot_w64(onehot) ? 0.0 : A[c * 4 + rr] * arinv_l;
+    }
+  }
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int c = 0; c < GM_MAX_EFC / 4; c++) {
+      if (c >= nchunk) continue;
+#pragma unroll
+      for (int rr = 0; rr < 4; rr++) {
+        const int r = c * 4 + rr;
+        const real fn = fmax(u, lb);
+        const real dl = fn - f;
+        const long long bits = __double_as_longlong(dl);
+        const int lo = __builtin_amdgcn_readlane((int)bits, r);
+        const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), r);
+        const real delta = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+        u = fma(-A[r], delta, u);
+        // lane == r as a scalar one-hot mask built in place (s_bfm_b64, no VALU compare);
+        // the opaque asm keeps the compiler from hoisting a 64-entry mask table out of
+        // the sweep loop (it would spill)
+        unsigned long long onehot;
+        asm volatile("s_bfm_b64 %0, 1, %1" : "=s"(onehot) : "i"(r));
+        f = __builtin_amdgcn_inverse_ballot_w64(onehot) ? fn : f;
+      }
+    }
+  }
+  S.efc_f[lane] = (lane < nefc) ? f : 0.0;
+  __syncthreads();
 }
 
 template <int CL, bool CAL>
@@ -1683,36 +1850,6 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
     Ajj += gj ? ab : 0.0;
     Ajj += gj ? ac : 0.0;
   }
-  // Delassus column A[:, lane] = Y D^-1 Y_lane^T, held in this lane's VGPRs
-  real A[GM_MAX_EFC];
-  // rows in chunks of 4 (the PGS granularity): fewer padding rows than chunks of 8
-  const int nchunk_a = (__builtin_amdgcn_readfirstlane(nefc) + 3) >> 2;
-#pragma unroll
-  for (int c = 0; c < GM_MAX_EFC / 4; c++) {
-#pragma unroll
-    for (int rr = 0; rr < 4; rr++) A[c * 4 + rr] = 0;
-    if (c >= nchunk_a) continue;
-#pragma unroll
-    for (int rr = 0; rr < 4; rr++) {
-      const int i = c * 4 + rr;
-      // rows past nefc hold stale data in LDS: their products are masked below
-      const real* Yi = S.Y[i];
-      const int gi = S.ygrp[i];
-      real ao = 0, ab = 0, ac = 0;
-#pragma unroll
-      for (int k = 0; k < 6; k++) ao = fma(Yd[k], Yi[k], ao);
-      ab = Yd[6] * Yi[6];
-#pragma unroll
-      for (int q = 1; q <= CL; q++) ac = fma(Yd[6 + q], Yi[6 + q], ac);
-      const bool valid = i < nefc;
-      const bool gi_chain = gi >= 0 && gi <= 3;
-      real acc = ao;
-      acc += (gj && gi_chain) ? ab : 0.0;
-      acc += (gj && gi == grp) ? ac : 0.0;
-      A[i] = valid ? acc : 0.0;
-    }
-  }
-  PH(13);
   // impedance / reference acceleration (mj_makeImpedance)
   real h = CAL ? S.s.dt : m->timestep;
   real tc = m->solref[0];
@@ -1739,76 +1876,27 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
   const int nchunk = (__builtin_amdgcn_readfirstlane(nefc) + 3) >> 2;
   const real lb = (is_contact || lane >= nefc) ? 0.0 : -__builtin_inf();
   const real arinv_l = (lane < nefc) ? arinv : 0.0;
-  real u = -(((lane < nefc) ? (a0 - aref) : 0.0) * arinv_l);   // f = 0: u = -ARinv b
-  real f = 0;
+  const real u = -(((lane < nefc) ? (a0 - aref) : 0.0) * arinv_l);   // f = 0: u = -ARinv b
 #ifdef GM_PHASE_SPLIT_PGS
   PH(15);   // developer split: impedance, ARinv, u init
 #endif
-#ifdef GM_PGS_GENERAL_ONLY
-  // test build (lib/libgm_pgsgen.so): every problem on the lane-per-row path, so the
-  // GPU tests can hold the DPP-row path against it on identical states
-  if (false) {
-#else
+#ifndef GM_PGS_GENERAL_ONLY
+  // (test build lib/libgm_pgsgen.so: every problem on the lane-per-row path, so the GPU
+  // tests can hold the DPP-row path against it on identical states)
   if (nchunk <= 8) {
-#endif
-    // nefc <= 32: replicated DPP-row layout (see pgs_small_row)
-    const real narinv = -arinv_l;
-    real nBrow[32];
-#pragma unroll
-    for (int r = 0; r < 32; r++) {
-      unsigned long long onehot;
-      asm volatile("s_bfm_b64 %0, 1, %1" : "=s"(onehot) : "i"(r));
-      // -0.0 mirrors the general path's fma(-A[r], d, u) with A[r] = 0 (same zero sign);
-      // A[r] is 0 for every r >= nefc (A build), so rows past nefc stay exact no-ops
-      nBrow[r] = __builtin_amdgcn_inverse_ballot_w64(onehot) ? -0.0 : A[r] * narinv;
-    }
-#ifdef GM_PHASE_SPLIT_PGS
-    PH(16);   // developer split: B scaling
-#endif
+    // nefc <= 32: split Delassus build + replicated DPP-row sweeps (see pgs_small_split)
+    PH(13);
     const int iters = m->pgs_iterations;
-    const real fl = (nchunk <= 4) ? pgs_small<false>(nBrow, u, nl, nchunk, iters, lane)
-                                  : pgs_small<true>(nBrow, u, nl, nchunk, iters, lane);
+    const real fl = (nchunk <= 4) ? pgs_small_split<CL, false>(S, nefc, -arinv_l, u, nl, nchunk, iters, lane)
+                                  : pgs_small_split<CL, true>(S, nefc, -arinv_l, u, nl, nchunk, iters, lane);
     PH(14);
     S.efc_f[lane] = (lane < nefc) ? fl : 0.0;
     __syncthreads();
     return;
   }
-#pragma unroll
-  for (int c = 0; c < GM_MAX_EFC / 4; c++) {
-    if (c >= nchunk) continue;
-#pragma unroll
-    for (int rr = 0; rr < 4; rr++) {
-      unsigned long long onehot;
-      asm volatile("s_bfm_b64 %0, 1, %1" : "=s"(onehot) : "i"(c * 4 + rr));
-      A[c * 4 + rr] = __builtin_amdgcn_inverse_ballot_w64(onehot) ? 0.0 : A[c * 4 + rr] * arinv_l;
-    }
-  }
-  for (int it = 0; it < m->pgs_iterations; it++) {
-#pragma unroll
-    for (int c = 0; c < GM_MAX_EFC / 4; c++) {
-      if (c >= nchunk) continue;
-#pragma unroll
-      for (int rr = 0; rr < 4; rr++) {
-        const int r = c * 4 + rr;
-        const real fn = fmax(u, lb);
-        const real dl = fn - f;
-        const long long bits = __double_as_longlong(dl);
-        const int lo = __builtin_amdgcn_readlane((int)bits, r);
-        const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), r);
-        const real delta = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-        u = fma(-A[r], delta, u);
-        // lane == r as a scalar one-hot mask built in place (s_bfm_b64, no VALU compare);
-        // the opaque asm keeps the compiler from hoisting a 64-entry mask table out of
-        // the sweep loop (it would spill)
-        unsigned long long onehot;
-        asm volatile("s_bfm_b64 %0, 1, %1" : "=s"(onehot) : "i"(r));
-        f = __builtin_amdgcn_inverse_ballot_w64(onehot) ? fn : f;
-      }
-    }
-  }
+#endif
+  pgs_general<CL>((GM_AS_LDS SharedT<CL>*)&S, nefc, arinv_l, u, lb, m->pgs_iterations, lane);
   PH(14);
-  S.efc_f[lane] = (lane < nefc) ? f : 0.0;
-  __syncthreads();
 }
 
 // qacc = qacc_smooth + H^-1 J^T f  via  z = D^-1 Y^T f,  x = L^-1 z
@@ -2341,7 +2429,6 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
 // measured slower -- 12.6 vs 10.0 ms per 4096-env step, the larger body allocates worse
 // (kinematics and the factor roughly doubled); inlining everything spills more still.
 #define GM_AS_GLOBAL __attribute__((address_space(1)))
-#define GM_AS_LDS __attribute__((address_space(3)))
 // One substep, outlined: its own register allocation (the fused kernel around it keeps
 // the env-step epilogue's state), parameters typed with their address spaces so the body
 // issues global loads for the model and LDS instructions for the per-env image rather

@@ -50,7 +50,7 @@ prev = None
 dump = []
 for t in range(8):
     ph = drive(profiled=True).astype(np.float64)
-    dump.append(ph[:, [0, 1, 2, 3, 4, 5, 6, 7, 23, 24, 25]].copy())
+    dump.append(ph.copy())   # all phase slots
     c, nefc, mpr = ph[:, 23], ph[:, 24], ph[:, 25]
     line = (f"step {t}: env cycles mean {c.mean():.3e} p90 {np.percentile(c, 90):.3e} "
             f"max {c.max():.3e}  ideal {c.sum() / slots:.3e}  in-order {makespan(c, range(n)):.3e}  "

@@ -160,3 +160,47 @@ def test_env_offset_shards_reproduce_the_unsharded_batch(setup):
             np.testing.assert_array_equal(th, tf[4 * k:4 * k + 4])
     for e in [full, *halves]:
         e.close()
+
+
+def test_shards_reproduce_the_batch_with_device_spawns_and_autoreset(setup):
+    """The bench's own mode, sharded: objects and poses drawn on the device per episode
+    from the global env id (spawn_into_scene search included), the scripted grasp mix and
+    device auto-reset at a 3-step episode limit.  Two 8-env shards equal the 16-env batch
+    bit for bit (observations, rewards, done flags, returns), so results do not depend on
+    the GPU count nor on the cost-sorted dispatch order each launch uses."""
+    gm, ol = setup
+    import bench
+    def make(n, off):
+        e = gm.BatchedGripperEnv(n, object_set="set6_synthetic", settings=gm.canonical_settings(noise=True, seed=31),
+                                 seed=31, env_offset=off)
+        e.set_scene_spawn(bench.mjenv_spawn_params(gm), max_tries=3)
+        e.reset()
+        return e
+    full = make(16, 0)
+    halves = [make(8, 8 * k) for k in range(2)]
+    for t in range(7):
+        of = full.observation()
+        for k, h in enumerate(halves):
+            np.testing.assert_array_equal(h.observation(), of[8 * k:8 * k + 8], err_msg=f"obs, step {t}")
+        for e in [full, *halves]:
+            a = e.scripted_actions(31)
+            e.set_action(a)
+            e.action_step()
+        rf, df = full.reward_done()
+        for k, h in enumerate(halves):
+            rh, dh = h.reward_done()
+            np.testing.assert_array_equal(rh, rf[8 * k:8 * k + 8])
+            np.testing.assert_array_equal(dh, df[8 * k:8 * k + 8])
+        rets = []
+        for e in [full, *halves]:
+            r = np.full(e.n_envs, np.nan, dtype=np.float32)
+            import torch
+            rt = torch.from_numpy(r).cuda()
+            e.autoreset_device(0, rt.data_ptr(), max_episode_steps=3)
+            torch.cuda.synchronize()
+            rets.append(rt.cpu().numpy())
+        np.testing.assert_array_equal(np.concatenate(rets[1:]), rets[0], err_msg=f"returns, step {t}")
+    st = gm.env_state_view(full.env_states())
+    assert st["episode"].max() >= 2, "no env went through an auto-reset"
+    for e in [full, *halves]:
+        e.close()

@@ -49,11 +49,11 @@ def ol():
     return oracle_lib
 
 
-def rollout(gm, n_envs, object_set, seed, steps=max(SNAPS) + 1, snaps=SNAPS, tweak=None):
+def rollout(gm, n_envs, object_set, seed, steps=max(SNAPS) + 1, snaps=SNAPS, tweak=None, model_params=None):
     settings = gm.canonical_settings(noise=False, seed=seed)
     if tweak is not None:
         tweak(settings)
-    env = gm.BatchedGripperEnv(n_envs, object_set=object_set, settings=settings, seed=seed)
+    env = gm.BatchedGripperEnv(n_envs, object_set=object_set, settings=settings, seed=seed, model_params=model_params)
     env.set_scene_spawn(gm.default_spawn_params(), max_tries=3)
     env.reset()
     script = gm.GraspScript(settings, n_envs, seed=seed)
@@ -176,4 +176,23 @@ def test_long_sensor_history_512(gm, ol):
     assert env.cfg.n_obs > gm.ConfigBlob(gm.canonical_settings(seed=1), env.model).n_obs
     rep = [compare_step(gm, ol, env, sn) for sn in snaps]
     print("long history", rep)
+    env.close()
+
+
+def test_ten_segment_fingers_256(gm, ol):
+    """N = 10 finger segments (the top of the reference's range: 44 dofs, 75 candidate
+    pairs -> the collision phase's second 64-pair batch) at the timestep the search gives
+    for it, on grasp states: same bounds as the canonical N = 8 batch."""
+    import ctypes as C
+    p = gm.ModelParams()
+    gm.load_library().gm_default_model_params(C.byref(p))
+    p.n_seg, p.timestep = 10, 2.1e-3
+    env, snaps = rollout(gm, 256, "set6_synthetic", 99, steps=53, snaps=(20, 38, 52), model_params=p)
+    assert env.model.nv == 44 and env.cfg.sim_steps_per_action == 96
+    rep = [compare_step(gm, ol, env, sn) for sn in snaps]
+    sub = [compare_substep(gm, ol, env, sn) for sn in snaps]
+    print("N=10", rep, sub)
+    last = gm.env_state_view(snaps[-1]["after"])
+    i_oc = gm.BINARY_EVENTS.index("object_contact")
+    assert (last["bev_abs"][:, i_oc] > 0).sum() > 32
     env.close()

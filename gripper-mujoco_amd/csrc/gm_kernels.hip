@@ -2192,6 +2192,20 @@ __device__ int s_ready(GmEnvHot& s, const gm_sensor& ss, int slot) {
   return 0;
 }
 
+// The earliest sim time at which one of monitor_sensors' four sensors becomes ready:
+// s_ready's test is time > last_read + tbr, so time <= min over the sensors of
+// (last_read + tbr) means none is, with the same operands and the same rounding.
+__device__ __forceinline__ double next_sensor_read(const GmEnvHot& s, const gm_settings& st) {
+  const gm_sensor* ss[4] = {&st.bending_gauge, &st.axial_gauge, &st.palm_sensor, &st.wrist_sensor_Z};
+  const int slot[4] = {SL_BEND, SL_AXIAL, SL_PALM, SL_WRISTZ};
+  double t = __builtin_inf();
+  for (int k = 0; k < 4; k++) {
+    const double tk = s.last_read[slot[k]] + (double)(1 / ss[k]->read_rate);
+    t = tk < t ? tk : t;
+  }
+  return t;
+}
+
 // bending gauge: cubic least squares through the N+1 joint points, evaluated at
 // gauge.xpos (read_armadillo_gauge, myfunctions.cpp:2699-2795).  Evaluated in fp64
 // (two reads per env-step at 10 Hz: negligible cost): the fitted value at 50 mm is
@@ -2793,6 +2807,7 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
   const int nsub = settle ? 400 : calib ? S.s.cal_steps : (mode == 2) ? 1 : C->sim_steps_per_action + S.s.extra_substeps;
   // a calibration run starts from a reset's mj_forward pose
   if (calib && lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
+  double next_read = (settle || calib) ? 0.0 : next_sensor_read(S.s, C->s);
   for (int i = 0; i < nsub; i++) {
     if (calib && S.s.tip_force != 0.0 && lane < T->nlock && m->lock_kind[lane] == 0) {
       // apply_segment_force locks the prismatic motors every step (set_constraint,
@@ -2807,7 +2822,12 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
     if (prof && lane == 0) S.tph[22] += t0 - tc;   // whole outlined call (phases 0-8 + call overhead)
     update_all(S, m, T, lane);
     PH(9);
-    if (!settle && !calib) monitor_sensors<CL>(S, m, C, T, lane);
+    // monitor_sensors only on the substeps where a sensor is due (two of ~63 per
+    // env-step at the 10 Hz read rates): the gate is the same comparison s_ready makes
+    if (!settle && !calib && S.s.time > next_read) {
+      monitor_sensors<CL>(S, m, C, T, lane);
+      next_read = next_sensor_read(S.s, C->s);
+    }
     PH(10);
     if (calib && S.s.badqacc) break;   // is_sim_unstable: the reference stops this run
   }

@@ -143,10 +143,54 @@ template <typename T> __device__ __forceinline__ void quatmul(T* r, const T* a, 
   T t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
   r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
 }
+// Correctly rounded fp64 sqrt, reciprocal and quotient on the compiler's own expansions
+// (v_rsq_f64 / v_rcp_f64 and the same FMA refinement steps, operation for operation) minus
+// their range pre-/post-scaling and special-value fix-ups, which cost a third of the
+// instructions and sit on the dependent chain.  Bit-identical to sqrt(x), 1.0 / b and a / b
+// wherever the scaling is inactive: x >= 2^-767 or x == +-0; |a|, |b|, |a / b| roughly
+// inside [2^-900, 2^900] -- every call site's operands are lengths in metres, masses,
+// pivots and contact quantities.  (b == 0 gives NaN where the library gives inf; every
+// caller guards its zero case or is in a blown-up state already.)  -DGM_LIBM_DIVSQRT
+// selects the library operations.
+#ifndef GM_LIBM_DIVSQRT
+__device__ __forceinline__ double sqrt_n(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = y * 0.5;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  double d = fma(-g, g, x);
+  h = fma(h, r, h);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  g = fma(d, h, g);
+  return x == 0.0 ? x : g;
+}
+__device__ __forceinline__ double rcp_refined(double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  double e = fma(-b, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-b, r, 1.0);
+  return fma(r, e, r);
+}
+__device__ __forceinline__ double rcp_n(double b) {
+  const double r = rcp_refined(b);
+  return fma(fma(-b, r, 1.0), r, r);
+}
+__device__ __forceinline__ double div_n(double a, double b) {
+  const double r = rcp_refined(b);
+  const double q = a * r;
+  return fma(fma(-b, q, a), r, q);
+}
+#else
+__device__ __forceinline__ double sqrt_n(double x) { return sqrt(x); }
+__device__ __forceinline__ double rcp_n(double b) { return 1.0 / b; }
+__device__ __forceinline__ double div_n(double a, double b) { return a / b; }
+#endif
+
 __device__ __forceinline__ void quatnorm(real* q) {
-  real n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  real n = sqrt_n(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
   if (n < 1e-15) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
-  const real in = 1.0 / n;
+  const real in = rcp_n(n);
   for (int i = 0; i < 4; i++) q[i] *= in;
 }
 __device__ __forceinline__ void ld3(float* r, const double* a) { r[0] = (float)a[0]; r[1] = (float)a[1]; r[2] = (float)a[2]; }
@@ -759,7 +803,7 @@ __device__ void factor(SharedT<CL>& S, const GmTopo* __restrict__ T, int lane) {
   for (int k = CL; k >= 1; k--) {
     const bool act = fing || (obj && k <= 5);
     const real hkk = row_bcast(h[k], k);
-    const real ihk = 1.0 / hkk;
+    const real ihk = rcp_n(hkk);
     const real a = h[k] * ihk;             // L[k][p] for p < k
     real hk[CL];
 #pragma unroll
@@ -780,7 +824,7 @@ __device__ void factor(SharedT<CL>& S, const GmTopo* __restrict__ T, int lane) {
 #pragma unroll
       for (int j = 0; j < CL; j++) if (j < p) Hs[TRI(p, j)] = h[j];
       Hs[TRI(p, p)] = h[p];
-      S.Df[rowf][p] = 1.0 / h[p];
+      S.Df[rowf][p] = rcp_n(h[p]);
     } else {
       S.bdelta[rowf] = -h[0];   // the base row accumulated -sum_k L[k][0]^2 D_k
     }
@@ -788,17 +832,17 @@ __device__ void factor(SharedT<CL>& S, const GmTopo* __restrict__ T, int lane) {
 #pragma unroll
     for (int j = 0; j < 5; j++) if (j < p) S.Ho[TRI(p, j)] = h[j];
     S.Ho[TRI(p, p)] = h[p];
-    S.Do[p] = 1.0 / h[p];
+    S.Do[p] = rcp_n(h[p]);
   } else if (lane == 63) {
     const real h11 = S.Hp[TRI(1, 1)], h10 = S.Hp[TRI(1, 0)];
-    const real ih = 1.0 / h11;
+    const real ih = rcp_n(h11);
     const real a = h10 * ih;
     S.bdelta[3] = h10 * a;
     S.Hp[TRI(1, 0)] = a;
-    S.Dp[1] = 1.0 / h11;
+    S.Dp[1] = rcp_n(h11);
   }
   __syncthreads();
-  if (lane == 0) S.Dbb = 1.0 / (S.Hbb - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3]));
+  if (lane == 0) S.Dbb = rcp_n(S.Hbb - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3]));
   __syncthreads();
 }
 
@@ -887,7 +931,7 @@ __device__ void make_frame(real* F, const real* n) {
   if (fabs(n[0]) < 0.5) a[0] = 1; else a[1] = 1;
   real d = dot3(a, n);
   real t1[3] = {a[0] - d * n[0], a[1] - d * n[1], a[2] - d * n[2]};
-  const real il = 1.0 / sqrt(dot3(t1, t1));
+  const real il = rcp_n(sqrt_n(dot3(t1, t1)));
   t1[0] *= il; t1[1] *= il; t1[2] *= il;
   real t2[3];
   cross3(t2, n, t1);
@@ -964,9 +1008,9 @@ __device__ __forceinline__ void cyl_frame(const GeomV& P, const GeomV& Cy, CylFr
   F.a[0] = Cy.R[2]; F.a[1] = Cy.R[5]; F.a[2] = Cy.R[8];
   real na = dot3(F.nz, F.a);
   real w[3] = {-F.nz[0] + na * F.a[0], -F.nz[1] + na * F.a[1], -F.nz[2] + na * F.a[2]};
-  real lw = sqrt(dot3(w, w));
+  real lw = sqrt_n(dot3(w, w));
   if (lw < 1e-6) { w[0] = Cy.R[0]; w[1] = Cy.R[3]; w[2] = Cy.R[6]; }
-  else { w[0] /= lw; w[1] /= lw; w[2] /= lw; }
+  else { w[0] = div_n(w[0], lw); w[1] = div_n(w[1], lw); w[2] = div_n(w[2], lw); }
   F.w[0] = w[0]; F.w[1] = w[1]; F.w[2] = w[2];
   cross3(F.axw, F.a, F.w);
 }
@@ -1017,11 +1061,11 @@ __device__ __forceinline__ int sphere_box(const GeomV& Sp, const GeomV& B, Hit& 
   real nl[3], dist, ql[3];
   if (!inside) {
     real df[3] = {cl[0] - q[0], cl[1] - q[1], cl[2] - q[2]};
-    real l = sqrt(dot3(df, df));
+    real l = sqrt_n(dot3(df, df));
     if (l < 1e-12) return 0;
     dist = l - r;
     if (!(dist < 0)) return 0;
-    nl[0] = -df[0] / l; nl[1] = -df[1] / l; nl[2] = -df[2] / l;
+    nl[0] = div_n(-df[0], l); nl[1] = div_n(-df[1], l); nl[2] = div_n(-df[2], l);
     ql[0] = q[0]; ql[1] = q[1]; ql[2] = q[2];
   } else {
     int kmin = 0;
@@ -1060,12 +1104,12 @@ __device__ __forceinline__ void support_geom(const GeomV& G, const real* d, real
   if (G.type == GM_GEOM_BOX) {
     for (int k = 0; k < 3; k++) pl[k] = fabs(dl[k]) < GM_SUPPORT_TIE ? 0.0 : (dl[k] >= 0 ? G.size[k] : -G.size[k]);
   } else if (G.type == GM_GEOM_CYLINDER) {
-    real rr = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
-    if (rr > 1e-12) { pl[0] = G.size[0] * dl[0] / rr; pl[1] = G.size[0] * dl[1] / rr; }
+    real rr = sqrt_n(dl[0] * dl[0] + dl[1] * dl[1]);
+    if (rr > 1e-12) { pl[0] = div_n(G.size[0] * dl[0], rr); pl[1] = div_n(G.size[0] * dl[1], rr); }
     pl[2] = fabs(dl[2]) < GM_SUPPORT_TIE ? 0.0 : (dl[2] >= 0 ? G.size[1] : -G.size[1]);
   } else if (G.type == GM_GEOM_SPHERE) {
-    real l = sqrt(dot3(dl, dl));
-    if (l > 1e-12) { pl[0] = dl[0] * G.size[0] / l; pl[1] = dl[1] * G.size[0] / l; pl[2] = dl[2] * G.size[0] / l; }
+    real l = sqrt_n(dot3(dl, dl));
+    if (l > 1e-12) { pl[0] = div_n(dl[0] * G.size[0], l); pl[1] = div_n(dl[1] * G.size[0], l); pl[2] = div_n(dl[2] * G.size[0], l); }
   }
   mulmv3(out, G.R, pl);
   out[0] += G.c[0]; out[1] += G.c[1]; out[2] += G.c[2];
@@ -1078,8 +1122,8 @@ __device__ __forceinline__ void mpr_support(const GeomV& A, const GeomV& B, cons
 }
 __device__ __forceinline__ int fzero(real x) { return fabs(x) < 1e-12; }
 __device__ __forceinline__ void normalize3(real* d) {
-  real l = sqrt(dot3(d, d));
-  if (l > 0) { real il = 1.0 / l; d[0] *= il; d[1] *= il; d[2] *= il; }
+  real l = sqrt_n(dot3(d, d));
+  if (l > 0) { real il = rcp_n(l); d[0] *= il; d[1] *= il; d[2] *= il; }
 }
 // The simplex vertices are four named values (not an array), conditional vertex copies
 // are per-component selects and every helper is inlined, so the whole MPR state stays in
@@ -1125,19 +1169,19 @@ __device__ __forceinline__ void tri_closest_origin(const real* a, const real* b,
   real d3 = dot3(ab, bp), d4 = dot3(ac, bp);
   if (d3 >= 0 && d4 <= d3) { out[0] = b[0]; out[1] = b[1]; out[2] = b[2]; return; }
   real vc = d1 * d4 - d3 * d2;
-  if (vc <= 0 && d1 >= 0 && d3 <= 0) { real v = d1 / (d1 - d3); for (int k = 0; k < 3; k++) out[k] = a[k] + v * ab[k]; return; }
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) { real v = div_n(d1, d1 - d3); for (int k = 0; k < 3; k++) out[k] = a[k] + v * ab[k]; return; }
   real cp[3] = {-c[0], -c[1], -c[2]};
   real d5 = dot3(ab, cp), d6 = dot3(ac, cp);
   if (d6 >= 0 && d5 <= d6) { out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; return; }
   real vb = d5 * d2 - d1 * d6;
-  if (vb <= 0 && d2 >= 0 && d6 <= 0) { real w = d2 / (d2 - d6); for (int k = 0; k < 3; k++) out[k] = a[k] + w * ac[k]; return; }
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) { real w = div_n(d2, d2 - d6); for (int k = 0; k < 3; k++) out[k] = a[k] + w * ac[k]; return; }
   real va = d3 * d6 - d5 * d4;
   if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
-    real w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    real w = div_n(d4 - d3, (d4 - d3) + (d5 - d6));
     for (int k = 0; k < 3; k++) out[k] = b[k] + w * (c[k] - b[k]);
     return;
   }
-  real den = 1.0 / (va + vb + vc);
+  real den = rcp_n(va + vb + vc);
   real v = vb * den, w = vc * den;
   for (int k = 0; k < 3; k++) out[k] = a[k] + ab[k] * v + ac[k] * w;
 }
@@ -1157,7 +1201,7 @@ __device__ __forceinline__ void mpr_pos(const SV& P0, const SV& P1, const SV& P2
     cross3(t, P1.v, P2.v); b3 = dot3(t, dir);
     sum = b1 + b2 + b3;
   }
-  real inv = 1.0 / sum;
+  real inv = rcp_n(sum);
   real p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
 #pragma unroll
   for (int k = 0; k < 3; k++) {
@@ -1177,11 +1221,11 @@ __device__ __forceinline__ int mpr(const GeomV& A, const GeomV& B, real tol, int
   mpr_support(A, B, d, P1);
   if (dot3(P1.v, d) <= 0) return 0;
   cross3(d, P0.v, P1.v);
-  if (fzero(sqrt(dot3(d, d)))) {
-    real l1 = sqrt(dot3(P1.v, P1.v));
+  if (fzero(sqrt_n(dot3(d, d)))) {
+    real l1 = sqrt_n(dot3(P1.v, P1.v));
     if (fzero(l1)) return 0;
     h.dist = -l1;
-    real il = 1.0 / l1;
+    real il = rcp_n(l1);
     for (int k = 0; k < 3; k++) { h.n[k] = P1.v[k] * il; h.pos[k] = 0.5 * (P1.p1[k] + P1.p2[k]); }
     return 1;
   }
@@ -1233,10 +1277,10 @@ __device__ __forceinline__ int mpr(const GeomV& A, const GeomV& B, real tol, int
     if (reach_tol(P1, P2, P3, v4, d, tol) || it > maxit) {
       real cp[3];
       tri_closest_origin(P1.v, P2.v, P3.v, cp);
-      real depth = sqrt(dot3(cp, cp));
+      real depth = sqrt_n(dot3(cp, cp));
       if (fzero(depth)) return 0;
       h.dist = -depth;
-      real id = 1.0 / depth;
+      real id = rcp_n(depth);
       h.n[0] = cp[0] * id; h.n[1] = cp[1] * id; h.n[2] = cp[2] * id;
       mpr_pos(P0, P1, P2, P3, h.pos);
       return depth > 0;
@@ -1859,9 +1903,9 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
   real Bd = 2.0 / (dmax * tc);
   real imp = impedance(m, pos);
   real aref = -Bd * vel - K * imp * pos;
-  real R = (1 - imp) / imp * Ajj;
+  real R = div_n(1 - imp, imp) * Ajj;
   if (R < 1e-15) R = 1e-15;
-  const real arinv = 1.0 / (Ajj + R);   // mj_solPGS's ARinv
+  const real arinv = rcp_n(Ajj + R);   // mj_solPGS's ARinv
   // projected Gauss-Seidel (mj_solPGS order: rows in sequence, fixed sweeps, cold start).
   // Lane j owns row j and keeps its unclamped Gauss-Seidel target current,
   //   u_j = f_j - ARinv_j (AR f + b)_j,      AR = A + diag(R)  (mj_solPGS's efc_AR),

@@ -1,5 +1,5 @@
 """Developer A/B probe: the bench's steady-state C3 workload for a given segment count N,
-mean kernel time over 10 env-steps.  usage: python tools/quick_bench_n.py N [envs]"""
+mean kernel time over 10 env-steps and a digest of the final fp64 env states.  usage: python tools/quick_bench_n.py N [envs]"""
 import ctypes as C
 import os
 import sys
@@ -40,5 +40,8 @@ ms = []
 for t in range(10):
     drive()
     ms.append(env.last_step_ms())
-print(f"N={N} n={n} lib={os.environ.get('GM_LIB', 'default')} kernel ms mean {np.mean(ms):.3f} min {np.min(ms):.3f}",
-      flush=True)
+import hashlib  # noqa: E402
+st = env.env_states()
+digest = hashlib.sha1(np.ascontiguousarray(st).tobytes()).hexdigest()[:12]   # bit-identity across builds
+print(f"N={N} n={n} lib={os.environ.get('GM_LIB', 'default')} kernel ms mean {np.mean(ms):.3f} min {np.min(ms):.3f}"
+      f" state sha1 {digest}", flush=True)

@@ -808,6 +808,7 @@ __device__ void factor(SharedT<CL>& S, const GmTopo* __restrict__ T, int lane) {
     real hk[CL];
 #pragma unroll
     for (int j = 0; j < k; j++) hk[j] = row_bcast(h[j], k);
+#ifdef GM_FACTOR_BRANCHY
     if (act && p < k) {
 #pragma unroll
       for (int j = 0; j < k; j++) h[j] -= hk[j] * a;
@@ -817,6 +818,18 @@ __device__ void factor(SharedT<CL>& S, const GmTopo* __restrict__ T, int lane) {
 #pragma unroll
       for (int j = 0; j < k; j++) h[j] *= ihk;   // row k of L; the pivot stays in h[k]
     }
+#else
+    // branch-free: rows p < k take h[j] - hk[j] a, the pivot row (p == k) h[j] / hkk (row
+    // k of L; the pivot stays in h[k]), every other lane h[j] - hk[j] 0 == h[j]; one
+    // update shape for all lanes instead of two predicated blocks (whose merges the
+    // compiler resolved with a register copy of the whole row per pivot)
+    const bool upd = act && p < k;
+    const real aa = upd ? a : 0.0;
+    const real sc = (act && p == k) ? ihk : 1.0;
+#pragma unroll
+    for (int j = 0; j < k; j++) h[j] = (h[j] - hk[j] * aa) * sc;
+    h[k] = upd ? a : h[k];
+#endif
   }
   if (fing) {
     if (p >= 1) {
@@ -1510,12 +1523,12 @@ __device__ __forceinline__ real impedance(const gm_model* __restrict__ m, real r
   real dmin = m->solimp[0], dmax = m->solimp[1], width = m->solimp[2];
   real mid = m->solimp[3], pw = m->solimp[4];
   if (dmin == dmax || width <= 1e-15) return dmin;
-  real x = fabs(r) / width;
+  real x = div_n(fabs(r), width);
   if (x >= 1) return dmax;
   if (x <= 0) return dmin;
   real y;
   if (pw == 1) y = x;
-  else if (pw == 2) y = (x <= mid) ? x * x / mid : 1 - (1 - x) * (1 - x) / (1 - mid);   // MuJoCo's default power
+  else if (pw == 2) y = (x <= mid) ? div_n(x * x, mid) : 1 - div_n((1 - x) * (1 - x), 1 - mid);   // MuJoCo's default power
   else if (x <= mid) y = pow(x, pw) / pow(mid, pw - 1);
   else y = 1 - pow(1 - x, pw) / pow(1 - mid, pw - 1);
   return dmin + y * (dmax - dmin);
@@ -1899,8 +1912,8 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
   real tc = m->solref[0];
   if (tc < 2 * h) tc = 2 * h;
   real dr = m->solref[1], dmax = m->solimp[1];
-  real K = 1.0 / (dmax * dmax * tc * tc * dr * dr);
-  real Bd = 2.0 / (dmax * tc);
+  real K = rcp_n(dmax * dmax * tc * tc * dr * dr);
+  real Bd = div_n(2.0, dmax * tc);
   real imp = impedance(m, pos);
   real aref = -Bd * vel - K * imp * pos;
   real R = div_n(1 - imp, imp) * Ajj;

@@ -1,5 +1,5 @@
 """Developer A/B probe: the bench's steady-state C3 workload for a given segment count N,
-mean kernel time over 10 env-steps and a digest of the final fp64 env states.  usage: python tools/quick_bench_n.py N [envs]"""
+mean kernel time over `steps` env-steps (10) and a digest of the final fp64 env states.  usage: python tools/quick_bench_n.py N [envs] [steps]"""
 import ctypes as C
 import os
 import sys
@@ -11,6 +11,7 @@ import bench
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 seed, MAX_EP = 1234, 250
 p = gmx.ModelParams()
 gmx.load_library().gm_default_model_params(C.byref(p))
@@ -37,7 +38,7 @@ for t in range(MAX_EP):
         env.lib.gm_reset(env.ctx, np.ascontiguousarray(m.astype(np.uint8)).ctypes.data_as(C.POINTER(C.c_uint8)), None)
     drive()
 ms = []
-for t in range(10):
+for t in range(steps):
     drive()
     ms.append(env.last_step_ms())
 import hashlib  # noqa: E402

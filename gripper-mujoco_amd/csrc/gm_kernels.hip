@@ -39,16 +39,9 @@
 // `real` is the dynamics type: fp64, MuJoCo's mjtNum.  Kinematics, dynamics, collision
 // geometry and the PGS solve all run in it (see DESIGN.md "Precision").
 typedef double real;
-// Developer switch: GM_SUBSTEP_INLINE inlines the physics substep into the step kernel and
-// outlines the per-substep / per-env-step bookkeeping instead (default: the substep is
-// the outlined unit).
-#ifdef GM_SUBSTEP_INLINE
-#define GM_SUBSTEP_ATTR __device__ __forceinline__
-#define GM_EPI_ATTR __device__ __noinline__
-#else
-#define GM_SUBSTEP_ATTR __device__ __noinline__
+// Env-step bookkeeping (sense / events / obs / done / reward) is inlined into the kernel;
+// the substep loop is one outlined call per env-step (substep_loop).
 #define GM_EPI_ATTR __device__
-#endif
 
 struct DebugOut {
   int32_t* ncon;      // [n_envs]
@@ -2495,10 +2488,6 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
   PH(8);
 }
 
-// Why per substep: outlining the whole substep loop instead (physics + update_all +
-// monitor_sensors in one call, callee-saved registers spilled once per env-step) was
-// measured slower -- 12.6 vs 10.0 ms per 4096-env step, the larger body allocates worse
-// (kinematics and the factor roughly doubled); inlining everything spills more still.
 #define GM_AS_GLOBAL __attribute__((address_space(1)))
 // One substep, outlined: its own register allocation (the fused kernel around it keeps
 // the env-step epilogue's state), parameters typed with their address spaces so the body
@@ -2515,11 +2504,73 @@ __device__ __forceinline__ const GM_AS_CONST P* uniform_const_ptr(const GM_AS_GL
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
   return (const GM_AS_CONST P*)(uintptr_t)(((uint64_t)hi << 32) | lo);
 }
+// The substep loop: one outlined call per env-step.  Its own register allocation (the
+// kernel around it keeps the env-step epilogue's state), parameters typed with their
+// address spaces so the body issues scalar / global loads for the model and LDS
+// instructions for the per-env image rather than generic (flat) accesses.  The
+// callee-saved registers it uses are saved and restored once per env-step (an outlined
+// call per substep paid that, ~92 VGPRs x 64 lanes x 2, every substep: 12 GB of scratch
+// traffic per 4096-env launch).  update_all and monitor_sensors are small calls of
+// their own inside the loop, so the loop body keeps the physics' register allocation.
+// Built with MachineLICM off (gmx/build.py): hoisting the sincos / polynomial constant
+// materialisations out of the loop would hold them live across the whole body and spill.
+template <int CL>
+__device__ __noinline__ void update_all_call(GM_AS_LDS SharedT<CL>* S_, const GM_AS_GLOBAL gm_model* m_,
+                                             const GM_AS_GLOBAL GmTopo* T_, int lane) {
+  update_all<CL>(*(SharedT<CL>*)S_, (const gm_model*)uniform_const_ptr(m_), (const GmTopo*)uniform_const_ptr(T_), lane);
+}
+template <int CL>
+__device__ __noinline__ void monitor_call(GM_AS_LDS SharedT<CL>* S_, const GM_AS_GLOBAL gm_model* m_,
+                                          const GM_AS_GLOBAL gm_config* C_, const GM_AS_GLOBAL GmTopo* T_, int lane) {
+  monitor_sensors<CL>(*(SharedT<CL>*)S_, (const gm_model*)uniform_const_ptr(m_), (const gm_config*)uniform_const_ptr(C_),
+                      (const GmTopo*)uniform_const_ptr(T_), lane);
+}
 template <int CL, bool CAL>
-GM_SUBSTEP_ATTR void physics_substep(GM_AS_LDS SharedT<CL>* S_, const GM_AS_GLOBAL gm_model* m_,
-                                             const GM_AS_GLOBAL GmTopo* T_, int lane, bool prof) {
-  physics_substep_body<CL, CAL>(*(SharedT<CL>*)S_, (const gm_model*)uniform_const_ptr(m_),
-                                (const GmTopo*)uniform_const_ptr(T_), lane, prof);
+__device__ __noinline__ void substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS_GLOBAL gm_model* m_,
+                                          const GM_AS_GLOBAL GmTopo* T_, const GM_AS_GLOBAL gm_config* C_, int lane_in,
+                                          bool prof_in, int nsub_in, bool settle_in) {
+  // nothing but scalars is carried across the loop body: the loop bounds and flags are
+  // wave-uniform (SGPRs), the lane id is recomputed, the next sensor-read time lives in LDS
+  SharedT<CL>& S = *(SharedT<CL>*)S_;
+  const gm_model* m_s = (const gm_model*)uniform_const_ptr(m_);
+  const GmTopo* T_s = (const GmTopo*)uniform_const_ptr(T_);
+  const gm_config* C = (const gm_config*)uniform_const_ptr(C_);
+  const int nsub = __builtin_amdgcn_readfirstlane(nsub_in);
+  const bool prof = __builtin_amdgcn_readfirstlane((int)prof_in) != 0;
+  const bool settle = __builtin_amdgcn_readfirstlane((int)settle_in) != 0;
+  (void)lane_in;
+  __shared__ double next_read;
+  if (__lane_id() == 0) next_read = (settle || CAL) ? 0.0 : next_sensor_read(S.s, C->s);
+  __syncthreads();
+#pragma nounroll
+  for (int i = 0; i < nsub; i++) {
+    // opaque per iteration: nothing derived from the lane id or the model / topology
+    // pointers is hoisted out of the loop and held live across the whole body
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const gm_model* m = m_s;
+    const GmTopo* T = T_s;
+    asm volatile("" : "+s"(m), "+s"(T));
+    if (CAL && S.s.tip_force != 0.0 && lane < T->nlock && m->lock_kind[lane] == 0) {
+      S.s.lock_active[lane] = 1;
+      S.s.lock_q[lane] = S.lock_pre[lane];
+    }
+    const unsigned long long tc = prof ? clock64() : 0;
+    physics_substep_body<CL, CAL>(S, m, T, lane, prof);
+    unsigned long long t0 = prof ? clock64() : 0;
+    if (prof && lane == 0) S.tph[22] += t0 - tc;
+    update_all_call<CL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)(uintptr_t)m,
+                        (const GM_AS_GLOBAL GmTopo*)(uintptr_t)T, __lane_id());
+    PH(9);
+    if (!settle && !CAL && S.s.time > next_read) {
+      monitor_call<CL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)(uintptr_t)m,
+                       (const GM_AS_GLOBAL gm_config*)(uintptr_t)C, (const GM_AS_GLOBAL GmTopo*)(uintptr_t)T, __lane_id());
+      if (__lane_id() == 0) next_read = next_sensor_read(S.s, C->s);
+      __syncthreads();
+    }
+    PH(10);
+    if (CAL && S.s.badqacc) break;
+  }
 }
 
 // ============================================================ env-step epilogue (lane 0)
@@ -2864,30 +2915,8 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
   const int nsub = settle ? 400 : calib ? S.s.cal_steps : (mode == 2) ? 1 : C->sim_steps_per_action + S.s.extra_substeps;
   // a calibration run starts from a reset's mj_forward pose
   if (calib && lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
-  double next_read = (settle || calib) ? 0.0 : next_sensor_read(S.s, C->s);
-  for (int i = 0; i < nsub; i++) {
-    if (calib && S.s.tip_force != 0.0 && lane < T->nlock && m->lock_kind[lane] == 0) {
-      // apply_segment_force locks the prismatic motors every step (set_constraint,
-      // myfunctions.cpp:1679-1685), anchored at the last mj_step1 pose
-      S.s.lock_active[lane] = 1;
-      S.s.lock_q[lane] = S.lock_pre[lane];
-    }
-    const unsigned long long tc = prof ? clock64() : 0;
-    physics_substep<CL, CAL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m, (const GM_AS_GLOBAL GmTopo*)T,
-                        lane, prof);
-    unsigned long long t0 = prof ? clock64() : 0;
-    if (prof && lane == 0) S.tph[22] += t0 - tc;   // whole outlined call (phases 0-8 + call overhead)
-    update_all(S, m, T, lane);
-    PH(9);
-    // monitor_sensors only on the substeps where a sensor is due (two of ~63 per
-    // env-step at the 10 Hz read rates): the gate is the same comparison s_ready makes
-    if (!settle && !calib && S.s.time > next_read) {
-      monitor_sensors<CL>(S, m, C, T, lane);
-      next_read = next_sensor_read(S.s, C->s);
-    }
-    PH(10);
-    if (calib && S.s.badqacc) break;   // is_sim_unstable: the reference stops this run
-  }
+  substep_loop<CL, CAL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m, (const GM_AS_GLOBAL GmTopo*)T,
+                        (const GM_AS_GLOBAL gm_config*)C, lane, prof, nsub, settle);
   if (settle || calib) {
     store_state(S, states + env, lane);
     return;

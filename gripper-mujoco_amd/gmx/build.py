@@ -10,7 +10,10 @@ SOURCES = ["csrc/gm_capi.hip", "csrc/gm_calib.hip", "csrc/gm_host_model.cpp", "c
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics",
-         "-ffp-contract=off"]
+         "-ffp-contract=off",
+         # MachineLICM off: in the outlined substep loop (gm_kernels.hip substep_loop) it
+         # hoists constant materialisations out of the loop and the body then spills
+         "-mllvm", "-disable-machine-licm"]
 
 
 def build(verbose: bool = False, force: bool = False) -> str:

@@ -1553,25 +1553,34 @@ __device__ __forceinline__ real vmax_f64(real a, real b) {
   return r;
 }
 
-// One row r of the small-problem sweep: the general path's arithmetic (f_n = max(u_r, lb_r),
-// d = f_n - f_r, u_j <- fma(-B_j[r], d, u_j), f_r <- f_n), with d broadcast inside each
-// 16-lane row by v_mov_b64_dpp row_newbcast instead of two v_readlane.  (Keeping each
-// row's f_n in a register of its own instead of the select measured a little faster in
-// isolation but pushed the outlined substep past 256 VGPRs; the select stays.)
+// One row R of the small-problem sweep: the general path's arithmetic (f_n = max(u_R, lb_R),
+// d = f_n - f_R, u_j <- fma(-B_j[R], d, u_j), f_R <- f_n).  The row's target u_R is
+// broadcast inside each 16-lane row (v_mov_b64_dpp row_newbcast from lane R & 15), so
+// every lane computes the same f_n and d and keeps the row's force in a register of its
+// own (fr[R], identical on all lanes): the force update is a register rename instead of
+// a one-hot select, 4 VALU per row (5 with TWO) instead of 6 (7).  The dependent chain per
+// row stays bcast -> max -> sub -> fma.  Rows past GM_PGS_FR (only when nefc > GM_PGS_FR)
+// keep the one-hot select on the lane that owns them: replicated registers for all 32
+// rows spill.
+#define GM_PGS_FR 24
 template <int R, bool TWO>
-__device__ __forceinline__ void pgs_small_row(real& u0, real& u1, real& f0, real& f1, real lb0, const real* nB0,
-                                              const real* nB1) {
+__device__ __forceinline__ void pgs_small_row(real& u0, real& u1, real* fr, real& f1, const real* lbr,
+                                              const real* nB0, const real* nB1) {
   constexpr int P = R & 15;
-  // lanes p == P of every 16-lane row: a scalar constant, no VALU compare
-  const bool mine = __builtin_amdgcn_inverse_ballot_w64(0x0001000100010001ull << P);
-  if constexpr (R < 16) {
-    const real fn = vmax_f64(u0, lb0);
-    const real d = row_bcast(fn - f0, P);
+  if constexpr (R < GM_PGS_FR) {
+    // lock rows come first (nl <= 4): rows 0..3 take the lock / contact bound, rows >= 4
+    // are contact edges or padding
+    const real lb = (R < 4) ? lbr[R] : 0.0;
+    const real ub = row_bcast((R < 16) ? u0 : u1, P);
+    const real fn = vmax_f64(ub, lb);
+    const real d = fn - fr[R];
     u0 = fma(nB0[R], d, u0);                  // == fma(-B_j[r], d, u_j): nB = -B exactly
     if constexpr (TWO) u1 = fma(nB1[R], d, u1);
-    f0 = mine ? fn : f0;
+    fr[R] = fn;
   } else {
-    const real fn = vmax_f64(u1, 0.0);      // rows >= 16 are contact edges or padding
+    // lanes p == P of every 16-lane row own row R (set 1): a scalar constant mask
+    const bool mine = __builtin_amdgcn_inverse_ballot_w64(0x0001000100010001ull << P);
+    const real fn = vmax_f64(u1, 0.0);
     const real d = row_bcast(fn - f1, P);
     u1 = fma(nB1[R], d, u1);
     u0 = fma(nB0[R], d, u0);
@@ -1580,63 +1589,77 @@ __device__ __forceinline__ void pgs_small_row(real& u0, real& u1, real& f0, real
 }
 
 template <int C, bool TWO>
-__device__ __forceinline__ void pgs_small_chunk(real& u0, real& u1, real& f0, real& f1, real lb0, const real* nB0,
-                                                const real* nB1) {
-  pgs_small_row<4 * C + 0, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
-  pgs_small_row<4 * C + 1, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
-  pgs_small_row<4 * C + 2, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
-  pgs_small_row<4 * C + 3, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
+__device__ __forceinline__ void pgs_small_chunk(real& u0, real& u1, real* fr, real& f1, const real* lbr,
+                                                const real* nB0, const real* nB1) {
+  pgs_small_row<4 * C + 0, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
+  pgs_small_row<4 * C + 1, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
+  pgs_small_row<4 * C + 2, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
+  pgs_small_row<4 * C + 3, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
 }
 
 template <int NCH, bool TWO>
-__device__ __forceinline__ void pgs_small_sweeps(int iters, real& u0, real& u1, real& f0, real& f1, real lb0,
+__device__ __forceinline__ void pgs_small_sweeps(int iters, real& u0, real& u1, real* fr, real& f1, const real* lbr,
                                                  const real* nB0, const real* nB1) {
   for (int it = 0; it < iters; it++) {
-    pgs_small_chunk<0, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
-    if constexpr (NCH > 1) pgs_small_chunk<1, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
-    if constexpr (NCH > 2) pgs_small_chunk<2, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
-    if constexpr (NCH > 3) pgs_small_chunk<3, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
-    if constexpr (NCH > 4) pgs_small_chunk<4, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
-    if constexpr (NCH > 5) pgs_small_chunk<5, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
-    if constexpr (NCH > 6) pgs_small_chunk<6, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
-    if constexpr (NCH > 7) pgs_small_chunk<7, TWO>(u0, u1, f0, f1, lb0, nB0, nB1);
+    pgs_small_chunk<0, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
+    if constexpr (NCH > 1) pgs_small_chunk<1, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
+    if constexpr (NCH > 2) pgs_small_chunk<2, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
+    if constexpr (NCH > 3) pgs_small_chunk<3, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
+    if constexpr (NCH > 4) pgs_small_chunk<4, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
+    if constexpr (NCH > 5) pgs_small_chunk<5, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
+    if constexpr (NCH > 6) pgs_small_chunk<6, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
+    if constexpr (NCH > 7) pgs_small_chunk<7, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
   }
 }
 
 // The whole small-problem solve: gather the scaled Delassus columns into the replicated
 // layout (lane p of every 16-lane row gets constraint p and, with TWO, p + 16), run the
-// fixed sweeps over the nchunk live chunks (rows past nefc in the last one are exact no-ops) and
-// return f of constraint `lane` (lanes 0..31).  nBrow is the general path's
+// fixed sweeps over the nchunk live chunks (rows past nefc in the last one are exact
+// no-ops: u = f = 0, lb = 0, zero B entries => d = 0) and write the rows' forces to
+// efc_f[0 .. NR-1] (the caller zeroes the rows past nefc).  nBrow is the general path's
 // lane-per-row scaled column (B_j[r] = ARinv_j AR_jr, zero on the diagonal), negated.
 // The sweeps on the replicated layout: nB0 / nB1 hold, in every 16-lane row, the scaled
 // negated Delassus columns of constraints p and p + 16 (p = lane & 15).
 template <bool TWO>
-__device__ __forceinline__ real pgs_small_solve(const real* nB0, const real* nB1, real u, int nl, int nchunk,
-                                                int iters, int lane) {
+__device__ __forceinline__ void pgs_small_solve(const real* nB0, const real* nB1, real u, int nl, int nchunk,
+                                                int iters, int lane, real* efc_f) {
+  constexpr int NR = TWO ? 32 : 16;
+  constexpr int NF = NR < GM_PGS_FR ? NR : GM_PGS_FR;
   const int p = lane & 15;
   const int a0 = p << 2, a1 = (p + 16) << 2;
   real u0 = bperm_f64(a0, u);
   real u1 = TWO ? bperm_f64(a1, u) : 0.0;
-  const real lb0 = (p < nl) ? -__builtin_inf() : 0.0;   // lock rows come first (nl <= 4)
-  real f0 = 0.0, f1 = 0.0;
+  const int nls = __builtin_amdgcn_readfirstlane(nl);
+  real lbr[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) lbr[r] = (r < nls) ? -__builtin_inf() : 0.0;
+  real fr[NF];
+#pragma unroll
+  for (int r = 0; r < NF; r++) fr[r] = 0.0;
+  real f1 = 0.0;   // rows >= GM_PGS_FR: constraint p + 16 of lane p
   // one branch-free sweep body per chunk count (a scalar branch inside the sweep costs
   // more than the padding rows it would skip)
   if constexpr (!TWO) {
     switch (nchunk) {
-      case 1: pgs_small_sweeps<1, false>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
-      case 2: pgs_small_sweeps<2, false>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
-      case 3: pgs_small_sweeps<3, false>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
-      default: pgs_small_sweeps<4, false>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
+      case 1: pgs_small_sweeps<1, false>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
+      case 2: pgs_small_sweeps<2, false>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
+      case 3: pgs_small_sweeps<3, false>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
+      default: pgs_small_sweeps<4, false>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
     }
   } else {
     switch (nchunk) {
-      case 5: pgs_small_sweeps<5, true>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
-      case 6: pgs_small_sweeps<6, true>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
-      case 7: pgs_small_sweeps<7, true>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
-      default: pgs_small_sweeps<8, true>(iters, u0, u1, f0, f1, lb0, nB0, nB1); break;
+      case 5: pgs_small_sweeps<5, true>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
+      case 6: pgs_small_sweeps<6, true>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
+      case 7: pgs_small_sweeps<7, true>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
+      default: pgs_small_sweeps<8, true>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
     }
   }
-  return (lane < 16) ? f0 : f1;   // constraint `lane` (lanes 0..15: set 0, 16..31: set 1)
+  // fr is wave-uniform: lane 0 writes its rows, the owners the rest
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < NF; r++) efc_f[r] = fr[r];
+  }
+  if (TWO && lane >= GM_PGS_FR - 16 && lane < 16) efc_f[lane + 16] = f1;
 }
 
 // The whole small-problem solve (nefc <= 32) with the Delassus matrix built split across
@@ -1648,7 +1671,7 @@ __device__ __forceinline__ real pgs_small_solve(const real* nB0, const real* nB1
 // bit-identical; ds_bpermute then gathers the replicated layout (lane p of every 16-lane
 // row: columns p and p + 16), scaled by the column's -ARinv with -0.0 on the diagonal.
 template <int CL, bool TWO>
-__device__ __forceinline__ real pgs_small_split(SharedT<CL>& S, int nefc, real narinv_own, real u, int nl,
+__device__ __forceinline__ void pgs_small_split(SharedT<CL>& S, int nefc, real narinv_own, real u, int nl,
                                                 int nchunk, int iters, int lane) {
   constexpr int K = TWO ? 16 : 4;
   const int c = TWO ? (lane & 31) : (lane & 15);
@@ -1710,7 +1733,7 @@ __device__ __forceinline__ real pgs_small_split(SharedT<CL>& S, int nefc, real n
       nB1[r] = 0.0;
     }
   }
-  return pgs_small_solve<TWO>(nB0, nB1, u, nl, nchunk, iters, lane);
+  pgs_small_solve<TWO>(nB0, nB1, u, nl, nchunk, iters, lane, S.efc_f);
 }
 
 // The general PGS path (nefc > 32, a few percent of envs at C3): lane j builds its whole
@@ -1937,10 +1960,12 @@ __device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, cons
     // nefc <= 32: split Delassus build + replicated DPP-row sweeps (see pgs_small_split)
     PH(13);
     const int iters = m->pgs_iterations;
-    const real fl = (nchunk <= 4) ? pgs_small_split<CL, false>(S, nefc, -arinv_l, u, nl, nchunk, iters, lane)
-                                  : pgs_small_split<CL, true>(S, nefc, -arinv_l, u, nl, nchunk, iters, lane);
+    // the solve writes rows 0 .. NR-1, then the rows past nefc become +0.0 (the LDS
+    // writes of one wave land in program order)
+    if (nchunk <= 4) pgs_small_split<CL, false>(S, nefc, -arinv_l, u, nl, nchunk, iters, lane);
+    else pgs_small_split<CL, true>(S, nefc, -arinv_l, u, nl, nchunk, iters, lane);
+    if (lane >= nefc) S.efc_f[lane] = 0.0;
     PH(14);
-    S.efc_f[lane] = (lane < nefc) ? fl : 0.0;
     __syncthreads();
     return;
   }

@@ -351,8 +351,8 @@ int gm_reset(gm_ctx* c, const uint8_t* mask, const gm_spawn* spawn) {
     HIPCHK(c, hipMemcpyAsync(c->d_spawn, spawn, sizeof(gm_spawn) * (size_t)c->n_envs, hipMemcpyHostToDevice, c->stream));
     ds = c->d_spawn;
   }
-  int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
-  hipLaunchKernelGGL(gm_reset_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
+  // gm_reset_kernel: one 64-lane workgroup per env
+  hipLaunchKernelGGL(gm_reset_kernel, dim3(c->n_envs), dim3(64), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
                      c->d_topo, c->d_eq, dm, ds, c->d_objs, c->n_objects, c->n_envs, c->d_scene, c->scene_tries,
                      c->d_obs, c->spawn_rand);
   HIPCHK(c, hipGetLastError());
@@ -847,7 +847,7 @@ int gm_autoreset(gm_ctx* c, int max_episode_steps, const gm_spawn* spawn, int sp
   hipLaunchKernelGGL(gm_autoreset_mask_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_done,
                      max_episode_steps, c->d_mask, returns, c->n_envs);
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(gm_reset_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
+  hipLaunchKernelGGL(gm_reset_kernel, dim3(c->n_envs), dim3(64), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
                      c->d_topo, c->d_eq, c->d_mask, ds, c->d_objs, c->n_objects, c->n_envs, c->d_scene,
                      c->scene_tries, c->d_obs, c->spawn_rand);
   HIPCHK(c, hipGetLastError());

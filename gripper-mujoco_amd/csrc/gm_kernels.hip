@@ -3226,11 +3226,14 @@ __device__ uint64_t uid_minstd(uint32_t& st, uint64_t a, uint64_t b) {
   const uint64_t urange = b - a;
   uint64_t ret;
   if (urngrange > urange) {
-    const uint64_t uerange = urange + 1;
-    const uint64_t scaling = urngrange / uerange;
-    const uint64_t past = uerange * scaling;
-    do ret = (uint64_t)lcg_next(st) - 1ull; while (ret >= past);
-    ret /= scaling;
+    // every operand is below 2^31 here: 32-bit division, the same quotients as the
+    // 64-bit ones libstdc++ computes (a 64-bit divide is a long software sequence)
+    const uint32_t uerange = (uint32_t)urange + 1u;
+    const uint32_t scaling = (uint32_t)urngrange / uerange;
+    const uint32_t past = uerange * scaling;
+    uint32_t r32;
+    do r32 = lcg_next(st) - 1u; while (r32 >= past);
+    ret = r32 / scaling;
   } else {
     ret = (uint64_t)lcg_next(st) - 1ull;   // urange == urngrange (grids are far smaller)
   }
@@ -3240,7 +3243,8 @@ __device__ uint64_t uid_minstd(uint32_t& st, uint64_t a, uint64_t b) {
 // (bits/stl_algo.h): when the engine range allows, positions are drawn two at a time
 // from one uniform_int over [0, (k + 1)(k + 2) - 1] (__gen_two_uniform_ints), with a
 // single leading {0, 1} draw for even n.  Shuffling indices permutes exactly like
-// shuffling the elements.
+// shuffling the elements.  (n <= GM_SPAWN_MAX_XY: the pair range and its quotients fit
+// 32 bits.)
 __device__ void shuffle_minstd(uint16_t* v, int n, uint32_t& st) {
   if (n <= 0) return;
   const uint64_t urngrange = 2147483645ull, urange = (uint64_t)n;
@@ -3252,9 +3256,9 @@ __device__ void shuffle_minstd(uint16_t* v, int n, uint32_t& st) {
       i++;
     }
     while (i != n) {
-      const uint64_t r = (uint64_t)i + 1;
-      const uint64_t x = uid_minstd(st, 0, r * (r + 1) - 1);
-      const int p1 = (int)(x / (r + 1)), p2 = (int)(x % (r + 1));
+      const uint32_t r = (uint32_t)i + 1u;
+      const uint32_t x = (uint32_t)uid_minstd(st, 0, (uint64_t)r * (r + 1) - 1);
+      const int p1 = (int)(x / (r + 1u)), p2 = (int)(x % (r + 1u));
       uint16_t t = v[i]; v[i] = v[p1]; v[p1] = t;
       i++;
       t = v[i]; v[i] = v[p2]; v[p2] = t;
@@ -3413,22 +3417,30 @@ extern "C" __global__ void gm_autoreset_mask_kernel(const GmEnvState* __restrict
 // MjClass::reset (mjclass.cpp:434-486) -> luke::reset / calibrate_reset (non-first call),
 // configure_settings RNG draws, random_base_Z_movement, then spawn_object.
 #ifndef GM_CAL_TU   // env-step translation unit only
-extern "C" __global__ void gm_reset_kernel(GmEnvState* __restrict__ states, const gm_model* __restrict__ m,
-                                           const gm_config* __restrict__ C, const GmTopo* __restrict__ T,
-                                           const double* __restrict__ eq_qpos, const uint8_t* __restrict__ mask,
-                                           const gm_spawn* __restrict__ spawn, const gm_object* __restrict__ objs,
-                                           int n_objects, int n_envs, const gm_spawn_params* __restrict__ scene,
-                                           int scene_tries, float* __restrict__ obs, GmSpawnRand sr) {
-  int env = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per env (grid = n_envs workgroups of 64; unmasked envs exit at once): the
+// wave clears the 11.6 KB record with coalesced 16-byte stores, lane 0 then runs the
+// reference's serial reset (RNG draws, spawn search) on it.
+extern "C" __global__ __launch_bounds__(64) void gm_reset_kernel(
+    GmEnvState* __restrict__ states, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
+    const GmTopo* __restrict__ T, const double* __restrict__ eq_qpos, const uint8_t* __restrict__ mask,
+    const gm_spawn* __restrict__ spawn, const gm_object* __restrict__ objs, int n_objects, int n_envs,
+    const gm_spawn_params* __restrict__ scene, int scene_tries, float* __restrict__ obs, GmSpawnRand sr) {
+  const int env = blockIdx.x;
   if (env >= n_envs) return;
   if (mask && !mask[env]) return;
   GmEnvState& s = states[env];
   // keep the per-env RNG stream and the function-static stepper flags (quirk)
-  uint32_t rng = s.rng;
-  int ox = s.old_x, oy = s.old_y, oz = s.old_z;
+  const uint32_t rng = s.rng;
+  const int ox = s.old_x, oy = s.old_y, oz = s.old_z;
   const int32_t episode = s.episode + 1;
-  uint32_t* w = reinterpret_cast<uint32_t*>(&s);
-  for (int i = 0; i < GM_STATE_WORDS; i++) w[i] = 0;
+  __syncthreads();   // every lane has read them before the record is cleared
+  {
+    static_assert(sizeof(GmEnvState) % 16 == 0, "GmEnvState is cleared in 16-byte words");
+    uint4* w = reinterpret_cast<uint4*>(&s);
+    for (int i = threadIdx.x; i < GM_STATE_WORDS / 4; i += 64) w[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
   s.rng = rng; s.old_x = ox; s.old_y = oy; s.old_z = oz;
   s.episode = episode;
   g_reset(s.end); g_reset(s.next);

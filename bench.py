@@ -113,7 +113,13 @@ def obs_parity(gmx, env, seed: int):
     rel = np.where(big, d / np.where(big, np.abs(ref), 1.0), 0.0).max(axis=1)
     ab = np.where(big, 0.0, d).max(axis=1)
     dv, ov = gmx.env_state_view(after), gmx.env_state_view(after_o)
-    return {"max_rel": float(rel.max()), "max_abs_small": float(ab.max()),
+    # where the worst relative error sits (env, observation index, values)
+    relm = np.where(big, d / np.where(big, np.abs(ref), 1.0), 0.0)
+    we, wi = np.unravel_index(int(np.argmax(relm)), relm.shape)
+    worst = {"env": int(we), "obs_index": int(wi), "ref": float(ref[we, wi]), "gpu": float(obs[we, wi]),
+             "abs_diff": float(d[we, wi]),
+             "env_qpos_max_abs_diff": float(np.abs(dv["qpos"][we] - ov["qpos"][we]).max())}
+    return {"max_rel": float(rel.max()), "max_abs_small": float(ab.max()), "worst": worst,
             "envs_over_1e-4": int(((rel > 1e-4) | (ab > 1e-4)).sum()), "envs": int(env.n_envs),
             "p99_rel": float(np.percentile(rel, 99)),
             "done_mismatch": int((done.astype(np.uint8) != done_o).sum()),

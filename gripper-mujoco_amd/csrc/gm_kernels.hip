@@ -2860,6 +2860,38 @@ __device__ int get_obs(const GmEnvHot& s, RingRef R, const gm_config* __restrict
   return n;
 }
 
+// get_obs with one stream per lane (the env-step epilogue): every lane walks the same
+// in-use stream list, in get_obs's order, to find its stream's sampler, settings and
+// output offset, then all streams are sampled at once -- the serial version's arithmetic
+// per stream, without its chain of dependent window reads on one lane.
+__device__ void get_obs_lanes(const GmEnvHot& s, RingRef R, const gm_config* __restrict__ C, float* out, int lane) {
+  const gm_settings& st = C->s;
+  const int sf = C->sensor_fcn, tf = C->state_fcn;
+  int k = 0, n = 0, my_mode = 0, my_st = -1, my_n = 0;
+  const gm_sensor* my_ss = nullptr;
+  auto visit = [&](bool in_use, int count, int mode, int st0, const gm_sensor& ss) {
+    if (!in_use) return;
+    const int size = (mode == GM_SAMPLE_RAW) ? ss.total_readings - 1 : 2 * ss.prev_steps + 1;
+    for (int c = 0; c < count; c++) {
+      if (k == lane) { my_mode = mode; my_st = st0 + c; my_ss = &ss; my_n = n; }
+      n += size;
+      k++;
+    }
+  };
+  visit(st.bending_gauge.in_use, 3, sf, ST_GAUGE, st.bending_gauge);
+  visit(st.axial_gauge.in_use, 3, sf, ST_AXIAL, st.axial_gauge);
+  visit(st.palm_sensor.in_use, 1, sf, ST_PALM, st.palm_sensor);
+  visit(st.wrist_sensor_XY.in_use, 1, sf, ST_WX, st.wrist_sensor_XY);
+  visit(st.wrist_sensor_XY.in_use, 1, sf, ST_WY, st.wrist_sensor_XY);
+  visit(st.wrist_sensor_Z.in_use, 1, sf, ST_WZ, st.wrist_sensor_XY);   // XY's counts (quirk, as get_obs)
+  visit(st.motor_state_sensor.in_use, 3, tf, ST_MOTOR, st.motor_state_sensor);
+  visit(st.base_state_sensor_XY.in_use, 2, tf, ST_BASE, st.base_state_sensor_XY);
+  visit(st.base_state_sensor_Z.in_use, 1, tf, ST_BASE + 2, st.base_state_sensor_Z);
+  visit(st.base_state_sensor_yaw.in_use, 1, tf, ST_YAW, st.base_state_sensor_yaw);
+  visit(st.cartesian_contacts_XYZ.in_use, 12, GM_SAMPLE_CHANGE, ST_CART, st.cartesian_contacts_XYZ);
+  if (my_st >= 0) sample_stream(s, R, my_mode, my_st, *my_ss, out + my_n);
+}
+
 GM_EPI_ATTR int is_done(const GmEnvHot& s, const gm_config* __restrict__ C) {
   const gm_settings& st = C->s;
   int k = 0;
@@ -2986,8 +3018,8 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
     store_state(S, states + env, lane);
     return;
   }
+  unsigned long long t0 = prof ? clock64() : 0;
   if (lane == 0) {
-    unsigned long long t0 = prof ? clock64() : 0;
     S.s.extra_substeps = 0;
     S.s.overflow = S.overflow;
     sense_gripper_state(S, m, C);
@@ -2995,9 +3027,11 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
     update_env(S, m, C, T);
     PH(19);
     S.s.num_action_steps += 1;
-    float* o = obs + (size_t)env * C->n_obs;
-    get_obs(S.s, S.gs->ring, C, o);
-    PH(20);
+  }
+  __syncthreads();   // lane 0's window appends (HBM) and indices (LDS) before the samplers
+  get_obs_lanes(S.s, S.gs->ring, C, obs + (size_t)env * C->n_obs, lane);
+  PH(20);
+  if (lane == 0) {
     int d = is_done(S.s, C);
     float r = reward(S.s, C);
     S.s.done = d;

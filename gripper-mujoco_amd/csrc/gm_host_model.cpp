@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <vector>
 #include <cstring>
 #include <cstdint>
 #include <string>
@@ -123,6 +124,189 @@ void box_inertia(double mass, double hx, double hy, double hz, double out[3]) {
 }  // namespace
 
 void gm_derive_model_constants(gm_model* m);
+void gm_derive_invweights(gm_model* m);
+
+// mj_setConst's body_invweight0 / dof_invweight0 at qpos0 (the inputs of mj_diagApprox):
+// forward kinematics, the joint-space inertia M (composite rigid bodies, + armature), the
+// centre-of-mass Jacobian of every body, A = J M^-1 J^T; a body's translational /
+// rotational weight is the mean of A's translational / rotational diagonal, a slide or
+// hinge dof's the diagonal of M^-1, a free joint's the mean of its three translational /
+// rotational diagonal entries.  Dense and sequential: a one-time host computation.
+void gm_derive_invweights(gm_model* m) {
+  const int nb = m->nbody, nv = m->nv;
+  std::vector<double> xpos(3 * nb, 0.0), xq(4 * nb, 0.0), R(9 * nb, 0.0), xi(3 * nb, 0.0);
+  std::vector<double> cdof(6 * nv, 0.0), cin(10 * nb, 0.0);
+  auto qmul = [](const double* a, const double* b, double* r) {
+    const double t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+    const double t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+    const double t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+    const double t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+    r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
+  };
+  auto q2m = [](const double* q, double* M) {
+    const double w = q[0], x = q[1], y = q[2], z = q[3];
+    M[0] = 1 - 2 * (y * y + z * z); M[1] = 2 * (x * y - w * z); M[2] = 2 * (x * z + w * y);
+    M[3] = 2 * (x * y + w * z); M[4] = 1 - 2 * (x * x + z * z); M[5] = 2 * (y * z - w * x);
+    M[6] = 2 * (x * z - w * y); M[7] = 2 * (y * z + w * x); M[8] = 1 - 2 * (x * x + y * y);
+  };
+  auto cross = [](const double* a, const double* b, double* r) {
+    const double t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+    r[0] = t0; r[1] = t1; r[2] = t2;
+  };
+  xq[0] = 1;
+  q2m(&xq[0], &R[0]);
+  for (int b = 1; b < nb; b++) {
+    const int p = m->body_parent[b];
+    for (int i = 0; i < 3; i++)
+      xpos[3 * b + i] = xpos[3 * p + i] + R[9 * p + 3 * i] * m->body_pos[b][0] + R[9 * p + 3 * i + 1] * m->body_pos[b][1] +
+                        R[9 * p + 3 * i + 2] * m->body_pos[b][2];
+    qmul(&xq[4 * p], m->body_quat[b], &xq[4 * b]);
+    const int j = m->body_jnt[b];
+    if (j >= 0) {
+      const int qa = m->jnt_qposadr[j];
+      if (m->jnt_type[j] == GM_JNT_SLIDE) {
+        double Rb[9];
+        q2m(&xq[4 * b], Rb);
+        for (int i = 0; i < 3; i++)
+          xpos[3 * b + i] += (Rb[3 * i] * m->jnt_axis[j][0] + Rb[3 * i + 1] * m->jnt_axis[j][1] + Rb[3 * i + 2] * m->jnt_axis[j][2]) * m->qpos0[qa];
+      } else if (m->jnt_type[j] == GM_JNT_HINGE) {
+        const double s = std::sin(0.5 * m->qpos0[qa]), c = std::cos(0.5 * m->qpos0[qa]);
+        const double ql[4] = {c, m->jnt_axis[j][0] * s, m->jnt_axis[j][1] * s, m->jnt_axis[j][2] * s};
+        double t[4];
+        qmul(&xq[4 * b], ql, t);
+        for (int k = 0; k < 4; k++) xq[4 * b + k] = t[k];
+      } else if (m->jnt_type[j] == GM_JNT_FREE) {
+        for (int k = 0; k < 3; k++) xpos[3 * b + k] = m->qpos0[qa + k];
+        for (int k = 0; k < 4; k++) xq[4 * b + k] = m->qpos0[qa + 3 + k];
+      }
+    }
+    double n = 0;
+    for (int k = 0; k < 4; k++) n += xq[4 * b + k] * xq[4 * b + k];
+    n = std::sqrt(n);
+    if (n < 1e-15) { xq[4 * b] = 1; xq[4 * b + 1] = xq[4 * b + 2] = xq[4 * b + 3] = 0; }
+    else for (int k = 0; k < 4; k++) xq[4 * b + k] /= n;
+    q2m(&xq[4 * b], &R[9 * b]);
+    for (int i = 0; i < 3; i++)
+      xi[3 * b + i] = xpos[3 * b + i] + R[9 * b + 3 * i] * m->body_ipos[b][0] + R[9 * b + 3 * i + 1] * m->body_ipos[b][1] +
+                      R[9 * b + 3 * i + 2] * m->body_ipos[b][2];
+    // spatial inertia about the world origin
+    const double* Rb = &R[9 * b];
+    const double* I = m->body_inertia[b];
+    const double mass = m->body_mass[b];
+    const double* c = &xi[3 * b];
+    double Iw[9];
+    for (int i = 0; i < 3; i++)
+      for (int k = 0; k < 3; k++)
+        Iw[3 * i + k] = Rb[3 * i] * I[0] * Rb[3 * k] + Rb[3 * i + 1] * I[1] * Rb[3 * k + 1] + Rb[3 * i + 2] * I[2] * Rb[3 * k + 2];
+    const double cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+    double* ci = &cin[10 * b];
+    ci[0] = Iw[0] + mass * (cc - c[0] * c[0]); ci[1] = Iw[4] + mass * (cc - c[1] * c[1]); ci[2] = Iw[8] + mass * (cc - c[2] * c[2]);
+    ci[3] = Iw[1] - mass * c[0] * c[1]; ci[4] = Iw[2] - mass * c[0] * c[2]; ci[5] = Iw[5] - mass * c[1] * c[2];
+    ci[6] = mass * c[0]; ci[7] = mass * c[1]; ci[8] = mass * c[2]; ci[9] = mass;
+  }
+  for (int d = 0; d < nv; d++) {
+    const int b = m->dof_body[d], j = m->body_jnt[b];
+    double* cd = &cdof[6 * d];
+    const double* Rb = &R[9 * b];
+    if (m->jnt_type[j] == GM_JNT_FREE) {
+      const int k = d - m->jnt_dofadr[j];
+      for (int t = 0; t < 6; t++) cd[t] = 0;
+      if (k < 3) cd[3 + k] = 1;
+      else { const double w[3] = {Rb[k - 3], Rb[3 + k - 3], Rb[6 + k - 3]}; cd[0] = w[0]; cd[1] = w[1]; cd[2] = w[2]; cross(&xpos[3 * b], w, cd + 3); }
+    } else {
+      double wa[3];
+      for (int i = 0; i < 3; i++) wa[i] = Rb[3 * i] * m->jnt_axis[j][0] + Rb[3 * i + 1] * m->jnt_axis[j][1] + Rb[3 * i + 2] * m->jnt_axis[j][2];
+      if (m->jnt_type[j] == GM_JNT_SLIDE) { cd[0] = cd[1] = cd[2] = 0; cd[3] = wa[0]; cd[4] = wa[1]; cd[5] = wa[2]; }
+      else { cd[0] = wa[0]; cd[1] = wa[1]; cd[2] = wa[2]; cross(&xpos[3 * b], wa, cd + 3); }
+    }
+  }
+  // composite inertias and M (CRB), + armature
+  std::vector<double> Ic(cin);
+  for (int b = nb - 1; b > 0; b--) {
+    const int p = m->body_parent[b];
+    if (p > 0) for (int k = 0; k < 10; k++) Ic[10 * p + k] += Ic[10 * b + k];
+  }
+  auto imul = [](const double* ci, const double* v, double* r) {
+    const double* w = v; const double* u = v + 3;
+    const double hxu[3] = {ci[7] * u[2] - ci[8] * u[1], ci[8] * u[0] - ci[6] * u[2], ci[6] * u[1] - ci[7] * u[0]};
+    const double hxw[3] = {ci[7] * w[2] - ci[8] * w[1], ci[8] * w[0] - ci[6] * w[2], ci[6] * w[1] - ci[7] * w[0]};
+    r[0] = ci[0] * w[0] + ci[3] * w[1] + ci[4] * w[2] + hxu[0];
+    r[1] = ci[3] * w[0] + ci[1] * w[1] + ci[5] * w[2] + hxu[1];
+    r[2] = ci[4] * w[0] + ci[5] * w[1] + ci[2] * w[2] + hxu[2];
+    r[3] = ci[9] * u[0] - hxw[0]; r[4] = ci[9] * u[1] - hxw[1]; r[5] = ci[9] * u[2] - hxw[2];
+  };
+  std::vector<double> M(nv * nv, 0.0);
+  for (int j = 0; j < nv; j++) {
+    double F[6];
+    imul(&Ic[10 * m->dof_body[j]], &cdof[6 * j], F);
+    for (int i = j; i >= 0; i = m->dof_parent[i]) {
+      double v = 0;
+      for (int t = 0; t < 6; t++) v += cdof[6 * i + t] * F[t];
+      M[j * nv + i] = v; M[i * nv + j] = v;
+    }
+    M[j * nv + j] += m->jnt_armature[m->body_jnt[m->dof_body[j]]];
+  }
+  // Cholesky of M
+  std::vector<double> L(M);
+  for (int k = 0; k < nv; k++) {
+    double s = L[k * nv + k];
+    for (int t = 0; t < k; t++) s -= L[k * nv + t] * L[k * nv + t];
+    L[k * nv + k] = std::sqrt(s > 0 ? s : 1e-300);
+    for (int i = k + 1; i < nv; i++) {
+      double t2 = L[i * nv + k];
+      for (int t = 0; t < k; t++) t2 -= L[i * nv + t] * L[k * nv + t];
+      L[i * nv + k] = t2 / L[k * nv + k];
+    }
+  }
+  auto solveM = [&](std::vector<double>& x) {
+    for (int i = 0; i < nv; i++) { double s = x[i]; for (int t = 0; t < i; t++) s -= L[i * nv + t] * x[t]; x[i] = s / L[i * nv + i]; }
+    for (int i = nv - 1; i >= 0; i--) { double s = x[i]; for (int t = i + 1; t < nv; t++) s -= L[t * nv + i] * x[t]; x[i] = s / L[i * nv + i]; }
+  };
+  auto is_anc = [&](int dof, int b) {
+    for (int x = b; x > 0; x = m->body_parent[x]) if (m->dof_body[dof] == x) return true;
+    return false;
+  };
+  for (int b = 0; b < GM_MAX_BODY; b++) m->body_invweight0[b][0] = m->body_invweight0[b][1] = 0.0;
+  for (int b = 1; b < nb; b++) {
+    // 6 x nv Jacobian of the centre of mass: rows 0-2 translation, 3-5 rotation
+    std::vector<std::vector<double>> Jr(6, std::vector<double>(nv, 0.0));
+    for (int d = 0; d < nv; d++) {
+      if (!is_anc(d, b)) continue;
+      const double* cd = &cdof[6 * d];
+      double wxp[3];
+      cross(cd, &xi[3 * b], wxp);
+      for (int k = 0; k < 3; k++) { Jr[k][d] = cd[3 + k] + wxp[k]; Jr[3 + k][d] = cd[k]; }
+    }
+    double diag[6];
+    for (int r = 0; r < 6; r++) {
+      std::vector<double> x(Jr[r]);
+      solveM(x);
+      double v = 0;
+      for (int d = 0; d < nv; d++) v += Jr[r][d] * x[d];
+      diag[r] = v;
+    }
+    m->body_invweight0[b][0] = (diag[0] + diag[1] + diag[2]) / 3.0;
+    m->body_invweight0[b][1] = (diag[3] + diag[4] + diag[5]) / 3.0;
+  }
+  for (int d = 0; d < GM_MAX_DOF; d++) m->dof_invweight0[d] = 0.0;
+  std::vector<double> minv(nv);
+  for (int d = 0; d < nv; d++) {
+    std::vector<double> e(nv, 0.0);
+    e[d] = 1.0;
+    solveM(e);
+    minv[d] = e[d];
+  }
+  for (int j = 0; j < m->njnt; j++) {
+    const int d0 = m->jnt_dofadr[j];
+    if (m->jnt_type[j] == GM_JNT_FREE) {
+      const double t = (minv[d0] + minv[d0 + 1] + minv[d0 + 2]) / 3.0;
+      const double r = (minv[d0 + 3] + minv[d0 + 4] + minv[d0 + 5]) / 3.0;
+      for (int k = 0; k < 3; k++) { m->dof_invweight0[d0 + k] = t; m->dof_invweight0[d0 + 3 + k] = r; }
+    } else {
+      m->dof_invweight0[d0] = minv[d0];
+    }
+  }
+}
 // Everything the reference derives from the MJCF's gripper numerics rather than reading
 // it (JointSettings::Dim / ctrl / gauge, myfunctions.cpp:207-296, 535): shared by the
 // builder and the MJCF loader (gm_mjcf.cpp) so both produce the same model bit for bit.
@@ -383,6 +567,7 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
   }
   if (m->nbody > GM_MAX_BODY || m->nv > GM_MAX_DOF || m->nq > GM_MAX_QPOS || m->ngeom > GM_MAX_GEOM)
     return GM_E_RANGE;
+  gm_derive_invweights(m);
   return GM_OK;
 }
 

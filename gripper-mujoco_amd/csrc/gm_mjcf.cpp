@@ -27,6 +27,7 @@
 #include <vector>
 
 void gm_derive_model_constants(gm_model* m);
+void gm_derive_invweights(gm_model* m);
 
 namespace {
 
@@ -391,6 +392,7 @@ int gm_model_from_mjcf(const char* xml, gm_model* out, char* err, int err_cap) {
     }
     return true;
   };
+  int nfree = 0;   // free joints seen (nq / GM_MAX_QPOS checked as they are added)
   std::function<bool(const XNode&, int)> walk = [&](const XNode& bx, int parent) -> bool {
     if (m->nbody >= GM_MAX_BODY) { berr = "too many bodies"; return false; }
     const int b = m->nbody++;
@@ -443,6 +445,8 @@ int gm_model_from_mjcf(const char* xml, gm_model* out, char* err, int err_cap) {
         m->jnt_damping[j] = x.get("damping") ? std::strtod(x.get("damping")->c_str(), nullptr) : 0.0;
         m->jnt_armature[j] = x.get("armature") ? std::strtod(x.get("armature")->c_str(), nullptr) : 0.0;
         const int ndof = type == GM_JNT_FREE ? 6 : 1;
+        if (type == GM_JNT_FREE && ++nfree > 1) { berr = "more than one free joint (the kernels hold one live object)"; return false; }
+        if (m->nq + (type == GM_JNT_FREE ? 7 : 1) > GM_MAX_QPOS) { berr = "too many qpos"; return false; }
         m->nq += type == GM_JNT_FREE ? 7 : 1;
         for (int q = 0; q < ndof; q++) {
           if (m->nv >= GM_MAX_DOF) { berr = "too many dofs"; return false; }
@@ -557,8 +561,9 @@ int gm_model_from_mjcf(const char* xml, gm_model* out, char* err, int err_cap) {
   m->hook_angle_degrees = num("hook_angle_degrees", 90.0);
   m->hook_length = num("hook_length", 35e-3);
   m->fixed_first_segment = (int32_t)num("fixed_first_segment", 0);
-  gm_derive_model_constants(m);
   if (m->nq > GM_MAX_QPOS) return fail("too many qpos");
+  gm_derive_model_constants(m);
+  gm_derive_invweights(m);
   return GM_OK;
 }
 

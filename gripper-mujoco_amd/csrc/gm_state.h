@@ -55,10 +55,12 @@ struct GmGrip {            // luke::Gripper (gripper.h:11-198)
   double last_read[SL_N];                                                              \
   double qpos[GM_MAX_QPOS];      /* fp64 like MuJoCo's mjtNum (reference physics type) */ \
   double qvel[GM_MAX_DOF];                                                             \
+  double qacc_warm[GM_MAX_DOF];  /* mjData qacc_warmstart: the last substep's qacc */   \
   double lock_q[GM_MAX_LOCK];                                                          \
   double start_qpos[7];                                                                \
   double obj_size[3];                                                                  \
   double obj_mass, obj_inertia[3], obj_friction, obj_rbound, obj_rest_z;               \
+  double obj_invw[2];            /* the live object's body_invweight0 (trans, rot) */   \
   double dt;                     /* this env's timestep (per env for calibration) */   \
   double tip_force;              /* calibration tip load, N; 0 = off */                \
   /* ---- floats ---- */                                                               \

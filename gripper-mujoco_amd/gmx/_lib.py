@@ -22,9 +22,9 @@ GM_MAX_QPOS = 48
 GM_RING = 64
 GM_MAX_GEOM = 40
 GM_MAX_PAIR = 80
-GM_MAX_CON = 15
-GM_MAX_EFC = 64
+GM_MAX_CON = 32
 GM_MAX_LOCK = 4
+GM_MAX_EFC = 4 * GM_MAX_CON + GM_MAX_LOCK
 GM_MAX_OBJSET = 64
 
 GEOM_SPHERE, GEOM_CYLINDER, GEOM_BOX = 2, 5, 6
@@ -343,8 +343,10 @@ def env_state_dtype():
     return np.dtype([
         ("time", "f8"), ("last_step_time", "f8"), ("end", grip), ("next", grip), ("base", "f8", 6),
         ("last_read", "f8", 10), ("qpos", "f8", GM_MAX_QPOS), ("qvel", "f8", GM_MAX_DOF),
+        ("qacc_warm", "f8", GM_MAX_DOF),
         ("lock_q", "f8", GM_MAX_LOCK), ("start_qpos", "f8", 7), ("obj_size", "f8", 3), ("obj_mass", "f8"),
         ("obj_inertia", "f8", 3), ("obj_friction", "f8"), ("obj_rbound", "f8"), ("obj_rest_z", "f8"),
+        ("obj_invw", "f8", 2),
         ("dt", "f8"), ("tip_force", "f8"),
         ("rand_mu", "f4", (10, 3)), ("lev_value", "f4", nl), ("lev_last", "f4", nl),
         ("cumulative_reward", "f4"), ("grp_peak_lateral", "f4"), ("reward", "f4"),

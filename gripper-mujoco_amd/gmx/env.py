@@ -11,7 +11,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import (GM_MAX_DOF, load_library, ModelBlob, ConfigBlob, ModelParams, Spawn, SpawnParams, make_object_set,
+from ._lib import (GM_MAX_CON, GM_MAX_DOF, GM_MAX_EFC, load_library, ModelBlob, ConfigBlob, ModelParams, Spawn, SpawnParams, make_object_set,
                    BINARY_EVENTS, LINEAR_EVENTS)
 from .settings import canonical_settings, MAX_EPISODE_STEPS
 
@@ -299,8 +299,8 @@ class BatchedGripperEnv:
         n = self.n_envs
         ncon = np.zeros(n, dtype=np.int32)
         nefc = np.zeros(n, dtype=np.int32)
-        con = np.zeros((n, 15, 16), dtype=np.float64)
-        f = np.zeros((n, 64), dtype=np.float64)
+        con = np.zeros((n, GM_MAX_CON, 16), dtype=np.float64)
+        f = np.zeros((n, GM_MAX_EFC), dtype=np.float64)
         qacc = np.zeros((n, GM_MAX_DOF), dtype=np.float64)
         w = np.zeros((n, 6), dtype=np.float64)
         d = C.POINTER(C.c_double)

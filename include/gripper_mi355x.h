@@ -32,8 +32,10 @@ extern "C" {
 #define GM_MAX_QPOS   48
 #define GM_MAX_GEOM   40
 #define GM_MAX_PAIR   80      /* 6 N + 15 candidate pairs; a lane per pair per 64-pair batch */
-#define GM_MAX_CON    15      /* contacts kept per env per substep             */
-#define GM_MAX_EFC    64      /* constraint rows: 4 per contact + motor locks  */
+#define GM_MAX_CON    32      /* contacts kept per env per substep (box-box: up to 8 per pair) */
+#define GM_MAX_EFC    (4 * GM_MAX_CON + GM_MAX_LOCK)   /* rows: motor locks + 4 pyramid edges per contact */
+#define GM_NEWTON_MAXIT 16    /* Newton iterations per substep (cap; converged runs stop earlier) */
+#define GM_NEWTON_MAXLS 16    /* exact line-search evaluations per Newton iteration (cap)          */
 #define GM_MAX_LOCK   4       /* prismatic x3 + palm (revolute locks disabled) */
 #define GM_MAX_OBJSET 64      /* objects in one synthetic object set          */
 #define GM_RING       64      /* sensor window: last 64 readings per stream (1 + rps * prev_steps <= 64) */
@@ -235,6 +237,12 @@ typedef struct gm_model {
   int32_t lock_kind[GM_MAX_LOCK];     /* 0 prismatic, 2 palm               */
   /* keyframe "initial pose" (myfunctions.cpp:171) */
   double  qpos0[GM_MAX_QPOS];
+  /* mj_setConst at qpos0: body_invweight0 (translation, rotation: the mean diagonal of
+   * J M^-1 J^T at the body's centre of mass) and dof_invweight0 (M^-1 diagonal); they set
+   * the constraint regulariser R = (1 - d) / d * diagApprox (mj_diagApprox).  Derived by
+   * gm_build_model / gm_model_from_mjcf; the live object's are per env. */
+  double  body_invweight0[GM_MAX_BODY][2];
+  double  dof_invweight0[GM_MAX_DOF];
   /* named indices */
   int32_t dof_base, dof_palm, dof_obj;
   int32_t dof_pris[3], dof_rev[3], dof_seg[3];   /* first segment dof per finger */
@@ -244,7 +252,7 @@ typedef struct gm_model {
   double  gravity[3];
   double  solref[2];                  /* timeconst, dampratio              */
   double  solimp[5];                  /* dmin, dmax, width, midpoint, power */
-  int32_t pgs_iterations;
+  int32_t pgs_iterations;             /* sweeps of the oracle's PGS cross-check (the engine: Newton) */
   double  mpr_tolerance;
   int32_t mpr_iterations;
   /* gripper dimensions used by the env logic (JointSettings::Dim) */

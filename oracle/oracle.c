@@ -6,12 +6,15 @@
  * un-vendored dependency pinned by reference buildsettings.mk:32) with the
  * deliberate, documented deviations listed in DESIGN.md ("Engine spec"):
  * the Euler step keeps MuJoCo's explicit joint springs and implicit joint damping but
- * folds the PD motor gains in implicitly, PGS on a pyramidal cone with a fixed sweep
- * count, MPR single-contact for box-box and box-cylinder.
+ * folds the PD motor gains in implicitly; the constraint problem (pyramidal cones, the
+ * diagApprox regulariser) is solved to its unique optimum by MuJoCo's Newton method.
+ * The physics substep (physics.c) follows the device kernels' association order
+ * operation for operation, so the two agree bit for bit from the same state.
  */
 #define _POSIX_C_SOURCE 200809L
 #include "oracle.h"
 #include "../gripper-mujoco_amd/csrc/gm_state.h"
+#include "../gripper-mujoco_amd/csrc/gm_math.h"
 
 #include <math.h>
 #include <stdlib.h>
@@ -253,26 +256,48 @@ typedef struct {
 /* sensor slots in settings order (SS macro order) */
 enum { S_MOTOR = 0, S_BASEZ, S_BASEXY, S_YAW, S_BEND, S_AXIAL, S_PALM, S_WRISTXY, S_WRISTZ, S_CART, S_N };
 
+/* the device's lane topology (gm_capi.hip build_topo) */
+typedef struct {
+  int CL;
+  int body_f0[3], dof_f0[3];
+  int body_grp[NB], body_cpos[NB];
+  int lane_body[64];
+  int kl_type[64], kl_qadr[64], kl_grp[64], kl_cpos[64];
+  double kl_pos[64][3], kl_quat[64][4], kl_axis[64][3];
+  int dof_grp[NV], dof_p[NV], dof_target[NV];
+  double dof_arm[NV], dof_dsum[NV], dof_ksum[NV], dof_stiff[NV], dof_damp[NV], dof_kp[NV], dof_kd[NV];
+  int geom_grp[NG];
+  int lane_opair[64][2], lane_gpair[64][2];   /* the lane body's geoms' pairs with the object / ground */
+} otopo;
+
+#define GM_TRIF ((GM_CHAIN + 1) * (GM_CHAIN + 2) / 2)
+
 struct or_env {
   gm_model m;
   gm_config c;
   gm_object objs[GM_MAX_OBJSET];
   int nobj;
   int64_t env_id;
+  otopo T;
   /* physics state */
   double qpos[NQ], qvel[NV], time;
+  double qacc_warm[NV];            /* mjData qacc_warmstart: the last substep's solution */
+  double obj_invw[2];              /* the live object's body_invweight0 (translation, rotation) */
   /* kinematics / dynamics scratch (mjData) */
-  double xpos[NB][3], xmat[NB][9], xquat[NB][4], xipos[NB][3];
-  double cinert[NB][10], cdof[NV][6], cdof_dot[NV][6], cvel[NB][6];
-  double xaxis[NB][3], xanchor[NB][3];
-  double gxpos[NG][3], gxmat[NG][9];
-  double M[NV][NV], L[NV][NV], D[NV];
-  double qfrc_bias[NV], qfrc_passive[NV], qfrc_act[NV], qacc_smooth[NV], qacc[NV];
-  int ncon, overflow;
+  double xpos[NB][3], xmat[NB][9], xquat[NB][4];
+  double cinert[NB][10], cdof[NV][6], Ic[NB][10], cfrc[NB][6];
+  double Hf[3][GM_TRIF], Hp[3], Ho[21], Hbb;   /* H~ tree blocks (TRI: finger p = 0 base .. CL) */
+  double frc[NV], qacc[NV];
+  int ncon, ncon_total, overflow;
   con_t con[NC];
-  int nefc;
-  double J[NE][NV], efc_f[NE], efc_R[NE], efc_b[NE];
+  int pair_off[GM_MAX_PAIR], pair_cnt[GM_MAX_PAIR];
+  int nefc, nl;
+  double efc_f[NE], efc_D[NE], efc_aref[NE];
   int efc_type[NE];  /* 0 equality, 1 pyramid edge */
+  int lock_row_dof[GM_MAX_LOCK];
+  int solver_pgs;                  /* 0: Newton (the engine); > 0: dense PGS cross-check, this many sweeps */
+  int stat_it, stat_ls;            /* Newton iterations / line-search evaluations of the last substep */
+  long stat_it_sum, stat_ls_sum, stat_solves, stat_it_max, stat_ncon_max, stat_nefc_sum;
   double qpos_pre[NQ];
   /* target (myfunctions.cpp:470, customtypes.h:574-694) */
   grip_t end, next;
@@ -336,836 +361,17 @@ static void apply_object(gm_model* m, const gm_object* o) {
     m->geom_rbound[g] = r;
   }
   m->body_mass[b] = mass;
-  m->body_inertia[b][0] = I0; m->body_inertia[b][1] = I1; m->body_inertia[b][2] = I2;
-}
-
-/* =====================================================================
- * kinematics (mj_kinematics + mj_comPos restatement)
- * ===================================================================== */
-static void fk(or_env* e) {
+  m->body_inertia[b][0] = I0; m->body_inertia[b][1] = I1; m->body_inertia[b][2] = I2;}
+/* body_invweight0 of the live object (mj_setConst at qpos0: a free body's translational
+ * J M^-1 J^T diagonal mean 1/m, rotational the mean of 1/I) */
+static void object_invweight(or_env* e) {
   const gm_model* m = &e->m;
-  for (int i = 0; i < 3; i++) e->xpos[0][i] = 0;
-  e->xquat[0][0] = 1; e->xquat[0][1] = e->xquat[0][2] = e->xquat[0][3] = 0;
-  quat2mat(e->xmat[0], e->xquat[0]);
-  for (int b = 1; b < m->nbody; b++) {
-    int p = m->body_parent[b];
-    double tmp[3];
-    mulmv3(tmp, e->xmat[p], m->body_pos[b]);
-    add3(e->xpos[b], e->xpos[p], tmp);
-    quatmul(e->xquat[b], e->xquat[p], m->body_quat[b]);
-    int j = m->body_jnt[b];
-    if (j >= 0) {
-      double R[9];
-      quat2mat(R, e->xquat[b]);
-      mulmv3(e->xaxis[b], R, m->jnt_axis[j]);
-      double an[3];
-      mulmv3(an, R, m->jnt_pos[j]);
-      add3(e->xanchor[b], e->xpos[b], an);
-      int qa = m->jnt_qposadr[j];
-      if (m->jnt_type[j] == GM_JNT_SLIDE) {
-        double d[3];
-        scl3(d, e->xaxis[b], e->qpos[qa]);
-        add3(e->xpos[b], e->xpos[b], d);
-        add3(e->xanchor[b], e->xanchor[b], d);
-      } else if (m->jnt_type[j] == GM_JNT_HINGE) {
-        double ang = e->qpos[qa], s = sin(0.5 * ang), c = cos(0.5 * ang);
-        const double* ax = m->jnt_axis[j];
-        double ql[4] = {c, ax[0] * s, ax[1] * s, ax[2] * s};
-        quatmul(e->xquat[b], e->xquat[b], ql);
-        /* anchor at body origin in this model: xpos unchanged */
-      } else if (m->jnt_type[j] == GM_JNT_FREE) {
-        copy3(e->xpos[b], &e->qpos[qa]);
-        for (int k = 0; k < 4; k++) e->xquat[b][k] = e->qpos[qa + 3 + k];
-        copy3(e->xanchor[b], e->xpos[b]);
-      }
-    }
-    quatnorm(e->xquat[b]);
-    quat2mat(e->xmat[b], e->xquat[b]);
-    double c[3];
-    mulmv3(c, e->xmat[b], m->body_ipos[b]);
-    add3(e->xipos[b], e->xpos[b], c);
-  }
-  for (int g = 0; g < m->ngeom; g++) {
-    int b = m->geom_body[g];
-    double t[3], Rg[9];
-    mulmv3(t, e->xmat[b], m->geom_pos[g]);
-    add3(e->gxpos[g], e->xpos[b], t);
-    quat2mat(Rg, m->geom_quat[g]);
-    mulmm3(e->gxmat[g], e->xmat[b], Rg);
-  }
-  /* spatial inertia about the world origin: I_O(6: xx,yy,zz,xy,xz,yz), h = m c, m */
-  for (int b = 0; b < m->nbody; b++) {
-    double* ci = e->cinert[b];
-    for (int k = 0; k < 10; k++) ci[k] = 0;
-    if (b == 0) continue;
-    const double* R = e->xmat[b];
-    const double* I = m->body_inertia[b];
-    double mass = m->body_mass[b];
-    const double* c = e->xipos[b];
-    double Iw[9];
-    for (int i = 0; i < 3; i++)
-      for (int j = 0; j < 3; j++)
-        Iw[3 * i + j] = R[3 * i] * I[0] * R[3 * j] + R[3 * i + 1] * I[1] * R[3 * j + 1] + R[3 * i + 2] * I[2] * R[3 * j + 2];
-    double cc = dot3(c, c);
-    ci[0] = Iw[0] + mass * (cc - c[0] * c[0]);
-    ci[1] = Iw[4] + mass * (cc - c[1] * c[1]);
-    ci[2] = Iw[8] + mass * (cc - c[2] * c[2]);
-    ci[3] = Iw[1] - mass * c[0] * c[1];
-    ci[4] = Iw[2] - mass * c[0] * c[2];
-    ci[5] = Iw[5] - mass * c[1] * c[2];
-    ci[6] = mass * c[0]; ci[7] = mass * c[1]; ci[8] = mass * c[2];
-    ci[9] = mass;
-  }
-  /* motion subspaces cdof = [angular; linear velocity of the world origin] */
-  for (int d = 0; d < m->nv; d++) {
-    int b = m->dof_body[d];
-    int j = m->body_jnt[b];
-    double* cd = e->cdof[d];
-    if (m->jnt_type[j] == GM_JNT_SLIDE) {
-      cd[0] = cd[1] = cd[2] = 0;
-      copy3(cd + 3, e->xaxis[b]);
-    } else if (m->jnt_type[j] == GM_JNT_HINGE) {
-      copy3(cd, e->xaxis[b]);
-      cross3(cd + 3, e->xanchor[b], e->xaxis[b]);
-    } else {
-      int k = d - m->jnt_dofadr[j];
-      if (k < 3) {
-        cd[0] = cd[1] = cd[2] = 0;
-        cd[3] = cd[4] = cd[5] = 0; cd[3 + k] = 1;
-      } else {
-        double w[3] = {e->xmat[b][k - 3], e->xmat[b][3 + k - 3], e->xmat[b][6 + k - 3]};
-        copy3(cd, w);
-        cross3(cd + 3, e->xpos[b], w);
-      }
-    }
-  }
+  const int b = m->body_obj;
+  e->obj_invw[0] = 1.0 / m->body_mass[b];
+  e->obj_invw[1] = ((1.0 / m->body_inertia[b][0] + 1.0 / m->body_inertia[b][1]) + 1.0 / m->body_inertia[b][2]) / 3.0;
 }
 
-/* spatial algebra (Plucker [angular; linear] about the world origin) */
-static void inert_mul(double* r, const double* ci, const double* v) {
-  const double* w = v; const double* u = v + 3;
-  double Iw[3] = {ci[0] * w[0] + ci[3] * w[1] + ci[4] * w[2],
-                  ci[3] * w[0] + ci[1] * w[1] + ci[5] * w[2],
-                  ci[4] * w[0] + ci[5] * w[1] + ci[2] * w[2]};
-  double hxu[3], hxw[3];
-  cross3(hxu, ci + 6, u);
-  cross3(hxw, ci + 6, w);
-  r[0] = Iw[0] + hxu[0]; r[1] = Iw[1] + hxu[1]; r[2] = Iw[2] + hxu[2];
-  r[3] = ci[9] * u[0] - hxw[0]; r[4] = ci[9] * u[1] - hxw[1]; r[5] = ci[9] * u[2] - hxw[2];
-}
-static void cross_motion(double* r, const double* v, const double* mv) {
-  double a[3], b[3], c[3];
-  cross3(a, v, mv);
-  cross3(b, v, mv + 3);
-  cross3(c, v + 3, mv);
-  r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
-  r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
-}
-static void cross_force(double* r, const double* v, const double* f) {
-  double a[3], b[3], c[3];
-  cross3(a, v, f);
-  cross3(b, v + 3, f + 3);
-  cross3(c, v, f + 3);
-  r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
-  r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
-}
-static double dot6(const double* a, const double* b) {
-  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
-}
-
-/* composite rigid body mass matrix (mj_crb) */
-static void crb(or_env* e) {
-  const gm_model* m = &e->m;
-  double Ic[NB][10];
-  memcpy(Ic, e->cinert, sizeof(Ic));
-  for (int b = m->nbody - 1; b > 0; b--) {
-    int p = m->body_parent[b];
-    if (p > 0) for (int k = 0; k < 10; k++) Ic[p][k] += Ic[b][k];
-  }
-  for (int i = 0; i < m->nv; i++) for (int j = 0; j < m->nv; j++) e->M[i][j] = 0;
-  for (int j = 0; j < m->nv; j++) {
-    double F[6];
-    inert_mul(F, Ic[m->dof_body[j]], e->cdof[j]);
-    for (int i = j; i >= 0; i = m->dof_parent[i]) {
-      double v = dot6(e->cdof[i], F);
-      e->M[j][i] = v; e->M[i][j] = v;
-    }
-  }
-}
-
-/* RNE bias with zero acceleration (mj_comVel + mj_rne(flg_acc=0)) */
-static void rne_bias(or_env* e) {
-  const gm_model* m = &e->m;
-  double cacc[NB][6], cfrc[NB][6];
-  for (int k = 0; k < 6; k++) { e->cvel[0][k] = 0; cacc[0][k] = 0; }
-  cacc[0][3] = -m->gravity[0]; cacc[0][4] = -m->gravity[1]; cacc[0][5] = -m->gravity[2];
-  for (int b = 1; b < m->nbody; b++) {
-    int p = m->body_parent[b];
-    double v[6];
-    memcpy(v, e->cvel[p], sizeof(v));
-    memcpy(cacc[b], cacc[p], sizeof(cacc[b]));
-    int j = m->body_jnt[b];
-    if (j >= 0) {
-      int d0 = m->jnt_dofadr[j];
-      if (m->jnt_type[j] == GM_JNT_FREE) {
-        for (int k = 0; k < 3; k++) for (int t = 0; t < 6; t++) e->cdof_dot[d0 + k][t] = 0;
-        for (int k = 0; k < 3; k++) for (int t = 0; t < 6; t++) v[t] += e->cdof[d0 + k][t] * e->qvel[d0 + k];
-        for (int k = 3; k < 6; k++) cross_motion(e->cdof_dot[d0 + k], v, e->cdof[d0 + k]);
-        for (int k = 3; k < 6; k++) for (int t = 0; t < 6; t++) v[t] += e->cdof[d0 + k][t] * e->qvel[d0 + k];
-        for (int k = 0; k < 6; k++) for (int t = 0; t < 6; t++) cacc[b][t] += e->cdof_dot[d0 + k][t] * e->qvel[d0 + k];
-      } else {
-        cross_motion(e->cdof_dot[d0], v, e->cdof[d0]);
-        for (int t = 0; t < 6; t++) v[t] += e->cdof[d0][t] * e->qvel[d0];
-        for (int t = 0; t < 6; t++) cacc[b][t] += e->cdof_dot[d0][t] * e->qvel[d0];
-      }
-    }
-    memcpy(e->cvel[b], v, sizeof(v));
-    double t1[6], t2[6];
-    inert_mul(cfrc[b], e->cinert[b], cacc[b]);
-    inert_mul(t1, e->cinert[b], v);
-    cross_force(t2, v, t1);
-    for (int t = 0; t < 6; t++) cfrc[b][t] += t2[t];
-  }
-  for (int b = m->nbody - 1; b > 0; b--) {
-    int p = m->body_parent[b];
-    if (p > 0) for (int t = 0; t < 6; t++) cfrc[p][t] += cfrc[b][t];
-  }
-  for (int d = 0; d < m->nv; d++) e->qfrc_bias[d] = dot6(e->cdof[d], cfrc[m->dof_body[d]]);
-}
-
-/* sparse LTDL of the tree mass matrix (mj_factorM): H = L^T D L, in place on L */
-static void factor(or_env* e, double H[NV][NV]) {
-  const gm_model* m = &e->m;
-  int nv = m->nv;
-  for (int k = nv - 1; k >= 0; k--) {
-    for (int i = m->dof_parent[k]; i >= 0; i = m->dof_parent[i]) {
-      double a = H[k][i] / H[k][k];
-      for (int j = i; j >= 0; j = m->dof_parent[j]) H[i][j] -= H[k][j] * a;
-      H[k][i] = a;
-    }
-  }
-  for (int k = 0; k < nv; k++) {
-    e->D[k] = H[k][k];
-    for (int i = 0; i < nv; i++) e->L[k][i] = 0;
-    e->L[k][k] = 1;
-    for (int i = m->dof_parent[k]; i >= 0; i = m->dof_parent[i]) e->L[k][i] = H[k][i];
-  }
-}
-/* solve H x = b with H = L^T D L (mj_solveLD) */
-static void solve(const or_env* e, double* x, const double* b) {
-  const gm_model* m = &e->m;
-  int nv = m->nv;
-  for (int i = 0; i < nv; i++) x[i] = b[i];
-  for (int k = nv - 1; k >= 0; k--)            /* L^T y = b : leaves to root */
-    for (int i = m->dof_parent[k]; i >= 0; i = m->dof_parent[i]) x[i] -= e->L[k][i] * x[k];
-  for (int k = 0; k < nv; k++) x[k] /= e->D[k];
-  for (int k = 0; k < nv; k++)                 /* L x = y : root to leaves */
-    for (int i = m->dof_parent[k]; i >= 0; i = m->dof_parent[i]) x[k] -= e->L[k][i] * x[i];
-}
-
-/* =====================================================================
- * collision (mj_collision restatement; engine spec)
- * ===================================================================== */
-static int add_contact(or_env* e, int g1, int g2, double dist, const double* pos, const double* n) {
-  if (e->ncon >= NC) { e->overflow = 1; return 0; }
-  con_t* c = &e->con[e->ncon++];
-  c->dist = dist;
-  copy3(c->pos, pos);
-  make_frame(c->frame, n);
-  c->g1 = g1; c->g2 = g2;
-  double f1 = e->m.geom_friction[g1], f2 = e->m.geom_friction[g2];
-  c->mu = f1 > f2 ? f1 : f2;
-  return 1;
-}
-
-static void plane_sphere(or_env* e, int gp, int gs) {
-  const double* n = &e->gxmat[gp][0];
-  double nz[3] = {e->gxmat[gp][2], e->gxmat[gp][5], e->gxmat[gp][8]};
-  (void)n;
-  double r = e->m.geom_size[gs][0];
-  double dv[3];
-  sub3(dv, e->gxpos[gs], e->gxpos[gp]);
-  double dist = dot3(dv, nz) - r;
-  if (dist < 0) {
-    double pos[3];
-    for (int i = 0; i < 3; i++) pos[i] = e->gxpos[gs][i] - nz[i] * (r + 0.5 * dist);
-    add_contact(e, gp, gs, dist, pos, nz);
-  }
-}
-static void plane_box(or_env* e, int gp, int gb) {
-  double nz[3] = {e->gxmat[gp][2], e->gxmat[gp][5], e->gxmat[gp][8]};
-  const double* h = e->m.geom_size[gb];
-  int cnt = 0;
-  for (int i = 0; i < 8 && cnt < 4; i++) {
-    double s[3] = {(i & 1) ? h[0] : -h[0], (i & 2) ? h[1] : -h[1], (i & 4) ? h[2] : -h[2]};
-    double v[3], dv[3];
-    mulmv3(v, e->gxmat[gb], s);
-    add3(v, v, e->gxpos[gb]);
-    sub3(dv, v, e->gxpos[gp]);
-    double d = dot3(dv, nz);
-    if (d < 0) {
-      double pos[3];
-      for (int k = 0; k < 3; k++) pos[k] = v[k] - 0.5 * d * nz[k];
-      add_contact(e, gp, gb, d, pos, nz);
-      cnt++;
-    }
-  }
-}
-static void plane_cylinder(or_env* e, int gp, int gc) {
-  double nz[3] = {e->gxmat[gp][2], e->gxmat[gp][5], e->gxmat[gp][8]};
-  const double* R = e->gxmat[gc];
-  double a[3] = {R[2], R[5], R[8]};
-  double r = e->m.geom_size[gc][0], hh = e->m.geom_size[gc][1];
-  double na = dot3(nz, a);
-  double w[3] = {-nz[0] + na * a[0], -nz[1] + na * a[1], -nz[2] + na * a[2]};
-  double lw = norm3(w);
-  if (lw < 1e-6) { w[0] = R[0]; w[1] = R[3]; w[2] = R[6]; }
-  else scl3(w, w, 1.0 / lw);
-  double axw[3];
-  cross3(axw, a, w);
-  int cnt = 0;
-  for (int s = 0; s < 2 && cnt < 4; s++) {
-    double sg = s == 0 ? 1.0 : -1.0;
-    double cc[3] = {e->gxpos[gc][0] + sg * hh * a[0], e->gxpos[gc][1] + sg * hh * a[1],
-                    e->gxpos[gc][2] + sg * hh * a[2]};
-    for (int k = 0; k < 4 && cnt < 4; k++) {
-      double dir[3];
-      if (k == 0) copy3(dir, w);
-      else if (k == 1) copy3(dir, axw);
-      else if (k == 2) scl3(dir, w, -1.0);
-      else scl3(dir, axw, -1.0);
-      double v[3] = {cc[0] + r * dir[0], cc[1] + r * dir[1], cc[2] + r * dir[2]};
-      double dv[3];
-      sub3(dv, v, e->gxpos[gp]);
-      double d = dot3(dv, nz);
-      if (d < 0) {
-        double pos[3];
-        for (int t = 0; t < 3; t++) pos[t] = v[t] - 0.5 * d * nz[t];
-        add_contact(e, gp, gc, d, pos, nz);
-        cnt++;
-      }
-    }
-  }
-}
-static void sphere_box(or_env* e, int gs, int gb) {
-  const double* R = e->gxmat[gb];
-  const double* h = e->m.geom_size[gb];
-  double r = e->m.geom_size[gs][0];
-  double dv[3], cl[3];
-  sub3(dv, e->gxpos[gs], e->gxpos[gb]);
-  mulmtv3(cl, R, dv);
-  double q[3];
-  int inside = 1;
-  for (int k = 0; k < 3; k++) {
-    q[k] = cl[k];
-    if (q[k] > h[k]) { q[k] = h[k]; inside = 0; }
-    if (q[k] < -h[k]) { q[k] = -h[k]; inside = 0; }
-  }
-  double nl[3], dist, ql[3];
-  if (!inside) {
-    double df[3];
-    sub3(df, cl, q);
-    double l = norm3(df);
-    if (l < 1e-12) return;
-    dist = l - r;
-    if (dist >= 0) return;
-    scl3(nl, df, -1.0 / l);
-    copy3(ql, q);
-  } else {
-    int kmin = 0;
-    double best = h[0] - fabs(cl[0]);
-    for (int k = 1; k < 3; k++) { double v = h[k] - fabs(cl[k]); if (v < best) { best = v; kmin = k; } }
-    double sg = cl[kmin] >= 0 ? 1.0 : -1.0;
-    nl[0] = nl[1] = nl[2] = 0; nl[kmin] = -sg;
-    dist = -(best + r);
-    copy3(ql, cl); ql[kmin] = sg * h[kmin];
-  }
-  double n[3], qw[3], sp[3], pos[3];
-  mulmv3(n, R, nl);
-  mulmv3(qw, R, ql);
-  add3(qw, qw, e->gxpos[gb]);
-  for (int k = 0; k < 3; k++) sp[k] = e->gxpos[gs][k] + n[k] * r;
-  for (int k = 0; k < 3; k++) pos[k] = 0.5 * (qw[k] + sp[k]);
-  add_contact(e, gs, gb, dist, pos, n);
-}
-
-/* ---- MPR (Minkowski portal refinement, libccd algorithm as used by MuJoCo's
- *      mjc_Convex for pairs without a dedicated collider) ---- */
-typedef struct { double v[3], p1[3], p2[3]; } sv_t;
-static void support_geom(const or_env* e, int g, const double* d, double* out) {
-  const double* R = e->gxmat[g];
-  const double* c = e->gxpos[g];
-  const double* s = e->m.geom_size[g];
-  double dl[3];
-  mulmtv3(dl, R, d);
-  double pl[3] = {0, 0, 0};
-  int t = e->m.geom_type[g];
-  /* A direction (numerically) perpendicular to a face or to the cylinder axis has the
-   * whole face / rim line as its support set; the face centre is taken there instead of
-   * a corner picked by the sign of a rounding-level component (|dl_k| < GM_SUPPORT_TIE),
-   * so aligned plates and faces -- the grasp configuration -- give one portal path
-   * rather than one chosen by ulp noise. */
-  if (t == GM_GEOM_BOX) {
-    for (int k = 0; k < 3; k++) pl[k] = fabs(dl[k]) < GM_SUPPORT_TIE ? 0.0 : (dl[k] >= 0 ? s[k] : -s[k]);
-  } else if (t == GM_GEOM_CYLINDER) {
-    double rr = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
-    if (rr > 1e-12) { pl[0] = s[0] * dl[0] / rr; pl[1] = s[0] * dl[1] / rr; }
-    pl[2] = fabs(dl[2]) < GM_SUPPORT_TIE ? 0.0 : (dl[2] >= 0 ? s[1] : -s[1]);
-  } else if (t == GM_GEOM_SPHERE) {
-    double l = norm3(dl);
-    if (l > 1e-12) scl3(pl, dl, s[0] / l);
-  }
-  mulmv3(out, R, pl);
-  add3(out, out, c);
-}
-static void mpr_support(const or_env* e, int g1, int g2, const double* d, sv_t* sv) {
-  double nd[3] = {-d[0], -d[1], -d[2]};
-  support_geom(e, g1, d, sv->p1);
-  support_geom(e, g2, nd, sv->p2);
-  sub3(sv->v, sv->p1, sv->p2);
-}
-static int is_zero(double x) { return fabs(x) < 1e-12; }
-static void portal_dir(const sv_t* P, double* dir) {
-  double a[3], b[3];
-  sub3(a, P[2].v, P[1].v);
-  sub3(b, P[3].v, P[1].v);
-  cross3(dir, a, b);
-  double l = norm3(dir);
-  if (l > 0) scl3(dir, dir, 1.0 / l);
-}
-static void expand_portal(sv_t* P, const sv_t* v4) {
-  double v4v0[3];
-  cross3(v4v0, v4->v, P[0].v);
-  double d = dot3(P[1].v, v4v0);
-  if (d > 0) {
-    d = dot3(P[2].v, v4v0);
-    if (d > 0) P[1] = *v4; else P[3] = *v4;
-  } else {
-    d = dot3(P[3].v, v4v0);
-    if (d > 0) P[2] = *v4; else P[1] = *v4;
-  }
-}
-static int reach_tol(const sv_t* P, const sv_t* v4, const double* dir, double tol) {
-  double dv1 = dot3(P[1].v, dir), dv2 = dot3(P[2].v, dir), dv3 = dot3(P[3].v, dir), dv4 = dot3(v4->v, dir);
-  double d1 = dv4 - dv1, d2 = dv4 - dv2, d3 = dv4 - dv3;
-  double dd = d1 < d2 ? d1 : d2;
-  dd = dd < d3 ? dd : d3;
-  return dd < tol || fabs(dd - tol) < 1e-12;
-}
-/* closest point on triangle (a,b,c) to the origin */
-static void tri_closest_origin(const double* a, const double* b, const double* c, double* out) {
-  double ab[3], ac[3], ap[3];
-  sub3(ab, b, a); sub3(ac, c, a); scl3(ap, a, -1.0);
-  double d1 = dot3(ab, ap), d2 = dot3(ac, ap);
-  if (d1 <= 0 && d2 <= 0) { copy3(out, a); return; }
-  double bp[3]; scl3(bp, b, -1.0);
-  double d3 = dot3(ab, bp), d4 = dot3(ac, bp);
-  if (d3 >= 0 && d4 <= d3) { copy3(out, b); return; }
-  double vc = d1 * d4 - d3 * d2;
-  if (vc <= 0 && d1 >= 0 && d3 <= 0) { double v = d1 / (d1 - d3); for (int k = 0; k < 3; k++) out[k] = a[k] + v * ab[k]; return; }
-  double cp[3]; scl3(cp, c, -1.0);
-  double d5 = dot3(ab, cp), d6 = dot3(ac, cp);
-  if (d6 >= 0 && d5 <= d6) { copy3(out, c); return; }
-  double vb = d5 * d2 - d1 * d6;
-  if (vb <= 0 && d2 >= 0 && d6 <= 0) { double w = d2 / (d2 - d6); for (int k = 0; k < 3; k++) out[k] = a[k] + w * ac[k]; return; }
-  double va = d3 * d6 - d5 * d4;
-  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
-    double w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
-    for (int k = 0; k < 3; k++) out[k] = b[k] + w * (c[k] - b[k]);
-    return;
-  }
-  double den = 1.0 / (va + vb + vc);
-  double v = vb * den, w = vc * den;
-  for (int k = 0; k < 3; k++) out[k] = a[k] + ab[k] * v + ac[k] * w;
-}
-static void mpr_pos(const sv_t* P, double* pos) {
-  double dir[3];
-  portal_dir(P, dir);
-  double t[3];
-  cross3(t, P[1].v, P[2].v); double b0 = dot3(t, P[3].v);
-  cross3(t, P[3].v, P[2].v); double b1 = dot3(t, P[0].v);
-  cross3(t, P[0].v, P[1].v); double b2 = dot3(t, P[3].v);
-  cross3(t, P[2].v, P[1].v); double b3 = dot3(t, P[0].v);
-  double sum = b0 + b1 + b2 + b3;
-  if (sum <= 0) {
-    b0 = 0;
-    cross3(t, P[2].v, P[3].v); b1 = dot3(t, dir);
-    cross3(t, P[3].v, P[1].v); b2 = dot3(t, dir);
-    cross3(t, P[1].v, P[2].v); b3 = dot3(t, dir);
-    sum = b1 + b2 + b3;
-  }
-  double inv = 1.0 / sum;
-  double p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
-  double bb[4] = {b0, b1, b2, b3};
-  for (int i = 0; i < 4; i++)
-    for (int k = 0; k < 3; k++) { p1[k] += bb[i] * P[i].p1[k]; p2[k] += bb[i] * P[i].p2[k]; }
-  for (int k = 0; k < 3; k++) pos[k] = 0.5 * (p1[k] + p2[k]) * inv;
-}
-/* returns 1 and fills depth/dir/pos on penetration; 0 otherwise */
-static int mpr_penetration(const or_env* e, int g1, int g2, double* depth, double* dir, double* pos) {
-  const double tol = e->m.mpr_tolerance;
-  const int maxit = e->m.mpr_iterations;
-  sv_t P[4];
-  /* discover portal */
-  sub3(P[0].v, e->gxpos[g1], e->gxpos[g2]);
-  copy3(P[0].p1, e->gxpos[g1]);
-  copy3(P[0].p2, e->gxpos[g2]);
-  if (is_zero(P[0].v[0]) && is_zero(P[0].v[1]) && is_zero(P[0].v[2])) P[0].v[0] += 1e-5;
-  double d[3];
-  scl3(d, P[0].v, -1.0);
-  double l = norm3(d); scl3(d, d, 1.0 / l);
-  mpr_support(e, g1, g2, d, &P[1]);
-  if (dot3(P[1].v, d) <= 0) return 0;
-  cross3(d, P[0].v, P[1].v);
-  if (is_zero(norm3(d))) {
-    if (is_zero(norm3(P[1].v))) return 0;   /* touching: depth 0 */
-    /* origin on segment v0-v1 */
-    *depth = norm3(P[1].v);
-    scl3(dir, P[1].v, 1.0 / *depth);
-    for (int k = 0; k < 3; k++) pos[k] = 0.5 * (P[1].p1[k] + P[1].p2[k]);
-    return *depth > 0;
-  }
-  l = norm3(d); scl3(d, d, 1.0 / l);
-  mpr_support(e, g1, g2, d, &P[2]);
-  if (dot3(P[2].v, d) <= 0) return 0;
-  double va[3], vb[3];
-  sub3(va, P[1].v, P[0].v); sub3(vb, P[2].v, P[0].v);
-  cross3(d, va, vb);
-  l = norm3(d); scl3(d, d, 1.0 / l);
-  if (dot3(d, P[0].v) > 0) { sv_t t = P[1]; P[1] = P[2]; P[2] = t; scl3(d, d, -1.0); }
-  int it = 0;
-  for (;;) {
-    mpr_support(e, g1, g2, d, &P[3]);
-    if (dot3(P[3].v, d) <= 0) return 0;
-    int cont = 0;
-    cross3(va, P[1].v, P[3].v);
-    if (dot3(va, P[0].v) < -1e-12) { P[2] = P[3]; cont = 1; }
-    if (!cont) {
-      cross3(va, P[3].v, P[2].v);
-      if (dot3(va, P[0].v) < -1e-12) { P[1] = P[3]; cont = 1; }
-    }
-    if (!cont) break;
-    sub3(va, P[1].v, P[0].v); sub3(vb, P[2].v, P[0].v);
-    cross3(d, va, vb);
-    l = norm3(d); scl3(d, d, 1.0 / l);
-    if (++it > maxit) return 0;
-  }
-  /* refine portal */
-  it = 0;
-  for (;;) {
-    portal_dir(P, d);
-    if (dot3(d, P[1].v) >= -1e-12) break;   /* portal encapsulates the origin */
-    sv_t v4;
-    mpr_support(e, g1, g2, d, &v4);
-    double dv4 = dot3(v4.v, d);
-    if (!(is_zero(dv4) || dv4 > 0)) return 0;
-    if (reach_tol(P, &v4, d, tol)) return 0;
-    expand_portal(P, &v4);
-    if (++it > maxit) return 0;
-  }
-  /* find penetration */
-  it = 0;
-  for (;;) {
-    portal_dir(P, d);
-    sv_t v4;
-    mpr_support(e, g1, g2, d, &v4);
-    if (reach_tol(P, &v4, d, tol) || it > maxit) {
-      double cp[3];
-      tri_closest_origin(P[1].v, P[2].v, P[3].v, cp);
-      *depth = norm3(cp);
-      if (is_zero(*depth)) return 0;
-      scl3(dir, cp, 1.0 / *depth);
-      mpr_pos(P, pos);
-      return 1;
-    }
-    expand_portal(P, &v4);
-    it++;
-  }
-}
-static void convex_pair(or_env* e, int g1, int g2) {
-  double depth, dir[3], pos[3];
-  if (mpr_penetration(e, g1, g2, &depth, dir, pos) && depth > 0) add_contact(e, g1, g2, -depth, pos, dir);
-}
-
-static void collision(or_env* e) {
-  const gm_model* m = &e->m;
-  e->ncon = 0;
-  e->overflow = 0;
-  for (int p = 0; p < m->npair; p++) {
-    int a = m->pair_a[p], b = m->pair_b[p];
-    int ta = m->geom_type[a], tb = m->geom_type[b];
-    int g1 = a, g2 = b;
-    if (ta > tb || (ta == tb && a > b)) { g1 = b; g2 = a; }
-    int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
-    /* bounding-sphere broadphase */
-    if (t1 == GM_GEOM_PLANE) {
-      double nz[3] = {e->gxmat[g1][2], e->gxmat[g1][5], e->gxmat[g1][8]}, dv[3];
-      sub3(dv, e->gxpos[g2], e->gxpos[g1]);
-      if (dot3(dv, nz) > m->geom_rbound[g2]) continue;
-    } else {
-      double dv[3];
-      sub3(dv, e->gxpos[g2], e->gxpos[g1]);
-      double rr = m->geom_rbound[g1] + m->geom_rbound[g2];
-      if (dot3(dv, dv) > rr * rr) continue;
-    }
-    if (t1 == GM_GEOM_PLANE) {
-      if (t2 == GM_GEOM_SPHERE) plane_sphere(e, g1, g2);
-      else if (t2 == GM_GEOM_BOX) plane_box(e, g1, g2);
-      else if (t2 == GM_GEOM_CYLINDER) plane_cylinder(e, g1, g2);
-    } else if (t1 == GM_GEOM_SPHERE && t2 == GM_GEOM_BOX) {
-      sphere_box(e, g1, g2);
-    } else {
-      convex_pair(e, g1, g2);
-    }
-  }
-}
-
-/* translational Jacobian column of dof d at world point p */
-static void jac_point_col(const or_env* e, int d, const double* p, double* out) {
-  const double* cd = e->cdof[d];
-  double wxp[3];
-  cross3(wxp, cd, p);
-  out[0] = cd[3] + wxp[0]; out[1] = cd[4] + wxp[1]; out[2] = cd[5] + wxp[2];
-}
-static int is_ancestor_body(const gm_model* m, int anc, int b) {
-  for (; b > 0; b = m->body_parent[b]) if (b == anc) return 1;
-  return anc == 0;
-}
-
-/* =====================================================================
- * constraint assembly + PGS (mj_makeConstraint / mj_makeImpedance / PGS)
- * ===================================================================== */
-static double impedance(const gm_model* m, double r) {
-  double dmin = m->solimp[0], dmax = m->solimp[1], width = m->solimp[2], mid = m->solimp[3], pw = m->solimp[4];
-  if (dmin == dmax || width <= 1e-15) return dmin;
-  double x = fabs(r) / width;
-  if (x >= 1) return dmax;
-  if (x <= 0) return dmin;
-  double y;
-  if (pw == 1) y = x;
-  /* pw == 2 (MuJoCo's default solimp power): x*x / mid, the correctly rounded square
-   * (glibc pow is within 0.52 ulp, so it can differ by one ulp); the device does the same */
-  else if (pw == 2) y = (x <= mid) ? x * x / mid : 1 - (1 - x) * (1 - x) / (1 - mid);
-  else if (x <= mid) y = pow(x, pw) / pow(mid, pw - 1);
-  else y = 1 - pow(1 - x, pw) / pow(1 - mid, pw - 1);
-  return dmin + y * (dmax - dmin);
-}
-
-static void constraint_solve(or_env* e) {
-  const gm_model* m = &e->m;
-  int nv = m->nv;
-  int n = 0;
-  double pos[NE], vel[NE];
-  /* motor locks (equality rows first) */
-  for (int k = 0; k < m->nlock; k++) {
-    if (!e->lock_active[k]) continue;
-    int d = m->lock_dof[k];
-    for (int i = 0; i < nv; i++) e->J[n][i] = 0;
-    e->J[n][d] = 1;
-    pos[n] = e->qpos[d] - e->lock_q[k];
-    e->efc_type[n] = 0;
-    n++;
-  }
-  /* contacts: 4 pyramid edges each */
-  for (int c = 0; c < e->ncon; c++) {
-    const con_t* C = &e->con[c];
-    double Jc[3][NV];
-    for (int r = 0; r < 3; r++) for (int i = 0; i < nv; i++) Jc[r][i] = 0;
-    int b1 = m->geom_body[C->g1], b2 = m->geom_body[C->g2];
-    for (int d = 0; d < nv; d++) {
-      int bd = m->dof_body[d];
-      double s = 0;
-      if (b2 > 0 && is_ancestor_body(m, bd, b2)) s += 1;
-      if (b1 > 0 && is_ancestor_body(m, bd, b1)) s -= 1;
-      if (s == 0) continue;
-      double col[3];
-      jac_point_col(e, d, C->pos, col);
-      for (int r = 0; r < 3; r++) Jc[r][d] = s * dot3(C->frame + 3 * r, col);
-    }
-    for (int k = 0; k < 2; k++) {
-      for (int sg = 0; sg < 2; sg++) {
-        double sgn = sg == 0 ? 1.0 : -1.0;
-        for (int i = 0; i < nv; i++) e->J[n][i] = Jc[0][i] + sgn * C->mu * Jc[1 + k][i];
-        pos[n] = C->dist;
-        e->efc_type[n] = 1;
-        n++;
-      }
-    }
-  }
-  e->nefc = n;
-  if (n == 0) return;
-  /* A = J H^-1 J^T */
-  double W[NE][NV];
-  double A[NE][NE];
-  for (int r = 0; r < n; r++) solve(e, W[r], e->J[r]);
-  for (int r = 0; r < n; r++)
-    for (int s = 0; s < n; s++) {
-      double v = 0;
-      for (int i = 0; i < nv; i++) v += e->J[r][i] * W[s][i];
-      A[r][s] = v;
-    }
-  double h = m->timestep;
-  double tc = m->solref[0] < 2 * h ? 2 * h : m->solref[0];
-  double dr = m->solref[1], dmax = m->solimp[1];
-  double K = 1.0 / (dmax * dmax * tc * tc * dr * dr);
-  double Bd = 2.0 / (dmax * tc);
-  for (int r = 0; r < n; r++) {
-    double jv = 0, ja = 0;
-    for (int i = 0; i < nv; i++) { jv += e->J[r][i] * e->qvel[i]; ja += e->J[r][i] * e->qacc_smooth[i]; }
-    vel[r] = jv;
-    double imp = impedance(m, pos[r]);
-    double aref = -Bd * jv - K * imp * pos[r];
-    double R = (1 - imp) / imp * A[r][r];
-    if (R < 1e-15) R = 1e-15;
-    e->efc_R[r] = R;
-    e->efc_b[r] = ja - aref;
-    e->efc_f[r] = 0;
-  }
-  /* projected Gauss-Seidel, fixed sweep count; like mj_solPGS the diagonal is
-   * inverted once (ARinv) and each row update multiplies by it */
-  double ARinv[NE];
-  for (int r = 0; r < n; r++) ARinv[r] = 1.0 / (A[r][r] + e->efc_R[r]);
-  for (int it = 0; it < m->pgs_iterations; it++) {
-    for (int r = 0; r < n; r++) {
-      double g = e->efc_b[r] + e->efc_R[r] * e->efc_f[r];
-      for (int s = 0; s < n; s++) g += A[r][s] * e->efc_f[s];
-      double f = e->efc_f[r] - g * ARinv[r];
-      if (e->efc_type[r] == 1 && f < 0) f = 0;
-      e->efc_f[r] = f;
-    }
-  }
-  (void)vel;
-  /* mj_contactForce for pyramidal cones: normal = sum of edges, t_k = mu (f+ - f-) */
-  int r0 = n - 4 * e->ncon;
-  for (int c = 0; c < e->ncon; c++) {
-    const double* fe = &e->efc_f[r0 + 4 * c];
-    e->con[c].force[0] = fe[0] + fe[1] + fe[2] + fe[3];
-    e->con[c].force[1] = e->con[c].mu * (fe[0] - fe[1]);
-    e->con[c].force[2] = e->con[c].mu * (fe[2] - fe[3]);
-  }
-}
-
-/* =====================================================================
- * one physics substep: before_step + step + after_step (physics part)
- * myfunctions.cpp:1864-1908
- * ===================================================================== */
-static void control(or_env* e, double* act) {
-  /* luke::control -> control_gripper(target_.next) + control_base (1912-2057) */
-  const gm_model* m = &e->m;
-  for (int d = 0; d < m->nv; d++) act[d] = 0;
-  for (int f = 0; f < 3; f++) {
-    int d = m->dof_pris[f];
-    double u = (e->qpos[d] - e->next.x) * m->kp_gripper[0] + e->qvel[d] * m->kd_gripper[0];
-    act[d] = -u;
-    d = m->dof_rev[f];
-    u = (e->qpos[d] - e->next.th) * m->kp_gripper[1] + e->qvel[d] * m->kd_gripper[1];
-    act[d] = -u;
-  }
-  int d = m->dof_palm;
-  double u = (e->qpos[d] - e->next.z) * m->kp_gripper[2] + e->qvel[d] * m->kd_gripper[2];
-  act[d] = -u;
-  d = m->dof_base;
-  u = (e->qpos[d] - e->base[2]) * m->kp_base[2] + e->qvel[d] * m->kd_base[2];
-  act[d] = -u;
-}
-
-/* PD gains acting on dof d (control_gripper / control_base) */
-static void ctrl_gains(const gm_model* m, int d, double* kp, double* kd) {
-  *kp = 0; *kd = 0;
-  for (int f = 0; f < 3; f++) {
-    if (d == m->dof_pris[f]) { *kp = m->kp_gripper[0]; *kd = m->kd_gripper[0]; }
-    if (d == m->dof_rev[f]) { *kp = m->kp_gripper[1]; *kd = m->kd_gripper[1]; }
-  }
-  if (d == m->dof_palm) { *kp = m->kp_gripper[2]; *kd = m->kd_gripper[2]; }
-  if (d == m->dof_base) { *kp = m->kp_base[2]; *kd = m->kd_base[2]; }
-}
-
-static void physics_substep(or_env* e) {
-  const gm_model* m = &e->m;
-  int nv = m->nv;
-  double h = m->timestep;
-  memcpy(e->qpos_pre, e->qpos, sizeof(e->qpos));
-  /* mj_step1 */
-  fk(e);
-  crb(e);
-  collision(e);
-  rne_bias(e);
-  for (int d = 0; d < nv; d++) {
-    int j = m->body_jnt[m->dof_body[d]];
-    e->qfrc_passive[d] = 0;
-    if (m->jnt_type[j] != GM_JNT_FREE) e->qfrc_passive[d] -= m->jnt_stiffness[j] * e->qpos[d];
-    e->qfrc_passive[d] -= m->jnt_damping[j] * e->qvel[d];
-  }
-  /* control between step1 and step2 */
-  control(e, e->qfrc_act);
-  /* mj_step2 (MuJoCo 2.1.5 Euler): joint springs explicit (qfrc_passive above), joint
-   * damping implicit in the factored matrix; the PD motor gains are folded in implicitly
-   * as well (engine spec) */
-  double H[NV][NV];
-  memcpy(H, e->M, sizeof(H));
-  for (int d = 0; d < nv; d++) {
-    /* implicit joint damping (mj_Euler) and implicit PD motor gains (engine spec) */
-    int j = m->body_jnt[m->dof_body[d]];
-    double kp, kd;
-    ctrl_gains(m, d, &kp, &kd);
-    double add = m->jnt_armature[j] + h * (m->jnt_damping[j] + kd);
-    if (m->jnt_type[j] != GM_JNT_FREE) add += h * h * kp;
-    H[d][d] += add;
-  }
-  factor(e, H);
-  double f[NV];
-  for (int d = 0; d < nv; d++) f[d] = e->qfrc_passive[d] + e->qfrc_act[d] - e->qfrc_bias[d];
-  if (e->tip_force != 0.0) {
-    /* resolve_segment_forces -> apply_segment_force (myfunctions.cpp:1642-1727): an
-     * xfrc_applied force at each finger's tip-link centre of mass along the finger's
-     * rest bending direction; J^T F into the generalized forces */
-    for (int fi = 0; fi < 3; fi++) {
-      int bt = m->body_tip[fi];
-      double F[3] = {e->tip_force * m->tip_dir[fi][0], e->tip_force * m->tip_dir[fi][1],
-                     e->tip_force * m->tip_dir[fi][2]};
-      for (int d = 0; d < nv; d++) {
-        if (!is_ancestor_body(m, m->dof_body[d], bt)) continue;
-        double col[3];
-        jac_point_col(e, d, e->xipos[bt], col);
-        f[d] += dot3(col, F);
-      }
-    }
-  }
-  solve(e, e->qacc_smooth, f);
-  constraint_solve(e);
-  double jtf[NV];
-  for (int d = 0; d < nv; d++) jtf[d] = 0;
-  for (int r = 0; r < e->nefc; r++)
-    for (int d = 0; d < nv; d++) jtf[d] += e->J[r][d] * e->efc_f[r];
-  double dq[NV];
-  solve(e, dq, jtf);
-  for (int d = 0; d < nv; d++) e->qacc[d] = e->qacc_smooth[d] + dq[d];
-  /* mj_checkAcc -> mjWARN_BADQACC (is_sim_unstable, myfunctions.cpp:4233-4242) */
-  for (int d = 0; d < nv; d++) if (!(fabs(e->qacc[d]) <= 1e10)) e->badqacc = 1;
-  /* semi-implicit Euler */
-  for (int d = 0; d < nv; d++) e->qvel[d] += h * e->qacc[d];
-  for (int b = 1; b < m->nbody; b++) {
-    int j = m->body_jnt[b];
-    if (j < 0) continue;
-    int qa = m->jnt_qposadr[j], da = m->jnt_dofadr[j];
-    if (m->jnt_type[j] == GM_JNT_FREE) {
-      for (int k = 0; k < 3; k++) e->qpos[qa + k] += h * e->qvel[da + k];
-      double* q = &e->qpos[qa + 3];
-      const double* w = &e->qvel[da + 3];
-      double wn = norm3(w);
-      if (wn > 1e-15) {
-        double ang = wn * h;
-        double s = sin(0.5 * ang) / wn, c = cos(0.5 * ang);
-        double dq4[4] = {c, w[0] * s, w[1] * s, w[2] * s};
-        quatmul(q, q, dq4);
-      }
-      quatnorm(q);
-    } else {
-      e->qpos[qa] += h * e->qvel[da];
-    }
-  }
-  e->time += h;
-}
+#include "physics.c"
 
 /* =====================================================================
  * after_step: update_all -> update_stepper / update_constraints, antiroll
@@ -1264,8 +470,10 @@ void or_gauge_points(const gm_model* m, const double* q, double* X, double* Y) {
   double cum = 0;
   for (int i = 0; i < N; i++) {
     cum = (i == 0) ? q[0] : cum + q[i];
-    X[i + 1] = X[i] + m->segment_length * cos(cum);
-    Y[i + 1] = Y[i] + m->segment_length * sin(cum);
+    double sn, cs;
+    gm_sincos(cum, &sn, &cs);
+    X[i + 1] = X[i] + m->segment_length * cs;
+    Y[i + 1] = Y[i] + m->segment_length * sn;
   }
 }
 
@@ -1853,6 +1061,7 @@ void or_step(or_env* e) {
 static void keyframe_state(or_env* e) {
   for (int i = 0; i < NQ; i++) e->qpos[i] = e->m.qpos0[i];
   for (int i = 0; i < NV; i++) e->qvel[i] = 0;
+  for (int i = 0; i < NV; i++) e->qacc_warm[i] = 0;
   e->time = 0;
   e->last_step_time = 0;
 }
@@ -1902,17 +1111,19 @@ void or_spawn(or_env* e, const gm_spawn* sp) {
   if (oi < 0 || oi >= e->nobj) oi = 0;
   e->obj_index = oi;
   apply_object(&e->m, &e->objs[oi]);
+  object_invweight(e);
   int qa = e->m.jnt_qposadr[e->m.body_jnt[e->m.body_obj]];
   double zr = sp ? sp->zrot : 0.0;
   /* quaternion exactly as the reference composes it: QPos (x,y,z,qx,qy,qz,qw) with
    * qx written to qpos[3] (MuJoCo's w slot) -- net effect: rotation pi+zrot about z */
-  double x2 = sin(-zr / 2.0), w2 = cos(-zr / 2.0);
-  double qw = w2, qx = x2, qy = 0, qz = 0;
+  double x2, w2;
+  gm_sincos(-zr / 2.0, &x2, &w2);
+  const double q4[4] = {x2, 0, 0, w2};
+  const double nq = sqrt(q4[0] * q4[0] + q4[1] * q4[1] + q4[2] * q4[2] + q4[3] * q4[3]);
   e->qpos[qa + 0] = sp ? sp->x : 0.0;
   e->qpos[qa + 1] = sp ? sp->y : 0.0;
   e->qpos[qa + 2] = object_rest_z(&e->objs[oi]) + 1e-6;
-  e->qpos[qa + 3] = qx; e->qpos[qa + 4] = qy; e->qpos[qa + 5] = qz; e->qpos[qa + 6] = qw;
-  quatnorm(&e->qpos[qa + 3]);
+  for (int k = 0; k < 4; k++) e->qpos[qa + 3 + k] = q4[k] / nq;
   for (int k = 0; k < 6; k++) e->qvel[e->m.dof_obj + k] = 0;
   for (int k = 0; k < 7; k++) e->start_qpos[k] = e->qpos[qa + k];
 }
@@ -2221,6 +1432,17 @@ int or_calibrate(const gm_model* m, const gm_config* c, const gm_object* objects
   return 0;
 }
 
+/* test hook: the constraint solver of envs created from now on (0 Newton, > 0 PGS sweeps) */
+static int g_solver_pgs = 0;
+void or_set_default_solver(int pgs_sweeps) { g_solver_pgs = pgs_sweeps; }
+void or_set_solver(or_env* e, int pgs_sweeps) { e->solver_pgs = pgs_sweeps; }
+/* solver statistics since creation: solves, Newton iterations, line-search evaluations,
+ * max iterations, max contacts generated, constraint rows */
+void or_get_stats(const or_env* e, int64_t* out) {
+  out[0] = e->stat_solves; out[1] = e->stat_it_sum; out[2] = e->stat_ls_sum; out[3] = e->stat_it_max;
+  out[4] = e->stat_ncon_max; out[5] = e->stat_nefc_sum;
+}
+
 or_env* or_create(const gm_model* m, const gm_config* c, const gm_object* objects, int n_objects,
                   int64_t env_id) {
   or_env* e = (or_env*)calloc(1, sizeof(or_env));
@@ -2230,9 +1452,11 @@ or_env* or_create(const gm_model* m, const gm_config* c, const gm_object* object
   e->nobj = n_objects > GM_MAX_OBJSET ? GM_MAX_OBJSET : n_objects;
   for (int i = 0; i < e->nobj; i++) e->objs[i] = objects[i];
   e->env_id = env_id;
+  e->solver_pgs = g_solver_pgs;
   e->rng = lcg_seed((uint64_t)c->s.random_seed + (uint64_t)env_id * 1000003ull);
   /* settle with the first object parked at the keyframe pose */
-  if (e->nobj > 0) apply_object(&e->m, &e->objs[0]);
+  topo_init(e);
+  if (e->nobj > 0) { apply_object(&e->m, &e->objs[0]); object_invweight(e); }
   settle(e);
   e->old_x = e->old_y = e->old_z = 0;
   return e;
@@ -2354,6 +1578,7 @@ int or_import_state(or_env* e, const void* state) {
   if (s->obj_index < 0 || s->obj_index >= e->nobj) return -2;
   e->obj_index = s->obj_index;
   apply_object(&e->m, &e->objs[s->obj_index]);
+  object_invweight(e);
   e->time = s->time;
   e->last_step_time = s->last_step_time;
   grip_in(&e->end, &s->end);
@@ -2362,6 +1587,8 @@ int or_import_state(or_env* e, const void* state) {
   for (int k = 0; k < S_N; k++) e->last_read[k] = s->last_read[k];
   for (int i = 0; i < NQ; i++) e->qpos[i] = i < m->nq ? s->qpos[i] : 0.0;
   for (int i = 0; i < NV; i++) e->qvel[i] = i < m->nv ? s->qvel[i] : 0.0;
+  for (int i = 0; i < NV; i++) e->qacc_warm[i] = i < m->nv ? s->qacc_warm[i] : 0.0;
+  e->obj_invw[0] = s->obj_invw[0]; e->obj_invw[1] = s->obj_invw[1];
   for (int k = 0; k < GM_MAX_LOCK; k++) { e->lock_q[k] = s->lock_q[k]; e->lock_active[k] = s->lock_active[k]; }
   for (int k = 0; k < 7; k++) e->start_qpos[k] = s->start_qpos[k];
   for (int k = 0; k < S_N; k++)
@@ -2406,6 +1633,8 @@ void or_export_state(const or_env* e, void* state) {
   for (int k = 0; k < S_N; k++) s->last_read[k] = e->last_read[k];
   for (int i = 0; i < m->nq; i++) s->qpos[i] = e->qpos[i];
   for (int i = 0; i < m->nv; i++) s->qvel[i] = e->qvel[i];
+  for (int i = 0; i < m->nv; i++) s->qacc_warm[i] = e->qacc_warm[i];
+  s->obj_invw[0] = e->obj_invw[0]; s->obj_invw[1] = e->obj_invw[1];
   for (int k = 0; k < GM_MAX_LOCK; k++) { s->lock_q[k] = e->lock_q[k]; s->lock_active[k] = e->lock_active[k]; }
   for (int k = 0; k < 7; k++) s->start_qpos[k] = e->start_qpos[k];
   {

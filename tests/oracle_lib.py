@@ -10,7 +10,7 @@ import os
 import subprocess
 
 import numpy as np
-from gmx._lib import GM_MAX_DOF  # noqa: E402
+from gmx._lib import GM_MAX_CON, GM_MAX_DOF, GM_MAX_EFC  # noqa: E402
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
@@ -68,6 +68,9 @@ def lib():
             "or_std_shuffle": (C.c_uint32, [C.c_uint32, i32, i32p]),
             "or_box2d_overlaps": (i32, [f64p, f64p, C.c_double]),
             "or_calibrate": (i32, [vp, vp, vp, i32, i32, vp, vp, vp, i32]),
+            "or_get_stats": (None, [vp, C.POINTER(C.c_int64)]),
+            "or_set_default_solver": (None, [i32]),
+            "or_set_solver": (None, [vp, i32]),
         }
         for n, (r, a) in sig.items():
             f = getattr(L, n)
@@ -173,8 +176,8 @@ class OracleEnv:
 
     def debug_substep(self):
         n = C.c_int32()
-        con = np.zeros((15, 16), dtype=np.float64)
-        f = np.zeros(64, dtype=np.float64)
+        con = np.zeros((GM_MAX_CON, 16), dtype=np.float64)
+        f = np.zeros(GM_MAX_EFC, dtype=np.float64)
         qacc = np.zeros(self.model.nv)
         d = C.POINTER(C.c_double)
         self.L.or_debug_substep(self.h, C.byref(n), con.ctypes.data_as(d), f.ctypes.data_as(d), qacc.ctypes.data_as(d),
@@ -218,11 +221,12 @@ def batch_step(model, cfg, objects, states, actions=None, discrete=None, threads
 
 def batch_substep(model, cfg, objects, states, threads=None):
     """One MjClass::step with diagnostics for every device state record (threaded).
-    Returns (ncon, nefc, contact [n,15,16], efc [n,64], qacc [n,40], wrench [n,6], states_after)."""
+    Returns (ncon, nefc, contact [n,GM_MAX_CON,16], efc [n,GM_MAX_EFC], qacc [n,GM_MAX_DOF], wrench [n,6],
+    states_after)."""
     st = np.array(states, dtype=np.uint8, copy=True, order="C")
     n = st.shape[0]
     ncon = np.zeros(n, dtype=np.int32); nefc = np.zeros(n, dtype=np.int32)
-    con = np.zeros((n, 15, 16)); efc = np.zeros((n, 64)); qacc = np.zeros((n, GM_MAX_DOF)); w = np.zeros((n, 6))
+    con = np.zeros((n, GM_MAX_CON, 16)); efc = np.zeros((n, GM_MAX_EFC)); qacc = np.zeros((n, GM_MAX_DOF)); w = np.zeros((n, 6))
     rc = lib().or_batch_substep(model.ptr, cfg.ptr, C.cast(objects, C.c_void_p), len(objects), n, st.ctypes.data,
                                 ncon.ctypes.data, nefc.ctypes.data, con.ctypes.data, efc.ctypes.data, qacc.ctypes.data,
                                 w.ctypes.data, threads or n_threads())

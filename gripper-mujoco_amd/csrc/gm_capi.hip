@@ -219,6 +219,31 @@ int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
     T.lock_grp[k] = T.body_group[b];
     T.lock_cpos[k] = T.body_cpos[b];
   }
+  // per scan lane: the lane body's pairs with the object / the ground (oracle topo_init)
+  T.lane_obj = 50;
+  T.pair_gobj = -1;
+  for (int l = 0; l < 64; l++)
+    for (int s = 0; s < 2; s++) { T.lane_opair[l][s] = -1; T.lane_gpair[l][s] = -1; }
+  for (int pr = 0; pr < m.npair; pr++) {
+    const int a = m.pair_a[pr], bg = m.pair_b[pr];
+    const bool with_obj = a == m.geom_obj || bg == m.geom_obj;
+    const bool with_gnd = a == m.geom_ground || bg == m.geom_ground;
+    if (with_obj && with_gnd) {
+      if (T.pair_gobj >= 0) { err = "more than one object-ground pair"; return GM_E_RANGE; }
+      T.pair_gobj = pr;
+      continue;
+    }
+    if (!with_obj && !with_gnd) { err = "gripper self-collision pairs are not supported"; return GM_E_RANGE; }
+    const int g = with_obj ? (a == m.geom_obj ? bg : a) : (a == m.geom_ground ? bg : a);
+    const int b = m.geom_body[g];
+    for (int l = 0; l < 64; l++) {
+      if (T.lane_body[l] != b || l == T.lane_obj) continue;
+      int32_t* slot = with_obj ? T.lane_opair[l] : T.lane_gpair[l];
+      if (slot[0] < 0) slot[0] = pr;
+      else if (slot[1] < 0) slot[1] = pr;
+      else { err = "a body has more than two object (or ground) pairs"; return GM_E_RANGE; }
+    }
+  }
   return GM_OK;
 }
 
@@ -761,9 +786,17 @@ int gm_get_env_states(gm_ctx* c, void* out) {
 int gm_set_env_states(gm_ctx* c, const void* in) {
   if (!c || !in) return GM_E_ARG;
   const GmEnvState* h = (const GmEnvState*)in;
-  for (int e = 0; e < c->n_envs; e++)
-    if (h[e].obj_index < 0 || h[e].obj_index >= c->n_objects || h[e].extra_substeps < 0)
-      return fail(c, GM_E_ARG, "gm_set_env_states: env " + std::to_string(e) + " is not a valid state");
+  // every field the kernels use as an index or a flag (a bad ring index would address
+  // outside the env's sensor windows)
+  for (int e = 0; e < c->n_envs; e++) {
+    const GmEnvState& r = h[e];
+    bool ok = r.obj_index >= 0 && r.obj_index < c->n_objects && r.extra_substeps >= 0 && r.cal_steps >= 0 &&
+              r.num_action_steps >= 0 && (r.done == 0 || r.done == 1) &&
+              (r.obj_type == GM_GEOM_BOX || r.obj_type == GM_GEOM_CYLINDER || r.obj_type == GM_GEOM_SPHERE);
+    for (int st = 0; st < GM_NSTREAM; st++) ok = ok && r.ring_i[st] >= -1 && r.ring_i[st] < GM_RING;
+    for (int k = 0; k < GM_MAX_LOCK; k++) ok = ok && (r.lock_active[k] == 0 || r.lock_active[k] == 1);
+    if (!ok) return fail(c, GM_E_ARG, "gm_set_env_states: env " + std::to_string(e) + " is not a valid state");
+  }
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipMemcpyAsync(c->d_state, in, sizeof(GmEnvState) * (size_t)c->n_envs, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "gm_state.h"
+#include "gm_math.h"
 
 #define NT 64
 // gm_step_kernel is instantiated per finger chain length (CL = n_seg + 2) so every chain
@@ -52,7 +53,8 @@ struct DebugOut {
   int32_t* nefc;      // [n_envs]
   double* wrench;     // [n_envs][6] the live object's cfrc_ext, [force; torque]
 };
-#define GM_NPHASE 26   // 0-23 shader clocks (see gmx.env PHASES), 24: sum of nefc, 25: substeps running MPR
+#define GM_NPHASE 28   // 0-23 shader clocks (see gmx.env PHASES), 24: sum of nefc, 25: substeps running MPR,
+                       // 26: Newton iterations, 27: line-search evaluations
 
 // Per-env LDS image, sized for the compile-time finger chain length CL = n_seg + 2:
 // NB = 3 CL + 4 bodies (world, base, 3 x CL finger links, palm, object),
@@ -64,22 +66,25 @@ struct __align__(16) SharedT {
   static constexpr int TRIC = (CL + 1) * (CL + 2) / 2;
   GmEnvHot s;                     // the env's state minus its sensor windows
   real lock_pre[GM_MAX_LOCK];     // pre-integration qpos of the lock dofs (weld re-anchoring)
-  real qacc[NV], z[NV];   // qacc: smooth, then total acceleration
+  real qacc[NV];                  // the Newton iterate; the substep's qacc at the end
+  real xs[NV];                    // the Newton point x (line search: the step d = x - q)
+  real Ma[NV], Mv[NV];            // H~ q and H~ d
   real xpos[NB][3];
   real xquat[NB][4];   // normalised body orientations; xmat = quat2mat(xquat)
-  real Hf[3][TRIC], Hp[3], Ho[21], Hbb;
-  real Df[3][CL + 1], Dp[2], Do[6], Dbb;   // INVERSE pivots 1/D of the LTDL factor
-  real bdelta[5];
-  // contact record: dist, pos[3], normal[3], mu, force[3] (contact frame); the
-  // tangents are make_frame(normal) wherever they are needed
-  real con[GM_MAX_CON][11];
+  real Hf[3][TRIC], Hp[3], Ho[21], Hbb;   // H~ tree blocks (finger rows p = 0 base .. CL)
+  real cdof[NV][6];
+  real frc[NV];                   // smooth force: passive + PD actuation - bias
+  real go[27];                    // the object's ground-contact K (21) and force (6)
+  // contact record: dist, pos[3], normal[3], t1[3] (t2 = normal x t1), mu, force[3]
+  // (contact frame, after the solve)
+  real con[GM_MAX_CON][14];
   int32_t cgeom[GM_MAX_CON][2];   // canonical (geom1, geom2)
-  // LDS shared in time: the dynamics / collision scratch is dead once every lane has
-  // built its constraint row, so the compact Jacobian rows reuse it
+  int16_t pair_off[GM_MAX_PAIR], pair_cnt[GM_MAX_PAIR];   // contact slots of each candidate pair
+  // LDS shared in time: the dynamics scratch is dead once H~ and the forces are formed; the
+  // Newton stages then reuse it (body velocities + per-contact Q / F; the chain-root stage;
+  // the factor's transfers; the debug copy of the row forces)
   union {
-    struct {                  // kinematics .. constraint rows
-      real cdof[NV][6];
-      real frc[NV];
+    struct {                  // kinematics .. mass matrix
       union {                 // composite inertia accumulates in place over cinert
         real cinert[NB][10];
         real Ic[NB][10];
@@ -87,14 +92,13 @@ struct __align__(16) SharedT {
       real cfrc[NB][6];
       real chain_f[5][6], chain_I[5][10];   // chain-root sums for the base body
     };
-    struct {                  // constraint rows .. constraint accelerations
-      real Y[GM_MAX_EFC][CW - 1];
-      int32_t ygrp[GM_MAX_EFC];   // chain group of each row (-1: object / locks only)
-    };
+    struct { real V[NB][6]; real QF[GM_MAX_CON][9]; } nw;
+    struct { real root[4][54]; real comp[54]; real oo[27]; } st;
+    struct { real lbub[3][CL][14]; real plb[14]; real bbx[28]; real ych[3][CL]; real ypalm; } fs;
+    struct { real efc[GM_MAX_EFC]; } dbg;
   };
-  real efc_f[GM_MAX_EFC];
-  int32_t ncon, nefc, nlockrows, overflow;
-  int32_t work_nefc, work_mpr;    // this env-step's constraint rows / substeps running MPR (dispatch cost model)
+  int32_t ncon, nefc, nl, overflow;
+  int32_t work_nefc, work_mpr, work_newton;   // this env-step's rows / MPR substeps / Newton iterations
   int32_t stp_fixed;              // update_all: `next` is a fixed point of the stepper this env-step (see there)
   float forces[32];            // extract_forces_faster results (see extract_forces)
   int32_t have_forces;
@@ -339,7 +343,7 @@ __device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const
         lp[0] += wa[0] * qv; lp[1] += wa[1] * qv; lp[2] += wa[2] * qv;
       } else if (type == GM_JNT_HINGE) {
         real sn, cs;
-        sincos(0.5 * qv, &sn, &cs);
+        gm_sincos(0.5 * qv, &sn, &cs);   // shared with the oracle (gm_math.h)
         const real ql[4] = {cs, ax[0] * sn, ax[1] * sn, ax[2] * sn};
         quatmul(lq, lq, ql);
       }
@@ -767,169 +771,6 @@ __device__ void mass_and_forces(SharedT<CL>& S, const gm_model* __restrict__ m, 
   __syncthreads();
 }
 
-// ============================================================ LTDL factor + solves
-// Tree LTDL of H~ (mj_factorM restated for the canonical tree) on the DPP-row layout:
-// DPP rows 0..2 hold the three finger blocks (base + chain) -- lane 16 f + p holds the
-// symmetric row p of finger f's block, p = 0 being the base column -- and lanes 48..53
-// the free object's 6x6 block.  The palm's 1-dof chain is done by lane 63 alone.  The
-// chains meet only in the base pivot: each finger / palm block returns its Schur
-// contribution (bdelta) and the base pivot is formed afterwards.
-// Factor: pivots k = CL..1 (object: 5..1); the pivot row is broadcast inside every DPP
-// row with row_newbcast:k and each lane p < k eliminates with its own (upper) element.
-template <int CL>
-__device__ void factor(SharedT<CL>& S, const GmTopo* __restrict__ T, int lane) {
-  const int rowf = lane >> 4, p = lane & 15;
-  const bool fing = rowf < 3 && p <= CL;
-  const bool obj = rowf == 3 && p < 6;
-  real h[CL + 1];
-#pragma unroll
-  for (int j = 0; j <= CL; j++) {
-    const int lo = p < j ? p : j, hi = p < j ? j : p;
-    real v = 0;
-    if (fing) {
-      if (hi > 0) v = S.Hf[rowf][TRI(hi, lo)];   // (0, 0) is the base pivot: not in the block
-    } else if (obj) {
-      if (j < 6) v = S.Ho[TRI(hi, lo)];
-    }
-    h[j] = v;
-  }
-#pragma unroll
-  for (int k = CL; k >= 1; k--) {
-    const bool act = fing || (obj && k <= 5);
-    const real hkk = row_bcast(h[k], k);
-    const real ihk = rcp_n(hkk);
-    const real a = h[k] * ihk;             // L[k][p] for p < k
-    real hk[CL];
-#pragma unroll
-    for (int j = 0; j < k; j++) hk[j] = row_bcast(h[j], k);
-#ifdef GM_FACTOR_BRANCHY
-    if (act && p < k) {
-#pragma unroll
-      for (int j = 0; j < k; j++) h[j] -= hk[j] * a;
-      h[k] = a;
-    }
-    if (act && p == k) {
-#pragma unroll
-      for (int j = 0; j < k; j++) h[j] *= ihk;   // row k of L; the pivot stays in h[k]
-    }
-#else
-    // branch-free: rows p < k take h[j] - hk[j] a, the pivot row (p == k) h[j] / hkk (row
-    // k of L; the pivot stays in h[k]), every other lane h[j] - hk[j] 0 == h[j]; one
-    // update shape for all lanes instead of two predicated blocks (whose merges the
-    // compiler resolved with a register copy of the whole row per pivot)
-    const bool upd = act && p < k;
-    const real aa = upd ? a : 0.0;
-    const real sc = (act && p == k) ? ihk : 1.0;
-#pragma unroll
-    for (int j = 0; j < k; j++) h[j] = (h[j] - hk[j] * aa) * sc;
-    h[k] = upd ? a : h[k];
-#endif
-  }
-  if (fing) {
-    if (p >= 1) {
-      real* Hs = S.Hf[rowf];
-#pragma unroll
-      for (int j = 0; j < CL; j++) if (j < p) Hs[TRI(p, j)] = h[j];
-      Hs[TRI(p, p)] = h[p];
-      S.Df[rowf][p] = rcp_n(h[p]);
-    } else {
-      S.bdelta[rowf] = -h[0];   // the base row accumulated -sum_k L[k][0]^2 D_k
-    }
-  } else if (obj) {
-#pragma unroll
-    for (int j = 0; j < 5; j++) if (j < p) S.Ho[TRI(p, j)] = h[j];
-    S.Ho[TRI(p, p)] = h[p];
-    S.Do[p] = rcp_n(h[p]);
-  } else if (lane == 63) {
-    const real h11 = S.Hp[TRI(1, 1)], h10 = S.Hp[TRI(1, 0)];
-    const real ih = rcp_n(h11);
-    const real a = h10 * ih;
-    S.bdelta[3] = h10 * a;
-    S.Hp[TRI(1, 0)] = a;
-    S.Dp[1] = rcp_n(h11);
-  }
-  __syncthreads();
-  if (lane == 0) S.Dbb = rcp_n(S.Hbb - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3]));
-  __syncthreads();
-}
-
-// L^T y = b on the DPP-row layout (leaves -> root): lane p holds y_p and column p of L;
-// a finger row's base lane accumulates -sum_k L[k][0] y_k.  Then y <- D^-1 y.
-template <int CL>
-__device__ __forceinline__ real rows_LT_D(SharedT<CL>& S, int rowf, int p, bool fing, bool obj, real y) {
-  real Lc[CL + 1];
-#pragma unroll
-  for (int k = 0; k <= CL; k++) {
-    real v = 0;
-    if (fing) { if (k > p) v = S.Hf[rowf][TRI(k, p)]; }
-    else if (obj) { if (k > p && k < 6) v = S.Ho[TRI(k, p)]; }
-    Lc[k] = v;
-  }
-  // Lc[k] is an exact zero wherever the update does not apply (k <= p, k > 5 on the
-  // object row, lanes off the blocks), so the update runs unpredicated
-#pragma unroll
-  for (int k = CL; k >= 1; k--) {
-    const real yk = row_bcast(y, k);
-    y -= Lc[k] * yk;
-  }
-  if (fing) { if (p >= 1) y *= S.Df[rowf][p]; }
-  else if (obj) y *= S.Do[p];
-  return y;
-}
-// x = L^-1 y on the DPP-row layout (root -> leaves); a finger row's base lane holds the
-// base solution
-template <int CL>
-__device__ __forceinline__ real rows_L(SharedT<CL>& S, int rowf, int p, bool fing, bool obj, real y) {
-  real Lr[CL];
-#pragma unroll
-  for (int k = 0; k < CL; k++) {
-    real v = 0;
-    if (fing) { if (k < p) v = S.Hf[rowf][TRI(p, k)]; }
-    else if (obj) { if (k < p) v = S.Ho[TRI(p, k)]; }
-    Lr[k] = v;
-  }
-  // Lr[k] is an exact zero wherever the update does not apply (unpredicated, as above)
-#pragma unroll
-  for (int k = 0; k < CL; k++) {
-    const real xk = row_bcast(y, k);
-    y -= Lr[k] * xk;
-  }
-  return y;
-}
-
-// x = H~^-1 b over full dof vectors (b, x in LDS, may alias)
-template <int CL>
-__device__ void solve_full(SharedT<CL>& S, const GmTopo* __restrict__ T, const real* b, real* x, int lane) {
-  const int rowf = lane >> 4, p = lane & 15;
-  const bool fing = rowf < 3 && p <= CL;
-  const bool obj = rowf == 3 && p < 6;
-  real y = 0;
-  if (fing) { if (p >= 1) y = b[T->dof_f0[rowf] + p - 1]; }
-  else if (obj) y = b[T->dof_obj + p];
-  y = rows_LT_D<CL>(S, rowf, p, fing, obj, y);
-  real ypalm = 0;
-  if (fing && p == 0) S.bdelta[rowf] = -y;
-  if (lane == 63) {
-    const real y1 = b[T->dof_palm];
-    S.bdelta[3] = S.Hp[TRI(1, 0)] * y1;
-    ypalm = y1 * S.Dp[1];
-  }
-  __syncthreads();
-  const real xbase = (b[T->dof_base] - (S.bdelta[0] + S.bdelta[1] + S.bdelta[2] + S.bdelta[3])) * S.Dbb;
-  __syncthreads();
-  if (fing && p == 0) y = xbase;
-  y = rows_L<CL>(S, rowf, p, fing, obj, y);
-  if (fing) {
-    if (p >= 1) x[T->dof_f0[rowf] + p - 1] = y;
-    else if (rowf == 0) x[T->dof_base] = xbase;
-  } else if (obj) {
-    x[T->dof_obj + p] = y;
-  } else if (lane == 63) {
-    x[T->dof_palm] = ypalm - S.Hp[TRI(1, 0)] * xbase;
-  }
-  __syncthreads();
-}
-
 // ============================================================ collision
 struct Hit { real dist, pos[3], n[3]; };
 
@@ -1307,13 +1148,18 @@ __device__ void write_contact(SharedT<CL>& S, int slot, int g1, int g2, const Hi
   real* C = S.con[slot];
   C[0] = h.dist;
   C[1] = h.pos[0]; C[2] = h.pos[1]; C[3] = h.pos[2];
-  C[4] = h.n[0]; C[5] = h.n[1]; C[6] = h.n[2];
-  C[7] = mu;
-  C[8] = 0; C[9] = 0; C[10] = 0;
+  real F[9];
+  make_frame(F, h.n);
+  C[4] = F[0]; C[5] = F[1]; C[6] = F[2];
+  C[7] = F[3]; C[8] = F[4]; C[9] = F[5];
+  C[10] = mu;
+  C[11] = 0; C[12] = 0; C[13] = 0;
   S.cgeom[slot][0] = g1; S.cgeom[slot][1] = g2;
 }
 
 __host__ __device__ constexpr int gm_pair_batches(int CL) { return CL <= 10 ? 1 : 2; }
+
+#include "gm_newton.hip"
 
 template <int CL>
 __device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
@@ -1330,10 +1176,12 @@ __device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const 
   for (int bi = 0; bi < NBATCH; bi++) {
     const int pr = bi * NT + lane;
     int cnt = 0, kind = 0, g1 = 0, g2 = 0;
-    unsigned hm = 0;   // plane-box / plane-cylinder: the counted corners (pass 2 revisits only these)
+    unsigned hm = 0;   // multi-point colliders: the counted candidates (pass 2 revisits only these)
     Hit single;
     GeomV A, B;
     CylFrame cf;
+    BBox bbs;
+    real ea[3], eb[3], da[3], db[3];
     if (pr < T->npair) {
       const int a = T->pr_g[pr][0], b = T->pr_g[pr][1];
       const int ta0 = T->pr_type[pr][0], tb0 = T->pr_type[pr][1];
@@ -1378,6 +1226,23 @@ __device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const 
           }
         } else if (A.type == GM_GEOM_SPHERE && B.type == GM_GEOM_BOX) {
           kind = 1; cnt = sphere_box(A, B, single);
+        } else if (A.type == GM_GEOM_BOX && B.type == GM_GEOM_BOX) {
+          // mjc_BoxBox: separating axes, then the face-clipped manifold or one edge contact
+          bb_setup(A, B, bbs, ea, eb, da, db);
+          if (bbs.kind == 1) {
+            kind = 4;
+#pragma unroll
+            for (int i = 0; i < BB_NCAND; i++) {
+              if (cnt < 8) {
+                real P[3], dep;
+                const int ok = bb_face_cand(bbs, i, P, dep);
+                hm |= (unsigned)ok << i;
+                cnt += ok;
+              }
+            }
+          } else if (bbs.kind == 2) {
+            kind = 1; cnt = bb_edge_hit(bbs, ea, eb, da, db, single);
+          }
         } else {
           ran_mpr = true;
           kind = 1; cnt = mpr(A, B, (real)m->mpr_tolerance, m->mpr_iterations, single);
@@ -1388,19 +1253,33 @@ __device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const 
 #ifdef GM_PHASE_SPLIT_COLL
     PH(16);   // developer split: broadphase + narrowphase
 #endif
-    // contact slots: exclusive prefix sum of the per-lane counts (0..4, three bits) from
-    // three ballots -- no LDS round trip
+    // contact slots: exclusive prefix sum of the per-lane counts (0..8, four bits) from
+    // four ballots -- no LDS round trip
     int off = written, total = 0;
 #pragma unroll
-    for (int bit = 0; bit < 3; bit++) {
+    for (int bit = 0; bit < 4; bit++) {
       const unsigned long long bal = __ballot((cnt >> bit) & 1);
       off += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u)) << bit;
       total += __popcll(bal) << bit;
     }
+    if (pr < T->npair) { S.pair_off[pr] = (int16_t)off; S.pair_cnt[pr] = (int16_t)cnt; }
     if (cnt > 0) {
       real mu = fmax(A.friction, B.friction);
       if (kind == 1) {
         if (off < GM_MAX_CON) write_contact(S, off, g1, g2, single, mu);
+      } else if (kind == 4) {
+        int w = 0;
+#pragma unroll
+        for (int i = 0; i < BB_NCAND; i++) {
+          if ((hm >> i) & 1u) {
+            real P[3], dep;
+            Hit t;
+            bb_face_cand(bbs, i, P, dep);
+            bb_face_hit(bbs, P, dep, t);
+            if (off + w < GM_MAX_CON) write_contact(S, off + w, g1, g2, t, mu);
+            w++;
+          }
+        }
       } else {
         Hit t;
         int w = 0;
@@ -1430,624 +1309,6 @@ __device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const 
   __syncthreads();
 }
 
-// ============================================================ constraints + PGS
-__device__ __forceinline__ int geom_chain(const GmTopo* T, int g) { return T->geom_group[g]; }
-
-// compact Jacobian row of contact c along unit direction `dir` (rows of the frame)
-// compact Jacobian row of contact c along the world direction `dir` (linear in dir, so
-// a pyramid edge n +- mu t is one pass); chain columns are unrolled to CL
-template <int CL>
-__device__ void contact_jac(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int c,
-                            const real* dir, real* J, int& grp) {
-#pragma unroll
-  for (int k = 0; k < CW; k++) J[k] = 0;
-  const real* C = S.con[c];
-  const real pos[3] = {C[1], C[2], C[3]};
-  grp = -1;
-#pragma unroll
-  for (int side = 0; side < 2; side++) {
-    const int g = S.cgeom[c][side];
-    const int grpg = T->geom_group[g];
-    if (grpg < 0) continue;
-    const real sgn = side == 0 ? -1.0 : 1.0;
-    if (grpg == GM_GRP_OBJECT) {
-#pragma unroll
-      for (int k = 0; k < 6; k++) {
-        const real* cd = S.cdof[T->dof_obj + k];
-        real wxp[3];
-        cross3(wxp, cd, pos);
-        const real col[3] = {cd[3] + wxp[0], cd[4] + wxp[1], cd[5] + wxp[2]};
-        J[k] += sgn * dot3(dir, col);
-      }
-    } else {
-      grp = grpg;
-      const int P = T->geom_cpos[g];
-      const int d0 = (grpg < 3) ? T->dof_f0[grpg] : T->dof_palm;
-#pragma unroll
-      for (int q = 0; q <= CL; q++) {
-        if (q > P) continue;
-        const int d = (q == 0) ? T->dof_base : d0 + q - 1;
-        const real* cd = S.cdof[d];
-        real wxp[3];
-        cross3(wxp, cd, pos);
-        const real col[3] = {cd[3] + wxp[0], cd[4] + wxp[1], cd[5] + wxp[2]};
-        J[6 + q] += sgn * dot3(dir, col);
-      }
-    }
-  }
-}
-
-// Y = J L^-1 on a compact row (in place)
-template <int CL>
-__device__ void row_LTsolve(SharedT<CL>& S, real* J, int grp) {
-#pragma unroll
-  for (int k = 5; k >= 1; k--)
-#pragma unroll
-    for (int i = k - 1; i >= 0; i--) J[i] -= S.Ho[TRI(k, i)] * J[k];
-  if (grp >= 0 && grp < 3) {
-    const real* Hs = S.Hf[grp];
-#pragma unroll
-    for (int k = CL; k >= 1; k--) {
-#pragma unroll
-      for (int i = k - 1; i >= 1; i--) J[6 + i] -= Hs[TRI(k, i)] * J[6 + k];
-      J[6] -= Hs[TRI(k, 0)] * J[6 + k];
-    }
-  } else if (grp == 3) {
-    J[6] -= S.Hp[TRI(1, 0)] * J[7];
-  }
-}
-template <int CL>
-__device__ __forceinline__ real row_dot_dofs(SharedT<CL>& S, const GmTopo* __restrict__ T, const real* J, int grp, const real* v) {
-  real acc = 0;
-#pragma unroll
-  for (int k = 0; k < 6; k++) acc += J[k] * v[T->dof_obj + k];
-  if (grp >= 0 && grp < 3) {
-    acc += J[6] * v[T->dof_base];
-    const int d0 = T->dof_f0[grp];
-#pragma unroll
-    for (int q = 1; q <= CL; q++) acc += J[6 + q] * v[d0 + q - 1];
-  } else if (grp == 3) {
-    acc += J[6] * v[T->dof_base];
-    acc += J[7] * v[T->dof_palm];
-  }
-  return acc;
-}
-
-__device__ __forceinline__ real impedance(const gm_model* __restrict__ m, real r) {
-  real dmin = m->solimp[0], dmax = m->solimp[1], width = m->solimp[2];
-  real mid = m->solimp[3], pw = m->solimp[4];
-  if (dmin == dmax || width <= 1e-15) return dmin;
-  real x = div_n(fabs(r), width);
-  if (x >= 1) return dmax;
-  if (x <= 0) return dmin;
-  real y;
-  if (pw == 1) y = x;
-  else if (pw == 2) y = (x <= mid) ? div_n(x * x, mid) : 1 - div_n((1 - x) * (1 - x), 1 - mid);   // MuJoCo's default power
-  else if (x <= mid) y = pow(x, pw) / pow(mid, pw - 1);
-  else y = 1 - pow(1 - x, pw) / pow(1 - mid, pw - 1);
-  return dmin + y * (dmax - dmin);
-}
-
-// ---------------------------------------------------------------- PGS, nefc <= 32
-// Small problems (the common case: <= 7 contacts) run on a replicated DPP-row layout:
-// every 16-lane row holds the whole problem, lane p of each row owning constraint rows p
-// ("set 0") and p + 16 ("set 1").  A row update then needs its change d only inside the
-// lane's own 16-lane row, which v_fmac_f64_dpp row_newbcast delivers as the FMA's source
-// operand -- no v_readlane / SGPR round trip on the dependent chain (fma -> max -> sub ->
-// fmac_dpp).  The arithmetic per row is the general path's, operation for operation
-// (f_n = max(u_r, lb_r), d = f_n - f_r, u_j <- fma(-B_j[r], d, u_j)), so the two paths
-// give bit-identical forces.
-
-// value of lane addr/4 (ds_bpermute: the LDS crossbar, no LDS storage), 64-bit
-__device__ __forceinline__ real bperm_f64(int addr, real x) {
-  const long long b = __double_as_longlong(x);
-  const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)b);
-  const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(b >> 32));
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// max(u, lb) without the canonicalising v_max x,x the compiler puts in front of fmax()
-// of a value it cannot prove canonical (u is a finite FMA result; lb is 0 or -inf)
-__device__ __forceinline__ real vmax_f64(real a, real b) {
-  real r;
-  asm volatile("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-
-// One row R of the small-problem sweep: the general path's arithmetic (f_n = max(u_R, lb_R),
-// d = f_n - f_R, u_j <- fma(-B_j[R], d, u_j), f_R <- f_n).  The row's target u_R is
-// broadcast inside each 16-lane row (v_mov_b64_dpp row_newbcast from lane R & 15), so
-// every lane computes the same f_n and d and keeps the row's force in a register of its
-// own (fr[R], identical on all lanes): the force update is a register rename instead of
-// a one-hot select, 4 VALU per row (5 with TWO) instead of 6 (7).  The dependent chain per
-// row stays bcast -> max -> sub -> fma.  Rows past GM_PGS_FR (only when nefc > GM_PGS_FR)
-// keep the one-hot select on the lane that owns them: replicated registers for all 32
-// rows spill.
-#define GM_PGS_FR 24
-template <int R, bool TWO>
-__device__ __forceinline__ void pgs_small_row(real& u0, real& u1, real* fr, real& f1, const real* lbr,
-                                              const real* nB0, const real* nB1) {
-  constexpr int P = R & 15;
-  if constexpr (R < GM_PGS_FR) {
-    // lock rows come first (nl <= 4): rows 0..3 take the lock / contact bound, rows >= 4
-    // are contact edges or padding
-    const real lb = (R < 4) ? lbr[R] : 0.0;
-    const real ub = row_bcast((R < 16) ? u0 : u1, P);
-    const real fn = vmax_f64(ub, lb);
-    const real d = fn - fr[R];
-    u0 = fma(nB0[R], d, u0);                  // == fma(-B_j[r], d, u_j): nB = -B exactly
-    if constexpr (TWO) u1 = fma(nB1[R], d, u1);
-    fr[R] = fn;
-  } else {
-    // lanes p == P of every 16-lane row own row R (set 1): a scalar constant mask
-    const bool mine = __builtin_amdgcn_inverse_ballot_w64(0x0001000100010001ull << P);
-    const real fn = vmax_f64(u1, 0.0);
-    const real d = row_bcast(fn - f1, P);
-    u1 = fma(nB1[R], d, u1);
-    u0 = fma(nB0[R], d, u0);
-    f1 = mine ? fn : f1;
-  }
-}
-
-template <int C, bool TWO>
-__device__ __forceinline__ void pgs_small_chunk(real& u0, real& u1, real* fr, real& f1, const real* lbr,
-                                                const real* nB0, const real* nB1) {
-  pgs_small_row<4 * C + 0, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
-  pgs_small_row<4 * C + 1, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
-  pgs_small_row<4 * C + 2, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
-  pgs_small_row<4 * C + 3, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
-}
-
-template <int NCH, bool TWO>
-__device__ __forceinline__ void pgs_small_sweeps(int iters, real& u0, real& u1, real* fr, real& f1, const real* lbr,
-                                                 const real* nB0, const real* nB1) {
-  for (int it = 0; it < iters; it++) {
-    pgs_small_chunk<0, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
-    if constexpr (NCH > 1) pgs_small_chunk<1, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
-    if constexpr (NCH > 2) pgs_small_chunk<2, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
-    if constexpr (NCH > 3) pgs_small_chunk<3, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
-    if constexpr (NCH > 4) pgs_small_chunk<4, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
-    if constexpr (NCH > 5) pgs_small_chunk<5, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
-    if constexpr (NCH > 6) pgs_small_chunk<6, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
-    if constexpr (NCH > 7) pgs_small_chunk<7, TWO>(u0, u1, fr, f1, lbr, nB0, nB1);
-  }
-}
-
-// The whole small-problem solve: gather the scaled Delassus columns into the replicated
-// layout (lane p of every 16-lane row gets constraint p and, with TWO, p + 16), run the
-// fixed sweeps over the nchunk live chunks (rows past nefc in the last one are exact
-// no-ops: u = f = 0, lb = 0, zero B entries => d = 0) and write the rows' forces to
-// efc_f[0 .. NR-1] (the caller zeroes the rows past nefc).  nBrow is the general path's
-// lane-per-row scaled column (B_j[r] = ARinv_j AR_jr, zero on the diagonal), negated.
-// The sweeps on the replicated layout: nB0 / nB1 hold, in every 16-lane row, the scaled
-// negated Delassus columns of constraints p and p + 16 (p = lane & 15).
-template <bool TWO>
-__device__ __forceinline__ void pgs_small_solve(const real* nB0, const real* nB1, real u, int nl, int nchunk,
-                                                int iters, int lane, real* efc_f) {
-  constexpr int NR = TWO ? 32 : 16;
-  constexpr int NF = NR < GM_PGS_FR ? NR : GM_PGS_FR;
-  const int p = lane & 15;
-  const int a0 = p << 2, a1 = (p + 16) << 2;
-  real u0 = bperm_f64(a0, u);
-  real u1 = TWO ? bperm_f64(a1, u) : 0.0;
-  const int nls = __builtin_amdgcn_readfirstlane(nl);
-  real lbr[4];
-#pragma unroll
-  for (int r = 0; r < 4; r++) lbr[r] = (r < nls) ? -__builtin_inf() : 0.0;
-  real fr[NF];
-#pragma unroll
-  for (int r = 0; r < NF; r++) fr[r] = 0.0;
-  real f1 = 0.0;   // rows >= GM_PGS_FR: constraint p + 16 of lane p
-  // one branch-free sweep body per chunk count (a scalar branch inside the sweep costs
-  // more than the padding rows it would skip)
-  if constexpr (!TWO) {
-    switch (nchunk) {
-      case 1: pgs_small_sweeps<1, false>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
-      case 2: pgs_small_sweeps<2, false>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
-      case 3: pgs_small_sweeps<3, false>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
-      default: pgs_small_sweeps<4, false>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
-    }
-  } else {
-    switch (nchunk) {
-      case 5: pgs_small_sweeps<5, true>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
-      case 6: pgs_small_sweeps<6, true>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
-      case 7: pgs_small_sweeps<7, true>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
-      default: pgs_small_sweeps<8, true>(iters, u0, u1, fr, f1, lbr, nB0, nB1); break;
-    }
-  }
-  // fr is wave-uniform: lane 0 writes its rows, the owners the rest
-  if (lane == 0) {
-#pragma unroll
-    for (int r = 0; r < NF; r++) efc_f[r] = fr[r];
-  }
-  if (TWO && lane >= GM_PGS_FR - 16 && lane < 16) efc_f[lane + 16] = f1;
-}
-
-// The whole small-problem solve (nefc <= 32) with the Delassus matrix built split across
-// the wave: lane l builds column c of A = Y D^-1 Y^T for K of its rows only -- without
-// TWO (nefc <= 16) c = l & 15 and the rows 4 (l >> 4) .. + 3, with TWO (nefc <= 32)
-// c = l & 31 and the rows 16 (l >> 5) .. + 15 -- instead of every lane building its whole
-// column (4x / 2x fewer dot products per lane).  Each entry is the lane-per-column
-// build's arithmetic operation for operation (same FMA order, same masks), so A is
-// bit-identical; ds_bpermute then gathers the replicated layout (lane p of every 16-lane
-// row: columns p and p + 16), scaled by the column's -ARinv with -0.0 on the diagonal.
-template <int CL, bool TWO>
-__device__ __forceinline__ void pgs_small_split(SharedT<CL>& S, int nefc, real narinv_own, real u, int nl,
-                                                int nchunk, int iters, int lane) {
-  constexpr int K = TWO ? 16 : 4;
-  const int c = TWO ? (lane & 31) : (lane & 15);
-  const int i0 = TWO ? 16 * (lane >> 5) : 4 * (lane >> 4);
-  // Y D^-1 of row c (the Yd phase's arithmetic on the LDS copy of the row); zero past nefc
-  real Ydc[CW - 1];
-  const bool cvalid = c < nefc;
-  const int gc = cvalid ? S.ygrp[c] : -1;
-  if (cvalid) {
-    const real* Yc = S.Y[c];
-    for (int k = 0; k < 6; k++) Ydc[k] = Yc[k] * S.Do[k];
-    Ydc[6] = Yc[6] * S.Dbb;
-    const bool fgrp = gc >= 0 && gc < 3;
-    const real* dsrc = fgrp ? &S.Df[gc][0] : &S.Dp[0];
-#pragma unroll
-    for (int q = 1; q <= CL; q++) {
-      const real v = dsrc[fgrp ? q : 1];
-      const real dv = (fgrp || (gc == 3 && q == 1)) ? v : 1.0;
-      Ydc[6 + q] = Yc[6 + q] * dv;
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < CW - 1; k++) Ydc[k] = 0;
-  }
-  const bool gj = gc >= 0 && gc <= 3;
-  const real narinv_c = bperm_f64(c << 2, narinv_own);
-  real Ah[K];
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    const int i = i0 + k;
-    // rows past nefc hold stale data in LDS: their products are masked below
-    const real* Yi = S.Y[i];
-    const int gi = S.ygrp[i];
-    real ao = 0, ab = 0, ac = 0;
-#pragma unroll
-    for (int t = 0; t < 6; t++) ao = fma(Ydc[t], Yi[t], ao);
-    ab = Ydc[6] * Yi[6];
-#pragma unroll
-    for (int q = 1; q <= CL; q++) ac = fma(Ydc[6 + q], Yi[6 + q], ac);
-    const bool valid = i < nefc;
-    const bool gi_chain = gi >= 0 && gi <= 3;
-    real acc = ao;
-    acc += (gj && gi_chain) ? ab : 0.0;
-    acc += (gj && gi == gc) ? ac : 0.0;
-    const real a = valid ? acc : 0.0;
-    // -0.0 mirrors the general path's fma(-A[r], d, u) with A[r] = 0 (same zero sign)
-    Ah[k] = (i == c) ? -0.0 : a * narinv_c;
-  }
-  constexpr int NR = TWO ? 32 : 16;
-  const int p = lane & 15;
-  real nB0[NR], nB1[NR];
-#pragma unroll
-  for (int r = 0; r < NR; r++) {
-    if constexpr (TWO) {
-      nB0[r] = bperm_f64((p + 32 * (r >> 4)) << 2, Ah[r & 15]);
-      nB1[r] = bperm_f64((p + 16 + 32 * (r >> 4)) << 2, Ah[r & 15]);
-    } else {
-      nB0[r] = bperm_f64((((r >> 2) << 4) + p) << 2, Ah[r & 3]);
-      nB1[r] = 0.0;
-    }
-  }
-  pgs_small_solve<TWO>(nB0, nB1, u, nl, nchunk, iters, lane, S.efc_f);
-}
-
-// The general PGS path (nefc > 32, a few percent of envs at C3): lane j builds its whole
-// Delassus column A[:, j] in VGPRs and the sweeps broadcast each row's change with a
-// v_readlane pair.  Outlined: the rare path's unrolled 64-row code stays out of the
-// substep's instruction stream and register allocation (keeping it inline measured 8 %
-// slower on every phase), at the price of a call when it runs.  Y D^-1 of the lane's row
-// is recomputed from the LDS copy of the row, operation for operation as in the Yd phase.
-#define GM_AS_LDS __attribute__((address_space(3)))
-template <int CL>
-__device__ __noinline__ void pgs_general(GM_AS_LDS SharedT<CL>* S_, int nefc, real arinv_l, real u, real lb, int iters,
-                                         int lane) {
-  SharedT<CL>& S = *(SharedT<CL>*)S_;
-  const int grp = (lane < nefc) ? S.ygrp[lane] : -1;
-  real Yd[CW - 1];
-  if (lane < nefc) {
-    const real* J = S.Y[lane];
-    for (int k = 0; k < 6; k++) Yd[k] = J[k] * S.Do[k];
-    Yd[6] = J[6] * S.Dbb;
-    const bool fgrp = grp >= 0 && grp < 3;
-    const real* dsrc = fgrp ? &S.Df[grp][0] : &S.Dp[0];
-#pragma unroll
-    for (int q = 1; q <= CL; q++) {
-      const real v = dsrc[fgrp ? q : 1];
-      const real dv = (fgrp || (grp == 3 && q == 1)) ? v : 1.0;
-      Yd[6 + q] = J[6 + q] * dv;
-    }
-  } else {
-    for (int k = 0; k < CW - 1; k++) Yd[k] = 0;
-  }
-  const bool gj = grp >= 0 && grp <= 3;
-  const int nchunk = (__builtin_amdgcn_readfirstlane(nefc) + 3) >> 2;
-  real f = 0;
-  // Delassus column A[:, lane] = Y D^-1 Y_lane^T, held in this lane's VGPRs
-  real A[GM_MAX_EFC];
-  // rows in chunks of 4 (the PGS granularity): fewer padding rows than chunks of 8
-  const int nchunk_a = (__builtin_amdgcn_readfirstlane(nefc) + 3) >> 2;
-#pragma unroll
-  for (int c = 0; c < GM_MAX_EFC / 4; c++) {
-#pragma unroll
-    for (int rr = 0; rr < 4; rr++) A[c * 4 + rr] = 0;
-    if (c >= nchunk_a) continue;
-#pragma unroll
-    for (int rr = 0; rr < 4; rr++) {
-      const int i = c * 4 + rr;
-      // rows past nefc hold stale data in LDS: their products are masked below
-      const real* Yi = S.Y[i];
-      const int gi = S.ygrp[i];
-      real ao = 0, ab = 0, ac = 0;
-#pragma unroll
-      for (int k = 0; k < 6; k++) ao = fma(Yd[k], Yi[k], ao);
-      ab = Yd[6] * Yi[6];
-#pragma unroll
-      for (int q = 1; q <= CL; q++) ac = fma(Yd[6 + q], Yi[6 + q], ac);
-      const bool valid = i < nefc;
-      const bool gi_chain = gi >= 0 && gi <= 3;
-      real acc = ao;
-      acc += (gj && gi_chain) ? ab : 0.0;
-      acc += (gj && gi == grp) ? ac : 0.0;
-      A[i] = valid ? acc : 0.0;
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < GM_MAX_EFC / 4; c++) {
-    if (c >= nchunk) continue;
-#pragma unroll
-    for (int rr = 0; rr < 4; rr++) {
-      unsigned long long onehot;
-      asm volatile("s_bfm_b64 %0, 1, %1" : "=s"(onehot) : "i"(c * 4 + rr));
-      A[c * 4 + rr] = __builtin_amdgcn_inverse_ballot_w64(onehot) ? 0.0 : A[c * 4 + rr] * arinv_l;
-    }
-  }
-  for (int it = 0; it < iters; it++) {
-#pragma unroll
-    for (int c = 0; c < GM_MAX_EFC / 4; c++) {
-      if (c >= nchunk) continue;
-#pragma unroll
-      for (int rr = 0; rr < 4; rr++) {
-        const int r = c * 4 + rr;
-        const real fn = fmax(u, lb);
-        const real dl = fn - f;
-        const long long bits = __double_as_longlong(dl);
-        const int lo = __builtin_amdgcn_readlane((int)bits, r);
-        const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), r);
-        const real delta = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-        u = fma(-A[r], delta, u);
-        // lane == r as a scalar one-hot mask built in place (s_bfm_b64, no VALU compare);
-        // the opaque asm keeps the compiler from hoisting a 64-entry mask table out of
-        // the sweep loop (it would spill)
-        unsigned long long onehot;
-        asm volatile("s_bfm_b64 %0, 1, %1" : "=s"(onehot) : "i"(r));
-        f = __builtin_amdgcn_inverse_ballot_w64(onehot) ? fn : f;
-      }
-    }
-  }
-  S.efc_f[lane] = (lane < nefc) ? f : 0.0;
-  __syncthreads();
-}
-
-template <int CL, bool CAL>
-__device__ void constraints(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
-                            bool prof = false) {
-  unsigned long long t0 = prof ? clock64() : 0;
-  // row layout: active locks (lock order) then 4 pyramid edges per contact
-  int nl = 0;
-  for (int k = 0; k < T->nlock; k++) nl += S.s.lock_active[k] ? 1 : 0;
-  int nefc = nl + 4 * S.ncon;
-  real J[CW];
-  int grp = -1;
-  real pos = 0;
-  int is_contact = 0;
-  if (lane < nefc) {
-    if (lane < nl) {
-      int k = 0, cntl = -1;
-      for (k = 0; k < T->nlock; k++) { if (S.s.lock_active[k]) cntl++; if (cntl == lane) break; }
-      int d = m->lock_dof[k];
-      for (int t = 0; t < CW; t++) J[t] = 0;
-      grp = T->lock_grp[k];
-      const int cpos = T->lock_cpos[k];
-#pragma unroll
-      for (int q = 0; q <= CL; q++) J[6 + q] = (q == cpos) ? 1.0 : 0.0;
-      pos = S.s.qpos[d] - S.s.lock_q[k];
-    } else {
-      int r = lane - nl;
-      int c = r >> 2, e = r & 3;
-      const real* C = S.con[c];
-      real Fr[9];
-      make_frame(Fr, C + 4);
-      const real smu = ((e & 1) ? -1.0 : 1.0) * C[7];
-      const real* t = Fr + 3 * (1 + (e >> 1));
-      const real dir[3] = {Fr[0] + smu * t[0], Fr[1] + smu * t[1], Fr[2] + smu * t[2]};
-      contact_jac(S, m, T, c, dir, J, grp);
-      pos = C[0];
-      is_contact = 1;
-    }
-  }
-  PH(11);
-  // a0 = J qacc_smooth, vel = J qvel (uses J before the in-place solve)
-  real a0 = 0, vel = 0;
-  if (lane < nefc) {
-    a0 = row_dot_dofs<CL>(S, T, J, grp, S.qacc);
-    vel = row_dot_dofs<CL>(S, T, J, grp, S.s.qvel);
-    row_LTsolve<CL>(S, J, grp);
-  }
-  __syncthreads();            // every lane is done with cdof before Y overwrites it
-  if (lane < nefc) {
-    for (int t = 0; t < CW - 1; t++) S.Y[lane][t] = J[t];
-    S.ygrp[lane] = grp;
-  }
-  if (lane == 0) { S.nefc = nefc; S.nlockrows = nl; }
-  if (lane == 0) {
-    S.work_nefc += nefc;
-    if (prof) S.tph[24] += nefc;
-  }
-  __syncthreads();
-  PH(12);
-  // Y D^-1 for this lane's row
-  real Yd[CW - 1];
-  if (lane < nefc) {
-    for (int k = 0; k < 6; k++) Yd[k] = J[k] * S.Do[k];
-    Yd[6] = J[6] * S.Dbb;
-    // branch-free pivot lookup: every lane reads a valid LDS word and selects (a branch
-    // per q serialised the reads behind exec masks)
-    const bool fgrp = grp >= 0 && grp < 3;
-    const real* dsrc = fgrp ? &S.Df[grp][0] : &S.Dp[0];
-#pragma unroll
-    for (int q = 1; q <= CL; q++) {
-      const real v = dsrc[fgrp ? q : 1];
-      const real dv = (fgrp || (grp == 3 && q == 1)) ? v : 1.0;
-      Yd[6 + q] = J[6 + q] * dv;
-    }
-  } else {
-    for (int k = 0; k < CW - 1; k++) Yd[k] = 0;
-  }
-  const bool gj = grp >= 0 && grp <= 3;
-  // diagonal A_jj from the lane's own row (J == S.Y[lane]), the A build's arithmetic for
-  // i == j operation for operation, instead of a 64-way select out of A[]
-  real Ajj = 0;
-  if (lane < nefc) {
-    real ao = 0, ac = 0;
-#pragma unroll
-    for (int k = 0; k < 6; k++) ao = fma(Yd[k], J[k], ao);
-    const real ab = Yd[6] * J[6];
-#pragma unroll
-    for (int q = 1; q <= CL; q++) ac = fma(Yd[6 + q], J[6 + q], ac);
-    Ajj = ao;
-    Ajj += gj ? ab : 0.0;
-    Ajj += gj ? ac : 0.0;
-  }
-  // impedance / reference acceleration (mj_makeImpedance)
-  real h = CAL ? S.s.dt : m->timestep;
-  real tc = m->solref[0];
-  if (tc < 2 * h) tc = 2 * h;
-  real dr = m->solref[1], dmax = m->solimp[1];
-  real K = rcp_n(dmax * dmax * tc * tc * dr * dr);
-  real Bd = div_n(2.0, dmax * tc);
-  real imp = impedance(m, pos);
-  real aref = -Bd * vel - K * imp * pos;
-  real R = div_n(1 - imp, imp) * Ajj;
-  if (R < 1e-15) R = 1e-15;
-  const real arinv = rcp_n(Ajj + R);   // mj_solPGS's ARinv
-  // projected Gauss-Seidel (mj_solPGS order: rows in sequence, fixed sweeps, cold start).
-  // Lane j owns row j and keeps its unclamped Gauss-Seidel target current,
-  //   u_j = f_j - ARinv_j (AR f + b)_j,      AR = A + diag(R)  (mj_solPGS's efc_AR),
-  // so a row update is f_r <- max(u_r, lb_r) and every lane follows a change d of f_r
-  // with u_j -= (ARinv_j AR_jr) d.  The scaled column B_j[r] = ARinv_j AR_jr is built
-  // once per substep; B_r[r] = 0 exactly (ARinv_r AR_rr = 1 cancels the change of f_r),
-  // so the dependent chain per row is fma -> max -> sub -> readlane.  Each d is
-  // broadcast with v_readlane (no LDS, no reductions).  Contact rows (pyramid edges) are
-  // clamped at 0, lock rows are unbounded.  Rows run in chunks of 4 with one scalar
-  // guard per chunk; rows past nefc inside the last chunk are exact no-ops (u = f = 0,
-  // lb = 0, zero B entries => d = 0).
-  const int nchunk = (__builtin_amdgcn_readfirstlane(nefc) + 3) >> 2;
-  const real lb = (is_contact || lane >= nefc) ? 0.0 : -__builtin_inf();
-  const real arinv_l = (lane < nefc) ? arinv : 0.0;
-  const real u = -(((lane < nefc) ? (a0 - aref) : 0.0) * arinv_l);   // f = 0: u = -ARinv b
-#ifdef GM_PHASE_SPLIT_PGS
-  PH(15);   // developer split: impedance, ARinv, u init
-#endif
-#ifndef GM_PGS_GENERAL_ONLY
-  // (test build lib/libgm_pgsgen.so: every problem on the lane-per-row path, so the GPU
-  // tests can hold the DPP-row path against it on identical states)
-  if (nchunk <= 8) {
-    // nefc <= 32: split Delassus build + replicated DPP-row sweeps (see pgs_small_split)
-    PH(13);
-    const int iters = m->pgs_iterations;
-    // the solve writes rows 0 .. NR-1, then the rows past nefc become +0.0 (the LDS
-    // writes of one wave land in program order)
-    if (nchunk <= 4) pgs_small_split<CL, false>(S, nefc, -arinv_l, u, nl, nchunk, iters, lane);
-    else pgs_small_split<CL, true>(S, nefc, -arinv_l, u, nl, nchunk, iters, lane);
-    if (lane >= nefc) S.efc_f[lane] = 0.0;
-    PH(14);
-    __syncthreads();
-    return;
-  }
-#endif
-  pgs_general<CL>((GM_AS_LDS SharedT<CL>*)&S, nefc, arinv_l, u, lb, m->pgs_iterations, lane);
-  PH(14);
-}
-
-// qacc = qacc_smooth + H^-1 J^T f  via  z = D^-1 Y^T f,  x = L^-1 z
-template <int CL>
-__device__ void constraint_accel(SharedT<CL>& S, const GmTopo* __restrict__ T, int lane) {
-  int nefc = S.nefc;
-  if (lane < T->nv) {
-    int d = lane;
-    int b = -1;
-    // classify the dof into (group, compact slot)
-    int grp_d, slot;
-    if (d >= T->dof_obj) { grp_d = GM_GRP_OBJECT; slot = d - T->dof_obj; }
-    else if (d == T->dof_base) { grp_d = GM_GRP_BASE; slot = 6; }
-    else if (d == T->dof_palm) { grp_d = 3; slot = 7; }
-    else { grp_d = (d - T->dof_f0[0]) / CL; slot = 6 + 1 + (d - T->dof_f0[grp_d]); }
-    (void)b;
-    // rows in chunks of 8 with the LDS reads of a chunk issued before its (sequential,
-    // same-order) accumulation; rows past nefc are masked, never read as data
-    real acc = 0;
-    const int nch = (__builtin_amdgcn_readfirstlane(nefc) + 7) >> 3;
-    for (int c = 0; c < nch; c++) {
-      real yv[8], fv[8];
-      int gv[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int r = c * 8 + k;
-        yv[k] = S.Y[r][slot];
-        fv[k] = S.efc_f[r];
-        gv[k] = S.ygrp[r];
-      }
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int g = gv[k];
-        const bool use = (c * 8 + k < nefc) &&
-                         ((grp_d == GM_GRP_OBJECT) || (grp_d == GM_GRP_BASE && g >= 0 && g <= 3) || (grp_d == g));
-        if (use) acc += yv[k] * fv[k];
-      }
-    }
-    real Dd;
-    if (grp_d == GM_GRP_OBJECT) Dd = S.Do[slot];
-    else if (grp_d == GM_GRP_BASE) Dd = S.Dbb;
-    else if (grp_d == 3) Dd = S.Dp[1];
-    else Dd = S.Df[grp_d][slot - 6];
-    S.z[d] = acc * Dd;
-  }
-  __syncthreads();
-  // x = L^-1 z : root -> leaves, on the DPP-row layout (see factor)
-  {
-    const int rowf = lane >> 4, p = lane & 15;
-    const bool fing = rowf < 3 && p <= CL;
-    const bool obj = rowf == 3 && p < 6;
-    real y = 0;
-    if (fing) y = (p == 0) ? S.z[T->dof_base] : S.z[T->dof_f0[rowf] + p - 1];
-    else if (obj) y = S.z[T->dof_obj + p];
-    y = rows_L<CL>(S, rowf, p, fing, obj, y);
-    if (fing) {
-      if (p >= 1) S.qacc[T->dof_f0[rowf] + p - 1] += y;
-      else if (rowf == 0) S.qacc[T->dof_base] += y;
-    } else if (obj) {
-      S.qacc[T->dof_obj + p] += y;
-    } else if (lane == 63) {
-      S.qacc[T->dof_palm] += S.z[T->dof_palm] - S.Hp[TRI(1, 0)] * S.z[T->dof_base];
-    }
-  }
-  // contact forces in the contact frame (mj_contactForce, pyramidal decode)
-  if (lane < S.ncon) {
-    const real* fe = &S.efc_f[S.nlockrows + 4 * lane];
-    real mu = S.con[lane][7];
-    S.con[lane][8] = fe[0] + fe[1] + fe[2] + fe[3];
-    S.con[lane][9] = mu * (fe[0] - fe[1]);
-    S.con[lane][10] = mu * (fe[2] - fe[3]);
-  }
-  __syncthreads();
-}
-
 // ============================================================ integrate
 template <int CL, bool CAL>
 __device__ void integrate(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
@@ -2071,7 +1332,9 @@ __device__ void integrate(SharedT<CL>& S, const gm_model* __restrict__ m, const 
     real wn = sqrt(dot3(w, w));
     if (wn > 1e-15) {
       real ang = wn * h;
-      real sn = sin(0.5 * ang) / wn, cs = cos(0.5 * ang);
+      real sn, cs;
+      gm_sincos(0.5 * ang, &sn, &cs);
+      sn = sn / wn;
       real dq[4] = {cs, w[0] * sn, w[1] * sn, w[2] * sn};
       quatmul(q, q, dq);
     }
@@ -2314,7 +1577,7 @@ __device__ float gauge_reading(const gm_model* __restrict__ m, const real* q) {
   for (int i = 0; i < NS; i++) {
     cum = (i == 0) ? (double)q[0] : cum + (double)q[i];
     double sn, cs;
-    sincos(cum, &sn, &cs);
+    gm_sincos(cum, &sn, &cs);
     X[i + 1] = X[i] + Ls * cs;
     Yv[i + 1] = Yv[i] + Ls * sn;
   }
@@ -2393,8 +1656,9 @@ __device__ void extract_forces(SharedT<CL>& S, const gm_model* __restrict__ m, c
     int w_gnd = (c1 == GM_CLS_GROUND || c2 == GM_CLS_GROUND);
     real g[3];
     real Fr[9];
-    make_frame(Fr, C + 4);
-    for (int k = 0; k < 3; k++) g[k] = Fr[k] * C[8] + Fr[3 + k] * C[9] + Fr[6 + k] * C[10];
+    Fr[0] = C[4]; Fr[1] = C[5]; Fr[2] = C[6]; Fr[3] = C[7]; Fr[4] = C[8]; Fr[5] = C[9];
+    cross3(Fr + 6, Fr, Fr + 3);
+    for (int k = 0; k < 3; k++) g[k] = Fr[k] * C[11] + Fr[3 + k] * C[12] + Fr[6 + k] * C[13];
     int wf[3] = {w_f0, w_f1, w_f2};
     if (w_obj) {
       for (int f = 0; f < 3; f++) if (wf[f]) for (int k = 0; k < 3; k++) og[f][k] += g[k];
@@ -2437,8 +1701,9 @@ __device__ void object_net_wrench(SharedT<CL>& S, const GmTopo* __restrict__ T, 
     const int g1 = S.cgeom[lane][0], g2 = S.cgeom[lane][1];
     const real sgn = (g2 == T->geom_obj) ? 1.0 : (g1 == T->geom_obj) ? -1.0 : 0.0;
     real Fr[9], g[3], r[3], t[3];
-    make_frame(Fr, C + 4);
-    for (int k = 0; k < 3; k++) g[k] = Fr[k] * C[8] + Fr[3 + k] * C[9] + Fr[6 + k] * C[10];
+    Fr[0] = C[4]; Fr[1] = C[5]; Fr[2] = C[6]; Fr[3] = C[7]; Fr[4] = C[8]; Fr[5] = C[9];
+    cross3(Fr + 6, Fr, Fr + 3);
+    for (int k = 0; k < 3; k++) g[k] = Fr[k] * C[11] + Fr[3 + k] * C[12] + Fr[6 + k] * C[13];
     const int bo = T->body_obj;
     for (int k = 0; k < 3; k++) r[k] = C[1 + k] - S.xpos[bo][k];
     cross3(t, r, g);
@@ -2514,20 +1779,15 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
   PH(1);
   mass_and_forces<CL, CAL>(S, m, T, lane);
   PH(2);
-  factor<CL>(S, T, lane);
-  PH(3);
-  solve_full<CL>(S, T, S.frc, S.qacc, lane);
-  PH(4);
   collision(S, m, T, lane, prof);
   PH(5);
-  constraints<CL, CAL>(S, m, T, lane, prof);
+  newton_solve<CL, CAL>(S, m, T, lane, prof);
   PH(6);
-  constraint_accel<CL>(S, T, lane);
-  PH(7);
   integrate<CL, CAL>(S, m, T, lane);
   PH(8);
 }
 
+#define GM_AS_LDS __attribute__((address_space(3)))
 #define GM_AS_GLOBAL __attribute__((address_space(1)))
 // One substep, outlined: its own register allocation (the fused kernel around it keeps
 // the env-step epilogue's state), parameters typed with their address spaces so the body
@@ -2981,7 +2241,7 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
   const bool calib = CAL;                   // calibration run (mode 3): S.s.cal_steps substeps, no sensors
   const bool prof = !settle && dbg.phase != nullptr;
   if (prof && lane < GM_NPHASE) S.tph[lane] = 0;
-  if (lane == 0) { S.work_nefc = 0; S.work_mpr = 0; S.stp_fixed = 0; }
+  if (lane == 0) { S.work_nefc = 0; S.work_mpr = 0; S.work_newton = 0; S.stp_fixed = 0; }
   const unsigned long long t_kernel = prof ? clock64() : 0;
   __syncthreads();
   const int nsub = settle ? 400 : calib ? S.s.cal_steps : (mode == 2) ? 1 : C->sim_steps_per_action + S.s.extra_substeps;
@@ -3002,13 +2262,13 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
         const real* Cc = S.con[lane];
         o[0] = Cc[0];
         for (int k = 0; k < 3; k++) o[1 + k] = Cc[1 + k];
-        real Fr[9];
-        make_frame(Fr, Cc + 4);
-        for (int k = 0; k < 9; k++) o[4 + k] = Fr[k];
-        o[13] = S.cgeom[lane][0]; o[14] = S.cgeom[lane][1]; o[15] = Cc[7];
+        for (int k = 0; k < 6; k++) o[4 + k] = Cc[4 + k];
+        cross3(o + 10, Cc + 4, Cc + 7);
+        o[13] = S.cgeom[lane][0]; o[14] = S.cgeom[lane][1]; o[15] = Cc[10];
       }
     }
-    dbg.efc_force[(size_t)env * GM_MAX_EFC + lane] = lane < S.nefc ? S.efc_f[lane] : 0.0;
+    for (int r = lane; r < GM_MAX_EFC; r += NT)
+      dbg.efc_force[(size_t)env * GM_MAX_EFC + r] = r < S.nefc ? S.dbg.efc[r] : 0.0;
     if (lane < GM_MAX_DOF) dbg.qacc[(size_t)env * GM_MAX_DOF + lane] = lane < T->nv ? S.qacc[lane] : 0.0;
     {
       real w[6];
@@ -3048,12 +2308,13 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
   if (cost && lane == 0) {
     // next env-step's dispatch cost: the measured one (shader clocks / 64; it carries
     // co-residency noise) averaged with a work model of this env-step (a fixed part, the
-    // PGS + Delassus work per constraint row, the convex collider's latency per substep
-    // that ran it; fitted on the C3 workload, tools/tail_bench.py): the blend orders the
+    // Hessian work per constraint row, each Newton iteration, the convex collider's
+    // latency per substep that ran it; fitted on the C3 workload, tools/tail_bench.py): the blend orders the
     // next launch closer to its true costs than either alone (LPT makespan 1.17 vs 1.21
     // of the ideal on recorded costs)
     const uint32_t now = (uint32_t)((__builtin_amdgcn_s_memtime() - t_start) >> 6);
-    const uint32_t model = 92000u + 25u * (uint32_t)S.work_nefc + 300u * (uint32_t)S.work_mpr;
+    const uint32_t model = 92000u + 25u * (uint32_t)S.work_nefc + 300u * (uint32_t)S.work_mpr +
+                           400u * (uint32_t)S.work_newton;
     cost[env] = (now >> 1) + (model >> 1);
   }
   store_state(S, states + env, lane);
@@ -3249,8 +2510,12 @@ __device__ void spawn_object(GmEnvState& s, const GmTopo* __restrict__ T, const 
   s.obj_inertia[0] = I0; s.obj_inertia[1] = I1; s.obj_inertia[2] = I2;
   s.obj_rbound = rb;
   s.obj_rest_z = restz;
+  // body_invweight0 of the live object (mj_setConst at qpos0; oracle object_invweight)
+  s.obj_invw[0] = 1.0 / o.mass;
+  s.obj_invw[1] = ((1.0 / I0 + 1.0 / I1) + 1.0 / I2) / 3.0;
   int qa = T->qadr_obj;
-  double x2 = sin(-sp.zrot / 2.0), w2 = cos(-sp.zrot / 2.0);
+  double x2, w2;
+  gm_sincos(-sp.zrot / 2.0, &x2, &w2);   // shared with the oracle (gm_math.h)
   double q4[4] = {x2, 0, 0, w2};   // reference QPos quirk: qx lands in MuJoCo's w slot
   double nq = sqrt(q4[0] * q4[0] + q4[1] * q4[1] + q4[2] * q4[2] + q4[3] * q4[3]);
   s.qpos[qa + 0] = sp.x;
@@ -3590,6 +2855,8 @@ extern "C" __global__ void gm_settle_init_kernel(GmEnvState* __restrict__ states
     s.obj_inertia[0] = s.obj_inertia[1] = s.obj_inertia[2] = (2 * o.mass * r * r / 5);
     s.obj_rbound = r;
   }
+  s.obj_invw[0] = 1.0 / o.mass;
+  s.obj_invw[1] = ((1.0 / s.obj_inertia[0] + 1.0 / s.obj_inertia[1]) + 1.0 / s.obj_inertia[2]) / 3.0;
 }
 #endif
 

@@ -1,0 +1,1002 @@
+// gm_newton.hip -- box-box collision and the constraint solve of the env-step kernel
+// (included by gm_kernels.hip after the kinematics / dynamics stages).
+//
+// The constraint problem is MuJoCo's (mj_makeConstraint / mj_makeImpedance with the
+// mj_diagApprox regulariser, pyramidal cones), solved to its unique optimum by MuJoCo's
+// Newton method (mj_solNewton: primal, in qacc space, exact line search, warm start from
+// the previous substep's qacc).  The Hessian H~ + J_a^T D_a J_a is assembled in spatial
+// form -- per contact the 3x3 Q = sum_e D_e u_e u_e^T of its active pyramid edges, per
+// body the 6x6 K = S Q S^T summed over the body's contacts, suffix-scanned along each
+// finger chain like composite inertias -- so its cost follows the bodies, not the
+// constraint rows, and no per-row Jacobian or Delassus matrix is ever formed.  It is
+// factored on the DPP-row layout: each finger chain's block on its 16-lane row with the
+// border [base, object 0..5] as extra columns (leaf-first LDL^T, row_newbcast pivots),
+// Schur complements into the border, a 7x7 border LDL^T on row 3.
+// oracle/physics.c restates every function here operation for operation (the oracle's
+// lane emulation), so device and oracle agree bit for bit from the same state.
+
+// ------------------------------------------------------------ box-box (mjc_BoxBox)
+// Separating axes, then the face-clipped manifold (see oracle/physics.c bb_setup): the
+// face case keeps up to 8 of 24 candidates (incident vertices inside the reference face,
+// reference corners inside the incident face, edge crossings) below the reference face.
+#define BB_NCAND 24
+struct BBox {
+  int kind;                     // 0 none, 1 face, 2 edge
+  real n[3], pen, sgn;
+  real crf[3], ru[3], rv[3], hu, hv;
+  real V[4][3], cinc[3], ninc[3], pu[4], pv[4];
+};
+
+__device__ __forceinline__ void bb_setup(const GeomV& A, const GeomV& B, BBox& S, real* ea, real* eb, real* da,
+                                         real* db) {
+  S.kind = 0;
+  const real d[3] = {B.c[0] - A.c[0], B.c[1] - A.c[1], B.c[2] - A.c[2]};
+  real a[3][3], b[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int k = 0; k < 3; k++) { a[i][k] = A.R[3 * k + i]; b[i][k] = B.R[3 * k + i]; }
+  real Ca[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) Ca[i][j] = fabs(dot3(a[i], b[j]));
+  real best = 0;
+  int code = -1;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const real rb = B.size[0] * Ca[i][0] + B.size[1] * Ca[i][1] + B.size[2] * Ca[i][2];
+    const real pen = (A.size[i] + rb) - fabs(dot3(d, a[i]));
+    if (pen < 0) return;
+    if (code < 0 || pen < best) { best = pen; code = i; }
+  }
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    const real ra = A.size[0] * Ca[0][j] + A.size[1] * Ca[1][j] + A.size[2] * Ca[2][j];
+    const real pen = (ra + B.size[j]) - fabs(dot3(d, b[j]));
+    if (pen < 0) return;
+    if (pen < best) { best = pen; code = 3 + j; }
+  }
+  real ebest = 0, eL[3] = {0, 0, 0};
+  int ecode = -1;
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      real L[3];
+      cross3(L, a[i], b[j]);
+      const real len = sqrt_n(dot3(L, L));
+      if (len < 1e-6) continue;
+      const real il = rcp_n(len);
+      L[0] *= il; L[1] *= il; L[2] *= il;
+      const real ra = A.size[0] * fabs(dot3(a[0], L)) + A.size[1] * fabs(dot3(a[1], L)) + A.size[2] * fabs(dot3(a[2], L));
+      const real rb = B.size[0] * fabs(dot3(b[0], L)) + B.size[1] * fabs(dot3(b[1], L)) + B.size[2] * fabs(dot3(b[2], L));
+      const real pen = (ra + rb) - fabs(dot3(d, L));
+      if (pen < 0) return;
+      if (ecode < 0 || pen < ebest) { ebest = pen; ecode = 3 * i + j; eL[0] = L[0]; eL[1] = L[1]; eL[2] = L[2]; }
+    }
+  if (ecode >= 0 && ebest < 0.95 * best) {
+    const int i = ecode / 3, j = ecode % 3;
+    real L[3] = {eL[0], eL[1], eL[2]};
+    if (dot3(d, L) < 0) { L[0] = -L[0]; L[1] = -L[1]; L[2] = -L[2]; }
+    S.kind = 2;
+    S.pen = ebest;
+    S.n[0] = L[0]; S.n[1] = L[1]; S.n[2] = L[2];
+#pragma unroll
+    for (int k = 0; k < 3; k++) { ea[k] = A.c[k]; eb[k] = B.c[k]; }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      da[k] = (i == 0) ? a[0][k] : (i == 1) ? a[1][k] : a[2][k];
+      db[k] = (j == 0) ? b[0][k] : (j == 1) ? b[1][k] : b[2][k];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (k != i) {
+        const real s = dot3(a[k], L) >= 0 ? A.size[k] : -A.size[k];
+#pragma unroll
+        for (int t = 0; t < 3; t++) ea[t] += s * a[k][t];
+      }
+      if (k != j) {
+        const real s = dot3(b[k], L) >= 0 ? -B.size[k] : B.size[k];
+#pragma unroll
+        for (int t = 0; t < 3; t++) eb[t] += s * b[k][t];
+      }
+    }
+    return;
+  }
+  const bool ref_is_a = code < 3;
+  const int ri = ref_is_a ? code : code - 3;
+  // reference / incident box data by selection (no pointer to a register array)
+  real rc[3], ic[3], rs[3], is[3], ra[3][3], ia[3][3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    rc[k] = ref_is_a ? A.c[k] : B.c[k];
+    ic[k] = ref_is_a ? B.c[k] : A.c[k];
+    rs[k] = ref_is_a ? A.size[k] : B.size[k];
+    is[k] = ref_is_a ? B.size[k] : A.size[k];
+#pragma unroll
+    for (int t = 0; t < 3; t++) { ra[k][t] = ref_is_a ? a[k][t] : b[k][t]; ia[k][t] = ref_is_a ? b[k][t] : a[k][t]; }
+  }
+  real rax[3], rau[3], rav[3];
+  const int ui = (ri + 1) % 3, vi = (ri + 2) % 3;
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    rax[t] = ri == 0 ? ra[0][t] : ri == 1 ? ra[1][t] : ra[2][t];
+    rau[t] = ui == 0 ? ra[0][t] : ui == 1 ? ra[1][t] : ra[2][t];
+    rav[t] = vi == 0 ? ra[0][t] : vi == 1 ? ra[1][t] : ra[2][t];
+  }
+  const real rsi = ri == 0 ? rs[0] : ri == 1 ? rs[1] : rs[2];
+  const real dd[3] = {ic[0] - rc[0], ic[1] - rc[1], ic[2] - rc[2]};
+  const real s0 = dot3(dd, rax) >= 0 ? 1.0 : -1.0;
+  S.kind = 1;
+  S.pen = best;
+  S.sgn = ref_is_a ? 1.0 : -1.0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) S.n[k] = s0 * rax[k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) { S.crf[k] = rc[k] + rsi * S.n[k]; S.ru[k] = rau[k]; S.rv[k] = rav[k]; }
+  S.hu = ui == 0 ? rs[0] : ui == 1 ? rs[1] : rs[2];
+  S.hv = vi == 0 ? rs[0] : vi == 1 ? rs[1] : rs[2];
+  int jm = 0;
+  real bm = fabs(dot3(S.n, ia[0]));
+#pragma unroll
+  for (int j = 1; j < 3; j++) { const real v = fabs(dot3(S.n, ia[j])); if (v > bm) { bm = v; jm = j; } }
+  real iaj[3], ie1[3], ie2[3];
+  const int e1 = (jm + 1) % 3, e2 = (jm + 2) % 3;
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    iaj[t] = jm == 0 ? ia[0][t] : jm == 1 ? ia[1][t] : ia[2][t];
+    ie1[t] = e1 == 0 ? ia[0][t] : e1 == 1 ? ia[1][t] : ia[2][t];
+    ie2[t] = e2 == 0 ? ia[0][t] : e2 == 1 ? ia[1][t] : ia[2][t];
+  }
+  const real isj = jm == 0 ? is[0] : jm == 1 ? is[1] : is[2];
+  const real h1 = e1 == 0 ? is[0] : e1 == 1 ? is[1] : is[2];
+  const real h2 = e2 == 0 ? is[0] : e2 == 1 ? is[1] : is[2];
+  const real sj = dot3(S.n, iaj) >= 0 ? -1.0 : 1.0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) { S.ninc[k] = sj * iaj[k]; S.cinc[k] = ic[k] + isj * S.ninc[k]; }
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const real su = (q == 1 || q == 2) ? 1.0 : -1.0, sv = (q >= 2) ? 1.0 : -1.0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) S.V[q][k] = S.cinc[k] + (su * h1) * ie1[k] + (sv * h2) * ie2[k];
+    const real r[3] = {S.V[q][0] - S.crf[0], S.V[q][1] - S.crf[1], S.V[q][2] - S.crf[2]};
+    S.pu[q] = dot3(r, S.ru);
+    S.pv[q] = dot3(r, S.rv);
+  }
+}
+// face candidate i (see oracle/physics.c bb_face_cand); i compile-time after unrolling
+__device__ __forceinline__ int bb_face_cand(const BBox& S, int i, real* P, real& depth) {
+  if (i < 4) {
+    if (!(fabs(S.pu[i]) <= S.hu && fabs(S.pv[i]) <= S.hv)) return 0;
+    P[0] = S.V[i][0]; P[1] = S.V[i][1]; P[2] = S.V[i][2];
+  } else if (i < 8) {
+    const int m = i - 4;
+    const real cu = (m == 1 || m == 2) ? S.hu : -S.hu, cv = (m >= 2) ? S.hv : -S.hv;
+    real sgn_min = 0, sgn_max = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int q1 = (q + 1) & 3;
+      const real ex = S.pu[q1] - S.pu[q], ey = S.pv[q1] - S.pv[q];
+      const real cr = ex * (cv - S.pv[q]) - ey * (cu - S.pu[q]);
+      if (q == 0) { sgn_min = cr; sgn_max = cr; }
+      else { sgn_min = fmin(sgn_min, cr); sgn_max = fmax(sgn_max, cr); }
+    }
+    if (!(sgn_min >= 0 || sgn_max <= 0)) return 0;
+    real Q[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) Q[k] = S.crf[k] + cu * S.ru[k] + cv * S.rv[k];
+    const real den = dot3(S.ninc, S.n);
+    if (fabs(den) < 1e-12) return 0;
+    const real r[3] = {S.cinc[0] - Q[0], S.cinc[1] - Q[1], S.cinc[2] - Q[2]};
+    const real t = div_n(dot3(S.ninc, r), den);
+#pragma unroll
+    for (int k = 0; k < 3; k++) P[k] = Q[k] + t * S.n[k];
+  } else {
+    const int q = (i - 8) >> 2, m = (i - 8) & 3;
+    const int q1 = (q + 1) & 3;
+    const real du = S.pu[q1] - S.pu[q], dv = S.pv[q1] - S.pv[q];
+    real t;
+    if (m < 2) {
+      if (fabs(du) < 1e-15) return 0;
+      const real bound = m == 0 ? -S.hu : S.hu;
+      t = div_n(bound - S.pu[q], du);
+      if (!(t > 0 && t < 1)) return 0;
+      const real vt = S.pv[q] + t * dv;
+      if (!(fabs(vt) < S.hv)) return 0;
+    } else {
+      if (fabs(dv) < 1e-15) return 0;
+      const real bound = m == 2 ? -S.hv : S.hv;
+      t = div_n(bound - S.pv[q], dv);
+      if (!(t > 0 && t < 1)) return 0;
+      const real ut = S.pu[q] + t * du;
+      if (!(fabs(ut) < S.hu)) return 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) P[k] = S.V[q][k] + t * (S.V[q1][k] - S.V[q][k]);
+  }
+  const real r[3] = {S.crf[0] - P[0], S.crf[1] - P[1], S.crf[2] - P[2]};
+  depth = dot3(S.n, r);
+  return depth > 0;
+}
+__device__ __forceinline__ void bb_face_hit(const BBox& S, const real* P, real depth, Hit& h) {
+  h.dist = -depth;
+#pragma unroll
+  for (int k = 0; k < 3; k++) { h.pos[k] = P[k] + (0.5 * depth) * S.n[k]; h.n[k] = S.sgn * S.n[k]; }
+}
+__device__ __forceinline__ int bb_edge_hit(const BBox& S, const real* ea, const real* eb, const real* da,
+                                           const real* db, Hit& h) {
+  const real w[3] = {ea[0] - eb[0], ea[1] - eb[1], ea[2] - eb[2]};
+  const real b = dot3(da, db), dd = dot3(da, w), e = dot3(db, w);
+  const real den = 1.0 - b * b;
+  if (!(den > 1e-12)) return 0;
+  const real s = div_n(b * e - dd, den), t = div_n(e - b * dd, den);
+  h.dist = -S.pen;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const real pa = ea[k] + s * da[k], pb = eb[k] + t * db[k];
+    h.pos[k] = 0.5 * (pa + pb);
+    h.n[k] = S.n[k];
+  }
+  return 1;
+}
+
+// ------------------------------------------------------------ constraint rows
+__device__ __forceinline__ real impedance(const gm_model* __restrict__ m, real r) {
+  const real dmin = m->solimp[0], dmax = m->solimp[1], width = m->solimp[2];
+  const real mid = m->solimp[3], pw = m->solimp[4];
+  if (dmin == dmax || width <= 1e-15) return dmin;
+  const real x = div_n(fabs(r), width);
+  if (x >= 1) return dmax;
+  if (x <= 0) return dmin;
+  real y;
+  if (pw == 1) y = x;
+  else if (pw == 2) y = (x <= mid) ? div_n(x * x, mid) : 1 - div_n((1 - x) * (1 - x), 1 - mid);   // MuJoCo's default power
+  else if (x <= mid) y = pow(x, pw) / pow(mid, pw - 1);
+  else y = 1 - pow(1 - x, pw) / pow(1 - mid, pw - 1);
+  return dmin + y * (dmax - dmin);
+}
+
+// spatial velocity [angular; linear at the world origin] of every body for the dof vector
+// v (LDS): chain prefix scans on the scan lanes plus the base, the object's free joint
+template <int CL>
+__device__ void body_vel(SharedT<CL>& S, const real* v, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
+                         int lane) {
+  const int db = T->dof_base;
+  const real vb = v[db];
+  real cvb[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) cvb[k] = S.cdof[db][k] * vb;
+  const int grp = T->kl_grp[lane];
+  const bool chain = grp >= 0 && grp <= 3;
+  const int p = T->kl_cpos[lane];
+  const int d = chain ? (grp < 3 ? T->dof_f0[grp] + p - 1 : T->dof_palm) : db;
+  const real vd = chain ? v[d] : 0.0;
+  real s[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) s[k] = (chain ? S.cdof[d][k] : 0.0) * vd;
+#pragma unroll
+  for (int off = 1; off < CL; off <<= 1)
+#pragma unroll
+    for (int k = 0; k < 6; k++) s[k] += row_shr(s[k], off);
+  const int b = T->lane_body[lane];
+  real (*V)[6] = S.nw.V;
+  if (chain) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) V[b][k] = s[k] + cvb[k];
+  } else if (lane == T->lane_base) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) V[T->body_base][k] = cvb[k];
+  } else if (b == T->body_obj) {
+    const int d0 = T->dof_obj;
+    real acc[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 6; k++)
+#pragma unroll
+      for (int t = 0; t < 6; t++) acc[t] += S.cdof[d0 + k][t] * v[d0 + k];
+#pragma unroll
+    for (int t = 0; t < 6; t++) V[b][t] = acc[t];
+  } else if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) V[0][k] = 0.0;
+  }
+  __syncthreads();
+}
+
+// J v of contact c's 4 pyramid edges from the body velocities (n + mu t1, n - mu t1,
+// n + mu t2, n - mu t2)
+template <int CL>
+__device__ __forceinline__ void contact_jv(const SharedT<CL>& S, const gm_model* __restrict__ m, int c, real* jv) {
+  const real* C = S.con[c];
+  const int b1 = m->geom_body[S.cgeom[c][0]], b2 = m->geom_body[S.cgeom[c][1]];
+  const real pos[3] = {C[1], C[2], C[3]};
+  real t1v[3], t2v[3];
+  cross3(t1v, S.nw.V[b1], pos);
+  cross3(t2v, S.nw.V[b2], pos);
+  const real v1[3] = {S.nw.V[b1][3] + t1v[0], S.nw.V[b1][4] + t1v[1], S.nw.V[b1][5] + t1v[2]};
+  const real v2[3] = {S.nw.V[b2][3] + t2v[0], S.nw.V[b2][4] + t2v[1], S.nw.V[b2][5] + t2v[2]};
+  const real dv[3] = {v2[0] - v1[0], v2[1] - v1[1], v2[2] - v1[2]};
+  const real n[3] = {C[4], C[5], C[6]}, t1[3] = {C[7], C[8], C[9]};
+  real t2[3];
+  cross3(t2, n, t1);
+  const real mu = C[10];
+  const real cn = dot3(n, dv), c1 = dot3(t1, dv), c2 = dot3(t2, dv);
+  const real m1 = mu * c1, m2 = mu * c2;
+  jv[0] = cn + m1; jv[1] = cn - m1; jv[2] = cn + m2; jv[3] = cn - m2;
+}
+// pyramid edge direction u_e of contact record C
+__device__ __forceinline__ void edge_dir(const real* C, const real* t2, int ed, real* u) {
+  const real* t = (ed >> 1) ? t2 : C + 7;
+  const real mt[3] = {C[10] * t[0], C[10] * t[1], C[10] * t[2]};
+  if (ed & 1) { u[0] = C[4] - mt[0]; u[1] = C[5] - mt[1]; u[2] = C[6] - mt[2]; }
+  else { u[0] = C[4] + mt[0]; u[1] = C[5] + mt[1]; u[2] = C[6] + mt[2]; }
+}
+// K = S Q S^T, S = [skew(p); I]: [A xx yy zz xy xz yz | B row-major | Q xx yy zz xy xz yz]
+__device__ __forceinline__ void spatial_K(const real* Q, const real* p, real* K) {
+  const real Qm[3][3] = {{Q[0], Q[3], Q[4]}, {Q[3], Q[1], Q[5]}, {Q[4], Q[5], Q[2]}};
+  real Bm[3][3];
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    real c[3];
+    cross3(c, p, Qm[j]);
+    Bm[0][j] = c[0]; Bm[1][j] = c[1]; Bm[2][j] = c[2];
+  }
+  real Am[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) cross3(Am[i], p, Bm[i]);
+  K[0] = Am[0][0]; K[1] = Am[1][1]; K[2] = Am[2][2]; K[3] = Am[0][1]; K[4] = Am[0][2]; K[5] = Am[1][2];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) K[6 + 3 * i + j] = Bm[i][j];
+#pragma unroll
+  for (int k = 0; k < 6; k++) K[15 + k] = Q[k];
+}
+__device__ __forceinline__ void symK_mul(const real* K, const real* v, real* y) {
+  const real *A = K, *B = K + 6, *Q = K + 15;
+  const real w0 = v[0], w1 = v[1], w2 = v[2], l0 = v[3], l1 = v[4], l2 = v[5];
+  y[0] = A[0] * w0 + A[3] * w1 + A[4] * w2 + B[0] * l0 + B[1] * l1 + B[2] * l2;
+  y[1] = A[3] * w0 + A[1] * w1 + A[5] * w2 + B[3] * l0 + B[4] * l1 + B[5] * l2;
+  y[2] = A[4] * w0 + A[5] * w1 + A[2] * w2 + B[6] * l0 + B[7] * l1 + B[8] * l2;
+  y[3] = B[0] * w0 + B[3] * w1 + B[6] * w2 + Q[0] * l0 + Q[3] * l1 + Q[4] * l2;
+  y[4] = B[1] * w0 + B[4] * w1 + B[7] * w2 + Q[3] * l0 + Q[1] * l1 + Q[5] * l2;
+  y[5] = B[2] * w0 + B[5] * w1 + B[8] * w2 + Q[4] * l0 + Q[5] * l1 + Q[2] * l2;
+}
+
+// xor butterfly over the wave: every lane ends with the same sum (oracle butterfly64)
+__device__ __forceinline__ real wave_sum(real v) {
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) v = v + __shfl_xor(v, s);
+  return v;
+}
+
+// H~ v on the tree blocks, lane = dof (oracle smooth_matvec); v, out in LDS
+template <int CL>
+__device__ void smooth_matvec(SharedT<CL>& S, const GmTopo* __restrict__ T, const real* v, real* out, int lane) {
+  if (lane < T->nv) {
+    const int d = lane, c = T->dof_grp[d], p = T->dof_p[d];
+    real acc;
+    if (c >= 0 && c < 3) {
+      const real* H = S.Hf[c];
+      const int f0 = T->dof_f0[c];
+      acc = H[TRI(p, 0)] * v[T->dof_base];
+#pragma unroll
+      for (int j = 1; j <= CL; j++) {
+        const real hv = (j <= p) ? H[TRI(p, j)] : H[TRI(j, p)];
+        acc = acc + hv * v[f0 + j - 1];
+      }
+    } else if (c == GM_GRP_BASE) {
+      acc = S.Hbb * v[T->dof_base];
+#pragma unroll
+      for (int f = 0; f < 3; f++)
+#pragma unroll
+        for (int q = 1; q <= CL; q++) acc = acc + S.Hf[f][TRI(q, 0)] * v[T->dof_f0[f] + q - 1];
+      acc = acc + S.Hp[TRI(1, 0)] * v[T->dof_palm];
+    } else if (c == GM_GRP_PALM) {
+      acc = S.Hp[TRI(1, 0)] * v[T->dof_base] + S.Hp[TRI(1, 1)] * v[T->dof_palm];
+    } else {
+      acc = 0;
+#pragma unroll
+      for (int l = 0; l < 6; l++) {
+        const real hv = (l <= p) ? S.Ho[TRI(p, l)] : S.Ho[TRI(l, p)];
+        acc = acc + hv * v[T->dof_obj + l];
+      }
+    }
+    out[d] = acc;
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------ Newton solve
+// Row data lives with its lane: contact c's 4 edges on lane c (D, aref, jar at the
+// iterate q, at the Newton point x), motor-lock row r on lane r (its own registers).
+struct RowsT {
+  real cD, caref[4], cjq[4], cjx[4];   // contact lane
+  real lD, laref, ljq, ljx;            // lock lane
+  int ldof;
+};
+
+// constraint setup (mj_makeConstraint / mj_makeImpedance): impedance, the regulariser
+// R = (1 - d) / d diagApprox (lock rows: dof_invweight0; pyramid edges:
+// tran + mu^2 tran, tran = the two bodies' invweight0), reference accelerations
+template <int CL, bool CAL>
+__device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
+                                 int lane, RowsT& R) {
+  const real h = CAL ? S.s.dt : m->timestep;
+  real tc = m->solref[0];
+  if (tc < 2 * h) tc = 2 * h;
+  const real dr = m->solref[1], dmax = m->solimp[1];
+  const real K = rcp_n(dmax * dmax * tc * tc * dr * dr);
+  const real Bd = div_n(2.0, dmax * tc);
+  // lock rows: the lane-th active lock
+  int nl = 0;
+  for (int k = 0; k < T->nlock; k++) nl += S.s.lock_active[k] ? 1 : 0;
+  R.lD = 0; R.laref = 0; R.ldof = 0;
+  if (lane < nl) {
+    int k = 0, cntl = -1;
+    for (k = 0; k < T->nlock; k++) { if (S.s.lock_active[k]) cntl++; if (cntl == lane) break; }
+    const int d = m->lock_dof[k];
+    const real pos = S.s.qpos[d] - S.s.lock_q[k];
+    const real vel = S.s.qvel[d];
+    const real imp = impedance(m, pos);
+    real Rr = div_n(1 - imp, imp) * m->dof_invweight0[d];
+    if (Rr < 1e-15) Rr = 1e-15;
+    R.lD = rcp_n(Rr);
+    R.laref = -Bd * vel - K * imp * pos;
+    R.ldof = d;
+  }
+  if (lane == 0) { S.nl = nl; S.nefc = nl + 4 * S.ncon; }
+  body_vel<CL>(S, S.s.qvel, m, T, lane);
+  R.cD = 0;
+#pragma unroll
+  for (int e = 0; e < 4; e++) R.caref[e] = 0;
+  if (lane < S.ncon) {
+    const real* C = S.con[lane];
+    const int b1 = m->geom_body[S.cgeom[lane][0]], b2 = m->geom_body[S.cgeom[lane][1]];
+    const real iw1 = (b1 == T->body_obj) ? S.s.obj_invw[0] : m->body_invweight0[b1][0];
+    const real iw2 = (b2 == T->body_obj) ? S.s.obj_invw[0] : m->body_invweight0[b2][0];
+    const real tran = iw1 + iw2;
+    const real mu = C[10];
+    const real diag = tran + (mu * mu) * tran;
+    const real imp = impedance(m, C[0]);
+    real Rr = div_n(1 - imp, imp) * diag;
+    if (Rr < 1e-15) Rr = 1e-15;
+    R.cD = rcp_n(Rr);
+    real vel[4];
+    contact_jv<CL>(S, m, lane, vel);
+#pragma unroll
+    for (int e = 0; e < 4; e++) R.caref[e] = -Bd * vel[e] - K * imp * C[0];
+  }
+  __syncthreads();
+}
+
+// J v - aref for every row at the dof vector v (LDS); into jr (contact) / jl (lock)
+template <int CL>
+__device__ __forceinline__ void rows_jar(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
+                                         const real* v, int lane, const RowsT& R, real* jr, real& jl) {
+  body_vel<CL>(S, v, m, T, lane);
+  jl = (lane < S.nl) ? v[R.ldof] - R.laref : 0.0;
+  if (lane < S.ncon) {
+    real jv[4];
+    contact_jv<CL>(S, m, lane, jv);
+#pragma unroll
+    for (int e = 0; e < 4; e++) jr[e] = jv[e] - R.caref[e];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; e++) jr[e] = 0.0;
+  }
+}
+
+// per-lane partial of a row sum (contact edges in order, then the lane's lock row) and the
+// wave butterfly (oracle row_reduce)
+__device__ __forceinline__ real row_sum(int lane, int ncon, int nl, const real* tc, real tl) {
+  real a = 0.0;
+  if (lane < ncon) a = ((tc[0] + tc[1]) + tc[2]) + tc[3];
+  if (lane < nl) a = a + tl;
+  return wave_sum(a);
+}
+
+// The Newton point x = H^-1 rhs for the active pattern (oracle newton_assemble +
+// newton_factor_solve).  Lane roles: contact lanes build Q / F; scan lanes (GmTopo
+// lane_body) sum their body's contacts and suffix-scan along the chains; factor lanes --
+// finger chain rows on 16 f + p (p = 1..CL), border rows [base, obj0..5] on 48..54, the
+// palm on 56 -- assemble H and rhs, factor, solve; x goes to S.xs.
+#define GM_LANE_PALM_F 56
+template <int CL>
+__device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
+                             const RowsT& R, const bool* act) {
+  const int ncon = S.ncon, nl = S.nl;
+  // ---- contact lanes: Q = sum_e D u u^T and F = sum_e D aref u over the active edges
+  if (lane < ncon) {
+    const real* C = S.con[lane];
+    real t2[3];
+    cross3(t2, C + 4, C + 7);
+    real Q[6] = {0, 0, 0, 0, 0, 0}, F[3] = {0, 0, 0};
+#pragma unroll
+    for (int ed = 0; ed < 4; ed++) {
+      real u[3];
+      edge_dir(C, t2, ed, u);
+      const real w = act[ed] ? R.cD : 0.0;
+      const real du[3] = {w * u[0], w * u[1], w * u[2]};
+      Q[0] += du[0] * u[0]; Q[1] += du[1] * u[1]; Q[2] += du[2] * u[2];
+      Q[3] += du[0] * u[1]; Q[4] += du[0] * u[2]; Q[5] += du[1] * u[2];
+      const real g = w * R.caref[ed];
+      F[0] += g * u[0]; F[1] += g * u[1]; F[2] += g * u[2];
+    }
+    real* qf = S.nw.QF[lane];
+#pragma unroll
+    for (int k = 0; k < 6; k++) qf[k] = Q[k];
+    qf[6] = F[0]; qf[7] = F[1]; qf[8] = F[2];
+  }
+  __syncthreads();
+  // ---- scan lanes: the body's contacts with the object (o) / the ground (g)
+  const int b = T->lane_body[lane];
+  real Ko[21], Kg[21], Fo[6], Fg[6];
+#pragma unroll
+  for (int k = 0; k < 21; k++) { Ko[k] = 0; Kg[k] = 0; }
+#pragma unroll
+  for (int k = 0; k < 6; k++) { Fo[k] = 0; Fg[k] = 0; }
+  bool have_g = false;
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+#pragma unroll
+    for (int og = 0; og < 2; og++) {
+      const int pr = og == 0 ? T->lane_opair[lane][s] : T->lane_gpair[lane][s];
+      if (pr < 0) continue;
+      const int c0 = S.pair_off[pr];
+      int c1 = c0 + S.pair_cnt[pr];
+      if (c1 > ncon) c1 = ncon;
+      for (int c = c0; c < c1; c++) {
+        const real* qf = S.nw.QF[c];
+        const real pos[3] = {S.con[c][1], S.con[c][2], S.con[c][3]};
+        const real sg = (m->geom_body[S.cgeom[c][1]] == b) ? 1.0 : -1.0;
+        real Kc[21], Fs[6];
+        spatial_K(qf, pos, Kc);
+        cross3(Fs, pos, qf + 6);
+        Fs[3] = qf[6]; Fs[4] = qf[7]; Fs[5] = qf[8];
+        if (og == 0) {
+#pragma unroll
+          for (int k = 0; k < 21; k++) Ko[k] += Kc[k];
+#pragma unroll
+          for (int k = 0; k < 6; k++) Fo[k] += sg * Fs[k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < 21; k++) Kg[k] += Kc[k];
+#pragma unroll
+          for (int k = 0; k < 6; k++) Fg[k] += sg * Fs[k];
+          have_g = true;
+        }
+      }
+    }
+  }
+  const bool any_g = __ballot(have_g) != 0ull;
+  // the object's ground contacts (its other contacts reach it through the base composite)
+  if (lane == T->lane_obj) {
+    real Kgo[21], Fgo[6];
+#pragma unroll
+    for (int k = 0; k < 21; k++) Kgo[k] = 0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) Fgo[k] = 0;
+    const int pr = T->pair_gobj;
+    if (pr >= 0) {
+      const int c0 = S.pair_off[pr];
+      int c1 = c0 + S.pair_cnt[pr];
+      if (c1 > ncon) c1 = ncon;
+      for (int c = c0; c < c1; c++) {
+        const real* qf = S.nw.QF[c];
+        const real pos[3] = {S.con[c][1], S.con[c][2], S.con[c][3]};
+        const real sg = (m->geom_body[S.cgeom[c][1]] == T->body_obj) ? 1.0 : -1.0;
+        real Kc[21], Fs[6];
+        spatial_K(qf, pos, Kc);
+        cross3(Fs, pos, qf + 6);
+        Fs[3] = qf[6]; Fs[4] = qf[7]; Fs[5] = qf[8];
+#pragma unroll
+        for (int k = 0; k < 21; k++) Kgo[k] += Kc[k];
+#pragma unroll
+        for (int k = 0; k < 6; k++) Fgo[k] += sg * Fs[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 21; k++) S.go[k] = Kgo[k];
+#pragma unroll
+    for (int k = 0; k < 6; k++) S.go[21 + k] = Fgo[k];
+  }
+  // ---- suffix sums along the chains (composite, like Ic)
+#pragma unroll
+  for (int off = 1; off < CL; off <<= 1) {
+#pragma unroll
+    for (int k = 0; k < 21; k++) Ko[k] += row_shl(Ko[k], off);
+#pragma unroll
+    for (int k = 0; k < 6; k++) Fo[k] += row_shl(Fo[k], off);
+  }
+  if (any_g) {
+#pragma unroll
+    for (int off = 1; off < CL; off <<= 1) {
+#pragma unroll
+      for (int k = 0; k < 21; k++) Kg[k] += row_shl(Kg[k], off);
+#pragma unroll
+      for (int k = 0; k < 6; k++) Fg[k] += row_shl(Fg[k], off);
+    }
+  }
+  __syncthreads();   // every lane is done with QF before the stage overwrites it
+  // ---- chain roots (fingers at position 1, the palm) to the stage; the ground-object pair
+  {
+    const int root = (lane == 1) ? 0 : (lane == 17) ? 1 : (lane == 33) ? 2 : (lane == 49) ? 3 : -1;
+    if (root >= 0) {
+      real* st = S.st.root[root];
+#pragma unroll
+      for (int k = 0; k < 21; k++) { st[k] = Ko[k]; st[21 + k] = Kg[k]; }
+#pragma unroll
+      for (int k = 0; k < 6; k++) { st[42 + k] = Fo[k]; st[48 + k] = Fg[k]; }
+    }
+  }
+  __syncthreads();
+  // ---- base composites (the four roots in order) and the object's totals
+  if (lane < 54) {
+    real acc = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) acc += S.st.root[c][lane];
+    S.st.comp[lane] = acc;
+  }
+  __syncthreads();
+  if (lane < 27) {
+    // Koo = KBo + Kgo (21), Fobj = Fgo - FBo (6)
+    S.st.oo[lane] = (lane < 21) ? S.st.comp[lane] + S.go[lane] : S.go[lane] - S.st.comp[42 + lane - 21];
+  }
+  __syncthreads();
+  // ---- H and rhs on the factor lanes
+  real h[CL + 1], hb[7], rhs = 0;
+#pragma unroll
+  for (int j = 0; j <= CL; j++) h[j] = 0;
+#pragma unroll
+  for (int k = 0; k < 7; k++) hb[k] = 0;
+  const int rowf = lane >> 4, p = lane & 15;
+  const real* cdb = S.cdof[T->dof_base];
+  if (rowf < 3 && p >= 1 && p <= CL) {
+    const int d = T->dof_f0[rowf] + p - 1;
+    real Kt[21], Ft[6];
+#pragma unroll
+    for (int k = 0; k < 21; k++) Kt[k] = any_g ? Ko[k] + Kg[k] : Ko[k];
+#pragma unroll
+    for (int k = 0; k < 6; k++) Ft[k] = any_g ? Fo[k] + Fg[k] : Fo[k];
+    real cd[6], y[6], yo[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
+    symK_mul(Kt, cd, y);
+    symK_mul(Ko, cd, yo);
+    const real* H = S.Hf[rowf];
+#pragma unroll
+    for (int j = 1; j <= CL; j++)
+      if (j <= p) h[j] = H[TRI(p, j)] + dot6(S.cdof[T->dof_f0[rowf] + j - 1], y);
+    hb[0] = H[TRI(p, 0)] + dot6(cdb, y);
+#pragma unroll
+    for (int k = 0; k < 6; k++) hb[1 + k] = -dot6(S.cdof[T->dof_obj + k], yo);
+    rhs = S.frc[d] + dot6(cd, Ft);
+  } else if (lane == GM_LANE_PALM_F) {
+    const int d = T->dof_palm;
+    const real* st = S.st.root[3];
+    real Kt[21], Ft[6], K0[21];
+#pragma unroll
+    for (int k = 0; k < 21; k++) { K0[k] = st[k]; Kt[k] = any_g ? st[k] + st[21 + k] : st[k]; }
+#pragma unroll
+    for (int k = 0; k < 6; k++) Ft[k] = any_g ? st[42 + k] + st[48 + k] : st[42 + k];
+    real cd[6], y[6], yo[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
+    symK_mul(Kt, cd, y);
+    symK_mul(K0, cd, yo);
+    h[1] = S.Hp[TRI(1, 1)] + dot6(cd, y);
+    hb[0] = S.Hp[TRI(1, 0)] + dot6(cdb, y);
+#pragma unroll
+    for (int k = 0; k < 6; k++) hb[1 + k] = -dot6(S.cdof[T->dof_obj + k], yo);
+    rhs = S.frc[d] + dot6(cd, Ft);
+  } else if (lane >= 48 && lane < 55) {
+    const int i = lane - 48;
+    const real* cp = S.st.comp;
+    real KBo[21], yob[6];
+#pragma unroll
+    for (int k = 0; k < 21; k++) KBo[k] = cp[k];
+    symK_mul(KBo, cdb, yob);
+    if (i == 0) {
+      real KBt[21], FBt[6], y[6];
+#pragma unroll
+      for (int k = 0; k < 21; k++) KBt[k] = any_g ? cp[k] + cp[21 + k] : cp[k];
+#pragma unroll
+      for (int k = 0; k < 6; k++) FBt[k] = any_g ? cp[42 + k] + cp[48 + k] : cp[42 + k];
+      symK_mul(KBt, cdb, y);
+      hb[0] = S.Hbb + dot6(cdb, y);
+      rhs = S.frc[T->dof_base] + dot6(cdb, FBt);
+    } else {
+      const int k = i - 1;
+      const real* cok = S.cdof[T->dof_obj + k];
+      real Koo[21], yk[6];
+#pragma unroll
+      for (int t = 0; t < 21; t++) Koo[t] = S.st.oo[t];
+      symK_mul(Koo, cok, yk);
+      hb[0] = -dot6(cok, yob);
+#pragma unroll
+      for (int l2 = 0; l2 < 6; l2++)
+        if (l2 <= k) hb[1 + l2] = S.Ho[TRI(k, l2)] + dot6(S.cdof[T->dof_obj + l2], yk);
+      rhs = S.frc[T->dof_obj + k] + dot6(cok, S.st.oo + 21);
+    }
+  }
+  // motor-lock rows (1-dof joint equalities): D on the diagonal, D aref on the rhs
+  for (int r = 0; r < nl; r++) {
+    const int d = __builtin_amdgcn_readlane(R.ldof, r);
+    const real lD = readlane_real(R.lD, r), lR = readlane_real(R.lD * R.laref, r);
+    if (T->dof_grp[d] < 3) {
+      const int f = T->dof_grp[d], pd = T->dof_p[d];
+      if (rowf == f && p == pd) {
+#pragma unroll
+        for (int j = 1; j <= CL; j++) if (j == pd) h[j] += lD;
+        rhs += lR;
+      }
+    } else if (lane == GM_LANE_PALM_F) {
+      h[1] += lD;
+      rhs += lR;
+    }
+  }
+  __syncthreads();   // the stage is read; the factor's transfers reuse the union
+  // ---- factor: finger chains (rows 0..2), pivots CL .. 1
+  real invd = 1.0;
+  if (lane < 48) {
+#pragma unroll
+    for (int k = CL; k >= 1; k--) {
+      const real hkk = row_bcast(h[k], k);
+      const real ihk = rcp_n(hkk);
+      real hk[CL + 1], hkb[7];
+#pragma unroll
+      for (int j = 1; j < k; j++) hk[j] = row_bcast(h[j], k);
+#pragma unroll
+      for (int t = 0; t < 7; t++) hkb[t] = row_bcast(hb[t], k);
+      const bool upd = p >= 1 && p < k, piv = p == k;
+      real Hpk = 0.0;
+#pragma unroll
+      for (int j = 1; j < k; j++) Hpk = (p == j) ? hk[j] : Hpk;
+      const real a = Hpk * ihk;
+      const real aa = upd ? a : 0.0;
+      const real sc = piv ? ihk : 1.0;
+      if (piv && rowf < 3) {
+        real* ub = S.fs.lbub[rowf][k - 1] + 7;
+#pragma unroll
+        for (int t = 0; t < 7; t++) ub[t] = hb[t];
+      }
+#pragma unroll
+      for (int j = 1; j < k; j++) h[j] = (h[j] - hk[j] * aa) * sc;
+#pragma unroll
+      for (int t = 0; t < 7; t++) hb[t] = (hb[t] - hkb[t] * aa) * sc;
+      h[k] = upd ? a : h[k];
+      invd = piv ? ihk : invd;
+    }
+    if (rowf < 3 && p >= 1 && p <= CL) {
+      real* lb = S.fs.lbub[rowf][p - 1];
+#pragma unroll
+      for (int t = 0; t < 7; t++) lb[t] = hb[t];
+    }
+  } else if (lane == GM_LANE_PALM_F) {
+    const real ih = rcp_n(h[1]);
+    real* pl = S.fs.plb;
+#pragma unroll
+    for (int t = 0; t < 7; t++) { pl[7 + t] = hb[t]; hb[t] = hb[t] * ih; pl[t] = hb[t]; }
+    invd = ih;
+  } else if (lane >= 48 && lane < 55) {
+    // border rows to the entry transfer: lower triangle, row-major
+    const int i = lane - 48;
+#pragma unroll
+    for (int j = 0; j < 7; j++)
+      if (j <= i) S.fs.bbx[i * (i + 1) / 2 + j] = hb[j];
+  }
+  __syncthreads();
+  // Schur complements: one lane per border entry (i, j), elimination order
+  if (lane < 28) {
+    int i = 0;
+#pragma unroll
+    for (int t = 1; t < 7; t++) i += (lane >= t * (t + 1) / 2) ? 1 : 0;
+    const int j = lane - i * (i + 1) / 2;
+    real v = S.fs.bbx[lane];
+#pragma unroll
+    for (int f = 0; f < 3; f++)
+#pragma unroll
+      for (int k = CL; k >= 1; k--) v = v - S.fs.lbub[f][k - 1][i] * S.fs.lbub[f][k - 1][7 + j];
+    v = v - S.fs.plb[i] * S.fs.plb[7 + j];
+    S.fs.bbx[lane] = v;
+  }
+  __syncthreads();
+  const int bi = lane - 48;
+  const bool border = lane >= 48 && lane < 55;
+  if (border) {
+#pragma unroll
+    for (int j = 0; j < 7; j++)
+      if (j <= bi) hb[j] = S.fs.bbx[bi * (bi + 1) / 2 + j];
+    // border LDL^T: pivots 6 .. 0 (row 3 lanes 48 + k)
+#pragma unroll
+    for (int k = 6; k >= 0; k--) {
+      const real ihk = rcp_n(row_bcast(hb[k], k));
+      real bk[7];
+#pragma unroll
+      for (int j = 0; j < k; j++) bk[j] = row_bcast(hb[j], k);
+      const bool upd = bi < k, piv = bi == k;
+      real Bik = 0.0;
+#pragma unroll
+      for (int j = 0; j < k; j++) Bik = (bi == j) ? bk[j] : Bik;
+      const real a = Bik * ihk;
+      const real aa = upd ? a : 0.0;
+      const real sc = piv ? ihk : 1.0;
+#pragma unroll
+      for (int j = 0; j < k; j++) hb[j] = (hb[j] - bk[j] * aa) * sc;
+      hb[k] = upd ? a : hb[k];
+      invd = piv ? ihk : invd;
+    }
+  }
+  // ---- solve: forward (chains leaf first, border sums, border), D, backward
+  real y = rhs;
+  if (lane < 48) {
+#pragma unroll
+    for (int k = CL; k >= 1; k--) {
+      const real yk = row_bcast(y, k);
+      const real Lc = (p >= 1 && p < k) ? h[k] : 0.0;
+      y = y - Lc * yk;
+    }
+    if (rowf < 3 && p >= 1 && p <= CL) S.fs.ych[rowf][p - 1] = y;
+  } else if (lane == GM_LANE_PALM_F) {
+    S.fs.ypalm = y;
+  }
+  __syncthreads();
+  if (border) {
+    real v = y;
+#pragma unroll
+    for (int f = 0; f < 3; f++)
+#pragma unroll
+      for (int k = CL; k >= 1; k--) v = v - S.fs.lbub[f][k - 1][bi] * S.fs.ych[f][k - 1];
+    v = v - S.fs.plb[bi] * S.fs.ypalm;
+    y = v;
+#pragma unroll
+    for (int k = 6; k >= 0; k--) {
+      const real yk = row_bcast(y, k);
+      const real Lc = (bi < k) ? hb[k] : 0.0;
+      y = y - Lc * yk;
+    }
+  }
+  y = y * invd;
+  if (border) {
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+      const real xj = row_bcast(y, j);
+      const real Lr = (j < bi) ? hb[j] : 0.0;
+      y = y - Lr * xj;
+    }
+  }
+  // the border solution to every lane (row 3 lanes 48..54)
+  real xb[7];
+#pragma unroll
+  for (int t = 0; t < 7; t++) xb[t] = readlane_real(y, 48 + t);
+  if (lane < 48) {
+#pragma unroll
+    for (int t = 0; t < 7; t++) y = y - hb[t] * xb[t];
+#pragma unroll
+    for (int j = 1; j < CL; j++) {
+      const real xj = row_bcast(y, j);
+      const real Lr = (j < p) ? h[j] : 0.0;
+      y = y - Lr * xj;
+    }
+    if (rowf < 3 && p >= 1 && p <= CL) S.xs[T->dof_f0[rowf] + p - 1] = y;
+  } else if (lane == GM_LANE_PALM_F) {
+#pragma unroll
+    for (int t = 0; t < 7; t++) y = y - hb[t] * xb[t];
+    S.xs[T->dof_palm] = y;
+  } else if (border) {
+    S.xs[bi == 0 ? T->dof_base : T->dof_obj + bi - 1] = y;
+  }
+  __syncthreads();
+}
+
+// mj_solNewton restated (oracle newton_solve): warm start, Newton point on the active
+// pattern, accept when the pattern at x is unchanged (x is then the exact optimum), else
+// an exact line search along x - q; contact forces and the warm start at the end.
+template <int CL, bool CAL>
+__device__ void newton_solve(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
+                             bool prof) {
+  unsigned long long t0 = prof ? clock64() : 0;
+  RowsT R;
+  constraint_setup<CL, CAL>(S, m, T, lane, R);
+  const int ncon = S.ncon, nl = S.nl, nv = T->nv;
+  const bool clane = lane < ncon;
+  if (lane < nv) S.qacc[lane] = S.s.qacc_warm[lane];
+  __syncthreads();
+  smooth_matvec<CL>(S, T, S.qacc, S.Ma, lane);
+  real jq[4], jql;
+  rows_jar<CL>(S, m, T, S.qacc, lane, R, jq, jql);
+  PH(11);
+  int it = 0, nls = 0;
+  for (it = 0; it < GM_NEWTON_MAXIT; it++) {
+    bool act[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) act[e] = clane && jq[e] < 0;
+    newton_point<CL>(S, m, T, lane, R, act);
+    real jx[4], jxl;
+    rows_jar<CL>(S, m, T, S.xs, lane, R, jx, jxl);
+    bool differ = false;
+#pragma unroll
+    for (int e = 0; e < 4; e++) differ = differ || (clane && ((jx[e] < 0) != act[e]));
+    if (__ballot(differ) == 0ull) {
+      if (lane < nv) S.qacc[lane] = S.xs[lane];
+#pragma unroll
+      for (int e = 0; e < 4; e++) jq[e] = jx[e];
+      jql = jxl;
+      it++;
+      break;
+    }
+    // exact line search along d = x - q (d overwrites x)
+    if (lane < nv) S.xs[lane] = S.xs[lane] - S.qacc[lane];
+    __syncthreads();
+    smooth_matvec<CL>(S, T, S.xs, S.Mv, lane);
+    const real dd = lane < nv ? S.xs[lane] : 0.0;
+    const real g0 = wave_sum(lane < nv ? dd * (S.Ma[lane] - S.frc[lane]) : 0.0);
+    const real h0 = wave_sum(lane < nv ? dd * S.Mv[lane] : 0.0);
+    real dj[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) dj[e] = jx[e] - jq[e];
+    const real djl = jxl - jql;
+    real alpha = 1.0, lo = 0.0, hi = 0.0;
+    bool hi_set = false, newton = false, have_prev = false;
+    unsigned prev = 0;
+    for (int ls = 0; ls < GM_NEWTON_MAXLS; ls++) {
+      nls++;
+      unsigned pat = 0;
+      real tg[4], th[4];
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const real j = jq[e] + alpha * dj[e];
+        const bool a = clane && j < 0;
+        pat |= (unsigned)a << e;
+        tg[e] = a ? (R.cD * j) * dj[e] : 0.0;
+        th[e] = a ? (R.cD * dj[e]) * dj[e] : 0.0;
+      }
+      const real jl = jql + alpha * djl;
+      const real tgl = (R.lD * jl) * djl, thl = (R.lD * djl) * djl;   // lock rows: always active
+      const bool same_piece = have_prev && __ballot(pat != prev) == 0ull;
+      if (newton && same_piece) break;
+      const real g = (g0 + alpha * h0) + row_sum(lane, ncon, nl, tg, tgl);
+      const real hh = h0 + row_sum(lane, ncon, nl, th, thl);
+      if (g == 0.0) break;
+      if (g < 0) lo = alpha; else { hi = alpha; hi_set = true; }
+      if (!(hh > 0)) break;
+      real an = alpha - div_n(g, hh);
+      newton = true;
+      if (!(an > lo) || (hi_set && !(an < hi))) { an = hi_set ? 0.5 * (lo + hi) : 2.0 * alpha; newton = false; }
+      prev = pat;
+      have_prev = true;
+      alpha = an;
+    }
+    if (lane < nv) {
+      S.qacc[lane] = S.qacc[lane] + alpha * S.xs[lane];
+      S.Ma[lane] = S.Ma[lane] + alpha * S.Mv[lane];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; e++) jq[e] = jq[e] + alpha * dj[e];
+    jql = jql + alpha * djl;
+    __syncthreads();
+  }
+  PH(13);
+  // constraint forces at the solution and the contact-frame forces (mj_contactForce)
+  real fe[4];
+#pragma unroll
+  for (int e = 0; e < 4; e++) fe[e] = (clane && jq[e] < 0) ? -(R.cD * jq[e]) : 0.0;
+  if (clane) {
+    real* C = S.con[lane];
+    const real mu = C[10];
+    C[11] = ((fe[0] + fe[1]) + fe[2]) + fe[3];
+    C[12] = mu * (fe[0] - fe[1]);
+    C[13] = mu * (fe[2] - fe[3]);
+#pragma unroll
+    for (int e = 0; e < 4; e++) S.dbg.efc[nl + 4 * lane + e] = fe[e];
+  }
+  if (lane < nl) S.dbg.efc[lane] = -(R.lD * jql);
+  if (lane < nv) S.s.qacc_warm[lane] = S.qacc[lane];
+  if (lane == 0) {
+    S.work_nefc += nl + 4 * ncon;
+    S.work_newton += it;
+    if (prof) { S.tph[24] += nl + 4 * ncon; S.tph[26] += it; S.tph[27] += nls; }
+  }
+  __syncthreads();
+}

@@ -237,4 +237,9 @@ struct GmTopo {
   double pr_rbound[GM_MAX_PAIR][2], pr_fric[GM_MAX_PAIR][2];
   // per motor lock: the locked dof's group and chain position
   int32_t lock_grp[GM_MAX_LOCK], lock_cpos[GM_MAX_LOCK];
+  // Newton Hessian assembly: per scan lane, the pairs of the lane body's geoms with the
+  // object / the ground (-1: none; the object lane holds none, its ground contacts come
+  // from pair_gobj); lane_obj is the object's scan lane
+  int32_t lane_opair[64][2], lane_gpair[64][2];
+  int32_t pair_gobj, lane_obj;
 };

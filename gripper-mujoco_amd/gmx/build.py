@@ -20,11 +20,10 @@ def build(verbose: bool = False, force: bool = False) -> str:
     """Compile each translation unit in parallel (the env-step kernel and the calibration
     variant are separate device modules), then link libgm.so."""
     srcs = [os.path.join(PKG_DIR, s) for s in SOURCES]
-    deps = srcs + [os.path.join(PKG_DIR, "csrc", f) for f in ("gm_kernels.hip", "gm_policy.hip", "gm_state.h")] + \
+    deps = srcs + [os.path.join(PKG_DIR, "csrc", f) for f in ("gm_kernels.hip", "gm_newton.hip", "gm_math.h", "gm_policy.hip", "gm_state.h")] + \
         [os.path.join(REPO_DIR, "include", f) for f in ("gripper_mi355x.h", "gm_settings.def")]
-    pgsgen = os.path.join(os.path.dirname(LIB_PATH), "libgm_pgsgen.so")
-    if not force and os.path.exists(LIB_PATH) and os.path.exists(pgsgen):
-        t = min(os.path.getmtime(LIB_PATH), os.path.getmtime(pgsgen))
+    if not force and os.path.exists(LIB_PATH):
+        t = os.path.getmtime(LIB_PATH)
         if all(os.path.getmtime(d) <= t for d in deps):
             return LIB_PATH
     objdir = os.path.join(os.path.dirname(LIB_PATH), "obj")
@@ -46,23 +45,4 @@ def build(verbose: bool = False, force: bool = False) -> str:
         print(" ".join(link))
     subprocess.run(link, check=True)
     os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    build_pgs_general(objdir, inc, verbose)
     return LIB_PATH
-
-
-PGSGEN_PATH = os.path.join(os.path.dirname(LIB_PATH), "libgm_pgsgen.so")
-
-
-def build_pgs_general(objdir: str, inc: list, verbose: bool = False) -> str:
-    """Test library: the step kernel with every constraint problem on the general
-    (lane-per-row, v_readlane) PGS path, for tests/test_pgs_paths.py."""
-    src = os.path.join(PKG_DIR, "csrc", "gm_capi.hip")
-    obj = os.path.join(objdir, "gm_capi_pgsgen.hip.o")
-    cmd = [HIPCC, *FLAGS, "-DGM_PGS_GENERAL_ONLY", *inc, "-c", src, "-o", obj]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
-    objs = [obj] + [os.path.join(objdir, os.path.basename(s) + ".o") for s in SOURCES[1:]]
-    subprocess.run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", PGSGEN_PATH + ".tmp"], check=True)
-    os.replace(PGSGEN_PATH + ".tmp", PGSGEN_PATH)
-    return PGSGEN_PATH

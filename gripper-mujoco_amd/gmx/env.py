@@ -116,6 +116,7 @@ class BatchedGripperEnv:
         env's global id and next episode (spawn_draws), with optional overrides."""
         n = self.n_envs
         gids = self.env_offset + np.arange(n)
+        self._sync_episode()
         si, sx, sy, sr = spawn_draws(self.seed, gids, self._episode + 1, len(self.objects))
         if idx is not None: si = np.broadcast_to(np.asarray(idx), (n,))
         if x is not None: sx = np.broadcast_to(np.asarray(x, dtype=np.float64), (n,))
@@ -125,6 +126,12 @@ class BatchedGripperEnv:
         for e in range(n):
             arr[e].object_index = int(si[e]); arr[e].x = float(sx[e]); arr[e].y = float(sy[e]); arr[e].zrot = float(sr[e])
         return arr
+
+    def _sync_episode(self):
+        """The device owns GmEnvState::episode (gm_autoreset and gm_set_env_states move it
+        without the host seeing): re-read it before drawing a spawn table."""
+        from ._lib import env_state_view
+        self._episode[:] = env_state_view(self.env_states())["episode"]
 
     def reset(self, mask=None, spawn=None):
         """MjClass::reset + spawn for masked envs; returns the observation (MjEnv.reset).
@@ -293,9 +300,9 @@ class BatchedGripperEnv:
         return o
 
     def debug_substep(self, full: bool = False):
-        """One MjClass::step on every env with fp64 diagnostics: (ncon, contact [n,15,16],
-        efc_force [n,64], qacc [n,40]) and, with full=True, also nefc [n] and the object's
-        cfrc_ext wrench [n,6]."""
+        """One MjClass::step on every env with fp64 diagnostics: (ncon, contact [n, GM_MAX_CON, 16],
+        efc_force [n, GM_MAX_EFC], qacc [n, GM_MAX_DOF]) and, with full=True, also nefc [n] and
+        the object's cfrc_ext wrench [n, 6]."""
         n = self.n_envs
         ncon = np.zeros(n, dtype=np.int32)
         nefc = np.zeros(n, dtype=np.int32)
@@ -311,13 +318,16 @@ class BatchedGripperEnv:
             return ncon, con, f, qacc, nefc, w
         return ncon, con, f, qacc
 
-    PHASES = ("kinematics", "crb_rne", "mass_forces", "factor", "smooth_solve", "collision",
-              "constraints_pgs", "constraint_accel", "integrate", "update_all", "monitor_sensors",
-              "  c:jac+rowsolve", "  c:Yd", "  c:A_build", "  c:PGS", "  k:A_hinge", "  k:B_chains",
-              "  crb:chains", "e:sense", "e:update_env", "e:get_obs", "e:done_reward")
+    PHASES = ("kinematics", "crb_rne", "mass_forces", "-", "-", "collision",
+              "newton_solve", "-", "integrate", "update_all", "monitor_sensors",
+              "  n:setup+warm", "-", "  n:iterations", "-", "  k:A_hinge", "  k:B_chains",
+              "  crb:chains", "e:sense", "e:update_env", "e:get_obs", "e:done_reward", "substep_body", "env_step")
+    # columns past the clocks: 24 sum of constraint rows, 25 substeps that ran MPR,
+    # 26 Newton iterations, 27 line-search evaluations
+    N_PHASE = 28
 
     def step_profiled(self):
         """One env-step with per-phase shader-clock counters (lane 0, summed over substeps)."""
-        ph = np.zeros((self.n_envs, 26), dtype=np.uint64)
+        ph = np.zeros((self.n_envs, self.N_PHASE), dtype=np.uint64)
         self._check(self.lib.gm_step_profiled(self._ctx, ph.ctypes.data_as(C.POINTER(C.c_uint64))))
         return ph

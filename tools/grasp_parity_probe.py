@@ -20,10 +20,12 @@ for sn in snaps:
     rel, ab = obs_err(sn["obs"], obs_o)
     bad = (rel > 1e-4) | (ab > 1e-4)
     dq = np.abs(dv["qpos"] - ov["qpos"]).max(axis=1)
+    exact = int((dv["qpos"] == ov["qpos"]).all(axis=1).sum())
+    exact_obs = int((sn["obs"] == obs_o).all(axis=1).sum())
     mism = {f: int((dv[f] != ov[f]).reshape(n, -1).any(axis=1).sum()) for f in ("bev_row", "lev_row", "rng", "ring_i", "lock_active", "old_x", "old_z")}
     print(f"k={sn['k']} oracle {time.time()-t1:.1f}s bad_obs={bad.sum()} rel_max={rel.max():.2e} p99={np.percentile(rel,99):.2e} "
           f"abs_max={ab.max():.2e} done_dev={int(sn['done'].sum())} done_or={int(done_o.sum())} done_mism={int((sn['done'].astype(np.uint8)!=done_o).sum())} "
-          f"rew_maxd={np.abs(sn['rew']-rew_o).max():.2e} qpos_max={dq.max():.2e} qpos_p50={np.median(dq):.2e} mism={mism}", flush=True)
+          f"rew_maxd={np.abs(sn['rew']-rew_o).max():.2e} qpos_max={dq.max():.2e} qpos_p50={np.median(dq):.2e} qpos_bitexact={exact}/{n} obs_bitexact={exact_obs}/{n} mism={mism}", flush=True)
     if bad.any():
         e = int(np.argmax(rel))
         print("   worst env", e, "obj", int(dv["obj_index"][e]), "obs dev", np.round(sn["obs"][e], 5).tolist())

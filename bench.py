@@ -241,6 +241,51 @@ def policy_rollout(gmx, torch, dev, stream, n: int, steps: int, seed: int, env_o
     return out
 
 
+def measure(drive, returns, K: int, W: int, world: int, dev, sync):
+    """The contract's timed region, independent of what steps the envs (the device here,
+    the oracle in tests/test_distributed.py): W untimed warmup drives, then EXACTLY K
+    drives bracketed by sync + barrier + sync on both sides; the wall time is the MAX over
+    ranks.  Every drive's episode returns are all-gathered (the one collective, SURVEY.md
+    8e) and the finished episodes counted over the whole job.  drive(k) takes the timed
+    index k (None when untimed); `returns` holds NaN where an env's episode did not end."""
+    import torch
+    import torch.distributed as dist
+    from gmx.shard import gather_returns, max_over_ranks
+    episodes = torch.zeros((), device=dev, dtype=torch.int64)
+
+    def step(k=None):
+        drive(k)
+        episodes.add_(torch.isfinite(gather_returns(returns, world)).sum())
+
+    # warmup counts episodes too, so every kernel the timed loop launches (incl. torch's
+    # isfinite / sum / add for the episode counter) is loaded before the clock starts
+    for _ in range(max(W, 1)):
+        step()
+    episodes.zero_()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(K):
+        step(k)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    return max_over_ranks(elapsed, dev), int(episodes.item())
+
+
+def headline(world: int, n: int, K: int, W: int, elapsed: float) -> dict:
+    """The contract fields of rank 0's JSON line: value = env-steps of ALL ranks / the
+    slowest rank's wall time (weak scaling: n envs per rank)."""
+    return {"metric": METRIC, "value": round(world * n * K / elapsed, 1), "unit": "env-steps/s", "n_gpus": world,
+            "steps": K, "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64", "data": "synthetic"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -276,7 +321,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     import gmx
-    from gmx.shard import shard_range, gather_returns, max_over_ranks
+    from gmx.shard import shard_range
     settings = gmx.canonical_settings(seed=args.seed)
     n = args.envs
     first_env, _ = shard_range(rank, world, n)
@@ -290,8 +335,6 @@ def main():
     env.reset()
     returns = torch.full((n,), float("nan"), device=dev)
     d_act = env.lib.gm_device_actions(env.ctx)
-    episodes = torch.zeros((), device=dev, dtype=torch.int64)
-    counting = [False]
 
     def drive(timed=None):
         """one MjEnv.step-equivalent for the whole batch, all on the device"""
@@ -303,8 +346,6 @@ def main():
         if timed is not None:
             ev[timed][1].record(stream)
         env.autoreset_device(0, returns.data_ptr(), max_episode_steps=MAX_EP)
-        if counting[0]:
-            episodes.add_(torch.isfinite(gather_returns(returns, world)).sum())
 
     # steady state: env e (global id) starts its episode at pre-roll step t_e, so after
     # MAX_EP untimed steps the batch covers episode steps 1..MAX_EP uniformly
@@ -318,25 +359,7 @@ def main():
                 __import__("ctypes").POINTER(__import__("ctypes").c_uint8)), None)
         drive()
     K, W = args.steps, args.warmup
-    # warmup counts episodes too, so every kernel the timed loop launches (incl. torch's
-    # isfinite / sum / add for the episode counter) is loaded before the clock starts
-    counting[0] = True
-    for i in range(max(W, 1)):
-        drive()
-    episodes.zero_()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(K):
-        drive(k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(elapsed, dev)
+    elapsed, episodes = measure(drive, returns, K, W, world, dev, torch.cuda.synchronize)
     steps_view = gmx.env_state_view(env.env_states())["num_action_steps"]
 
     kern_ms = [a.elapsed_time(b) for a, b in ev]
@@ -346,6 +369,16 @@ def main():
     parity = None if (args.no_parity or rank != 0) else obs_parity(gmx, env, args.seed)
     # contact load of the batch state (one probing substep after the timed window)
     ncon_m, _, _, _, nefc_m, _ = env.debug_substep(full=True)
+    # the constraint solver's work on the same states (one profiled env-step after it):
+    # Newton iterations and exact-line-search evaluations per substep solve
+    ph = env.step_profiled().astype(np.float64)
+    n_solves = float(n * S)
+    solver = {"method": "primal Newton (mj_solNewton) with exact line search, warm-started",
+              "iterations_per_solve": round(ph[:, 26].sum() / n_solves, 4),
+              "max_iterations_in_env_step": int(ph[:, 26].max()),
+              "line_search_evals_per_solve": round(ph[:, 27].sum() / n_solves, 4),
+              "rows_per_solve": round(ph[:, 24].sum() / n_solves, 3),
+              "states": "the batch after the timed window, one profiled env-step"}
 
     if rank == 0:
         B = algorithmic_bytes_per_substep(env.model)
@@ -357,7 +390,12 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "kernel": "gm_step_kernel", "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
-                "traffic_source": traffic_src}
+                "traffic_source": traffic_src,
+                # the same roofline with the per-substep bytes at the batch's measured mean
+                # contact count instead of SURVEY.md 8d's nominal 12
+                "achieved_at_measured_ncon": round(n * S * Bm["bytes"] / kern_avg_s / 1e9, 2),
+                "frac_at_measured_ncon": round(n * S * Bm["bytes"] / kern_avg_s / 1e9 / HBM_PEAK_GBS, 5),
+                "measured_ncon": Bm["ncon"]}
         cpu = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(gmx, args.cpu_envs * args.cpu_threads // 4, args.cpu_steps, args.cpu_threads)
@@ -365,12 +403,8 @@ def main():
         c2 = None if (args.no_c2 or world > 1) else c2_line(gmx, torch, dev, stream, K, args.seed, first_env)
         c5 = None if (args.no_policy or world > 1) else policy_rollout(gmx, torch, dev, stream, n, max(3, K // 2), args.seed,
                                                         first_env)
-        value = world * n * K / elapsed
-        out = {
-            "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
-            "steps": K, "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f64", "data": "synthetic",
+        out = headline(world, n, K, W, elapsed)
+        out.update({
             "config": {"workload": "C3: set6_synthetic 20 mixed objects, randomised spawn (object drawn per "
                                    "episode, spawn_into_scene grid search on the device), steady state: envs "
                                    "staggered over episode steps 1..250 by an untimed pre-roll, scripted grasp "
@@ -381,21 +415,22 @@ def main():
                        "B_substep_bytes": B["bytes"], "B_substep_ncon": B["ncon"], "B_substep_nefc": B["nefc"],
                        "measured_contacts": {"mean_ncon": round(float(ncon_m.mean()), 3),
                                              "mean_nefc": round(float(nefc_m.mean()), 3),
-                                             "frac_nefc_gt_32": round(float((nefc_m > 32).mean()), 4),
+                                             "max_ncon": int(ncon_m.max()), "max_nefc": int(nefc_m.max()),
                                              "B_substep_bytes_at_mean_ncon": Bm["bytes"],
                                              "episode_step_spread": [int(steps_view.min()), int(steps_view.max()),
                                                                      round(float(steps_view.mean()), 1)]},
                        "model": {"nq": env.model.nq, "nv": env.model.nv, "nbody": env.model.nbody,
                                  "ngeom": env.model.ngeom, "nM": env.model.nM, "nlock": env.model.nlock},
-                       "dtype_detail": "f64 dynamics, collision and PGS; f32 sensor windows / observations (as the reference)"},
+                       "dtype_detail": "f64 dynamics, collision and constraint solver; f32 sensor windows / observations (as the reference)"},
             "roofline": roof,
+            "constraint_solver": solver,
             "cpu_baseline": cpu,
             "obs_max_rel_err": parity,
             "c2_single_cylinder_256": c2,
             "c5_device_policy_rollout": c5,
-            "episodes_finished": int(episodes.item()),
+            "episodes_finished": episodes,
             "overflow_envs": overflow, "finite": finite,
-        }
+        })
         print(json.dumps(out), flush=True)
     env.close()
     if world > 1:

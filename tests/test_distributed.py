@@ -87,3 +87,102 @@ def test_two_rank_gather_matches_single_process(gm):
     ref = run_envs(range(world * N_PER_RANK), STEPS)
     np.testing.assert_array_equal(np.array(got, dtype=np.float32), ref)
     assert tmax == 1.5
+
+
+# ---------------------------------------------------------------- bench.py's timed loop
+BENCH_N, BENCH_K, BENCH_W, BENCH_EP = 2, 4, 1, 2
+
+
+class OracleRollout:
+    """A rank's envs stepped by the oracle behind the same drive(k) / returns interface
+    the device path gives bench.measure: each drive is one env-step of every env; an env
+    whose episode ends (done, or BENCH_EP steps) hands its return over and is reset."""
+
+    def __init__(self, env_ids, sleep_s=0.0):
+        import gmx
+        import oracle_lib
+        s = gmx.canonical_settings(noise=True, seed=11)
+        self.model = gmx.ModelBlob()
+        self.cfg = gmx.ConfigBlob(s, self.model)
+        self.objs = gmx.make_object_set("set1_synthetic", 11)
+        self.ids = [int(g) for g in env_ids]
+        self.envs = [oracle_lib.OracleEnv(self.model, self.cfg, self.objs, g) for g in self.ids]
+        self.rng = [np.random.default_rng(2000 + g) for g in self.ids]
+        self.steps = [0] * len(self.ids)
+        self.ret = [np.float32(0)] * len(self.ids)
+        self.returns = torch.full((len(self.ids),), float("nan"))
+        self.ended = 0          # episodes ended inside the timed drives
+        self.sleep_s = sleep_s
+        for i in range(len(self.ids)):
+            self._reset(i)
+
+    def _reset(self, i):
+        import gmx
+        sp = gmx.Spawn()
+        sp.object_index = self.ids[i] % len(self.objs)
+        sp.x, sp.y, sp.zrot = 0.0, 0.0, 0.0
+        self.envs[i].reset(sp)
+        self.steps[i] = 0
+        self.ret[i] = np.float32(0)
+
+    def drive(self, k=None):
+        import time
+        self.returns.fill_(float("nan"))
+        for i, e in enumerate(self.envs):
+            _, r, d = e.step(self.rng[i].uniform(-1, 1, size=self.cfg.n_actions).astype(np.float32))
+            self.ret[i] = np.float32(self.ret[i] + np.float32(r))
+            self.steps[i] += 1
+            if d or self.steps[i] >= BENCH_EP:
+                self.returns[i] = float(self.ret[i])
+                self.ended += k is not None
+                self._reset(i)
+        if self.sleep_s:
+            time.sleep(self.sleep_s)
+
+
+def bench_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        from gmx.shard import shard_range
+        lo, hi = shard_range(rank, world, BENCH_N)
+        ro = OracleRollout(range(lo, hi), sleep_s=0.25 if rank == 1 else 0.0)   # rank 1 is the slow one
+        elapsed, episodes = bench.measure(ro.drive, ro.returns, BENCH_K, BENCH_W, world, torch.device("cpu"),
+                                          lambda: None)
+        line = bench.headline(world, BENCH_N, BENCH_K, BENCH_W, elapsed)
+        q.put((rank, line, episodes, elapsed, ro.ended))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_timed_loop_two_ranks(gm):
+    """bench.py's measure/headline over 2 gloo ranks: the all-gathered episode count covers
+    both ranks, the wall time is the slowest rank's, and rank 0's line carries the contract
+    fields with value = all ranks' env-steps / that time."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=240)
+        res[r[0]] = r[1:]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    line, episodes, elapsed, _ = res[0]
+    ended = res[0][3] + res[1][3]
+    assert episodes == res[1][1] == ended > 0          # every rank counts the whole job's episodes
+    assert elapsed == res[1][2] >= BENCH_K * 0.25     # the max over ranks: rank 1 slept 0.25 s per drive
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data"):
+        assert key in line, key
+    assert line["n_gpus"] == world and line["steps"] == BENCH_K and line["warmup"] == BENCH_W
+    assert line["scaling"] == "weak" and line["higher_is_better"] is True
+    assert line["value"] == round(world * BENCH_N * BENCH_K / elapsed, 1)
+    assert line["ms_per_step"] == round(elapsed / BENCH_K * 1e3, 3)

@@ -277,13 +277,15 @@ def measure(drive, returns, K: int, W: int, world: int, dev, sync):
     return max_over_ranks(elapsed, dev), int(episodes.item())
 
 
-def headline(world: int, n: int, K: int, W: int, elapsed: float) -> dict:
+def headline(world: int, n: int, K: int, W: int, elapsed: float, episodes: int) -> dict:
     """The contract fields of rank 0's JSON line: value = env-steps of ALL ranks / the
     slowest rank's wall time (weak scaling: n envs per rank)."""
     return {"metric": METRIC, "value": round(world * n * K / elapsed, 1), "unit": "env-steps/s", "n_gpus": world,
             "steps": K, "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f64", "data": "synthetic"}
+            "dtype": "f64", "data": "synthetic",
+            "config": {"envs_per_gpu": n, "global_envs": world * n, "parallelism": f"env-shard x{world}"},
+            "episodes_finished": episodes}
 
 
 def main():
@@ -403,15 +405,13 @@ def main():
         c2 = None if (args.no_c2 or world > 1) else c2_line(gmx, torch, dev, stream, K, args.seed, first_env)
         c5 = None if (args.no_policy or world > 1) else policy_rollout(gmx, torch, dev, stream, n, max(3, K // 2), args.seed,
                                                         first_env)
-        out = headline(world, n, K, W, elapsed)
-        out.update({
-            "config": {"workload": "C3: set6_synthetic 20 mixed objects, randomised spawn (object drawn per "
+        out = headline(world, n, K, W, elapsed, episodes)
+        out["config"].update({"workload": "C3: set6_synthetic 20 mixed objects, randomised spawn (object drawn per "
                                    "episode, spawn_into_scene grid search on the device), steady state: envs "
                                    "staggered over episode steps 1..250 by an untimed pre-roll, scripted grasp "
                                    "mix (close / squeeze / palm / lift + jitter), canonical sensor/reward "
                                    "config, device auto-reset at done / 250 steps",
-                       "envs_per_gpu": n, "global_envs": world * n, "substeps_per_env_step": S,
-                       "parallelism": f"env-shard x{world}",
+                       "substeps_per_env_step": S,
                        "B_substep_bytes": B["bytes"], "B_substep_ncon": B["ncon"], "B_substep_nefc": B["nefc"],
                        "measured_contacts": {"mean_ncon": round(float(ncon_m.mean()), 3),
                                              "mean_nefc": round(float(nefc_m.mean()), 3),
@@ -421,14 +421,14 @@ def main():
                                                                      round(float(steps_view.mean()), 1)]},
                        "model": {"nq": env.model.nq, "nv": env.model.nv, "nbody": env.model.nbody,
                                  "ngeom": env.model.ngeom, "nM": env.model.nM, "nlock": env.model.nlock},
-                       "dtype_detail": "f64 dynamics, collision and constraint solver; f32 sensor windows / observations (as the reference)"},
+                       "dtype_detail": "f64 dynamics, collision and constraint solver; f32 sensor windows / observations (as the reference)"})
+        out.update({
             "roofline": roof,
             "constraint_solver": solver,
             "cpu_baseline": cpu,
             "obs_max_rel_err": parity,
             "c2_single_cylinder_256": c2,
             "c5_device_policy_rollout": c5,
-            "episodes_finished": episodes,
             "overflow_envs": overflow, "finite": finite,
         })
         print(json.dumps(out), flush=True)

@@ -197,6 +197,33 @@ class OracleEnv:
         return out
 
 
+def set_default_solver(pgs_sweeps: int):
+    """Constraint solver of every oracle env created from now on: 0 = the engine's Newton
+    solver (the default), k > 0 = the dense PGS cross-check run to k sweeps."""
+    lib().or_set_default_solver(int(pgs_sweeps))
+
+
+class pgs_solver:
+    """with pgs_solver(800): ... -- oracle envs created inside use dense PGS"""
+
+    def __init__(self, sweeps: int):
+        self.sweeps = sweeps
+
+    def __enter__(self):
+        set_default_solver(self.sweeps)
+
+    def __exit__(self, *exc):
+        set_default_solver(0)
+
+
+def solver_stats(env) -> dict:
+    """Newton iteration statistics accumulated by one OracleEnv."""
+    st = np.zeros(6, dtype=np.int64)
+    lib().or_get_stats(env.h, st.ctypes.data_as(C.POINTER(C.c_int64)))
+    return dict(solves=int(st[0]), iterations=int(st[1]), line_search_evals=int(st[2]), max_iterations=int(st[3]),
+                max_contacts=int(st[4]), rows=int(st[5]))
+
+
 def n_threads():
     return max(1, min(16, os.cpu_count() or 1))
 

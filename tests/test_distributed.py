@@ -151,7 +151,7 @@ def bench_worker(rank, world, port, q):
         ro = OracleRollout(range(lo, hi), sleep_s=0.25 if rank == 1 else 0.0)   # rank 1 is the slow one
         elapsed, episodes = bench.measure(ro.drive, ro.returns, BENCH_K, BENCH_W, world, torch.device("cpu"),
                                           lambda: None)
-        line = bench.headline(world, BENCH_N, BENCH_K, BENCH_W, elapsed)
+        line = bench.headline(world, BENCH_N, BENCH_K, BENCH_W, elapsed, episodes)
         q.put((rank, line, episodes, elapsed, ro.ended))
     finally:
         dist.destroy_process_group()
@@ -186,3 +186,5 @@ def test_bench_timed_loop_two_ranks(gm):
     assert line["scaling"] == "weak" and line["higher_is_better"] is True
     assert line["value"] == round(world * BENCH_N * BENCH_K / elapsed, 1)
     assert line["ms_per_step"] == round(elapsed / BENCH_K * 1e3, 3)
+    assert line["config"]["global_envs"] == world * BENCH_N and line["config"]["envs_per_gpu"] == BENCH_N
+    assert line["episodes_finished"] == ended

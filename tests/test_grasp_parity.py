@@ -196,3 +196,20 @@ def test_ten_segment_fingers_256(gm, ol):
     i_oc = gm.BINARY_EVENTS.index("object_contact")
     assert (last["bev_abs"][:, i_oc] > 0).sum() > 32
     env.close()
+
+
+def test_c3_newton_matches_converged_pgs_4096(gm, ol):
+    """The constraint solve is converged: the device's Newton solver and the oracle's dense
+    PGS run to 800 sweeps (MuJoCo's PGS contract, a different algorithm on the same
+    regularised problem, which has one optimum) give the same observations, 1e-4 for every
+    env of the C3 batch on grasp states."""
+    env, snaps = rollout(gm, 4096, "set6_synthetic", 1234, steps=53, snaps=(52,))
+    sn = snaps[0]
+    with ol.pgs_solver(800):
+        obs_p, rew_p, done_p, _ = ol.batch_step(env.model, env.cfg, env.objects, sn["rec"], actions=sn["a"])
+    rel, ab = obs_err(sn["obs"], obs_p)
+    bad = np.where((rel > OBS_RTOL) | (ab > OBS_ATOL))[0]
+    print(f"\nNewton (device) vs PGS-800 (oracle): max rel {rel.max():.3e}, abs {ab.max():.3e}, over {bad.size}")
+    assert bad.size == 0, (bad[:8], rel.max(), ab.max())
+    np.testing.assert_array_equal(sn["done"].astype(np.uint8), done_p)
+    env.close()

@@ -455,11 +455,55 @@ float or_polyfit_eval(const double* X, const double* Y, int P, int order, double
   return y * 1000;
 }
 
+/* The engine's evaluation of the same cubic fit (the device's gauge_reading, operation
+ * for operation): Householder QR on the Vandermonde matrix of the abscissa centred on
+ * and scaled by half the finger length (better conditioned than the raw one; the same
+ * least-squares solution, pinned to numpy.polyfit through or_polyfit_eval in
+ * tests/test_oracle_golden.py). */
 float or_gauge_reading(const gm_model* m, const double* q) {
   int N = m->n_seg, P = N + 1;
-  double X[GM_MAX_SEG + 1], Y[GM_MAX_SEG + 1];
-  or_gauge_points(m, q, X, Y);
-  return or_polyfit_eval(X, Y, P, m->gauge_order, m->gauge_xpos);
+  double X[GM_MAX_SEG + 1], Yv[GM_MAX_SEG + 1];
+  or_gauge_points(m, q, X, Yv);
+  const double half = 0.5 * m->finger_length;
+  const double ihalf = 1.0 / half;
+  double A[GM_MAX_SEG + 1][4], b[GM_MAX_SEG + 1];
+  for (int i = 0; i < P; i++) {
+    const double t = (X[i] - half) * ihalf;
+    A[i][0] = t * t * t; A[i][1] = t * t; A[i][2] = t; A[i][3] = 1.0;
+    b[i] = Yv[i];
+  }
+  for (int k = 0; k < 4; k++) {
+    double nrm = 0;
+    for (int i = k; i < P; i++) nrm += A[i][k] * A[i][k];
+    nrm = sqrt(nrm);
+    const double alpha = A[k][k] > 0 ? -nrm : nrm;
+    double v[GM_MAX_SEG + 1];
+    for (int i = 0; i < P; i++) v[i] = (i >= k) ? A[i][k] : 0.0;
+    v[k] -= alpha;
+    double vv = 0;
+    for (int i = k; i < P; i++) vv += v[i] * v[i];
+    if (vv < 1e-300) continue;
+    const double ivv = 2.0 / vv;
+    for (int j = k; j < 4; j++) {
+      double sacc = 0;
+      for (int i = k; i < P; i++) sacc += v[i] * A[i][j];
+      sacc *= ivv;
+      for (int i = k; i < P; i++) A[i][j] -= sacc * v[i];
+    }
+    double sacc = 0;
+    for (int i = k; i < P; i++) sacc += v[i] * b[i];
+    sacc *= ivv;
+    for (int i = k; i < P; i++) b[i] -= sacc * v[i];
+  }
+  double coeff[4];
+  for (int k = 3; k >= 0; k--) {
+    double sacc = b[k];
+    for (int j = k + 1; j < 4; j++) sacc -= A[k][j] * coeff[j];
+    coeff[k] = sacc / A[k][k];
+  }
+  const double tg = (m->gauge_xpos - half) * ihalf;
+  const double y = ((coeff[0] * tg + coeff[1]) * tg + coeff[2]) * tg + coeff[3];
+  return (float)y * 1000;
 }
 
 /* finger joint points (myfunctions.cpp:2699-2740): cumulative segment angles */

@@ -105,8 +105,10 @@ def test_autoreset_matches_oracle(gm, ol):
             steps[e] += 1
             reset = d or steps[e] >= max_steps
             if reset:
+                # the return is a float sum of per-step rewards, each within the reward bound
+                # of tests/test_grasp_parity.py (the gauge fit's rounding differs at ~1e-7)
                 assert ret[e] == pytest.approx(o.export_state().view(gm.env_state_dtype())[0]["cumulative_reward"],
-                                               rel=0, abs=0), (t, e)
+                                               rel=1e-5, abs=1e-6), (t, e)
                 episode[e] += 1
                 steps[e] = 0
                 oracle_mjenv_reset(gm, o, seed, e, int(episode[e]), len(env.objects), params)

@@ -46,8 +46,9 @@ def test_gripper_sequences_cover_clamps():
 
 
 def test_sliding_window_reads():
-    """SlidingWindow::add / read_element (slidingwindow.h:36-55): the oracle's ring of
-    GM_RING=8 returns the same last-k readings for every k the observation uses (<= 7)."""
+    """SlidingWindow::add / read_element (slidingwindow.h:36-55): the oracle's ring (the
+    device's GM_RING = 64 deep window) returns the same last-k readings as the reference
+    for every k the golden trace holds (<= 7)."""
     w = load("sliding_window.json")
     rows = np.array(w["rows"])
     trace = oracle_lib.ring_trace(w["adds"], 7)
@@ -126,3 +127,16 @@ def test_gauge_points_follow_joint_angles(model):
     X, Y = oracle_lib.gauge_points(model, np.full(N, 0.01))
     assert np.all(np.diff(Y) > 0)
     assert oracle_lib.gauge_reading(model, np.full(N, 0.01)) > 0
+
+
+def test_engine_gauge_fit_equals_the_pinned_fit(model):
+    """The engine's gauge evaluation (centred Vandermonde, shared by device and oracle)
+    gives the reading of the numpy-pinned raw fit (or_polyfit_eval) on bent fingers."""
+    rng = np.random.default_rng(3)
+    N = model.n_seg
+    for _ in range(50):
+        q = rng.uniform(-0.05, 0.05, size=N)
+        X, Y = oracle_lib.gauge_points(model, q)
+        ref = oracle_lib.polyfit_eval(X, Y, 3, 50e-3)        # gm_host_model.cpp gauge_xpos
+        got = oracle_lib.gauge_reading(model, q)
+        assert got == pytest.approx(ref, rel=1e-5, abs=1e-6)

@@ -9,9 +9,10 @@ import oracle_lib as ol
 from test_grasp_parity import rollout, obs_err, SNAPS
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+SNAPS = tuple(int(x) for x in sys.argv[3].split(",")) if len(sys.argv) > 3 else SNAPS
 oset = sys.argv[2] if len(sys.argv) > 2 else "set6_synthetic"
 t0 = time.time()
-env, snaps = rollout(gm, n, oset, 1234)
+env, snaps = rollout(gm, n, oset, 1234, steps=max(SNAPS) + 1, snaps=SNAPS)
 print(f"rollout {time.time()-t0:.1f}s", flush=True)
 for sn in snaps:
     t1 = time.time()
@@ -26,6 +27,18 @@ for sn in snaps:
     print(f"k={sn['k']} oracle {time.time()-t1:.1f}s bad_obs={bad.sum()} rel_max={rel.max():.2e} p99={np.percentile(rel,99):.2e} "
           f"abs_max={ab.max():.2e} done_dev={int(sn['done'].sum())} done_or={int(done_o.sum())} done_mism={int((sn['done'].astype(np.uint8)!=done_o).sum())} "
           f"rew_maxd={np.abs(sn['rew']-rew_o).max():.2e} qpos_max={dq.max():.2e} qpos_p50={np.median(dq):.2e} qpos_bitexact={exact}/{n} obs_bitexact={exact_obs}/{n} mism={mism}", flush=True)
+    if sn is snaps[0] or sn is snaps[-1]:
+        od = (sn["obs"] != obs_o)
+        print("   obs mismatch count per index", od.sum(axis=0).tolist())
+        for f in ("qpos", "qvel", "qacc_warm", "base", "last_read", "lock_q", "time"):
+            a, b = dv[f].reshape(n, -1), ov[f].reshape(n, -1)
+            print(f"   {f}: envs differing {int((a != b).any(axis=1).sum())}, per-column {(a != b).sum(axis=0).tolist()[:48]}")
+        for g in ("end", "next"):
+            for f in ("x", "y", "z", "th"):
+                print(f"   {g}.{f}: envs differing {int((dv[g][f] != ov[g][f]).sum())}")
+        rd, ro = dv["ring"], ov["ring"]
+        print("   ring streams differing (envs):", [int((rd[:, st] != ro[:, st]).any(axis=1).sum()) for st in range(rd.shape[1])])
+        # the same env-step from the device's states but with the input state == oracle's: isolate
     if bad.any():
         e = int(np.argmax(rel))
         print("   worst env", e, "obj", int(dv["obj_index"][e]), "obs dev", np.round(sn["obs"][e], 5).tolist())

@@ -12,5 +12,5 @@ fi
 timeout -k 10 600 python -u $R/bench.py --steps 20 --warmup 3 > $R/gpurun_out/${tag}_bench.json 2> $R/gpurun_out/${tag}_bench.err || { echo "bench failed"; tail -20 $R/gpurun_out/${tag}_bench.err; exit 1; }
 cut -c1-600 $R/gpurun_out/${tag}_bench.json
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${tag}_prof -o run -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu --no-parity --no-c2 --no-policy > $R/gpurun_out/${tag}_prof.log 2>&1 || { echo "rocprof failed"; tail -20 $R/gpurun_out/${tag}_prof.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${tag}_prof -o run -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu --no-parity --no-c2 --no-policy > $R/gpurun_out/${tag}_prof.log 2>&1 || { echo "rocprof failed"; tail -20 $R/gpurun_out/${tag}_prof.log; exit 1; }
 find $R/gpurun_out/${tag}_prof -name "*kernel_stats.csv" | head -3

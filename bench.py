@@ -376,10 +376,10 @@ def main():
     ph = env.step_profiled().astype(np.float64)
     n_solves = float(n * S)
     solver = {"method": "primal Newton (mj_solNewton) with exact line search, warm-started",
-              "iterations_per_solve": round(ph[:, 26].sum() / n_solves, 4),
-              "max_iterations_in_env_step": int(ph[:, 26].max()),
-              "line_search_evals_per_solve": round(ph[:, 27].sum() / n_solves, 4),
-              "rows_per_solve": round(ph[:, 24].sum() / n_solves, 3),
+              "iterations_per_solve": round(ph[:, env.PH_NEWTON].sum() / n_solves, 4),
+              "max_iterations_in_env_step": int(ph[:, env.PH_NEWTON].max()),
+              "line_search_evals_per_solve": round(ph[:, env.PH_LS].sum() / n_solves, 4),
+              "rows_per_solve": round(ph[:, env.PH_NEFC].sum() / n_solves, 3),
               "states": "the batch after the timed window, one profiled env-step"}
 
     if rank == 0:

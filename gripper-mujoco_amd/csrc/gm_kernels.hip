@@ -53,8 +53,8 @@ struct DebugOut {
   int32_t* nefc;      // [n_envs]
   double* wrench;     // [n_envs][6] the live object's cfrc_ext, [force; torque]
 };
-#define GM_NPHASE 28   // 0-23 shader clocks (see gmx.env PHASES), 24: sum of nefc, 25: substeps running MPR,
-                       // 26: Newton iterations, 27: line-search evaluations
+#define GM_NPHASE 32   // 0-27 shader clocks (see gmx.env PHASES), 28: sum of nefc, 29: substeps running MPR,
+                       // 30: Newton iterations, 31: line-search evaluations
 
 // Per-env LDS image, sized for the compile-time finger chain length CL = n_seg + 2:
 // NB = 3 CL + 4 bodies (world, base, 3 x CL finger links, palm, object),
@@ -93,6 +93,7 @@ struct __align__(16) SharedT {
       real chain_f[5][6], chain_I[5][10];   // chain-root sums for the base body
     };
     struct { real V[NB][6]; real QF[GM_MAX_CON][9]; } nw;
+    struct { real V[NB][6]; real V2[NB][6]; } nw2;   // setup: qvel and warm-start velocities
     struct { real root[4][54]; real comp[54]; real oo[27]; } st;
     struct { real lbub[3][CL][14]; real plb[14]; real bbx[28]; real ych[3][CL]; real ypalm; } fs;
     struct { real efc[GM_MAX_EFC]; } dbg;
@@ -318,7 +319,7 @@ __device__ __forceinline__ real readlane_real(real x, int l) {
 }
 
 template <int CL>
-__device__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
+__device__ __forceinline__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                            bool prof = false) {
   unsigned long long t0 = prof ? clock64() : 0;
   // A: local transform of every body (model constants + its joint), lane = body:
@@ -527,7 +528,7 @@ __device__ __forceinline__ void chain_sums(SharedT<CL>& S, int b0, real* fs, rea
 }
 
 template <int CL>
-__device__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
+__device__ __forceinline__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                         bool prof = false) {
   unsigned long long t0 = prof ? clock64() : 0;
   // Lanes = bodies.  Along each finger / palm chain the velocities and bias accelerations
@@ -698,7 +699,7 @@ __device__ __forceinline__ void ctrl_gains(const gm_model* __restrict__ m, const
 // lane per dof: H row entries (compact), bias/passive/actuator force
 // CAL: the calibration variant (per-env timestep, tip load); the env-step kernel is CAL = false
 template <int CL, bool CAL>
-__device__ void mass_and_forces(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+__device__ __forceinline__ void mass_and_forces(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
   if (lane < T->nv) {
     const int d = lane;
     const int b = T->dof_body[d];
@@ -1162,7 +1163,7 @@ __host__ __device__ constexpr int gm_pair_batches(int CL) { return CL <= 10 ? 1 
 #include "gm_newton.hip"
 
 template <int CL>
-__device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
+__device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                           bool prof = false) {
   unsigned long long t0 = prof ? clock64() : 0;
   (void)t0;
@@ -1299,7 +1300,7 @@ __device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const 
     const bool any_mpr = __ballot(ran_mpr) != 0;
     if (lane == 0 && any_mpr) {
       S.work_mpr += 1;
-      if (prof) S.tph[25] += 1;
+      if (prof) S.tph[29] += 1;
     }
   }
   if (lane == 0) {
@@ -1311,7 +1312,7 @@ __device__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const 
 
 // ============================================================ integrate
 template <int CL, bool CAL>
-__device__ void integrate(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
+__device__ __forceinline__ void integrate(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
   const real h = CAL ? S.s.dt : m->timestep;
   if constexpr (CAL) {
     // mj_checkAcc's mjWARN_BADQACC (is_sim_unstable, myfunctions.cpp:4233-4242): a
@@ -1832,8 +1833,8 @@ __device__ __noinline__ void substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS
   // nothing but scalars is carried across the loop body: the loop bounds and flags are
   // wave-uniform (SGPRs), the lane id is recomputed, the next sensor-read time lives in LDS
   SharedT<CL>& S = *(SharedT<CL>*)S_;
-  const gm_model* m_s = (const gm_model*)uniform_const_ptr(m_);
-  const GmTopo* T_s = (const GmTopo*)uniform_const_ptr(T_);
+  const GM_AS_CONST gm_model* m_s = uniform_const_ptr(m_);
+  const GM_AS_CONST GmTopo* T_s = uniform_const_ptr(T_);
   const gm_config* C = (const gm_config*)uniform_const_ptr(C_);
   const int nsub = __builtin_amdgcn_readfirstlane(nsub_in);
   const bool prof = __builtin_amdgcn_readfirstlane((int)prof_in) != 0;
@@ -1848,9 +1849,14 @@ __device__ __noinline__ void substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS
     // pointers is hoisted out of the loop and held live across the whole body
     int lane;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-    const gm_model* m = m_s;
-    const GmTopo* T = T_s;
-    asm volatile("" : "+s"(m), "+s"(T));
+    // (the opaque copy keeps the constant address space: every model / topology access
+    // stays a scalar load when its index is uniform, a global load otherwise -- a generic
+    // pointer would make them flat loads that wait on LDS traffic too)
+    const GM_AS_CONST gm_model* mc = m_s;
+    const GM_AS_CONST GmTopo* Tc = T_s;
+    asm volatile("" : "+s"(mc), "+s"(Tc));
+    const gm_model* m = (const gm_model*)mc;
+    const GmTopo* T = (const GmTopo*)Tc;
     if (CAL && S.s.tip_force != 0.0 && lane < T->nlock && m->lock_kind[lane] == 0) {
       S.s.lock_active[lane] = 1;
       S.s.lock_q[lane] = S.lock_pre[lane];

@@ -257,64 +257,79 @@ __device__ __forceinline__ real impedance(const gm_model* __restrict__ m, real r
   return dmin + y * (dmax - dmin);
 }
 
-// spatial velocity [angular; linear at the world origin] of every body for the dof vector
-// v (LDS): chain prefix scans on the scan lanes plus the base, the object's free joint
-template <int CL>
-__device__ void body_vel(SharedT<CL>& S, const real* v, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
-                         int lane) {
+// spatial velocity [angular; linear at the world origin] of every body for NVEC dof
+// vectors v[0..NVEC) (LDS) into V[0..NVEC): chain prefix scans on the scan lanes plus the
+// base, the object's free joint (two vectors scan interleaved: one pass of latency)
+template <int CL, int NVEC>
+__device__ void body_vel(SharedT<CL>& S, const real* const* v, real (*const* V)[6], const gm_model* __restrict__ m,
+                         const GmTopo* __restrict__ T, int lane) {
   const int db = T->dof_base;
-  const real vb = v[db];
-  real cvb[6];
-#pragma unroll
-  for (int k = 0; k < 6; k++) cvb[k] = S.cdof[db][k] * vb;
   const int grp = T->kl_grp[lane];
   const bool chain = grp >= 0 && grp <= 3;
   const int p = T->kl_cpos[lane];
   const int d = chain ? (grp < 3 ? T->dof_f0[grp] + p - 1 : T->dof_palm) : db;
-  const real vd = chain ? v[d] : 0.0;
-  real s[6];
+  real cvb[NVEC][6], s[NVEC][6];
 #pragma unroll
-  for (int k = 0; k < 6; k++) s[k] = (chain ? S.cdof[d][k] : 0.0) * vd;
+  for (int n = 0; n < NVEC; n++) {
+    const real vb = v[n][db];
+    const real vd = chain ? v[n][d] : 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      cvb[n][k] = S.cdof[db][k] * vb;
+      s[n][k] = (chain ? S.cdof[d][k] : 0.0) * vd;
+    }
+  }
 #pragma unroll
   for (int off = 1; off < CL; off <<= 1)
 #pragma unroll
-    for (int k = 0; k < 6; k++) s[k] += row_shr(s[k], off);
+    for (int n = 0; n < NVEC; n++)
+#pragma unroll
+      for (int k = 0; k < 6; k++) s[n][k] += row_shr(s[n][k], off);
   const int b = T->lane_body[lane];
-  real (*V)[6] = S.nw.V;
   if (chain) {
 #pragma unroll
-    for (int k = 0; k < 6; k++) V[b][k] = s[k] + cvb[k];
+    for (int n = 0; n < NVEC; n++)
+#pragma unroll
+      for (int k = 0; k < 6; k++) V[n][b][k] = s[n][k] + cvb[n][k];
   } else if (lane == T->lane_base) {
 #pragma unroll
-    for (int k = 0; k < 6; k++) V[T->body_base][k] = cvb[k];
+    for (int n = 0; n < NVEC; n++)
+#pragma unroll
+      for (int k = 0; k < 6; k++) V[n][T->body_base][k] = cvb[n][k];
   } else if (b == T->body_obj) {
     const int d0 = T->dof_obj;
-    real acc[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < 6; k++)
+    for (int n = 0; n < NVEC; n++) {
+      real acc[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-      for (int t = 0; t < 6; t++) acc[t] += S.cdof[d0 + k][t] * v[d0 + k];
+      for (int k = 0; k < 6; k++)
 #pragma unroll
-    for (int t = 0; t < 6; t++) V[b][t] = acc[t];
+        for (int t = 0; t < 6; t++) acc[t] += S.cdof[d0 + k][t] * v[n][d0 + k];
+#pragma unroll
+      for (int t = 0; t < 6; t++) V[n][b][t] = acc[t];
+    }
   } else if (lane == 0) {
 #pragma unroll
-    for (int k = 0; k < 6; k++) V[0][k] = 0.0;
+    for (int n = 0; n < NVEC; n++)
+#pragma unroll
+      for (int k = 0; k < 6; k++) V[n][0][k] = 0.0;
   }
   __syncthreads();
 }
 
-// J v of contact c's 4 pyramid edges from the body velocities (n + mu t1, n - mu t1,
+// J v of contact c's 4 pyramid edges from the body velocities V (n + mu t1, n - mu t1,
 // n + mu t2, n - mu t2)
 template <int CL>
-__device__ __forceinline__ void contact_jv(const SharedT<CL>& S, const gm_model* __restrict__ m, int c, real* jv) {
+__device__ __forceinline__ void contact_jv(const SharedT<CL>& S, const real (*V)[6], const gm_model* __restrict__ m,
+                                           int c, real* jv) {
   const real* C = S.con[c];
   const int b1 = m->geom_body[S.cgeom[c][0]], b2 = m->geom_body[S.cgeom[c][1]];
   const real pos[3] = {C[1], C[2], C[3]};
   real t1v[3], t2v[3];
-  cross3(t1v, S.nw.V[b1], pos);
-  cross3(t2v, S.nw.V[b2], pos);
-  const real v1[3] = {S.nw.V[b1][3] + t1v[0], S.nw.V[b1][4] + t1v[1], S.nw.V[b1][5] + t1v[2]};
-  const real v2[3] = {S.nw.V[b2][3] + t2v[0], S.nw.V[b2][4] + t2v[1], S.nw.V[b2][5] + t2v[2]};
+  cross3(t1v, V[b1], pos);
+  cross3(t2v, V[b2], pos);
+  const real v1[3] = {V[b1][3] + t1v[0], V[b1][4] + t1v[1], V[b1][5] + t1v[2]};
+  const real v2[3] = {V[b2][3] + t2v[0], V[b2][4] + t2v[1], V[b2][5] + t2v[2]};
   const real dv[3] = {v2[0] - v1[0], v2[1] - v1[1], v2[2] - v1[2]};
   const real n[3] = {C[4], C[5], C[6]}, t1[3] = {C[7], C[8], C[9]};
   real t2[3];
@@ -421,7 +436,7 @@ struct RowsT {
 // tran + mu^2 tran, tran = the two bodies' invweight0), reference accelerations
 template <int CL, bool CAL>
 __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
-                                 int lane, RowsT& R) {
+                                 int lane, RowsT& R, real* jq, real& jql) {
   const real h = CAL ? S.s.dt : m->timestep;
   real tc = m->solref[0];
   if (tc < 2 * h) tc = 2 * h;
@@ -446,7 +461,16 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
     R.ldof = d;
   }
   if (lane == 0) { S.nl = nl; S.nefc = nl + 4 * S.ncon; }
-  body_vel<CL>(S, S.s.qvel, m, T, lane);
+  // body velocities at qvel (reference accelerations) and at the warm start (the first
+  // iterate's J q - aref), one fused pass
+  {
+    const real* vv[2] = {S.s.qvel, S.s.qacc_warm};
+    real (*VV[2])[6] = {S.nw2.V, S.nw2.V2};
+    body_vel<CL, 2>(S, vv, VV, m, T, lane);
+  }
+  jql = (lane < nl) ? S.s.qacc_warm[R.ldof] - R.laref : 0.0;
+#pragma unroll
+  for (int e = 0; e < 4; e++) jq[e] = 0.0;
   R.cD = 0;
 #pragma unroll
   for (int e = 0; e < 4; e++) R.caref[e] = 0;
@@ -462,10 +486,14 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
     real Rr = div_n(1 - imp, imp) * diag;
     if (Rr < 1e-15) Rr = 1e-15;
     R.cD = rcp_n(Rr);
-    real vel[4];
-    contact_jv<CL>(S, m, lane, vel);
+    real vel[4], jv[4];
+    contact_jv<CL>(S, S.nw2.V, m, lane, vel);
+    contact_jv<CL>(S, S.nw2.V2, m, lane, jv);
 #pragma unroll
-    for (int e = 0; e < 4; e++) R.caref[e] = -Bd * vel[e] - K * imp * C[0];
+    for (int e = 0; e < 4; e++) {
+      R.caref[e] = -Bd * vel[e] - K * imp * C[0];
+      jq[e] = jv[e] - R.caref[e];
+    }
   }
   __syncthreads();
 }
@@ -474,11 +502,15 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
 template <int CL>
 __device__ __forceinline__ void rows_jar(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
                                          const real* v, int lane, const RowsT& R, real* jr, real& jl) {
-  body_vel<CL>(S, v, m, T, lane);
+  {
+    const real* vv[1] = {v};
+    real (*VV[1])[6] = {S.nw.V};
+    body_vel<CL, 1>(S, vv, VV, m, T, lane);
+  }
   jl = (lane < S.nl) ? v[R.ldof] - R.laref : 0.0;
   if (lane < S.ncon) {
     real jv[4];
-    contact_jv<CL>(S, m, lane, jv);
+    contact_jv<CL>(S, S.nw.V, m, lane, jv);
 #pragma unroll
     for (int e = 0; e < 4; e++) jr[e] = jv[e] - R.caref[e];
   } else {
@@ -504,7 +536,8 @@ __device__ __forceinline__ real row_sum(int lane, int ncon, int nl, const real* 
 #define GM_LANE_PALM_F 56
 template <int CL>
 __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
-                             const RowsT& R, const bool* act) {
+                             const RowsT& R, const bool* act, bool prof) {
+  unsigned long long t0 = prof ? clock64() : 0;
   const int ncon = S.ncon, nl = S.nl;
   // ---- contact lanes: Q = sum_e D u u^T and F = sum_e D aref u over the active edges
   if (lane < ncon) {
@@ -570,6 +603,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     }
   }
   const bool any_g = __ballot(have_g) != 0ull;
+  PH(3);
   // the object's ground contacts (its other contacts reach it through the base composite)
   if (lane == T->lane_obj) {
     real Kgo[21], Fgo[6];
@@ -644,6 +678,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     S.st.oo[lane] = (lane < 21) ? S.st.comp[lane] + S.go[lane] : S.go[lane] - S.st.comp[42 + lane - 21];
   }
   __syncthreads();
+  PH(4);
   // ---- H and rhs on the factor lanes
   real h[CL + 1], hb[7], rhs = 0;
 #pragma unroll
@@ -654,16 +689,21 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
   const real* cdb = S.cdof[T->dof_base];
   if (rowf < 3 && p >= 1 && p <= CL) {
     const int d = T->dof_f0[rowf] + p - 1;
-    real Kt[21], Ft[6];
-#pragma unroll
-    for (int k = 0; k < 21; k++) Kt[k] = any_g ? Ko[k] + Kg[k] : Ko[k];
-#pragma unroll
-    for (int k = 0; k < 6; k++) Ft[k] = any_g ? Fo[k] + Fg[k] : Fo[k];
-    real cd[6], y[6], yo[6];
+    real cd[6], y[6], yo[6], Ft[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
-    symK_mul(Kt, cd, y);
     symK_mul(Ko, cd, yo);
+    if (any_g) {   // wave-uniform: ground contacts on gripper bodies (rare)
+      real Kt[21];
+#pragma unroll
+      for (int k = 0; k < 21; k++) Kt[k] = Ko[k] + Kg[k];
+#pragma unroll
+      for (int k = 0; k < 6; k++) Ft[k] = Fo[k] + Fg[k];
+      symK_mul(Kt, cd, y);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 6; k++) { Ft[k] = Fo[k]; y[k] = yo[k]; }
+    }
     const real* H = S.Hf[rowf];
 #pragma unroll
     for (int j = 1; j <= CL; j++)
@@ -675,16 +715,24 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
   } else if (lane == GM_LANE_PALM_F) {
     const int d = T->dof_palm;
     const real* st = S.st.root[3];
-    real Kt[21], Ft[6], K0[21];
+    real Ft[6], K0[21];
 #pragma unroll
-    for (int k = 0; k < 21; k++) { K0[k] = st[k]; Kt[k] = any_g ? st[k] + st[21 + k] : st[k]; }
-#pragma unroll
-    for (int k = 0; k < 6; k++) Ft[k] = any_g ? st[42 + k] + st[48 + k] : st[42 + k];
+    for (int k = 0; k < 21; k++) K0[k] = st[k];
     real cd[6], y[6], yo[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
-    symK_mul(Kt, cd, y);
     symK_mul(K0, cd, yo);
+    if (any_g) {
+      real Kt[21];
+#pragma unroll
+      for (int k = 0; k < 21; k++) Kt[k] = st[k] + st[21 + k];
+#pragma unroll
+      for (int k = 0; k < 6; k++) Ft[k] = st[42 + k] + st[48 + k];
+      symK_mul(Kt, cd, y);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 6; k++) { Ft[k] = st[42 + k]; y[k] = yo[k]; }
+    }
     h[1] = S.Hp[TRI(1, 1)] + dot6(cd, y);
     hb[0] = S.Hp[TRI(1, 0)] + dot6(cdb, y);
 #pragma unroll
@@ -698,12 +746,18 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     for (int k = 0; k < 21; k++) KBo[k] = cp[k];
     symK_mul(KBo, cdb, yob);
     if (i == 0) {
-      real KBt[21], FBt[6], y[6];
+      real FBt[6], y[6];
+      if (any_g) {
+        real KBt[21];
 #pragma unroll
-      for (int k = 0; k < 21; k++) KBt[k] = any_g ? cp[k] + cp[21 + k] : cp[k];
+        for (int k = 0; k < 21; k++) KBt[k] = cp[k] + cp[21 + k];
 #pragma unroll
-      for (int k = 0; k < 6; k++) FBt[k] = any_g ? cp[42 + k] + cp[48 + k] : cp[42 + k];
-      symK_mul(KBt, cdb, y);
+        for (int k = 0; k < 6; k++) FBt[k] = cp[42 + k] + cp[48 + k];
+        symK_mul(KBt, cdb, y);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 6; k++) { FBt[k] = cp[42 + k]; y[k] = yob[k]; }
+      }
       hb[0] = S.Hbb + dot6(cdb, y);
       rhs = S.frc[T->dof_base] + dot6(cdb, FBt);
     } else {
@@ -737,6 +791,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     }
   }
   __syncthreads();   // the stage is read; the factor's transfers reuse the union
+  PH(7);
   // ---- factor: finger chains (rows 0..2), pivots CL .. 1
   real invd = 1.0;
   if (lane < 48) {
@@ -828,6 +883,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
       invd = piv ? ihk : invd;
     }
   }
+  PH(14);
   // ---- solve: forward (chains leaf first, border sums, border), D, backward
   real y = rhs;
   if (lane < 48) {
@@ -888,31 +944,33 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     S.xs[bi == 0 ? T->dof_base : T->dof_obj + bi - 1] = y;
   }
   __syncthreads();
+  PH(24);
 }
 
 // mj_solNewton restated (oracle newton_solve): warm start, Newton point on the active
 // pattern, accept when the pattern at x is unchanged (x is then the exact optimum), else
 // an exact line search along x - q; contact forces and the warm start at the end.
 template <int CL, bool CAL>
-__device__ void newton_solve(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
+__device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                              bool prof) {
   unsigned long long t0 = prof ? clock64() : 0;
   RowsT R;
-  constraint_setup<CL, CAL>(S, m, T, lane, R);
+  real jq[4], jql;
+  constraint_setup<CL, CAL>(S, m, T, lane, R, jq, jql);
+  PH(11);
   const int ncon = S.ncon, nl = S.nl, nv = T->nv;
   const bool clane = lane < ncon;
   if (lane < nv) S.qacc[lane] = S.s.qacc_warm[lane];
   __syncthreads();
-  smooth_matvec<CL>(S, T, S.qacc, S.Ma, lane);
-  real jq[4], jql;
-  rows_jar<CL>(S, m, T, S.qacc, lane, R, jq, jql);
-  PH(11);
+  PH(12);
   int it = 0, nls = 0;
   for (it = 0; it < GM_NEWTON_MAXIT; it++) {
     bool act[4];
 #pragma unroll
     for (int e = 0; e < 4; e++) act[e] = clane && jq[e] < 0;
-    newton_point<CL>(S, m, T, lane, R, act);
+    PH(13);
+    newton_point<CL>(S, m, T, lane, R, act, prof);
+    if (prof) t0 = clock64();
     real jx[4], jxl;
     rows_jar<CL>(S, m, T, S.xs, lane, R, jx, jxl);
     bool differ = false;
@@ -926,7 +984,9 @@ __device__ void newton_solve(SharedT<CL>& S, const gm_model* __restrict__ m, con
       it++;
       break;
     }
-    // exact line search along d = x - q (d overwrites x)
+    // exact line search along d = x - q (d overwrites x); H~ q formed when first needed
+    // (only iteration 0 reaches here with q unchanged: the oracle does the same)
+    if (it == 0) smooth_matvec<CL>(S, T, S.qacc, S.Ma, lane);
     if (lane < nv) S.xs[lane] = S.xs[lane] - S.qacc[lane];
     __syncthreads();
     smooth_matvec<CL>(S, T, S.xs, S.Mv, lane);
@@ -996,7 +1056,7 @@ __device__ void newton_solve(SharedT<CL>& S, const gm_model* __restrict__ m, con
   if (lane == 0) {
     S.work_nefc += nl + 4 * ncon;
     S.work_newton += it;
-    if (prof) { S.tph[24] += nl + 4 * ncon; S.tph[26] += it; S.tph[27] += nls; }
+    if (prof) { S.tph[28] += nl + 4 * ncon; S.tph[30] += it; S.tph[31] += nls; }
   }
   __syncthreads();
 }

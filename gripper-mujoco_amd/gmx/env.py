@@ -318,13 +318,14 @@ class BatchedGripperEnv:
             return ncon, con, f, qacc, nefc, w
         return ncon, con, f, qacc
 
-    PHASES = ("kinematics", "crb_rne", "mass_forces", "-", "-", "collision",
-              "newton_solve", "-", "integrate", "update_all", "monitor_sensors",
-              "  n:setup+warm", "-", "  n:iterations", "-", "  k:A_hinge", "  k:B_chains",
-              "  crb:chains", "e:sense", "e:update_env", "e:get_obs", "e:done_reward", "substep_body", "env_step")
-    # columns past the clocks: 24 sum of constraint rows, 25 substeps that ran MPR,
-    # 26 Newton iterations, 27 line-search evaluations
-    N_PHASE = 28
+    PHASES = ("kinematics", "crb_rne", "mass_forces", "  n:QF+bodies", "  n:scans+composites", "collision",
+              "newton_solve", "  n:H_assembly", "integrate", "update_all", "monitor_sensors",
+              "  n:setup", "  n:warm_start", "  n:jar+line_search", "  n:factor", "  k:A_hinge", "  k:B_chains",
+              "  crb:chains", "e:sense", "e:update_env", "e:get_obs", "e:done_reward", "substep_body", "env_step",
+              "  n:solve", "-", "-", "-")
+    # counter columns past the clocks
+    PH_NEFC, PH_MPR, PH_NEWTON, PH_LS = 28, 29, 30, 31
+    N_PHASE = 32
 
     def step_profiled(self):
         """One env-step with per-phase shader-clock counters (lane 0, summed over substeps)."""

@@ -1625,7 +1625,6 @@ static void newton_solve(or_env* e) {
   double jq[NE], jx[NE], dj[NE], tg[NE], th[NE];
   int act[NE], actx[NE];
   for (int i = 0; i < nv; i++) q[i] = e->qacc_warm[i];
-  smooth_matvec(e, q, Ma);
   rows_jar(e, q, jq);
   int it = 0;
   e->stat_ls = 0;
@@ -1643,7 +1642,10 @@ static void newton_solve(or_env* e) {
       it++;
       break;
     }
-    /* exact line search along d = x - q */
+    /* exact line search along d = x - q.  H~ q is formed here, when first needed: the
+     * search is only reached at iteration 0 with q still the warm start, later
+     * iterations update it incrementally (the device does the same) */
+    if (it == 0) smooth_matvec(e, q, Ma);
     for (int i = 0; i < nv; i++) d[i] = xv[i] - q[i];
     smooth_matvec(e, d, Mv);
     for (int i = 0; i < nv; i++) tmp[i] = d[i] * (Ma[i] - e->frc[i]);

@@ -17,17 +17,20 @@ for t in range(3):
     tot += ph.mean(axis=0)
 tot /= 3
 S = env.cfg.sim_steps_per_action if hasattr(env.cfg, 'sim_steps_per_action') else 63
-allc = tot[:11].sum()
+TOP = [0, 1, 2, 5, 6, 8, 9, 10]
+allc = tot[TOP].sum()
 print(f"n={n} mean cycles per env-step (lane 0) total {allc:.3e}  per substep {allc/63:.3e}")
-for k, name in enumerate(env.PHASES[:22]):
+for k, name in enumerate(env.PHASES):
+    if k in (22, 23):
+        continue
     if name == "-":
         continue
     if name.startswith("e:"):
         print(f"  {name:18s} {tot[k]:10.0f} cyc/env-step  (= {tot[k]/63:.0f} per substep)")
     else:
         print(f"  {name:18s} {tot[k]/63:10.0f} cyc/substep  {100*tot[k]/allc:5.1f}%")
-print(f"  outlined-call overhead {(tot[22] - tot[:9].sum())/63:10.0f} cyc/substep (prologue/epilogue, CSR save/restore)")
-print(f"  whole env-step on one wave {tot[23]:.3e} cyc (phases account for {100*(tot[:11].sum()+tot[18:22].sum())/max(tot[23],1):.1f}%)")
-print(f"  rows per substep {tot[24]/63:.1f}; Newton iterations per solve {tot[26]/63:.3f}; line-search evals per solve {tot[27]/63:.3f}")
+print(f"  outlined-call overhead {(tot[22] - tot[[0, 1, 2, 5, 6, 8]].sum())/63:10.0f} cyc/substep (prologue/epilogue, CSR save/restore)")
+print(f"  whole env-step on one wave {tot[23]:.3e} cyc (phases account for {100*(allc+tot[18:22].sum())/max(tot[23],1):.1f}%)")
+print(f"  rows per substep {tot[env.PH_NEFC]/63:.1f}; Newton iterations per solve {tot[env.PH_NEWTON]/63:.3f}; line-search evals per solve {tot[env.PH_LS]/63:.3f}")
 ncon, _, _, _ = env.debug_substep()
 print("ncon per env: mean %.2f  max %d  histogram %s" % (ncon.mean(), ncon.max(), np.bincount(ncon, minlength=16).tolist()))

@@ -51,7 +51,7 @@ dump = []
 for t in range(8):
     ph = drive(profiled=True).astype(np.float64)
     dump.append(ph.copy())   # all phase slots
-    c, nefc, mpr = ph[:, 23], ph[:, 24], ph[:, 25]
+    c, nefc, mpr = ph[:, 23], ph[:, env.PH_NEFC], ph[:, env.PH_MPR]
     line = (f"step {t}: env cycles mean {c.mean():.3e} p90 {np.percentile(c, 90):.3e} "
             f"max {c.max():.3e}  ideal {c.sum() / slots:.3e}  in-order {makespan(c, range(n)):.3e}  "
             f"sorted-oracle {makespan(c, np.argsort(-c)):.3e}")

@@ -16,23 +16,25 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          "-mllvm", "-disable-machine-licm"]
 
 
-def build(verbose: bool = False, force: bool = False) -> str:
+def build(verbose: bool = False, force: bool = False, out: str | None = None, extra_flags=()) -> str:
     """Compile each translation unit in parallel (the env-step kernel and the calibration
-    variant are separate device modules), then link libgm.so."""
+    variant are separate device modules), then link libgm.so (or `out`: developer A/B
+    builds, with `extra_flags` added to every compile)."""
+    lib_path = out or LIB_PATH
     srcs = [os.path.join(PKG_DIR, s) for s in SOURCES]
     deps = srcs + [os.path.join(PKG_DIR, "csrc", f) for f in ("gm_kernels.hip", "gm_newton.hip", "gm_math.h", "gm_policy.hip", "gm_state.h")] + \
         [os.path.join(REPO_DIR, "include", f) for f in ("gripper_mi355x.h", "gm_settings.def")]
-    if not force and os.path.exists(LIB_PATH):
+    if not force and out is None and os.path.exists(LIB_PATH):
         t = os.path.getmtime(LIB_PATH)
         if all(os.path.getmtime(d) <= t for d in deps):
             return LIB_PATH
-    objdir = os.path.join(os.path.dirname(LIB_PATH), "obj")
+    objdir = os.path.join(os.path.dirname(LIB_PATH), "obj" if out is None else "obj_" + os.path.basename(out))
     os.makedirs(objdir, exist_ok=True)
     inc = ["-I" + os.path.join(REPO_DIR, "include"), "-I" + os.path.join(PKG_DIR, "csrc")]
     procs, objs = [], []
     for src in srcs:
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
-        cmd = [HIPCC, *FLAGS, *inc, "-c", src, "-o", obj]
+        cmd = [HIPCC, *FLAGS, *extra_flags, *inc, "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append((subprocess.Popen(cmd), cmd))
@@ -40,9 +42,9 @@ def build(verbose: bool = False, force: bool = False) -> str:
     for p, cmd in procs:
         if p.wait() != 0:
             raise subprocess.CalledProcessError(p.returncode, cmd)
-    link = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", LIB_PATH + ".tmp"]
+    link = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", lib_path + ".tmp"]
     if verbose:
         print(" ".join(link))
     subprocess.run(link, check=True)
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    os.replace(lib_path + ".tmp", lib_path)
+    return lib_path

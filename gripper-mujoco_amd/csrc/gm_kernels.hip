@@ -78,7 +78,8 @@ struct __align__(16) SharedT {
   // contact record: dist, pos[3], normal[3], t1[3] (t2 = normal x t1), mu, force[3]
   // (contact frame, after the solve)
   real con[GM_MAX_CON][14];
-  int32_t cgeom[GM_MAX_CON][2];   // canonical (geom1, geom2)
+  int16_t cgeom[GM_MAX_CON][2];   // canonical (geom1, geom2)
+  int16_t cbody[GM_MAX_CON][2];   // their bodies
   int16_t pair_off[GM_MAX_PAIR], pair_cnt[GM_MAX_PAIR];   // contact slots of each candidate pair
   // LDS shared in time: the dynamics scratch is dead once H~ and the forces are formed; the
   // Newton stages then reuse it (body velocities + per-contact Q / F; the chain-root stage;
@@ -1145,7 +1146,7 @@ __device__ __forceinline__ void canon_pair(int a, int b, int ta, int tb, int& g1
 }
 
 template <int CL>
-__device__ void write_contact(SharedT<CL>& S, int slot, int g1, int g2, const Hit& h, real mu) {
+__device__ void write_contact(SharedT<CL>& S, int slot, int g1, int g2, int b1, int b2, const Hit& h, real mu) {
   real* C = S.con[slot];
   C[0] = h.dist;
   C[1] = h.pos[0]; C[2] = h.pos[1]; C[3] = h.pos[2];
@@ -1155,7 +1156,8 @@ __device__ void write_contact(SharedT<CL>& S, int slot, int g1, int g2, const Hi
   C[7] = F[3]; C[8] = F[4]; C[9] = F[5];
   C[10] = mu;
   C[11] = 0; C[12] = 0; C[13] = 0;
-  S.cgeom[slot][0] = g1; S.cgeom[slot][1] = g2;
+  S.cgeom[slot][0] = (int16_t)g1; S.cgeom[slot][1] = (int16_t)g2;
+  S.cbody[slot][0] = (int16_t)b1; S.cbody[slot][1] = (int16_t)b2;
 }
 
 __host__ __device__ constexpr int gm_pair_batches(int CL) { return CL <= 10 ? 1 : 2; }
@@ -1176,7 +1178,7 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
 #pragma unroll
   for (int bi = 0; bi < NBATCH; bi++) {
     const int pr = bi * NT + lane;
-    int cnt = 0, kind = 0, g1 = 0, g2 = 0;
+    int cnt = 0, kind = 0, g1 = 0, g2 = 0, b1 = 0, b2 = 0;
     unsigned hm = 0;   // multi-point colliders: the counted candidates (pass 2 revisits only these)
     Hit single;
     GeomV A, B;
@@ -1189,6 +1191,7 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
       const int ta = ta0 < 0 ? S.s.obj_type : ta0, tb = tb0 < 0 ? S.s.obj_type : tb0;
       canon_pair(a, b, ta, tb, g1, g2);
       const int s1 = (g1 == a) ? 0 : 1;
+      b1 = T->pr_body[pr][s1]; b2 = T->pr_body[pr][1 - s1];   // kept with the contact (LDS)
       load_pair_geom(S, T, pr, s1, A);
       load_pair_geom(S, T, pr, 1 - s1, B);
 #ifdef GM_PHASE_SPLIT_COLL
@@ -1267,7 +1270,7 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
     if (cnt > 0) {
       real mu = fmax(A.friction, B.friction);
       if (kind == 1) {
-        if (off < GM_MAX_CON) write_contact(S, off, g1, g2, single, mu);
+        if (off < GM_MAX_CON) write_contact(S, off, g1, g2, b1, b2, single, mu);
       } else if (kind == 4) {
         int w = 0;
 #pragma unroll
@@ -1277,7 +1280,7 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
             Hit t;
             bb_face_cand(bbs, i, P, dep);
             bb_face_hit(bbs, P, dep, t);
-            if (off + w < GM_MAX_CON) write_contact(S, off + w, g1, g2, t, mu);
+            if (off + w < GM_MAX_CON) write_contact(S, off + w, g1, g2, b1, b2, t, mu);
             w++;
           }
         }
@@ -1289,7 +1292,7 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
           hm &= hm - 1;
           if (kind == 2) plane_box_point(A, B, i, t);
           else plane_cyl_point(A, B, cf, i, t);
-          if (off + w < GM_MAX_CON) write_contact(S, off + w, g1, g2, t, mu);
+          if (off + w < GM_MAX_CON) write_contact(S, off + w, g1, g2, b1, b2, t, mu);
           w++;
         }
       }

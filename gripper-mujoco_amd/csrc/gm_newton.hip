@@ -323,7 +323,7 @@ template <int CL>
 __device__ __forceinline__ void contact_jv(const SharedT<CL>& S, const real (*V)[6], const gm_model* __restrict__ m,
                                            int c, real* jv) {
   const real* C = S.con[c];
-  const int b1 = m->geom_body[S.cgeom[c][0]], b2 = m->geom_body[S.cgeom[c][1]];
+  const int b1 = S.cbody[c][0], b2 = S.cbody[c][1];
   const real pos[3] = {C[1], C[2], C[3]};
   real t1v[3], t2v[3];
   cross3(t1v, V[b1], pos);
@@ -476,7 +476,7 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
   for (int e = 0; e < 4; e++) R.caref[e] = 0;
   if (lane < S.ncon) {
     const real* C = S.con[lane];
-    const int b1 = m->geom_body[S.cgeom[lane][0]], b2 = m->geom_body[S.cgeom[lane][1]];
+    const int b1 = S.cbody[lane][0], b2 = S.cbody[lane][1];
     const real iw1 = (b1 == T->body_obj) ? S.s.obj_invw[0] : m->body_invweight0[b1][0];
     const real iw2 = (b2 == T->body_obj) ? S.s.obj_invw[0] : m->body_invweight0[b2][0];
     const real tran = iw1 + iw2;
@@ -582,7 +582,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
       for (int c = c0; c < c1; c++) {
         const real* qf = S.nw.QF[c];
         const real pos[3] = {S.con[c][1], S.con[c][2], S.con[c][3]};
-        const real sg = (m->geom_body[S.cgeom[c][1]] == b) ? 1.0 : -1.0;
+        const real sg = (S.cbody[c][1] == b) ? 1.0 : -1.0;
         real Kc[21], Fs[6];
         spatial_K(qf, pos, Kc);
         cross3(Fs, pos, qf + 6);
@@ -619,7 +619,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
       for (int c = c0; c < c1; c++) {
         const real* qf = S.nw.QF[c];
         const real pos[3] = {S.con[c][1], S.con[c][2], S.con[c][3]};
-        const real sg = (m->geom_body[S.cgeom[c][1]] == T->body_obj) ? 1.0 : -1.0;
+        const real sg = (S.cbody[c][1] == T->body_obj) ? 1.0 : -1.0;
         real Kc[21], Fs[6];
         spatial_K(qf, pos, Kc);
         cross3(Fs, pos, qf + 6);

@@ -113,36 +113,6 @@ struct __align__(16) SharedT {
 #define PH(k) do { if (prof) { unsigned long long t_ = clock64(); if (lane == 0) S.tph[k] += t_ - t0; t0 = t_; } } while (0)
 
 // ------------------------------------------------------------ small math
-template <typename T> __device__ __forceinline__ T dot3(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-template <typename T> __device__ __forceinline__ void cross3(T* r, const T* a, const T* b) {
-  T t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
-  r[0] = t0; r[1] = t1; r[2] = t2;
-}
-template <typename T> __device__ __forceinline__ void mulmv3(T* r, const T* M, const T* v) {
-  T t0 = M[0] * v[0] + M[1] * v[1] + M[2] * v[2];
-  T t1 = M[3] * v[0] + M[4] * v[1] + M[5] * v[2];
-  T t2 = M[6] * v[0] + M[7] * v[1] + M[8] * v[2];
-  r[0] = t0; r[1] = t1; r[2] = t2;
-}
-template <typename T> __device__ __forceinline__ void mulmtv3(T* r, const T* M, const T* v) {
-  T t0 = M[0] * v[0] + M[3] * v[1] + M[6] * v[2];
-  T t1 = M[1] * v[0] + M[4] * v[1] + M[7] * v[2];
-  T t2 = M[2] * v[0] + M[5] * v[1] + M[8] * v[2];
-  r[0] = t0; r[1] = t1; r[2] = t2;
-}
-template <typename T> __device__ __forceinline__ void quat2mat(T* R, const T* q) {
-  T w = q[0], x = q[1], y = q[2], z = q[3];
-  R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z);     R[2] = 2 * (x * z + w * y);
-  R[3] = 2 * (x * y + w * z);     R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
-  R[6] = 2 * (x * z - w * y);     R[7] = 2 * (y * z + w * x);     R[8] = 1 - 2 * (x * x + y * y);
-}
-template <typename T> __device__ __forceinline__ void quatmul(T* r, const T* a, const T* b) {
-  T t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
-  T t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
-  T t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
-  T t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
-  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
-}
 // Correctly rounded fp64 sqrt, reciprocal and quotient on the compiler's own expansions
 // (v_rsq_f64 / v_rcp_f64 and the same FMA refinement steps, operation for operation) minus
 // their range pre-/post-scaling and special-value fix-ups, which cost a third of the
@@ -187,44 +157,17 @@ __device__ __forceinline__ double rcp_n(double b) { return 1.0 / b; }
 __device__ __forceinline__ double div_n(double a, double b) { return a / b; }
 #endif
 
-__device__ __forceinline__ void quatnorm(real* q) {
-  real n = sqrt_n(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-  if (n < 1e-15) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
-  const real in = rcp_n(n);
-  for (int i = 0; i < 4; i++) q[i] *= in;
-}
 __device__ __forceinline__ void ld3(float* r, const double* a) { r[0] = (float)a[0]; r[1] = (float)a[1]; r[2] = (float)a[2]; }
 __device__ __forceinline__ void ld3(double* r, const double* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
 __device__ __forceinline__ void ld4(double* r, const double* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3]; }
 __device__ __forceinline__ void ld4(float* r, const double* a) { r[0] = (float)a[0]; r[1] = (float)a[1]; r[2] = (float)a[2]; r[3] = (float)a[3]; }
 
-// spatial inertia (I_O sym6, h = m c, m) times motion [w; v]
-__device__ __forceinline__ void inert_mul(real* r, const real* ci, const real* v) {
-  const real* w = v; const real* u = v + 3;
-  real Iw0 = ci[0] * w[0] + ci[3] * w[1] + ci[4] * w[2];
-  real Iw1 = ci[3] * w[0] + ci[1] * w[1] + ci[5] * w[2];
-  real Iw2 = ci[4] * w[0] + ci[5] * w[1] + ci[2] * w[2];
-  real hxu[3], hxw[3];
-  cross3(hxu, ci + 6, u);
-  cross3(hxw, ci + 6, w);
-  r[0] = Iw0 + hxu[0]; r[1] = Iw1 + hxu[1]; r[2] = Iw2 + hxu[2];
-  r[3] = ci[9] * u[0] - hxw[0]; r[4] = ci[9] * u[1] - hxw[1]; r[5] = ci[9] * u[2] - hxw[2];
-}
-__device__ __forceinline__ void cross_motion(real* r, const real* v, const real* mv) {
-  real a[3], b[3], c[3];
-  cross3(a, v, mv); cross3(b, v, mv + 3); cross3(c, v + 3, mv);
-  r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
-  r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
-}
-__device__ __forceinline__ void cross_force(real* r, const real* v, const real* f) {
-  real a[3], b[3], c[3];
-  cross3(a, v, f); cross3(b, v + 3, f + 3); cross3(c, v, f + 3);
-  r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
-  r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
-}
-__device__ __forceinline__ real dot6(const real* a, const real* b) {
-  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
-}
+#include "gm_fphelpers.inc"
+template <int CL>
+__device__ __forceinline__ void body_R(const SharedT<CL>& S, int b, real* R) {
+  const real q[4] = {S.xquat[b][0], S.xquat[b][1], S.xquat[b][2], S.xquat[b][3]};
+  quat2mat(R, q);
+}   // (one definition: ADL on SharedT would make a second one ambiguous)
 
 // ------------------------------------------------------------ topology helpers
 // chain c: 0..2 finger, 3 palm, 4 object.  Chain lengths (positions >= 1).
@@ -242,11 +185,6 @@ __device__ __forceinline__ int chain_dof(const GmTopo* T, int c, int p) {
 // H/L storage accessor: chain c, positions p >= q (object: 0..5, others: 0 = base)
 
 // ============================================================ kinematics
-template <int CL>
-__device__ __forceinline__ void body_R(const SharedT<CL>& S, int b, real* R) {
-  const real q[4] = {S.xquat[b][0], S.xquat[b][1], S.xquat[b][2], S.xquat[b][3]};
-  quat2mat(R, q);
-}
 // mj_kinematics restated (oracle.c fk): phase A, one lane per body, the hinge joint
 // rotations (the only transcendental work) ; phase B, one lane per chain, the pose
 // recursion root -> leaf entirely in registers (chain length compile-time, unrolled,
@@ -318,6 +256,25 @@ __device__ __forceinline__ real readlane_real(real x, int l) {
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+
+__host__ __device__ constexpr int gm_pair_batches(int CL) { return CL <= 10 ? 1 : 2; }
+
+// The physics substep (kinematics .. integrate, the collider and the constraint solver)
+// is compiled with FMA contraction: its dot products and small matrix products issue as
+// fused multiply-adds (fewer fp64 instructions and shorter dependent chains, -11 % kernel
+// time).  The oracle evaluates the same expressions unfused, so device and oracle physics
+// agree to ~1e-12 per substep instead of bit for bit (tests/test_grasp_parity.py bounds);
+// everything after the namespace -- stepper, sensors, events, observations, resets and
+// spawns -- keeps contraction off and stays bit-exact.  The calibration build (gm_calib.hip)
+// keeps it off too: its timestep search compares stability verdicts at the edge of
+// stability, candidate for candidate with the oracle.
+#ifdef GM_CAL_TU
+#pragma clang fp contract(off)
+#else
+#pragma clang fp contract(fast)
+#endif
+namespace gmf {
+#include "gm_fphelpers.inc"
 
 template <int CL>
 __device__ __forceinline__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
@@ -1160,7 +1117,6 @@ __device__ void write_contact(SharedT<CL>& S, int slot, int g1, int g2, int b1, 
   S.cbody[slot][0] = (int16_t)b1; S.cbody[slot][1] = (int16_t)b2;
 }
 
-__host__ __device__ constexpr int gm_pair_batches(int CL) { return CL <= 10 ? 1 : 2; }
 
 #include "gm_newton.hip"
 
@@ -1347,6 +1303,15 @@ __device__ __forceinline__ void integrate(SharedT<CL>& S, const gm_model* __rest
   }
   __syncthreads();
 }
+
+}  // namespace gmf
+#pragma clang fp contract(off)
+using gmf::kinematics;
+using gmf::crb_rne;
+using gmf::mass_and_forces;
+using gmf::collision;
+using gmf::newton_solve;
+using gmf::integrate;
 
 // ============================================================ reference scalar logic (lane 0)
 // luke::Gripper in fp64 (gripper.cpp), bit-for-bit the same operations as the reference

@@ -22,7 +22,7 @@ def build(verbose: bool = False, force: bool = False, out: str | None = None, ex
     builds, with `extra_flags` added to every compile)."""
     lib_path = out or LIB_PATH
     srcs = [os.path.join(PKG_DIR, s) for s in SOURCES]
-    deps = srcs + [os.path.join(PKG_DIR, "csrc", f) for f in ("gm_kernels.hip", "gm_newton.hip", "gm_math.h", "gm_policy.hip", "gm_state.h")] + \
+    deps = srcs + [os.path.join(PKG_DIR, "csrc", f) for f in ("gm_kernels.hip", "gm_newton.hip", "gm_math.h", "gm_fphelpers.inc", "gm_policy.hip", "gm_state.h")] + \
         [os.path.join(REPO_DIR, "include", f) for f in ("gripper_mi355x.h", "gm_settings.def")]
     if not force and out is None and os.path.exists(LIB_PATH):
         t = os.path.getmtime(LIB_PATH)

@@ -11,8 +11,9 @@ or_import_state), both run the same env-step, and the results are compared:
 - done flags, event rows / abs counters, stepper step counts: bit-exact;
 - reward: |d| <= 1e-6 + 1e-5 |r| (a float sum of the same terms);
 - one MjClass::step (substep) from the same states: contact pair ids bit-exact, contact
-  geometry, constraint forces, accelerations and the object's cfrc_ext near bit level
-  (both sides fp64 with FMA contraction off), and the contact-force-sum invariant of
+  geometry, constraint forces, accelerations and the object's cfrc_ext to ~1e-12 (both
+  sides fp64; the device physics fuses multiply-adds, the oracle does not), and the
+  contact-force-sum invariant of
   ObjectHandler::check_contact_forces (objecthandler.cpp:994-1032, tol 1e-5).
 
 The batch is asserted to contain the hard cases: finger-object contacts, constraint
@@ -76,7 +77,8 @@ def compare_step(gm, ol, env, snap):
     rel, ab = obs_err(snap["obs"], obs_o)
     bad_obs = np.where((rel > OBS_RTOL) | (ab > OBS_ATOL))[0]
     # every env meets the bound: both sides run the same tree-ordered factor and solves,
-    # the same sin/cos (gm_math.h) and the same converged Newton solve
+    # the same sin/cos (gm_math.h) and the same converged Newton solve; they differ only by
+    # the device's fused multiply-adds in the physics (~1e-12 per substep)
     assert bad_obs.size == 0, (
         f"step {snap['k']}: {bad_obs.size} envs exceed the obs bound, worst rel {rel.max():.3e} abs {ab.max():.3e} "
         f"(envs {bad_obs[:8]})")

@@ -342,6 +342,10 @@ void gm_default_model_params(gm_model_params* p) {
   p->timestep = 3.187e-3;
   p->pgs_iterations = 24;
   p->collision_half_thickness = 1.5e-3;
+  p->segment_damping = 0.24;
+  p->segment_damping_power = 1.0;
+  p->segment_armature = 0.0;
+  p->segment_armature_power = 0.0;
 }
 
 int gm_build_model(const gm_model_params* p, gm_model* m) {
@@ -421,7 +425,8 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
   // own measured stable timesteps (rl/juypter/thesis_plots/mujoco_timesteps.csv, the
   // t = 0.9 mm, w = 28 mm, inertia x50 column) within a few percent for N = 5..10
   // (tests/test_calibration.py).
-  const double seg_damping = 0.24 / N;
+  const double seg_damping = p->segment_damping * std::pow((double)N, -p->segment_damping_power);
+  const double seg_armature = p->segment_armature * std::pow((double)N, -p->segment_armature_power);
 
   int first_finger_geom = m->ngeom;
   for (int f = 0; f < 3; f++) {
@@ -486,7 +491,7 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
       }
       int bs = B.add_body(parent, GM_GRP_FINGER0 + f, pos, id4, mass, ipos, in);
       double axs[3] = {0, 0, 1};
-      int d = B.add_joint(bs, GM_JNT_HINGE, axs, seg_stiffness(k), seg_damping, 0, parent_dof);
+      int d = B.add_joint(bs, GM_JNT_HINGE, axs, seg_stiffness(k), seg_damping, seg_armature, parent_dof);
       if (k == 1) m->dof_seg[f] = d;
       B.add_geom(bs, GM_GEOM_BOX, GM_CLS_FINGER1 + f, gpos, id4, gsz, 1.0);
       if (last) m->body_tip[f] = bs;

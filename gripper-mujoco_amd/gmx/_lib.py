@@ -102,7 +102,9 @@ class ModelParams(C.Structure):
                 ("hook_length", C.c_double), ("hook_angle_degrees", C.c_double),
                 ("fingertip_clearance", C.c_double), ("segment_inertia_scaling", C.c_double),
                 ("timestep", C.c_double), ("pgs_iterations", C.c_int32),
-                ("collision_half_thickness", C.c_double)]
+                ("collision_half_thickness", C.c_double), ("segment_damping", C.c_double),
+                ("segment_damping_power", C.c_double), ("segment_armature", C.c_double),
+                ("segment_armature_power", C.c_double)]
 
 
 class Object(C.Structure):

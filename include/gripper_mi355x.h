@@ -192,6 +192,13 @@ typedef struct gm_model_params {      /* numerics the MJCF would carry (myfuncti
   double  timestep;                   /* 3.187e-3 (test.cpp:207)              */
   int32_t pgs_iterations;             /* fixed sweep count (deterministic)    */
   double  collision_half_thickness;   /* finger plate collision half-thickness */
+  /* segment hinge damping d = segment_damping * N^-segment_damping_power and armature
+   * a = segment_armature * N^-segment_armature_power (absent from the reference sources:
+   * fitted to its measured stable timesteps, tests/test_calibration.py) */
+  double  segment_damping;
+  double  segment_damping_power;
+  double  segment_armature;
+  double  segment_armature_power;
 } gm_model_params;
 
 typedef struct gm_model {

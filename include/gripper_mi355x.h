@@ -190,7 +190,7 @@ typedef struct gm_model_params {      /* numerics the MJCF would carry (myfuncti
   double  fingertip_clearance;        /* 10e-3                                */
   double  segment_inertia_scaling;    /* 50                                   */
   double  timestep;                   /* 3.187e-3 (test.cpp:207)              */
-  int32_t pgs_iterations;             /* fixed sweep count (deterministic)    */
+  int32_t pgs_iterations;             /* sweeps of the oracle's PGS cross-check */
   double  collision_half_thickness;   /* finger plate collision half-thickness */
   /* segment hinge damping d = segment_damping * N^-segment_damping_power and armature
    * a = segment_armature * N^-segment_armature_power (absent from the reference sources:
@@ -519,10 +519,11 @@ int  gm_last_step_ms(gm_ctx* ctx, float* ms);
 int  gm_debug_substep(gm_ctx* ctx, int32_t* ncon, double* contact, double* efc_force,
                       double* qacc, int32_t* nefc, double* obj_wrench);
 /* diagnostic: one gm_step with per-phase shader-clock cycle counters, lane-0 view,
-   summed over substeps: out[n_envs][24] = kinematics, crb_rne, mass+forces, factor,
-   smooth solve, collision, constraint build+PGS, constraint accel, integrate,
-   update_all, monitor_sensors, then sub-phases (constraint rows, Yd, Delassus,
-   PGS, FK hinge rotations, FK chains, CRB/RNE chains), (rest spare) */
+   summed over substeps: out[n_envs][32]; columns 0-27 are clocks (names in gmx.env
+   BatchedGripperEnv.PHASES: kinematics, crb_rne, mass+forces, collision, newton_solve,
+   integrate, update_all, monitor_sensors, the Newton sub-phases, the env-step epilogue),
+   28 = constraint rows summed, 29 = substeps that ran MPR, 30 = Newton iterations,
+   31 = line-search evaluations */
 int  gm_step_profiled(gm_ctx* ctx, uint64_t* phase_cycles);
 
 /* ---- on-device DQN policy ----

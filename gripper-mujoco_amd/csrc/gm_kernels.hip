@@ -93,9 +93,10 @@ struct __align__(16) SharedT {
       real cfrc[NB][6];
       real chain_f[5][6], chain_I[5][10];   // chain-root sums for the base body
     };
-    struct { real V[NB][6]; real QF[GM_MAX_CON][9]; } nw;
+    struct { real QF[GM_MAX_CON][9]; real V[NB][6]; } nw;
     struct { real V[NB][6]; real V2[NB][6]; } nw2;   // setup: qvel and warm-start velocities
-    struct { real root[4][54]; real comp[54]; real oo[27]; } st;
+    // the chain-root stage sits after the per-contact Q / F (the ground pass re-reads them)
+    struct { real qf_[GM_MAX_CON][9]; real root[4][54]; real comp[54]; real oo[27]; } st;
     struct { real lbub[3][CL][14]; real plb[14]; real bbx[28]; real ych[3][CL]; real ypalm; } fs;
     struct { real efc[GM_MAX_EFC]; } dbg;
   };

@@ -562,44 +562,37 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     qf[6] = F[0]; qf[7] = F[1]; qf[8] = F[2];
   }
   __syncthreads();
-  // ---- scan lanes: the body's contacts with the object (o) / the ground (g)
+  // ---- scan lanes: the body's contacts with the object.  Contacts of gripper bodies with
+  // the ground (rare) are added in a second pass below, so the common path keeps one
+  // 27-value composite per lane in registers instead of two.
   const int b = T->lane_body[lane];
-  real Ko[21], Kg[21], Fo[6], Fg[6];
+  real Ko[21], Fo[6];
 #pragma unroll
-  for (int k = 0; k < 21; k++) { Ko[k] = 0; Kg[k] = 0; }
+  for (int k = 0; k < 21; k++) Ko[k] = 0;
 #pragma unroll
-  for (int k = 0; k < 6; k++) { Fo[k] = 0; Fg[k] = 0; }
+  for (int k = 0; k < 6; k++) Fo[k] = 0;
   bool have_g = false;
 #pragma unroll
   for (int s = 0; s < 2; s++) {
+    const int pr = T->lane_opair[lane][s];
+    const int pg = T->lane_gpair[lane][s];
+    if (pg >= 0 && S.pair_cnt[pg] > 0 && S.pair_off[pg] < ncon) have_g = true;
+    if (pr < 0) continue;
+    const int c0 = S.pair_off[pr];
+    int c1 = c0 + S.pair_cnt[pr];
+    if (c1 > ncon) c1 = ncon;
+    for (int c = c0; c < c1; c++) {
+      const real* qf = S.nw.QF[c];
+      const real pos[3] = {S.con[c][1], S.con[c][2], S.con[c][3]};
+      const real sg = (S.cbody[c][1] == b) ? 1.0 : -1.0;
+      real Kc[21], Fs[6];
+      spatial_K(qf, pos, Kc);
+      cross3(Fs, pos, qf + 6);
+      Fs[3] = qf[6]; Fs[4] = qf[7]; Fs[5] = qf[8];
 #pragma unroll
-    for (int og = 0; og < 2; og++) {
-      const int pr = og == 0 ? T->lane_opair[lane][s] : T->lane_gpair[lane][s];
-      if (pr < 0) continue;
-      const int c0 = S.pair_off[pr];
-      int c1 = c0 + S.pair_cnt[pr];
-      if (c1 > ncon) c1 = ncon;
-      for (int c = c0; c < c1; c++) {
-        const real* qf = S.nw.QF[c];
-        const real pos[3] = {S.con[c][1], S.con[c][2], S.con[c][3]};
-        const real sg = (S.cbody[c][1] == b) ? 1.0 : -1.0;
-        real Kc[21], Fs[6];
-        spatial_K(qf, pos, Kc);
-        cross3(Fs, pos, qf + 6);
-        Fs[3] = qf[6]; Fs[4] = qf[7]; Fs[5] = qf[8];
-        if (og == 0) {
+      for (int k = 0; k < 21; k++) Ko[k] += Kc[k];
 #pragma unroll
-          for (int k = 0; k < 21; k++) Ko[k] += Kc[k];
-#pragma unroll
-          for (int k = 0; k < 6; k++) Fo[k] += sg * Fs[k];
-        } else {
-#pragma unroll
-          for (int k = 0; k < 21; k++) Kg[k] += Kc[k];
-#pragma unroll
-          for (int k = 0; k < 6; k++) Fg[k] += sg * Fs[k];
-          have_g = true;
-        }
-      }
+      for (int k = 0; k < 6; k++) Fo[k] += sg * Fs[k];
     }
   }
   const bool any_g = __ballot(have_g) != 0ull;
@@ -643,34 +636,26 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
 #pragma unroll
     for (int k = 0; k < 6; k++) Fo[k] += row_shl(Fo[k], off);
   }
-  if (any_g) {
-#pragma unroll
-    for (int off = 1; off < CL; off <<= 1) {
-#pragma unroll
-      for (int k = 0; k < 21; k++) Kg[k] += row_shl(Kg[k], off);
-#pragma unroll
-      for (int k = 0; k < 6; k++) Fg[k] += row_shl(Fg[k], off);
-    }
-  }
-  __syncthreads();   // every lane is done with QF before the stage overwrites it
-  // ---- chain roots (fingers at position 1, the palm) to the stage; the ground-object pair
+  // ---- chain roots (fingers at position 1, the palm) to the stage (which sits after the
+  // per-contact Q / F in the union: the ground pass below still reads them)
   {
     const int root = (lane == 1) ? 0 : (lane == 17) ? 1 : (lane == 33) ? 2 : (lane == 49) ? 3 : -1;
     if (root >= 0) {
       real* st = S.st.root[root];
 #pragma unroll
-      for (int k = 0; k < 21; k++) { st[k] = Ko[k]; st[21 + k] = Kg[k]; }
+      for (int k = 0; k < 21; k++) st[k] = Ko[k];
 #pragma unroll
-      for (int k = 0; k < 6; k++) { st[42 + k] = Fo[k]; st[48 + k] = Fg[k]; }
+      for (int k = 0; k < 6; k++) st[42 + k] = Fo[k];
     }
   }
   __syncthreads();
   // ---- base composites (the four roots in order) and the object's totals
-  if (lane < 54) {
+  if (lane < 27) {
+    const int k = lane < 21 ? lane : 42 + lane - 21;
     real acc = 0;
 #pragma unroll
-    for (int c = 0; c < 4; c++) acc += S.st.root[c][lane];
-    S.st.comp[lane] = acc;
+    for (int c = 0; c < 4; c++) acc += S.st.root[c][k];
+    S.st.comp[k] = acc;
   }
   __syncthreads();
   if (lane < 27) {
@@ -689,55 +674,32 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
   const real* cdb = S.cdof[T->dof_base];
   if (rowf < 3 && p >= 1 && p <= CL) {
     const int d = T->dof_f0[rowf] + p - 1;
-    real cd[6], y[6], yo[6], Ft[6];
+    real cd[6], y[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
-    symK_mul(Ko, cd, yo);
-    if (any_g) {   // wave-uniform: ground contacts on gripper bodies (rare)
-      real Kt[21];
-#pragma unroll
-      for (int k = 0; k < 21; k++) Kt[k] = Ko[k] + Kg[k];
-#pragma unroll
-      for (int k = 0; k < 6; k++) Ft[k] = Fo[k] + Fg[k];
-      symK_mul(Kt, cd, y);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 6; k++) { Ft[k] = Fo[k]; y[k] = yo[k]; }
-    }
+    symK_mul(Ko, cd, y);
     const real* H = S.Hf[rowf];
 #pragma unroll
     for (int j = 1; j <= CL; j++)
       if (j <= p) h[j] = H[TRI(p, j)] + dot6(S.cdof[T->dof_f0[rowf] + j - 1], y);
     hb[0] = H[TRI(p, 0)] + dot6(cdb, y);
 #pragma unroll
-    for (int k = 0; k < 6; k++) hb[1 + k] = -dot6(S.cdof[T->dof_obj + k], yo);
-    rhs = S.frc[d] + dot6(cd, Ft);
+    for (int k = 0; k < 6; k++) hb[1 + k] = -dot6(S.cdof[T->dof_obj + k], y);
+    rhs = S.frc[d] + dot6(cd, Fo);
   } else if (lane == GM_LANE_PALM_F) {
     const int d = T->dof_palm;
     const real* st = S.st.root[3];
-    real Ft[6], K0[21];
+    real K0[21], cd[6], y[6];
 #pragma unroll
     for (int k = 0; k < 21; k++) K0[k] = st[k];
-    real cd[6], y[6], yo[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
-    symK_mul(K0, cd, yo);
-    if (any_g) {
-      real Kt[21];
-#pragma unroll
-      for (int k = 0; k < 21; k++) Kt[k] = st[k] + st[21 + k];
-#pragma unroll
-      for (int k = 0; k < 6; k++) Ft[k] = st[42 + k] + st[48 + k];
-      symK_mul(Kt, cd, y);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 6; k++) { Ft[k] = st[42 + k]; y[k] = yo[k]; }
-    }
+    symK_mul(K0, cd, y);
     h[1] = S.Hp[TRI(1, 1)] + dot6(cd, y);
     hb[0] = S.Hp[TRI(1, 0)] + dot6(cdb, y);
 #pragma unroll
-    for (int k = 0; k < 6; k++) hb[1 + k] = -dot6(S.cdof[T->dof_obj + k], yo);
-    rhs = S.frc[d] + dot6(cd, Ft);
+    for (int k = 0; k < 6; k++) hb[1 + k] = -dot6(S.cdof[T->dof_obj + k], y);
+    rhs = S.frc[d] + dot6(cd, st + 42);
   } else if (lane >= 48 && lane < 55) {
     const int i = lane - 48;
     const real* cp = S.st.comp;
@@ -746,20 +708,8 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     for (int k = 0; k < 21; k++) KBo[k] = cp[k];
     symK_mul(KBo, cdb, yob);
     if (i == 0) {
-      real FBt[6], y[6];
-      if (any_g) {
-        real KBt[21];
-#pragma unroll
-        for (int k = 0; k < 21; k++) KBt[k] = cp[k] + cp[21 + k];
-#pragma unroll
-        for (int k = 0; k < 6; k++) FBt[k] = cp[42 + k] + cp[48 + k];
-        symK_mul(KBt, cdb, y);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 6; k++) { FBt[k] = cp[42 + k]; y[k] = yob[k]; }
-      }
-      hb[0] = S.Hbb + dot6(cdb, y);
-      rhs = S.frc[T->dof_base] + dot6(cdb, FBt);
+      hb[0] = S.Hbb + dot6(cdb, yob);
+      rhs = S.frc[T->dof_base] + dot6(cdb, cp + 42);
     } else {
       const int k = i - 1;
       const real* cok = S.cdof[T->dof_obj + k];
@@ -772,6 +722,80 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
       for (int l2 = 0; l2 < 6; l2++)
         if (l2 <= k) hb[1 + l2] = S.Ho[TRI(k, l2)] + dot6(S.cdof[T->dof_obj + l2], yk);
       rhs = S.frc[T->dof_obj + k] + dot6(cok, S.st.oo + 21);
+    }
+  }
+  // ---- contacts of gripper bodies with the ground (wave-uniform, rare): their composite
+  // Kg is added to the chain rows' and the base's entries (the object rows do not see it)
+  if (any_g) {
+    real Kg[21], Fg[6];
+#pragma unroll
+    for (int k = 0; k < 21; k++) Kg[k] = 0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) Fg[k] = 0;
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      const int pr = T->lane_gpair[lane][s];
+      if (pr < 0) continue;
+      const int c0 = S.pair_off[pr];
+      int c1 = c0 + S.pair_cnt[pr];
+      if (c1 > ncon) c1 = ncon;
+      for (int c = c0; c < c1; c++) {
+        const real* qf = S.nw.QF[c];
+        const real pos[3] = {S.con[c][1], S.con[c][2], S.con[c][3]};
+        const real sg = (S.cbody[c][1] == b) ? 1.0 : -1.0;
+        real Kc[21], Fs[6];
+        spatial_K(qf, pos, Kc);
+        cross3(Fs, pos, qf + 6);
+        Fs[3] = qf[6]; Fs[4] = qf[7]; Fs[5] = qf[8];
+#pragma unroll
+        for (int k = 0; k < 21; k++) Kg[k] += Kc[k];
+#pragma unroll
+        for (int k = 0; k < 6; k++) Fg[k] += sg * Fs[k];
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < CL; off <<= 1) {
+#pragma unroll
+      for (int k = 0; k < 21; k++) Kg[k] += row_shl(Kg[k], off);
+#pragma unroll
+      for (int k = 0; k < 6; k++) Fg[k] += row_shl(Fg[k], off);
+    }
+    const int root = (lane == 1) ? 0 : (lane == 17) ? 1 : (lane == 33) ? 2 : (lane == 49) ? 3 : -1;
+    if (root >= 0) {
+      real* st = S.st.root[root];
+#pragma unroll
+      for (int k = 0; k < 21; k++) st[21 + k] = Kg[k];
+#pragma unroll
+      for (int k = 0; k < 6; k++) st[48 + k] = Fg[k];
+    }
+    __syncthreads();
+    const bool chainrow = rowf < 3 && p >= 1 && p <= CL;
+    if (lane == GM_LANE_PALM_F) {
+#pragma unroll
+      for (int k = 0; k < 21; k++) Kg[k] = S.st.root[3][21 + k];
+#pragma unroll
+      for (int k = 0; k < 6; k++) Fg[k] = S.st.root[3][48 + k];
+    } else if (lane == 48) {
+#pragma unroll
+      for (int k = 0; k < 21; k++) Kg[k] = ((S.st.root[0][21 + k] + S.st.root[1][21 + k]) + S.st.root[2][21 + k]) + S.st.root[3][21 + k];
+#pragma unroll
+      for (int k = 0; k < 6; k++) Fg[k] = ((S.st.root[0][48 + k] + S.st.root[1][48 + k]) + S.st.root[2][48 + k]) + S.st.root[3][48 + k];
+    }
+    if (chainrow || lane == GM_LANE_PALM_F || lane == 48) {
+      const int d = chainrow ? T->dof_f0[rowf] + p - 1 : lane == 48 ? T->dof_base : T->dof_palm;
+      real cd[6], yg[6];
+#pragma unroll
+      for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
+      symK_mul(Kg, cd, yg);
+      if (chainrow) {
+#pragma unroll
+        for (int j = 1; j <= CL; j++)
+          if (j <= p) h[j] += dot6(S.cdof[T->dof_f0[rowf] + j - 1], yg);
+      } else if (lane == GM_LANE_PALM_F) {
+        h[1] += dot6(cd, yg);
+      }
+      hb[0] += dot6(cdb, yg);
+      rhs += dot6(cd, Fg);
     }
   }
   // motor-lock rows (1-dof joint equalities): D on the diagonal, D aref on the rhs

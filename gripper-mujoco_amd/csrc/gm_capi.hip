@@ -218,6 +218,7 @@ int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
     const int b = m.dof_body[m.lock_dof[k]];
     T.lock_grp[k] = T.body_group[b];
     T.lock_cpos[k] = T.body_cpos[b];
+    T.lock_tran[k] = m.body_invweight0[b][0] + m.body_invweight0[m.body_parent[b]][0];
   }
   // per scan lane: the lane body's pairs with the object / the ground (oracle topo_init)
   T.lane_obj = 50;

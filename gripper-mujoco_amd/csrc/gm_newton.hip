@@ -453,11 +453,25 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
     const int d = m->lock_dof[k];
     const real pos = S.s.qpos[d] - S.s.lock_q[k];
     const real vel = S.s.qvel[d];
-    const real imp = impedance(m, pos);
-    real Rr = div_n(1 - imp, imp) * m->dof_invweight0[d];
-    if (Rr < 1e-15) Rr = 1e-15;
-    R.lD = rcp_n(Rr);
-    R.laref = -Bd * vel - K * imp * pos;
+    // the reference's weld on a slide as one row on the dof (oracle constraint_setup):
+    // per world axis r the weld row a_r qdot with its own impedance and the weld's
+    // regulariser, summed: D = sum D_r a_r^2, D aref = sum D_r a_r aref_r
+    const real tran = T->lock_tran[k];
+    real De = 0.0, Dar = 0.0;
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      const real a = S.cdof[d][3 + r];
+      if (a == 0.0) continue;
+      const real pr = a * pos, vr = a * vel;
+      const real imp = impedance(m, pr);
+      real Rr = div_n(1 - imp, imp) * tran;
+      if (Rr < 1e-15) Rr = 1e-15;
+      const real Da = rcp_n(Rr) * a;
+      De = De + Da * a;
+      Dar = Dar + Da * (-Bd * vr - K * imp * pr);
+    }
+    R.lD = De;
+    R.laref = div_n(Dar, De);
     R.ldof = d;
   }
   if (lane == 0) { S.nl = nl; S.nefc = nl + 4 * S.ncon; }

@@ -242,4 +242,6 @@ struct GmTopo {
   // from pair_gobj); lane_obj is the object's scan lane
   int32_t lane_opair[64][2], lane_gpair[64][2];
   int32_t pair_gobj, lane_obj;
+  // per motor lock: its weld's regulariser sum, body_invweight0 of the slide's two bodies
+  double lock_tran[GM_MAX_LOCK];
 };

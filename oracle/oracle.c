@@ -29,7 +29,7 @@
 #define NQ GM_MAX_QPOS
 #define NG GM_MAX_GEOM
 #define NC GM_MAX_CON
-#define NE GM_MAX_EFC
+#define NE (GM_MAX_EFC + 2 * GM_MAX_LOCK)   /* + the weld-lock variant's extra rows */
 #define PI_D 3.14159265358979323846
 
 /* =====================================================================
@@ -294,7 +294,9 @@ struct or_env {
   int nefc, nl;
   double efc_f[NE], efc_D[NE], efc_aref[NE];
   int efc_type[NE];  /* 0 equality, 1 pyramid edge */
-  int lock_row_dof[GM_MAX_LOCK];
+  int lock_row_dof[3 * GM_MAX_LOCK];
+  double lock_row_a[3 * GM_MAX_LOCK];   /* the row's Jacobian on its dof (1 for a joint lock) */
+  int weld_locks;                       /* motor locks as MuJoCo weld rows (test variant) */
   int solver_pgs;                  /* 0: Newton (the engine); > 0: dense PGS cross-check, this many sweeps */
   int stat_it, stat_ls;            /* Newton iterations / line-search evaluations of the last substep */
   long stat_it_sum, stat_ls_sum, stat_solves, stat_it_max, stat_ncon_max, stat_nefc_sum;
@@ -1479,6 +1481,10 @@ int or_calibrate(const gm_model* m, const gm_config* c, const gm_object* objects
 /* test hook: the constraint solver of envs created from now on (0 Newton, > 0 PGS sweeps) */
 static int g_solver_pgs = 0;
 void or_set_default_solver(int pgs_sweeps) { g_solver_pgs = pgs_sweeps; }
+/* test variant: the reference's motor locks as 6-row weld equalities between the slide's
+ * two bodies (myfunctions.cpp:1177-1279) instead of the engine's 1-row joint locks */
+static int g_weld_locks = 0;
+void or_set_default_weld_locks(int on) { g_weld_locks = on; }
 void or_set_solver(or_env* e, int pgs_sweeps) { e->solver_pgs = pgs_sweeps; }
 /* solver statistics since creation: solves, Newton iterations, line-search evaluations,
  * max iterations, max contacts generated, constraint rows */
@@ -1497,6 +1503,7 @@ or_env* or_create(const gm_model* m, const gm_config* c, const gm_object* object
   for (int i = 0; i < e->nobj; i++) e->objs[i] = objects[i];
   e->env_id = env_id;
   e->solver_pgs = g_solver_pgs;
+  e->weld_locks = g_weld_locks;
   e->rng = lcg_seed((uint64_t)c->s.random_seed + (uint64_t)env_id * 1000003ull);
   /* settle with the first object parked at the keyframe pose */
   topo_init(e);
@@ -1578,7 +1585,7 @@ void or_debug_substep(or_env* e, int32_t* ncon, double* contact, double* efc_for
       o[13] = C->g1; o[14] = C->g2; o[15] = C->mu;
     }
   }
-  if (efc_force) for (int r = 0; r < NE; r++) efc_force[r] = r < e->nefc ? e->efc_f[r] : 0.0;
+  if (efc_force) for (int r = 0; r < GM_MAX_EFC; r++) efc_force[r] = r < e->nefc ? e->efc_f[r] : 0.0;
   if (qacc) for (int d = 0; d < e->m.nv; d++) qacc[d] = e->qacc[d];
   if (obj_wrench) or_object_net_wrench(e, obj_wrench);
 }
@@ -1801,7 +1808,7 @@ static void* sub_worker(void* arg) {
     if (or_import_state(e, st) != 0) { j->err = k + 1; continue; }
     double qacc[NV];
     or_debug_substep(e, j->ncon ? &j->ncon[k] : NULL, j->contact ? j->contact + (size_t)k * NC * 16 : NULL,
-                     j->efc ? j->efc + (size_t)k * NE : NULL, qacc, j->wrench ? j->wrench + (size_t)k * 6 : NULL);
+                     j->efc ? j->efc + (size_t)k * GM_MAX_EFC : NULL, qacc, j->wrench ? j->wrench + (size_t)k * 6 : NULL);
     if (j->qacc) for (int d = 0; d < NV; d++) j->qacc[(size_t)k * NV + d] = d < e->m.nv ? qacc[d] : 0.0;
     if (j->nefc) j->nefc[k] = e->nefc;
     or_export_state(e, st);

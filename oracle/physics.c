@@ -1339,7 +1339,10 @@ static void newton_assemble(or_env* e, const int* act, nsys_t* S) {
   for (int d = 0; d < NV; d++) { lockon[d] = 0; lockD[d] = 0; lockR[d] = 0; }
   for (int r = 0; r < e->nl; r++) {
     const int d = e->lock_row_dof[r];
-    lockon[d] = 1; lockD[d] = e->efc_D[r]; lockR[d] = e->efc_D[r] * e->efc_aref[r];
+    const double a = e->lock_row_a[r];
+    if (a == 1.0 && !lockon[d]) { lockD[d] = e->efc_D[r]; lockR[d] = e->efc_D[r] * e->efc_aref[r]; }
+    else { lockD[d] += (e->efc_D[r] * a) * a; lockR[d] += (e->efc_D[r] * a) * e->efc_aref[r]; }
+    lockon[d] = 1;
   }
   const double* cdb = e->cdof[m->dof_base];
   /* finger chain rows */
@@ -1547,13 +1550,55 @@ static void constraint_setup(or_env* e) {
     const int d = m->lock_dof[k];
     const double pos = e->qpos[d] - e->lock_q[k];
     const double vel = e->qvel[d];
-    const double imp = impedance(m, pos);
-    double R = ((1 - imp) / imp) * m->dof_invweight0[d];
-    if (R < 1e-15) R = 1e-15;
-    e->efc_D[n] = 1.0 / R;
-    e->efc_aref[n] = -Bd * vel - K * imp * pos;
+    if (e->weld_locks) {
+      /* a weld between the slide's child and parent bodies: of its 6 rows only the
+       * translational ones along the slide axis have a nonzero Jacobian (the joint fixes
+       * every other relative motion); per world axis r the row is a_r qdot_d with its
+       * own violation a_r pos, impedance, and the weld regulariser (mj_diagApprox:
+       * translational body_invweight0 of both bodies) */
+      const int b = m->dof_body[d], pb = m->body_parent[b];
+      const double tran = body_invw(e, b) + body_invw(e, pb);
+      for (int r = 0; r < 3; r++) {
+        const double a = e->cdof[d][3 + r];
+        if (fabs(a) < 1e-12) continue;
+        const double pr = a * pos, vr = a * vel;
+        const double imp = impedance(m, pr);
+        double R = ((1 - imp) / imp) * tran;
+        if (R < 1e-15) R = 1e-15;
+        e->efc_D[n] = 1.0 / R;
+        e->efc_aref[n] = -Bd * vr - K * imp * pr;
+        e->efc_type[n] = 0;
+        e->lock_row_dof[n] = d;
+        e->lock_row_a[n] = a;
+        n++;
+      }
+      continue;
+    }
+    /* the reference's weld (myfunctions.cpp:1177-1279) on a slide: of its 6 rows only the
+     * translational ones have a nonzero Jacobian (a_r, the slide axis' world component r;
+     * the joint fixes every other relative motion), each with its own violation a_r pos,
+     * impedance and the weld regulariser (mj_diagApprox for mjEQ_WELD: the two bodies'
+     * translational body_invweight0).  Their sum on the dof is one row with
+     * D = sum_r D_r a_r^2 and D aref = sum_r D_r a_r aref_r, the same cost exactly. */
+    const int b = m->dof_body[d], pb = m->body_parent[b];
+    const double tran = body_invw(e, b) + body_invw(e, pb);
+    double De = 0.0, Dar = 0.0;
+    for (int r = 0; r < 3; r++) {
+      const double a = e->cdof[d][3 + r];
+      if (a == 0.0) continue;
+      const double pr = a * pos, vr = a * vel;
+      const double imp = impedance(m, pr);
+      double R = ((1 - imp) / imp) * tran;
+      if (R < 1e-15) R = 1e-15;
+      const double Da = (1.0 / R) * a;
+      De = De + Da * a;
+      Dar = Dar + Da * (-Bd * vr - K * imp * pr);
+    }
+    e->efc_D[n] = De;
+    e->efc_aref[n] = Dar / De;
     e->efc_type[n] = 0;
     e->lock_row_dof[n] = d;
+    e->lock_row_a[n] = 1.0;
     n++;
   }
   e->nl = n;
@@ -1583,7 +1628,8 @@ static void constraint_setup(or_env* e) {
 static void rows_jar(or_env* e, const double* v, double* jar) {
   double V[NB][6];
   body_vel(e, v, V);
-  for (int r = 0; r < e->nl; r++) jar[r] = v[e->lock_row_dof[r]] - e->efc_aref[r];
+  for (int r = 0; r < e->nl; r++)
+    jar[r] = (e->lock_row_a[r] == 1.0 ? v[e->lock_row_dof[r]] : e->lock_row_a[r] * v[e->lock_row_dof[r]]) - e->efc_aref[r];
   for (int c = 0; c < e->ncon; c++) {
     double jv[4];
     contact_jv(e, c, V, jv);
@@ -1740,7 +1786,7 @@ static void ref_pgs_solve(or_env* e, int sweeps) {
   chol_solve(nv, Lf, qs);
   /* dense Jacobian rows */
   for (int r = 0; r < n; r++) for (int i = 0; i < NV; i++) J[r][i] = 0;
-  for (int r = 0; r < e->nl; r++) J[r][e->lock_row_dof[r]] = 1.0;
+  for (int r = 0; r < e->nl; r++) J[r][e->lock_row_dof[r]] = e->lock_row_a[r];
   for (int i = 0; i < nv; i++) {
     double ev[NV];
     for (int k = 0; k < NV; k++) ev[k] = (k == i) ? 1.0 : 0.0;

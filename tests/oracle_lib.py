@@ -70,6 +70,7 @@ def lib():
             "or_calibrate": (i32, [vp, vp, vp, i32, i32, vp, vp, vp, i32]),
             "or_get_stats": (None, [vp, C.POINTER(C.c_int64)]),
             "or_set_default_solver": (None, [i32]),
+            "or_set_default_weld_locks": (None, [i32]),
             "or_set_solver": (None, [vp, i32]),
         }
         for n, (r, a) in sig.items():
@@ -214,6 +215,18 @@ class pgs_solver:
 
     def __exit__(self, *exc):
         set_default_solver(0)
+
+
+class weld_locks:
+    """with weld_locks(): ... -- oracle envs created inside hold their stopped motors with
+    the reference's weld equalities (rows along the slide axis with the weld's
+    regulariser) instead of the engine's 1-row joint locks"""
+
+    def __enter__(self):
+        lib().or_set_default_weld_locks(1)
+
+    def __exit__(self, *exc):
+        lib().or_set_default_weld_locks(0)
 
 
 def solver_stats(env) -> dict:

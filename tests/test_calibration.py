@@ -223,3 +223,52 @@ def test_timestep_search_all_72_points_within_stated_bands(world):
                 assert got[(n, t, w, s2)] >= ms, (n, t, w, s, s2)
         if n < 10:
             assert got[(n + 1, t, w, s)] < ms, (n, t, w, s)
+
+
+# validate_curve_under_force's retry branch (mjclass.cpp:4073-4090), forced: at a 4.8 ms
+# model step with a 10x saturation load the loaded 50 s settle reaches mjWARN_BADQACC, the
+# run is repeated at 0.8x the step and settles.
+RETRY_DT, RETRY_SAT = 4.8e-3, 10.0
+
+
+def retry_world(gm):
+    import ctypes as C
+    p = gm.ModelParams()
+    gm.load_library().gm_default_model_params(C.byref(p))
+    p.timestep = RETRY_DT
+    model = gm.ModelBlob(p)
+    s = gm.canonical_settings(noise=False, seed=1)
+    s.saturation_yield_factor = RETRY_SAT
+    return model, gm.ConfigBlob(s, model), gm.make_object_set("set1_synthetic", 1), p
+
+
+def test_gauge_calibration_retry_is_forced_on_the_oracle(world):
+    """The retry runs the whole loaded settle again at 0.8x the step (the engine's
+    intentional fix of the reference's resume-without-load): the
+    result equals a first-try calibration at that reduced step."""
+    import ctypes as C
+    gm = world[0]
+    model, cfg, objs, p = retry_world(gm)
+    cal, _ = oracle_lib.calibrate(model, cfg, objs, 2)
+    assert cal.gauge_retries == 1
+    assert cal.timestep == pytest.approx(0.8 * RETRY_DT, rel=1e-12)
+    p.timestep = 0.8 * RETRY_DT
+    model2 = gm.ModelBlob(p)
+    s = gm.canonical_settings(noise=False, seed=1)
+    s.saturation_yield_factor = RETRY_SAT
+    cal2, _ = oracle_lib.calibrate(model2, gm.ConfigBlob(s, model2), objs, 2)
+    assert cal2.gauge_retries == 0
+    assert cal.bending_normalise == cal2.bending_normalise
+
+
+@pytest.mark.gpu
+def test_gpu_gauge_calibration_retry_matches_oracle(world):
+    if not gpu_available():
+        pytest.skip("no GPU")
+    gm = world[0]
+    model, cfg, objs, _ = retry_world(gm)
+    dev, _ = gm.calibrate(model, cfg, objs, what=gm.CAL_GAUGES)
+    ref, _ = oracle_lib.calibrate(model, cfg, objs, 2)
+    assert dev.gauge_retries == ref.gauge_retries == 1
+    assert dev.timestep == ref.timestep
+    assert dev.bending_normalise == pytest.approx(ref.bending_normalise, rel=1e-4)

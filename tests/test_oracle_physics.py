@@ -86,3 +86,45 @@ def test_gripper_at_rest_reads_near_zero_bend(world):
     for _ in range(3):
         obs, _, _ = e.step(np.zeros(4, dtype=np.float32))
     assert np.all(np.abs(obs[:21]) < 0.05)
+
+
+def test_motor_locks_equal_the_reference_weld():
+    """The reference holds a stopped motor with a weld equality between the slide's two
+    bodies (myfunctions.cpp:1177-1279): 6 rows, of which only the translational ones
+    along the slide axis have a nonzero Jacobian, each with its own impedance and the
+    weld's regulariser (the bodies' translational body_invweight0).  The engine folds
+    them into one row on the slide dof; an oracle variant that keeps the weld's rows
+    separate gives the same rollout (scripted grasps on set6 objects)."""
+    import gmx
+    import oracle_lib as ol
+    n, steps = 12, 45
+    settings = gmx.canonical_settings(noise=False, seed=1234)
+    model = gmx.ModelBlob()
+    cfg = gmx.ConfigBlob(settings, model)
+    objs = gmx.make_object_set("set6_synthetic", 1234)
+
+    def roll(weld):
+        if weld:
+            with ol.weld_locks():
+                envs = [ol.OracleEnv(model, cfg, objs, e) for e in range(n)]
+        else:
+            envs = [ol.OracleEnv(model, cfg, objs, e) for e in range(n)]
+        si, sx, sy, sr = gmx.env.spawn_draws(1234, np.arange(n), np.ones(n, dtype=np.int64), len(objs))
+        for e, o in enumerate(envs):
+            o.reset(gmx.Spawn(int(si[e]), float(sx[e]), float(sy[e]), float(sr[e])))
+        script = gmx.GraspScript(settings, n, seed=1234)
+        obs, done = [], []
+        for k in range(steps):
+            a = script.actions(k)
+            out = [o.step(a[e]) for e, o in enumerate(envs)]
+            obs.append([x[0] for x in out])
+            done.append([x[2] for x in out])
+        st = gmx.env_state_view(np.stack([o.export_state() for o in envs]))
+        return np.array(obs), np.array(done), st
+
+    o1, d1, s1 = roll(False)
+    o2, d2, s2 = roll(True)
+    assert (s1["lock_active"].sum() > 0) and (s1["lock_active"] == s2["lock_active"]).all()
+    np.testing.assert_array_equal(d1, d2)
+    np.testing.assert_allclose(o1, o2, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(s1["qpos"], s2["qpos"], rtol=0, atol=1e-9)

@@ -130,7 +130,19 @@ def compare_substep(gm, ol, env, snap):
     assert np.abs(fsum - w[:, :3]).max() <= 1e-5, "contact-force sum differs from cfrc_ext"
     dv, ov = gm.env_state_view(after_d), gm.env_state_view(after_o)
     np.testing.assert_allclose(dv["qpos"], ov["qpos"], rtol=0, atol=1e-9, err_msg="qpos after one substep")
+    # box-box manifolds (mjc_BoxBox): a finger/palm box against a box object with >= 2
+    # contacts in one pair
+    is_box = gm.env_state_view(snap["rec"])["obj_type"] == 6
+    n_bb = 0
+    for e in np.where(is_box)[0]:
+        pairs = {}
+        for c in range(ncon[e]):
+            g1, g2 = int(con[e, c, 13]), int(con[e, c, 14])
+            if (g1 == obj or g2 == obj) and 0 not in (g1, g2):
+                pairs[(g1, g2)] = pairs.get((g1, g2), 0) + 1
+        n_bb += any(v >= 2 for v in pairs.values())
     return dict(k=snap["k"], ncon_max=int(ncon.max()), nefc_max=int(nefc.max()), n_big=int((nefc > 32).sum()),
+                n_boxbox_manifold_envs=int(n_bb),
                 efc_err=float(np.abs((efc - efc_o) / fs).max()), qacc_err=float(np.abs((qacc - qacc_o) / qs).max()))
 
 
@@ -154,6 +166,7 @@ def test_c3_grasp_states_4096(gm, ol):
     assert (last["bev_abs"][:, i_oc] > 0).sum() > 1000, "too few envs reached finger-object contact"
     assert sum(r["done"] for r in rep) > 0, "no env reached done == 1"
     assert sum(s["n_big"] for s in sub) > 0, "no constraint problem with nefc > 32 was checked"
+    assert sum(s["n_boxbox_manifold_envs"] for s in sub) > 100, "too few multi-point box-box grasps were checked"
 
 
 def test_c2_single_cylinder_256(gm, ol):

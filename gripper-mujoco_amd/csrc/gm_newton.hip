@@ -886,12 +886,14 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
 #pragma unroll
     for (int t = 1; t < 7; t++) i += (lane >= t * (t + 1) / 2) ? 1 : 0;
     const int j = lane - i * (i + 1) / 2;
+    // one partial sum per finger chain: three independent dependent-chains of CL terms
+    real acc[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = CL; k >= 1; k--)
+#pragma unroll
+      for (int f = 0; f < 3; f++) acc[f] = acc[f] + S.fs.lbub[f][k - 1][i] * S.fs.lbub[f][k - 1][7 + j];
     real v = S.fs.bbx[lane];
-#pragma unroll
-    for (int f = 0; f < 3; f++)
-#pragma unroll
-      for (int k = CL; k >= 1; k--) v = v - S.fs.lbub[f][k - 1][i] * S.fs.lbub[f][k - 1][7 + j];
-    v = v - S.fs.plb[i] * S.fs.plb[7 + j];
+    v = (((v - acc[0]) - acc[1]) - acc[2]) - S.fs.plb[i] * S.fs.plb[7 + j];
     S.fs.bbx[lane] = v;
   }
   __syncthreads();
@@ -937,13 +939,12 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
   }
   __syncthreads();
   if (border) {
-    real v = y;
+    real acc[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-    for (int f = 0; f < 3; f++)
+    for (int k = CL; k >= 1; k--)
 #pragma unroll
-      for (int k = CL; k >= 1; k--) v = v - S.fs.lbub[f][k - 1][bi] * S.fs.ych[f][k - 1];
-    v = v - S.fs.plb[bi] * S.fs.ypalm;
-    y = v;
+      for (int f = 0; f < 3; f++) acc[f] = acc[f] + S.fs.lbub[f][k - 1][bi] * S.fs.ych[f][k - 1];
+    y = (((y - acc[0]) - acc[1]) - acc[2]) - S.fs.plb[bi] * S.fs.ypalm;
 #pragma unroll
     for (int k = 6; k >= 0; k--) {
       const real yk = row_bcast(y, k);

@@ -1485,6 +1485,10 @@ void or_set_default_solver(int pgs_sweeps) { g_solver_pgs = pgs_sweeps; }
  * two bodies (myfunctions.cpp:1177-1279) instead of the engine's 1-row joint locks */
 static int g_weld_locks = 0;
 void or_set_default_weld_locks(int on) { g_weld_locks = on; }
+/* test variant: MuJoCo 2.1.5's actuator path -- the PD forces explicit, only joint
+ * damping implicit in the Euler step (the engine folds kp, kd into H~) */
+int g_explicit_pd = 0;
+void or_set_explicit_pd(int on) { g_explicit_pd = on; }
 void or_set_solver(or_env* e, int pgs_sweeps) { e->solver_pgs = pgs_sweeps; }
 /* solver statistics since creation: solves, Newton iterations, line-search evaluations,
  * max iterations, max contacts generated, constraint rows */

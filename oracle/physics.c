@@ -428,8 +428,10 @@ static void mass_and_forces(or_env* e) {
     const int b = m->dof_body[d];
     const int c = T->dof_grp[d];
     const int p = T->dof_p[d];
+    extern int g_explicit_pd;
     double add = T->dof_arm[d] + h * T->dof_dsum[d];
     add += h * h * T->dof_ksum[d];
+    if (g_explicit_pd) add = T->dof_arm[d] + h * T->dof_damp[d];
     const double* cd = e->cdof[d];
     double F[6];
     inert_mul(F, e->Ic[b], cd);

@@ -272,3 +272,21 @@ def test_gpu_gauge_calibration_retry_matches_oracle(world):
     assert dev.gauge_retries == ref.gauge_retries == 1
     assert dev.timestep == ref.timestep
     assert dev.bending_normalise == pytest.approx(ref.bending_normalise, rel=1e-4)
+
+
+def test_explicit_pd_is_unstable_so_the_engine_integrates_it_implicitly(world):
+    """MuJoCo 2.1.5's actuator path keeps the PD forces explicit (only joint damping is
+    implicit).  With this model that is unstable at every timestep the search tries, down
+    to 50 us (oracle variant or_set_explicit_pd), which is why the engine folds kp and kd
+    into H~; the engine's own search finds the reference's 4.3 ms."""
+    import ctypes as C
+    gm = world[0]
+    L = oracle_lib.lib()
+    L.or_set_explicit_pd.argtypes = [C.c_int]
+    try:
+        L.or_set_explicit_pd(1)
+        with pytest.raises(RuntimeError):
+            search_ms(gm, 8, 0.9, 28.0, 50.0)
+    finally:
+        L.or_set_explicit_pd(0)
+    assert search_ms(gm, 8, 0.9, 28.0, 50.0)[0] == pytest.approx(4.3, rel=0.08)

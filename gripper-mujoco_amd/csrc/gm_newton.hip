@@ -585,7 +585,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
   for (int k = 0; k < 21; k++) Ko[k] = 0;
 #pragma unroll
   for (int k = 0; k < 6; k++) Fo[k] = 0;
-  bool have_g = false;
+  bool have_g = false, have_o = false;
 #pragma unroll
   for (int s = 0; s < 2; s++) {
     const int pr = T->lane_opair[lane][s];
@@ -595,6 +595,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     const int c0 = S.pair_off[pr];
     int c1 = c0 + S.pair_cnt[pr];
     if (c1 > ncon) c1 = ncon;
+    have_o = have_o || c1 > c0;
     for (int c = c0; c < c1; c++) {
       const real* qf = S.nw.QF[c];
       const real pos[3] = {S.con[c][1], S.con[c][2], S.con[c][3]};
@@ -610,6 +611,9 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     }
   }
   const bool any_g = __ballot(have_g) != 0ull;
+  // no gripper body touches the object (wave-uniform): the gripper rows' composites are
+  // zero and their Hessian entries are H~'s own
+  const bool any_o = __ballot(have_o) != 0ull;
   PH(3);
   // the object's ground contacts (its other contacts reach it through the base composite)
   if (lane == T->lane_obj) {
@@ -643,12 +647,14 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     for (int k = 0; k < 6; k++) S.go[21 + k] = Fgo[k];
   }
   // ---- suffix sums along the chains (composite, like Ic)
+  if (any_o) {
 #pragma unroll
-  for (int off = 1; off < CL; off <<= 1) {
+    for (int off = 1; off < CL; off <<= 1) {
 #pragma unroll
-    for (int k = 0; k < 21; k++) Ko[k] += row_shl(Ko[k], off);
+      for (int k = 0; k < 21; k++) Ko[k] += row_shl(Ko[k], off);
 #pragma unroll
-    for (int k = 0; k < 6; k++) Fo[k] += row_shl(Fo[k], off);
+      for (int k = 0; k < 6; k++) Fo[k] += row_shl(Fo[k], off);
+    }
   }
   // ---- chain roots (fingers at position 1, the palm) to the stage (which sits after the
   // per-contact Q / F in the union: the ground pass below still reads them)
@@ -688,18 +694,30 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
   const real* cdb = S.cdof[T->dof_base];
   if (rowf < 3 && p >= 1 && p <= CL) {
     const int d = T->dof_f0[rowf] + p - 1;
-    real cd[6], y[6];
-#pragma unroll
-    for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
-    symK_mul(Ko, cd, y);
     const real* H = S.Hf[rowf];
+    if (any_o) {
+      real cd[6], y[6];
 #pragma unroll
-    for (int j = 1; j <= CL; j++)
-      if (j <= p) h[j] = H[TRI(p, j)] + dot6(S.cdof[T->dof_f0[rowf] + j - 1], y);
-    hb[0] = H[TRI(p, 0)] + dot6(cdb, y);
+      for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
+      symK_mul(Ko, cd, y);
 #pragma unroll
-    for (int k = 0; k < 6; k++) hb[1 + k] = -dot6(S.cdof[T->dof_obj + k], y);
-    rhs = S.frc[d] + dot6(cd, Fo);
+      for (int j = 1; j <= CL; j++)
+        if (j <= p) h[j] = H[TRI(p, j)] + dot6(S.cdof[T->dof_f0[rowf] + j - 1], y);
+      hb[0] = H[TRI(p, 0)] + dot6(cdb, y);
+#pragma unroll
+      for (int k = 0; k < 6; k++) hb[1 + k] = -dot6(S.cdof[T->dof_obj + k], y);
+      rhs = S.frc[d] + dot6(cd, Fo);
+    } else {
+#pragma unroll
+      for (int j = 1; j <= CL; j++)
+        if (j <= p) h[j] = H[TRI(p, j)];
+      hb[0] = H[TRI(p, 0)];
+      rhs = S.frc[d];
+    }
+  } else if (lane == GM_LANE_PALM_F && !any_o) {
+    h[1] = S.Hp[TRI(1, 1)];
+    hb[0] = S.Hp[TRI(1, 0)];
+    rhs = S.frc[T->dof_palm];
   } else if (lane == GM_LANE_PALM_F) {
     const int d = T->dof_palm;
     const real* st = S.st.root[3];
@@ -717,13 +735,16 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
   } else if (lane >= 48 && lane < 55) {
     const int i = lane - 48;
     const real* cp = S.st.comp;
-    real KBo[21], yob[6];
+    real yob[6] = {0, 0, 0, 0, 0, 0};
+    if (any_o) {
+      real KBo[21];
 #pragma unroll
-    for (int k = 0; k < 21; k++) KBo[k] = cp[k];
-    symK_mul(KBo, cdb, yob);
+      for (int k = 0; k < 21; k++) KBo[k] = cp[k];
+      symK_mul(KBo, cdb, yob);
+    }
     if (i == 0) {
-      hb[0] = S.Hbb + dot6(cdb, yob);
-      rhs = S.frc[T->dof_base] + dot6(cdb, cp + 42);
+      hb[0] = any_o ? S.Hbb + dot6(cdb, yob) : S.Hbb;
+      rhs = any_o ? S.frc[T->dof_base] + dot6(cdb, cp + 42) : S.frc[T->dof_base];
     } else {
       const int k = i - 1;
       const real* cok = S.cdof[T->dof_obj + k];

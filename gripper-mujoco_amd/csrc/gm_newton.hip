@@ -262,7 +262,9 @@ __device__ __forceinline__ real impedance(const gm_model* __restrict__ m, real r
 // base, the object's free joint (two vectors scan interleaved: one pass of latency)
 template <int CL, int NVEC>
 __device__ void body_vel(SharedT<CL>& S, const real* const* v, real (*const* V)[6], const gm_model* __restrict__ m,
-                         const GmTopo* __restrict__ T, int lane) {
+                         const GmTopo* __restrict__ T, int lane, bool obj_only = false) {
+  // obj_only (wave-uniform): every contact is the object on the ground, so only the
+  // object's velocity (and the world's zero) is read: the chain scans are skipped
   const int db = T->dof_base;
   const int grp = T->kl_grp[lane];
   const bool chain = grp >= 0 && grp <= 3;
@@ -279,19 +281,21 @@ __device__ void body_vel(SharedT<CL>& S, const real* const* v, real (*const* V)[
       s[n][k] = (chain ? S.cdof[d][k] : 0.0) * vd;
     }
   }
+  if (!obj_only) {
 #pragma unroll
-  for (int off = 1; off < CL; off <<= 1)
+    for (int off = 1; off < CL; off <<= 1)
 #pragma unroll
-    for (int n = 0; n < NVEC; n++)
+      for (int n = 0; n < NVEC; n++)
 #pragma unroll
-      for (int k = 0; k < 6; k++) s[n][k] += row_shr(s[n][k], off);
+        for (int k = 0; k < 6; k++) s[n][k] += row_shr(s[n][k], off);
+  }
   const int b = T->lane_body[lane];
-  if (chain) {
+  if (chain && !obj_only) {
 #pragma unroll
     for (int n = 0; n < NVEC; n++)
 #pragma unroll
       for (int k = 0; k < 6; k++) V[n][b][k] = s[n][k] + cvb[n][k];
-  } else if (lane == T->lane_base) {
+  } else if (lane == T->lane_base && !obj_only) {
 #pragma unroll
     for (int n = 0; n < NVEC; n++)
 #pragma unroll
@@ -436,7 +440,7 @@ struct RowsT {
 // tran + mu^2 tran, tran = the two bodies' invweight0), reference accelerations
 template <int CL, bool CAL>
 __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
-                                 int lane, RowsT& R, real* jq, real& jql) {
+                                 int lane, RowsT& R, real* jq, real& jql, bool& obj_only) {
   const real h = CAL ? S.s.dt : m->timestep;
   real tc = m->solref[0];
   if (tc < 2 * h) tc = 2 * h;
@@ -480,7 +484,13 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
   {
     const real* vv[2] = {S.s.qvel, S.s.qacc_warm};
     real (*VV[2])[6] = {S.nw2.V, S.nw2.V2};
-    body_vel<CL, 2>(S, vv, VV, m, T, lane);
+    bool og = true;
+    if (lane < S.ncon) {
+      const int b1 = S.cbody[lane][0], b2 = S.cbody[lane][1];
+      og = (b1 == 0 && b2 == T->body_obj) || (b2 == 0 && b1 == T->body_obj);
+    }
+    obj_only = __ballot(!og) == 0ull;
+    body_vel<CL, 2>(S, vv, VV, m, T, lane, obj_only);
   }
   jql = (lane < nl) ? S.s.qacc_warm[R.ldof] - R.laref : 0.0;
 #pragma unroll
@@ -514,12 +524,12 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
 
 // J v - aref for every row at the dof vector v (LDS); into jr (contact) / jl (lock)
 template <int CL>
-__device__ __forceinline__ void rows_jar(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
+__device__ __forceinline__ void rows_jar(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, bool obj_only,
                                          const real* v, int lane, const RowsT& R, real* jr, real& jl) {
   {
     const real* vv[1] = {v};
     real (*VV[1])[6] = {S.nw.V};
-    body_vel<CL, 1>(S, vv, VV, m, T, lane);
+    body_vel<CL, 1>(S, vv, VV, m, T, lane, obj_only);
   }
   jl = (lane < S.nl) ? v[R.ldof] - R.laref : 0.0;
   if (lane < S.ncon) {
@@ -1016,7 +1026,8 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
   unsigned long long t0 = prof ? clock64() : 0;
   RowsT R;
   real jq[4], jql;
-  constraint_setup<CL, CAL>(S, m, T, lane, R, jq, jql);
+  bool obj_only;
+  constraint_setup<CL, CAL>(S, m, T, lane, R, jq, jql, obj_only);
   PH(11);
   const int ncon = S.ncon, nl = S.nl, nv = T->nv;
   const bool clane = lane < ncon;
@@ -1032,7 +1043,7 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
     newton_point<CL>(S, m, T, lane, R, act, prof);
     if (prof) t0 = clock64();
     real jx[4], jxl;
-    rows_jar<CL>(S, m, T, S.xs, lane, R, jx, jxl);
+    rows_jar<CL>(S, m, T, obj_only, S.xs, lane, R, jx, jxl);
     bool differ = false;
 #pragma unroll
     for (int e = 0; e < 4; e++) differ = differ || (clane && ((jx[e] < 0) != act[e]));

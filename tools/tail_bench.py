@@ -51,20 +51,20 @@ dump = []
 for t in range(8):
     ph = drive(profiled=True).astype(np.float64)
     dump.append(ph.copy())   # all phase slots
-    c, nefc, mpr = ph[:, 23], ph[:, env.PH_NEFC], ph[:, env.PH_MPR]
+    c, nefc, mpr, nwt = ph[:, 23], ph[:, env.PH_NEFC], ph[:, env.PH_MPR], ph[:, env.PH_NEWTON]
     line = (f"step {t}: env cycles mean {c.mean():.3e} p90 {np.percentile(c, 90):.3e} "
             f"max {c.max():.3e}  ideal {c.sum() / slots:.3e}  in-order {makespan(c, range(n)):.3e}  "
             f"sorted-oracle {makespan(c, np.argsort(-c)):.3e}")
     if prev is not None:
-        pc, pn, pm = prev
-        X = np.stack([np.ones(n), pn, pm], axis=1)
+        pc, pn, pm, pw = prev
+        X = np.stack([np.ones(n), pn, pm, pw], axis=1)
         beta = np.linalg.lstsq(X, pc, rcond=None)[0]
         pred = X @ beta
         line += (f"  by-prev-cost {makespan(c, np.argsort(-pc)):.3e} (corr {np.corrcoef(pc, c)[0, 1]:.3f})"
                  f"  by-work-model {makespan(c, np.argsort(-pred)):.3e} (corr {np.corrcoef(pred, c)[0, 1]:.3f},"
-                 f" beta {beta[0]:.3g} {beta[1]:.3g} {beta[2]:.3g})")
+                 f" beta {beta[0]:.3g} {beta[1]:.3g} {beta[2]:.3g} {beta[3]:.3g})")
     print(line, flush=True)
-    prev = (c, nefc, mpr)
+    prev = (c, nefc, mpr, nwt)
 
 if len(sys.argv) > 3:
     np.save(sys.argv[3], np.stack(dump))   # [step, env, (phases 0-7, total, nefc sum, mpr substeps)]

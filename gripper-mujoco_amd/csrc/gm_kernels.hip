@@ -2288,8 +2288,8 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
     // next launch closer to its true costs than either alone (LPT makespan 1.17 vs 1.21
     // of the ideal on recorded costs)
     const uint32_t now = (uint32_t)((__builtin_amdgcn_s_memtime() - t_start) >> 6);
-    const uint32_t model = 92000u + 25u * (uint32_t)S.work_nefc + 300u * (uint32_t)S.work_mpr +
-                           400u * (uint32_t)S.work_newton;
+    const uint32_t model = 14000u + 19u * (uint32_t)S.work_nefc + 188u * (uint32_t)S.work_mpr +
+                           940u * (uint32_t)S.work_newton;
     cost[env] = (now >> 1) + (model >> 1);
   }
   store_state(S, states + env, lane);

@@ -111,7 +111,7 @@ struct __align__(16) SharedT {
 };
 
 // per-phase shader-clock accounting (gm_step_profiled); needs `prof`, `lane`, `t0` in scope
-#define PH(k) do { if (prof) { unsigned long long t_ = clock64(); if (lane == 0) S.tph[k] += t_ - t0; t0 = t_; } } while (0)
+#define PH(k) do { if (__builtin_expect(prof, 0)) { unsigned long long t_ = clock64(); if (lane == 0) S.tph[k] += t_ - t0; t0 = t_; } } while (0)
 
 // ------------------------------------------------------------ small math
 // Correctly rounded fp64 sqrt, reciprocal and quotient on the compiler's own expansions

@@ -771,7 +771,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
   }
   // ---- contacts of gripper bodies with the ground (wave-uniform, rare): their composite
   // Kg is added to the chain rows' and the base's entries (the object rows do not see it)
-  if (any_g) {
+  if (__builtin_expect(any_g, 0)) {   // cold: keep it out of the hot code's cache lines
     real Kg[21], Fg[6];
 #pragma unroll
     for (int k = 0; k < 21; k++) Kg[k] = 0;
@@ -1047,7 +1047,7 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
     bool differ = false;
 #pragma unroll
     for (int e = 0; e < 4; e++) differ = differ || (clane && ((jx[e] < 0) != act[e]));
-    if (__ballot(differ) == 0ull) {
+    if (__builtin_expect(__ballot(differ) == 0ull, 1)) {
       if (lane < nv) S.qacc[lane] = S.xs[lane];
 #pragma unroll
       for (int e = 0; e < 4; e++) jq[e] = jx[e];

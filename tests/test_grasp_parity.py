@@ -223,3 +223,19 @@ def test_c3_newton_matches_converged_pgs_4096(gm, ol):
     assert bad.size == 0, (bad[:8], rel.max(), ab.max())
     np.testing.assert_array_equal(sn["done"].astype(np.uint8), done_p)
     env.close()
+
+
+@pytest.mark.parametrize("n_seg", [5, 6])
+def test_short_fingers_256(gm, ol, n_seg):
+    """N = 5, 6 segments (CL = 7, 8 builds of the step kernel) on grasp states at the
+    timestep the reference's search gives them, same bounds as the canonical batch."""
+    import ctypes as C
+    p = gm.ModelParams()
+    gm.load_library().gm_default_model_params(C.byref(p))
+    p.n_seg, p.timestep = n_seg, {5: 6.76e-3, 6: 4.94e-3}[n_seg]
+    env, snaps = rollout(gm, 256, "set6_synthetic", 40 + n_seg, steps=41, snaps=(20, 40), model_params=p)
+    assert env.model.nv == 3 * (n_seg + 2) + 8
+    rep = [compare_step(gm, ol, env, sn) for sn in snaps]
+    sub = [compare_substep(gm, ol, env, sn) for sn in snaps]
+    print(f"N={n_seg}", rep, sub)
+    env.close()

@@ -1103,17 +1103,16 @@ __device__ __forceinline__ void canon_pair(int a, int b, int ta, int tb, int& g1
   if (ta > tb || (ta == tb && a > b)) { g1 = b; g2 = a; } else { g1 = a; g2 = b; }
 }
 
+// pass 2 stores the hit (depth, point, normal), friction and the geom/body ids; the contact
+// frame's tangent and the zeroed tail are filled by collision()'s lane-per-contact epilogue
 template <int CL>
-__device__ void write_contact(SharedT<CL>& S, int slot, int g1, int g2, int b1, int b2, const Hit& h, real mu) {
+__device__ __forceinline__ void write_contact(SharedT<CL>& S, int slot, int g1, int g2, int b1, int b2, const Hit& h,
+                                              real mu) {
   real* C = S.con[slot];
   C[0] = h.dist;
   C[1] = h.pos[0]; C[2] = h.pos[1]; C[3] = h.pos[2];
-  real F[9];
-  make_frame(F, h.n);
-  C[4] = F[0]; C[5] = F[1]; C[6] = F[2];
-  C[7] = F[3]; C[8] = F[4]; C[9] = F[5];
+  C[4] = h.n[0]; C[5] = h.n[1]; C[6] = h.n[2];
   C[10] = mu;
-  C[11] = 0; C[12] = 0; C[13] = 0;
   S.cgeom[slot][0] = (int16_t)g1; S.cgeom[slot][1] = (int16_t)g2;
   S.cbody[slot][0] = (int16_t)b1; S.cbody[slot][1] = (int16_t)b2;
 }
@@ -1263,8 +1262,21 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
       if (prof) S.tph[29] += 1;
     }
   }
+  // contact frames, one contact per lane (GM_MAX_CON <= 64): the normal and a tangent, as
+  // make_frame builds them; the rest of the frame is implied by the two
+  static_assert(GM_MAX_CON <= NT, "contact frames: one lane per contact");
+  const int ncon = written < GM_MAX_CON ? written : GM_MAX_CON;
+  __syncthreads();
+  if (lane < ncon) {
+    real* C = S.con[lane];
+    const real n[3] = {C[4], C[5], C[6]};
+    real F[9];
+    make_frame(F, n);
+    C[7] = F[3]; C[8] = F[4]; C[9] = F[5];
+    C[11] = 0; C[12] = 0; C[13] = 0;
+  }
   if (lane == 0) {
-    S.ncon = written < GM_MAX_CON ? written : GM_MAX_CON;
+    S.ncon = ncon;
     S.overflow = written > GM_MAX_CON;
   }
   __syncthreads();

@@ -252,8 +252,12 @@ __device__ __forceinline__ real impedance(const gm_model* __restrict__ m, real r
   real y;
   if (pw == 1) y = x;
   else if (pw == 2) y = (x <= mid) ? div_n(x * x, mid) : 1 - div_n((1 - x) * (1 - x), 1 - mid);   // MuJoCo's default power
-  else if (x <= mid) y = pow(x, pw) / pow(mid, pw - 1);
-  else y = 1 - pow(1 - x, pw) / pow(1 - mid, pw - 1);
+  else {
+    // general power (cold): one pow pair serves both halves of the sigmoid
+    const bool lo = x <= mid;
+    const real t = pow(lo ? x : 1 - x, pw) / pow(lo ? mid : 1 - mid, pw - 1);
+    y = lo ? t : 1 - t;
+  }
   return dmin + y * (dmax - dmin);
 }
 
@@ -462,7 +466,7 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
     // regulariser, summed: D = sum D_r a_r^2, D aref = sum D_r a_r aref_r
     const real tran = T->lock_tran[k];
     real De = 0.0, Dar = 0.0;
-#pragma unroll
+#pragma unroll 1   // one inlined impedance, not three
     for (int r = 0; r < 3; r++) {
       const real a = S.cdof[d][3 + r];
       if (a == 0.0) continue;

@@ -41,7 +41,7 @@ hipError_t gm_cal_launch_step(int n_seg, int n_envs, hipStream_t st, GmEnvState*
   case N:                                                                                                  \
     hipLaunchKernelGGL((gm_step_kernel<N + 2, true>), dim3(n_envs), dim3(NT), 0, st, states, m, C, T,      \
                        (float*)nullptr, (float*)nullptr, (uint8_t*)nullptr, n_envs, 3, dbg,                \
-                       (const int32_t*)nullptr, (uint32_t*)nullptr);                                       \
+                       (const int32_t*)nullptr, (uint32_t*)nullptr, GmChunkQ{});                           \
     return hipGetLastError();
     GM_NSEG_LIST
 #undef X

@@ -7,7 +7,9 @@
 // leave a message for gm_last_error().
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstddef>
+#include <cstdlib>
 #include <cstdio>
 #include <cmath>
 #include <cstring>
@@ -55,6 +57,12 @@ struct gm_ctx {
   gm_spawn* d_spawn = nullptr;
   int32_t* d_order = nullptr;          // workgroup -> env dispatch order (cost-sorted)
   uint32_t* d_cost = nullptr;          // per-env cost of the last env-step (clocks / 64)
+  // chunked env-step (gm_step_chunked_kernel): queue counters, per-XCD continuation rings,
+  // per-env carry; chunk = substeps per chunk (0: the one-shot kernel)
+  uint32_t* d_chunk_ctr = nullptr;
+  uint64_t* d_chunk_ring = nullptr;
+  GmChunkCarry* d_chunk_carry = nullptr;
+  int chunk = 0, chunk_grid = 0, chunk_cap = 0, chunk_margin = 25, chunk_yields = 1;
   gm_spawn_params* d_scene = nullptr;  // gm_set_scene_spawn parameters (NULL: plain spawn_object)
   int scene_tries = 0;
   GmSpawnRand spawn_rand{};            // gm_set_random_spawn (enable = 0: spawn tables)
@@ -87,12 +95,18 @@ hipError_t launch_step(gm_ctx* c, int grid, int n_envs, int mode, DebugOut dbg) 
   // the full env-step (mode 0) runs in cost-sorted order and records each env's cost
   const int32_t* order = (mode == 0 && grid == c->n_envs) ? c->d_order : nullptr;
   uint32_t* cost = (mode == 0 && grid == c->n_envs) ? c->d_cost : nullptr;
+  // the chunked work queue (gm_kernels.hip chunked_env_steps): one workgroup per resident
+  // wave slot, each pulling env chunks until every env has finished
+  const bool chunked = order && c->chunk > 0 && c->chunk_grid > 0 && dbg.phase == nullptr;
+  const GmChunkQ q{c->d_chunk_ctr, c->d_chunk_ring, c->d_chunk_carry, c->chunk_cap, chunked ? c->chunk : 0,
+                   c->chunk_margin, c->chunk_yields};
+  if (chunked) grid = c->chunk_grid;
   switch (c->model.n_seg) {
 #define X(N)                                                                                               \
   case N:                                                                                                  \
     hipLaunchKernelGGL((gm_step_kernel<N + 2, false>), dim3(grid), dim3(NT), 0, c->stream, c->d_state,      \
                        c->d_model, c->d_cfg, c->d_topo, c->d_obs, c->d_rew, c->d_done, n_envs, mode, dbg,    \
-                       order, cost);                                                                         \
+                       order, cost, q);                                                                      \
     return hipGetLastError();
     GM_NSEG_LIST
 #undef X
@@ -316,7 +330,34 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   HIPCHK(c, hipMalloc(&c->d_order, sizeof(int32_t) * (size_t)n_envs));
   HIPCHK(c, hipMalloc(&c->d_cost, sizeof(uint32_t) * (size_t)n_envs));
   HIPCHK(c, hipMemsetAsync(c->d_cost, 0, sizeof(uint32_t) * (size_t)n_envs, c->stream));
-  hipLaunchKernelGGL(gm_dispatch_order_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_cost, c->d_order, n_envs);
+  {
+    // chunked env-step: as many workgroups as wave slots are resident (occupancy query),
+    // GM_CHUNK_SUBSTEPS substeps per chunk (default 8; 0 selects the one-shot kernel)
+    const char* ev = std::getenv("GM_CHUNK_SUBSTEPS");
+    c->chunk = ev ? std::atoi(ev) : 8;
+    if (const char* e2 = std::getenv("GM_CHUNK_MARGIN")) c->chunk_margin = std::atoi(e2);
+    if (const char* e3 = std::getenv("GM_CHUNK_YIELDS")) c->chunk_yields = std::atoi(e3);
+    int per_cu = 0, n_cu = 0;
+    switch (c->model.n_seg) {
+#define X(N)                                                                                              \
+  case N:                                                                                                 \
+    HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gm_step_kernel<N + 2, false>, NT, 0)); \
+    break;
+      GM_NSEG_LIST
+#undef X
+      default: break;
+    }
+    HIPCHK(c, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
+    c->chunk_grid = std::min(n_envs, per_cu * n_cu);
+    c->chunk_cap = n_envs + c->chunk_grid;
+    HIPCHK(c, hipMalloc(&c->d_chunk_ctr, sizeof(uint32_t) * GM_CQ_ALLOC));
+    HIPCHK(c, hipMemsetAsync(c->d_chunk_ctr, 0, sizeof(uint32_t) * GM_CQ_ALLOC, c->stream));
+    HIPCHK(c, hipMalloc(&c->d_chunk_ring, sizeof(uint64_t) * 8 * (size_t)c->chunk_cap));
+    HIPCHK(c, hipMalloc(&c->d_chunk_carry, sizeof(GmChunkCarry) * (size_t)n_envs));
+    HIPCHK(c, hipMemsetAsync(c->d_chunk_ring, 0, sizeof(uint64_t) * 8 * (size_t)c->chunk_cap, c->stream));
+  }
+  hipLaunchKernelGGL(gm_dispatch_order_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_cost, c->d_order, n_envs,
+                     c->d_chunk_ctr);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemsetAsync(c->d_state, 0, sizeof(GmEnvState) * (size_t)n_envs, c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_obs, 0, sizeof(float) * (size_t)n_envs * (cfg->n_obs > 0 ? cfg->n_obs : 1), c->stream));
@@ -347,6 +388,7 @@ void gm_destroy(gm_ctx* c) {
   (void)hipFree(c->d_eq); (void)hipFree(c->d_obs); (void)hipFree(c->d_rew); (void)hipFree(c->d_done); (void)hipFree(c->d_act);
   (void)hipFree(c->d_dact); (void)hipFree(c->d_mask); (void)hipFree(c->d_spawn);
   (void)hipFree(c->d_order); (void)hipFree(c->d_cost); (void)hipFree(c->d_scene);
+  (void)hipFree(c->d_chunk_ctr); (void)hipFree(c->d_chunk_ring); (void)hipFree(c->d_chunk_carry);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -686,9 +728,22 @@ int gm_step(gm_ctx* c) {
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   HIPCHK(c, launch_step(c, c->n_envs, c->n_envs, 0, dbg));
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-  hipLaunchKernelGGL(gm_dispatch_order_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_cost, c->d_order, c->n_envs);
+  hipLaunchKernelGGL(gm_dispatch_order_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_cost, c->d_order, c->n_envs,
+                     c->d_chunk_ctr);
   HIPCHK(c, hipGetLastError());
   c->timed = true;
+  return GM_OK;
+}
+
+int gm_chunk_stats(gm_ctx* c, uint32_t* out) {
+  if (!c || !out) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  uint32_t w[36];
+  HIPCHK(c, hipMemcpyAsync(w, c->d_chunk_ctr + 320, sizeof(w), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  out[0] = std::min<uint32_t>(w[0], (uint32_t)c->n_envs);
+  out[1] = w[32]; out[2] = w[33]; out[3] = w[34];
+  out[4] = (uint32_t)c->chunk; out[5] = (uint32_t)c->chunk_grid;
   return GM_OK;
 }
 

@@ -106,6 +106,8 @@ struct __align__(16) SharedT {
   float forces[32];            // extract_forces_faster results (see extract_forces)
   int32_t have_forces;
   float gauge_tmp[3];
+  int32_t bend_ready;             // monitor_sensors: the bending gauges read this substep
+  double next_read;               // substep_loop: sim time after which a sensor becomes ready
   unsigned long long tph[GM_NPHASE];
   GmEnvState* gs;                 // the env's record in HBM (sensor windows read / written there)
 };
@@ -1703,9 +1705,11 @@ __device__ void object_net_wrench(SharedT<CL>& S, const GmTopo* __restrict__ T, 
 template <int CL>
 GM_EPI_ATTR void monitor_sensors(SharedT<CL>& S, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
                                 const GmTopo* __restrict__ T, int lane) {
-  __shared__ int bend_ready;
-  if (lane == 0) bend_ready = s_ready(S.s, C->s.bending_gauge, SL_BEND);
+  // (per-env LDS fields, no function-scope __shared__: substep_loop and monitor_sensors are
+  // reached from two kernels, and such variables would cost a per-kernel offset lookup)
+  if (lane == 0) S.bend_ready = s_ready(S.s, C->s.bending_gauge, SL_BEND);
   __syncthreads();
+  const int bend_ready = S.bend_ready;
   if (bend_ready && lane < 3) S.gauge_tmp[lane] = gauge_reading<CL - 2>(m, &S.s.qpos[T->dof_f0[lane] + 2]);
   __syncthreads();
   if (lane == 0) {
@@ -1807,10 +1811,26 @@ __device__ __noinline__ void monitor_call(GM_AS_LDS SharedT<CL>* S_, const GM_AS
   monitor_sensors<CL>(*(SharedT<CL>*)S_, (const gm_model*)uniform_const_ptr(m_), (const gm_config*)uniform_const_ptr(C_),
                       (const GmTopo*)uniform_const_ptr(T_), lane);
 }
+// Preemption test of the chunked env-step (chunked_env_steps): every `every` substeps the
+// loop yields when the predicted work left in this env, own * left / total (the env's last
+// dispatch cost, shader clocks / 64, spread evenly over its substeps), has dropped below the
+// next unstarted env's cost -- longest-remaining-work-first at substep granularity.
+struct GmPreempt {
+  const uint32_t* fresh_head;   // the queue's next-unstarted index (agent-scope loads)
+  const int32_t* order;
+  const uint32_t* cost;
+  uint32_t n, own;
+  int left, total, every;       // every = 0: never yield
+  int margin;                   // percent
+};
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// returns the substeps run (nsub unless the preemption test yielded)
 template <int CL, bool CAL>
-__device__ __noinline__ void substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS_GLOBAL gm_model* m_,
-                                          const GM_AS_GLOBAL GmTopo* T_, const GM_AS_GLOBAL gm_config* C_, int lane_in,
-                                          bool prof_in, int nsub_in, bool settle_in) {
+__device__ __noinline__ int substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS_GLOBAL gm_model* m_,
+                                         const GM_AS_GLOBAL GmTopo* T_, const GM_AS_GLOBAL gm_config* C_, int lane_in,
+                                         bool prof_in, int nsub_in, bool settle_in, GmPreempt pre) {
   // nothing but scalars is carried across the loop body: the loop bounds and flags are
   // wave-uniform (SGPRs), the lane id is recomputed, the next sensor-read time lives in LDS
   SharedT<CL>& S = *(SharedT<CL>*)S_;
@@ -1821,11 +1841,24 @@ __device__ __noinline__ void substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS
   const bool prof = __builtin_amdgcn_readfirstlane((int)prof_in) != 0;
   const bool settle = __builtin_amdgcn_readfirstlane((int)settle_in) != 0;
   (void)lane_in;
-  __shared__ double next_read;
-  if (__lane_id() == 0) next_read = (settle || CAL) ? 0.0 : next_sensor_read(S.s, C->s);
+  const int every = CAL ? 0 : __builtin_amdgcn_readfirstlane(pre.every);
+  if (__lane_id() == 0) S.next_read = (settle || CAL) ? 0.0 : next_sensor_read(S.s, C->s);
   __syncthreads();
+  int i = 0;
 #pragma nounroll
-  for (int i = 0; i < nsub; i++) {
+  for (; i < nsub; i++) {
+    if (every > 0 && i > 0 && i % every == 0) {
+      const uint32_t fh = __builtin_amdgcn_readfirstlane(ld_agent(pre.fresh_head));
+      const uint32_t n = __builtin_amdgcn_readfirstlane(pre.n);
+      if (fh < n) {
+        const uint32_t next = __builtin_amdgcn_readfirstlane(pre.cost[pre.order[fh]]);
+        const uint64_t left = (uint64_t)__builtin_amdgcn_readfirstlane(pre.own) *
+                              (uint64_t)(__builtin_amdgcn_readfirstlane(pre.left) - i);
+        // (with a margin: a yield costs a state hand-off)
+        if (left * (uint64_t)(100 + __builtin_amdgcn_readfirstlane(pre.margin)) <
+            (uint64_t)next * (uint64_t)__builtin_amdgcn_readfirstlane(pre.total) * 100u) break;
+      }
+    }
     // opaque per iteration: nothing derived from the lane id or the model / topology
     // pointers is hoisted out of the loop and held live across the whole body
     int lane;
@@ -1849,15 +1882,16 @@ __device__ __noinline__ void substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS
     update_all_call<CL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)(uintptr_t)m,
                         (const GM_AS_GLOBAL GmTopo*)(uintptr_t)T, __lane_id());
     PH(9);
-    if (!settle && !CAL && S.s.time > next_read) {
+    if (!settle && !CAL && S.s.time > S.next_read) {
       monitor_call<CL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)(uintptr_t)m,
                        (const GM_AS_GLOBAL gm_config*)(uintptr_t)C, (const GM_AS_GLOBAL GmTopo*)(uintptr_t)T, __lane_id());
-      if (__lane_id() == 0) next_read = next_sensor_read(S.s, C->s);
+      if (__lane_id() == 0) S.next_read = next_sensor_read(S.s, C->s);
       __syncthreads();
     }
     PH(10);
     if (CAL && S.s.badqacc) break;
   }
+  return i;
 }
 
 // ============================================================ env-step epilogue (lane 0)
@@ -2191,6 +2225,37 @@ __device__ float reward(GmEnvHot& s, const gm_config* __restrict__ C) {
 }
 
 // ============================================================ kernels
+// action_step's tail after the substeps: sense_gripper_state, update_env, the observation,
+// is_done and reward (mjclass.cpp:1483-1508, MjEnv.py:2170-2220)
+template <int CL>
+__device__ __forceinline__ void env_step_epilogue(SharedT<CL>& S, const gm_model* __restrict__ m,
+                                                  const gm_config* __restrict__ C, const GmTopo* __restrict__ T,
+                                                  float* __restrict__ obs, float* __restrict__ rew,
+                                                  uint8_t* __restrict__ done, int env, int lane, bool prof,
+                                                  unsigned long long& t0) {
+  if (lane == 0) {
+    S.s.extra_substeps = 0;
+    S.s.overflow = S.overflow;
+    sense_gripper_state(S, m, C);
+    PH(18);
+    update_env(S, m, C, T);
+    PH(19);
+    S.s.num_action_steps += 1;
+  }
+  __syncthreads();   // lane 0's window appends (HBM) and indices (LDS) before the samplers
+  get_obs_lanes(S.s, S.gs->ring, C, obs + (size_t)env * C->n_obs, lane);
+  PH(20);
+  if (lane == 0) {
+    int d = is_done(S.s, C);
+    float r = reward(S.s, C);
+    S.s.done = d;
+    S.s.reward = r;
+    rew[env] = r;
+    done[env] = (uint8_t)d;
+    PH(21);
+  }
+}
+
 template <int CL>
 __device__ __forceinline__ void load_state(SharedT<CL>& S, GmEnvState* __restrict__ g, int lane) {
   const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
@@ -2207,6 +2272,177 @@ __device__ __forceinline__ void store_state(const SharedT<CL>& S, GmEnvState* __
   for (int i = lane; i < GM_HOT_WORDS; i += NT) dst[i] = src[i];
 }
 
+// ---------------------------------------------------------------- chunked env-step
+// gm_step as a persistent work queue over env CHUNKS of a few substeps (DESIGN.md §5,
+// "Chunked dispatch").  One env-step is ~2.9 ms on a wave; with 4096 envs on 2048 resident
+// waves, whole env-steps leave the chip partly idle for the last third of the launch (the
+// last env starts ~5 ms in).  Here a wave runs one chunk of an env, stores the env's hot
+// state and hands the env on; any wave of the same XCD continues it.  Results are
+// bit-identical to the one-shot kernel: the substeps, their order and the epilogue are the
+// same code on the same state.
+//
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): an env's chunks all run on
+// the XCD that started it (each XCD has its own continuation ring, a wave serves the ring of
+// the XCD it runs on, read from HW_REG_XCC_ID), so the L2 is shared between producer and
+// consumer.  Producer: plain stores of the state and carry, s_waitcnt vmcnt(0), then the
+// ring entry by an agent-scope (sc1) store.  Consumer: sc1 poll of the entry, agent-scope
+// acquire (invalidates its CU's L1) and its wait, then plain loads.
+struct GmChunkCarry {        // what a chunk hands the next besides the hot state
+  int32_t sub_done, nsub;
+  int32_t work_nefc, work_mpr, work_newton, stp_fixed;
+  uint32_t clk;              // s_memtime / 64 summed over this env-step's chunks
+  int32_t yielded;           // yields so far this env-step (at most GmChunkQ::max_yields)
+};
+// counters (zeroed by gm_dispatch_order_kernel before every launch), one 128-B line each:
+// [x * 32 + 0] ring head of XCD x, [x * 32 + 1] its tail; [256] fresh head, [288] envs done,
+// [289] yields, [290] resumes; [320 ..] the previous launch's [256 .. 291] (diagnostics)
+#define GM_CQ_WORDS (10 * 32)
+#define GM_CQ_ALLOC (11 * 32)
+struct GmChunkQ {
+  uint32_t* ctr;             // GM_CQ_ALLOC words
+  uint64_t* ring;            // [8][cap] (predicted work left << 32) | (env + 1), 0 = empty
+  GmChunkCarry* carry;       // [n_envs]
+  int cap;                   // ring slots per XCD: n_envs + launched waves
+  int chunk;                 // substeps between preemption tests
+  int margin;                // yield when work left * (100 + margin) < next unstarted env's * 100
+  int max_yields;            // per env per env-step
+};
+__device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_agent64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t add_agent(uint32_t* p, uint32_t v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the persistent loop of gm_step_kernel's chunked mode (a mode of the one kernel, not a
+// kernel of its own: substep_loop keeps its single caller and so its constant LDS base)
+template <int CL>
+__device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __restrict__ states,
+                                                  const gm_model* __restrict__ m, const gm_config* __restrict__ C,
+                                                  const GmTopo* __restrict__ T, float* __restrict__ obs,
+                                                  float* __restrict__ rew, uint8_t* __restrict__ done, int n_envs,
+                                                  const int32_t* __restrict__ order, uint32_t* __restrict__ cost,
+                                                  const GmChunkQ& q, int lane) {
+  int xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  xcc &= 7;
+  uint32_t* head = q.ctr + xcc * 32;
+  uint32_t* tail = head + 1;
+  uint64_t* ring = q.ring + (size_t)xcc * q.cap;
+  uint32_t* fresh_head = q.ctr + 256;
+  uint32_t* n_done = q.ctr + 288;
+  const uint32_t n = (uint32_t)n_envs;
+  for (;;) {
+    // take work (lane 0): a continuation queued on this XCD first, else a fresh env in
+    // cost order; -1 once every env has finished its env-step
+    int pick = -1, fresh = 0;
+    if (lane == 0) {
+      for (;;) {
+        // a preempted env of this XCD (its predicted work left rides in the ring entry; an
+        // entry still in flight reads 0 and counts as large) against the next unstarted env
+        const uint32_t h = ld_agent(head), fh = ld_agent(fresh_head);
+        const bool have_c = h < ld_agent(tail), have_f = fh < n;
+        bool take_c = have_c;
+        if (have_c && have_f) {
+          const uint64_t e = ld_agent64(ring + h % (uint32_t)q.cap);
+          take_c = e == 0ull || (uint32_t)(e >> 32) >= cost[order[fh]];
+        }
+        if (take_c) {
+          const uint32_t i = add_agent(head, 1u) % (uint32_t)q.cap;
+          uint64_t v;
+          while ((v = ld_agent64(ring + i)) == 0ull && ld_agent(n_done) < n) __builtin_amdgcn_s_sleep(2);
+          if (v == 0ull) break;            // everything finished while waiting
+          st_agent(ring + i, 0ull);
+          add_agent(q.ctr + 290, 1u);
+          pick = (int)(uint32_t)v - 1;
+          break;
+        }
+        if (have_f) {
+          const uint32_t i = add_agent(fresh_head, 1u);
+          if (i < n) { pick = order[i]; fresh = 1; break; }
+        }
+        if (ld_agent(n_done) >= n) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    pick = __builtin_amdgcn_readfirstlane(pick);
+    fresh = __builtin_amdgcn_readfirstlane(fresh);
+    if (pick < 0) break;
+    const int env = pick;
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+    if (!fresh) {
+      // the previous chunk's stores (another CU of this XCD) through this CU's L1
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    GmEnvState* g = states + env;
+    load_state(S, g, lane);
+    GmChunkCarry cr;
+    if (fresh) {
+      cr.sub_done = 0;
+      cr.nsub = C->sim_steps_per_action + S.s.extra_substeps;
+      cr.work_nefc = 0; cr.work_mpr = 0; cr.work_newton = 0; cr.stp_fixed = 0;
+      cr.clk = 0;
+      cr.yielded = 0;
+    } else {
+      // agent-scope loads: never served by a scalar cache that the acquire does not reach
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(q.carry + env);
+      uint32_t* dst = reinterpret_cast<uint32_t*>(&cr);
+#pragma unroll
+      for (int w = 0; w < (int)(sizeof(GmChunkCarry) / 4); w++) dst[w] = ld_agent(src + w);
+    }
+    if (lane == 0) {
+      S.work_nefc = cr.work_nefc; S.work_mpr = cr.work_mpr; S.work_newton = cr.work_newton;
+      S.stp_fixed = cr.stp_fixed;
+    }
+    __syncthreads();
+    // run to the end of the env-step unless an unstarted env has become the longer job
+    const int left = cr.nsub - cr.sub_done;
+    const uint32_t own = cost[env];
+    const GmPreempt pre{fresh_head, order, cost, n, own, left, cr.nsub,
+                        cr.yielded < q.max_yields ? q.chunk : 0, q.margin};
+    const int k = substep_loop<CL, false>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
+                                          (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
+                                          false, left, false, pre);
+    cr.sub_done += k;
+    if (cr.sub_done >= cr.nsub) {
+      unsigned long long t0 = 0;
+      env_step_epilogue(S, m, C, T, obs, rew, done, env, lane, false, t0);
+      if (cost && lane == 0) {
+        // the dispatch cost (see gm_step_kernel): clocks of this env-step's chunks, blended
+        // with the work model
+        const uint32_t now = cr.clk + (uint32_t)((__builtin_amdgcn_s_memtime() - t_start) >> 6);
+        const uint32_t model = 14000u + 19u * (uint32_t)S.work_nefc + 188u * (uint32_t)S.work_mpr +
+                               940u * (uint32_t)S.work_newton;
+        cost[env] = (now >> 1) + (model >> 1);
+      }
+      store_state(S, g, lane);
+      if (lane == 0) add_agent(n_done, 1u);
+    } else {
+      store_state(S, g, lane);
+      if (lane == 0) {
+        cr.work_nefc = S.work_nefc; cr.work_mpr = S.work_mpr; cr.work_newton = S.work_newton;
+        cr.stp_fixed = S.stp_fixed;
+        cr.yielded += 1;
+        cr.clk += (uint32_t)((__builtin_amdgcn_s_memtime() - t_start) >> 6);
+        q.carry[env] = cr;
+      }
+      // every lane's stores have reached the L2 before the env is handed on
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (lane == 0) {
+        const uint64_t rem = (uint64_t)own * (uint64_t)(cr.nsub - cr.sub_done) / (uint64_t)cr.nsub;
+        add_agent(q.ctr + 289, 1u);
+        const uint32_t t = add_agent(tail, 1u) % (uint32_t)q.cap;
+        st_agent(ring + t, ((rem > 0xFFFFFFFFull ? 0xFFFFFFFFull : rem) << 32) | ((uint64_t)env + 1u));
+      }
+    }
+    __syncthreads();   // LDS image reused by the next pick
+  }
+}
 // mode 0: action_step + obs/done/reward; mode 1: calibrate_reset settle (400 substeps,
 // no sensors); mode 2: one full substep with diagnostics
 template <int CL, bool CAL>
@@ -2214,9 +2450,15 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
     GmEnvState* __restrict__ states, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
     const GmTopo* __restrict__ T, float* __restrict__ obs, float* __restrict__ rew,
     uint8_t* __restrict__ done, int n_envs, int mode, DebugOut dbg, const int32_t* __restrict__ order,
-    uint32_t* __restrict__ cost) {
+    uint32_t* __restrict__ cost, GmChunkQ q) {
   __shared__ SharedT<CL> S;
   const int lane = threadIdx.x;
+  if constexpr (!CAL) {
+    if (q.chunk > 0) {   // chunked work queue (gm_step): the grid is the resident wave slots
+      chunked_env_steps<CL>(S, states, m, C, T, obs, rew, done, n_envs, order, cost, q, lane);
+      return;
+    }
+  }
   if ((int)blockIdx.x >= n_envs) return;
   // cost-sorted dispatch: workgroups start in blockIdx order, so the envs that were the
   // most expensive last env-step are started first (longest-processing-time list
@@ -2228,6 +2470,9 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
   const bool calib = CAL;                   // calibration run (mode 3): S.s.cal_steps substeps, no sensors
   const bool prof = !settle && dbg.phase != nullptr;
   if (prof && lane < GM_NPHASE) S.tph[lane] = 0;
+  // profiling timeline: start / end on the 100 MHz constant clock and the wave's CU, for
+  // the dispatch-occupancy analysis (tools/tail_bench.py)
+  if (prof && lane == 0) { S.tph[25] = __builtin_amdgcn_s_memrealtime(); S.tph[27] = __smid(); }
   if (lane == 0) { S.work_nefc = 0; S.work_mpr = 0; S.work_newton = 0; S.stp_fixed = 0; }
   const unsigned long long t_kernel = prof ? clock64() : 0;
   __syncthreads();
@@ -2235,7 +2480,7 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
   // a calibration run starts from a reset's mj_forward pose
   if (calib && lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
   substep_loop<CL, CAL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m, (const GM_AS_GLOBAL GmTopo*)T,
-                        (const GM_AS_GLOBAL gm_config*)C, lane, prof, nsub, settle);
+                        (const GM_AS_GLOBAL gm_config*)C, lane, prof, nsub, settle, GmPreempt{});
   if (settle || calib) {
     store_state(S, states + env, lane);
     return;
@@ -2266,29 +2511,12 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
     return;
   }
   unsigned long long t0 = prof ? clock64() : 0;
-  if (lane == 0) {
-    S.s.extra_substeps = 0;
-    S.s.overflow = S.overflow;
-    sense_gripper_state(S, m, C);
-    PH(18);
-    update_env(S, m, C, T);
-    PH(19);
-    S.s.num_action_steps += 1;
-  }
-  __syncthreads();   // lane 0's window appends (HBM) and indices (LDS) before the samplers
-  get_obs_lanes(S.s, S.gs->ring, C, obs + (size_t)env * C->n_obs, lane);
-  PH(20);
-  if (lane == 0) {
-    int d = is_done(S.s, C);
-    float r = reward(S.s, C);
-    S.s.done = d;
-    S.s.reward = r;
-    rew[env] = r;
-    done[env] = (uint8_t)d;
-    PH(21);
-  }
+  env_step_epilogue(S, m, C, T, obs, rew, done, env, lane, prof, t0);
   if (prof) {
-    if (lane == 0) S.tph[23] = clock64() - t_kernel;   // whole env-step on this wave
+    if (lane == 0) {
+      S.tph[23] = clock64() - t_kernel;   // whole env-step on this wave
+      S.tph[26] = __builtin_amdgcn_s_memrealtime();
+    }
     __syncthreads();
     if (lane < GM_NPHASE) dbg.phase[(size_t)env * GM_NPHASE + lane] = S.tph[lane];
   }
@@ -2307,16 +2535,21 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
   store_state(S, states + env, lane);
 }
 
+
 // Dispatch order for the next env-step: envs by descending cost of their last env-step
 // (shader clocks / 64, written by gm_step_kernel), bucketed into 256 cost classes.
 // One 1024-thread workgroup; the order only changes which env a workgroup slot runs
 // first, never any result.
 #ifndef GM_CAL_TU   // env-step translation unit only
 extern "C" __global__ __launch_bounds__(1024) void gm_dispatch_order_kernel(const uint32_t* __restrict__ cost,
-                                                                            int32_t* __restrict__ order, int n) {
+                                                                            int32_t* __restrict__ order, int n,
+                                                                            uint32_t* __restrict__ chunk_ctr) {
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t cmax;
   const int t = threadIdx.x;
+  if (chunk_ctr && t < 36) chunk_ctr[320 + t] = chunk_ctr[256 + t];   // last launch's, for diagnostics
+  __syncthreads();
+  if (chunk_ctr && t < GM_CQ_WORDS) chunk_ctr[t] = 0;   // the chunked launch's queue counters
   if (t < 256) cnt[t] = 0;
   if (t == 0) cmax = 1;
   __syncthreads();

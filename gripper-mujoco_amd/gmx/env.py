@@ -244,6 +244,12 @@ class BatchedGripperEnv:
         self._check(self.lib.gm_last_step_ms(self._ctx, C.byref(v)))
         return float(v.value)
 
+    def chunk_stats(self) -> dict:
+        """The last gm_step's chunked-dispatch counters (include/gripper_mi355x.h gm_chunk_stats)."""
+        v = (C.c_uint32 * 6)()
+        self._check(self.lib.gm_chunk_stats(self._ctx, v))
+        return dict(started=v[0], finished=v[1], yields=v[2], resumes=v[3], every=v[4], workgroups=v[5])
+
     # ------------------------------------------------------------ inspection
     def state(self):
         """fp64 qpos [n, nq], qvel [n, nv], time [n] (mjData's precision)."""
@@ -322,7 +328,7 @@ class BatchedGripperEnv:
               "newton_solve", "  n:H_assembly", "integrate", "update_all", "monitor_sensors",
               "  n:setup", "  n:warm_start", "  n:jar+line_search", "  n:factor", "  k:A_hinge", "  k:B_chains",
               "  crb:chains", "e:sense", "e:update_env", "e:get_obs", "e:done_reward", "substep_body", "env_step",
-              "  n:solve", "-", "-", "-")
+              "  n:solve", "t:start", "t:end", "cu")   # 25-27: timeline (100 MHz clock) and CU id, not clocks
     # counter columns past the clocks
     PH_NEFC, PH_MPR, PH_NEWTON, PH_LS = 28, 29, 30, 31
     N_PHASE = 32

@@ -21,7 +21,7 @@ TOP = [0, 1, 2, 5, 6, 8, 9, 10]
 allc = tot[TOP].sum()
 print(f"n={n} mean cycles per env-step (lane 0) total {allc:.3e}  per substep {allc/63:.3e}")
 for k, name in enumerate(env.PHASES):
-    if k in (22, 23):
+    if k in (22, 23, 25, 26, 27):
         continue
     if name == "-":
         continue

@@ -44,5 +44,6 @@ for t in range(steps):
 import hashlib  # noqa: E402
 st = env.env_states()
 digest = hashlib.sha1(np.ascontiguousarray(st).tobytes()).hexdigest()[:12]   # bit-identity across builds
+cs = env.chunk_stats() if hasattr(env, "chunk_stats") else {}
 print(f"N={N} n={n} lib={os.environ.get('GM_LIB', 'default')} kernel ms mean {np.mean(ms):.3f} min {np.min(ms):.3f}"
-      f" state sha1 {digest}", flush=True)
+      f" state sha1 {digest} yields {cs.get('yields', '-')} resumes {cs.get('resumes', '-')}", flush=True)

@@ -64,6 +64,22 @@ for t in range(8):
                  f"  by-work-model {makespan(c, np.argsort(-pred)):.3e} (corr {np.corrcoef(pred, c)[0, 1]:.3f},"
                  f" beta {beta[0]:.3g} {beta[1]:.3g} {beta[2]:.3g} {beta[3]:.3g})")
     print(line, flush=True)
+    # the launch's real timeline (100 MHz constant clock, start / end of every env's wave)
+    t0, t1 = ph[:, 25], ph[:, 26]
+    base = t0.min()
+    t0, t1 = (t0 - base) * 10e-9, (t1 - base) * 10e-9
+    span = t1.max()
+    busy = (t1 - t0).sum()
+    ev = np.concatenate([np.stack([t0, np.ones(n)], 1), np.stack([t1, -np.ones(n)], 1)])
+    ev = ev[np.argsort(ev[:, 0], kind="stable")]
+    conc = np.cumsum(ev[:, 1])
+    dt = np.diff(ev[:, 0], append=span)
+    full = dt[conc >= 0.95 * conc.max()].sum()
+    print(f"        timeline: span {span * 1e3:.3f} ms, wave-busy {busy / (conc.max() * span):.3f} of "
+          f"{int(conc.max())} peak-resident slots x span; >=95% resident for {full * 1e3:.3f} ms; "
+          f"shader clock {np.median(c / np.maximum(t1 - t0, 1e-9)) / 1e6:.0f} MHz; "
+          f"mean env {np.mean(t1 - t0) * 1e3:.3f} ms, max {np.max(t1 - t0) * 1e3:.3f} ms, "
+          f"last start {t0.max() * 1e3:.3f} ms", flush=True)
     prev = (c, nefc, mpr, nwt)
 
 if len(sys.argv) > 3:

@@ -62,7 +62,8 @@ struct gm_ctx {
   uint32_t* d_chunk_ctr = nullptr;
   uint64_t* d_chunk_ring = nullptr;
   GmChunkCarry* d_chunk_carry = nullptr;
-  int chunk = 0, chunk_grid = 0, chunk_cap = 0, chunk_margin = 25, chunk_yields = 1;
+  unsigned long long* d_chunk_st = nullptr;
+  int chunk = 0, chunk_grid = 0, chunk_cap = 0, chunk_margin = 100, chunk_yields = 6, chunk_cmargin = 100;
   gm_spawn_params* d_scene = nullptr;  // gm_set_scene_spawn parameters (NULL: plain spawn_object)
   int scene_tries = 0;
   GmSpawnRand spawn_rand{};            // gm_set_random_spawn (enable = 0: spawn tables)
@@ -99,7 +100,7 @@ hipError_t launch_step(gm_ctx* c, int grid, int n_envs, int mode, DebugOut dbg) 
   // wave slot, each pulling env chunks until every env has finished
   const bool chunked = order && c->chunk > 0 && c->chunk_grid > 0 && dbg.phase == nullptr;
   const GmChunkQ q{c->d_chunk_ctr, c->d_chunk_ring, c->d_chunk_carry, c->chunk_cap, chunked ? c->chunk : 0,
-                   c->chunk_margin, c->chunk_yields};
+                   c->chunk_margin, c->chunk_yields, c->chunk_cmargin, c->d_chunk_st};
   if (chunked) grid = c->chunk_grid;
   switch (c->model.n_seg) {
 #define X(N)                                                                                               \
@@ -337,6 +338,7 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
     c->chunk = ev ? std::atoi(ev) : 8;
     if (const char* e2 = std::getenv("GM_CHUNK_MARGIN")) c->chunk_margin = std::atoi(e2);
     if (const char* e3 = std::getenv("GM_CHUNK_YIELDS")) c->chunk_yields = std::atoi(e3);
+    if (const char* e4 = std::getenv("GM_CHUNK_CMARGIN")) c->chunk_cmargin = std::atoi(e4);
     int per_cu = 0, n_cu = 0;
     switch (c->model.n_seg) {
 #define X(N)                                                                                              \
@@ -352,12 +354,14 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
     c->chunk_cap = n_envs + c->chunk_grid;
     HIPCHK(c, hipMalloc(&c->d_chunk_ctr, sizeof(uint32_t) * GM_CQ_ALLOC));
     HIPCHK(c, hipMemsetAsync(c->d_chunk_ctr, 0, sizeof(uint32_t) * GM_CQ_ALLOC, c->stream));
-    HIPCHK(c, hipMalloc(&c->d_chunk_ring, sizeof(uint64_t) * 8 * (size_t)c->chunk_cap));
+    HIPCHK(c, hipMalloc(&c->d_chunk_st, sizeof(unsigned long long) * 16));
+    HIPCHK(c, hipMemsetAsync(c->d_chunk_st, 0, sizeof(unsigned long long) * 16, c->stream));
+    HIPCHK(c, hipMalloc(&c->d_chunk_ring, sizeof(uint64_t) * 8 * GM_CQ_NB * (size_t)c->chunk_cap));
     HIPCHK(c, hipMalloc(&c->d_chunk_carry, sizeof(GmChunkCarry) * (size_t)n_envs));
-    HIPCHK(c, hipMemsetAsync(c->d_chunk_ring, 0, sizeof(uint64_t) * 8 * (size_t)c->chunk_cap, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_chunk_ring, 0, sizeof(uint64_t) * 8 * GM_CQ_NB * (size_t)c->chunk_cap, c->stream));
   }
   hipLaunchKernelGGL(gm_dispatch_order_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_cost, c->d_order, n_envs,
-                     c->d_chunk_ctr);
+                     c->d_chunk_ctr, c->d_chunk_st);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemsetAsync(c->d_state, 0, sizeof(GmEnvState) * (size_t)n_envs, c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_obs, 0, sizeof(float) * (size_t)n_envs * (cfg->n_obs > 0 ? cfg->n_obs : 1), c->stream));
@@ -389,6 +393,7 @@ void gm_destroy(gm_ctx* c) {
   (void)hipFree(c->d_dact); (void)hipFree(c->d_mask); (void)hipFree(c->d_spawn);
   (void)hipFree(c->d_order); (void)hipFree(c->d_cost); (void)hipFree(c->d_scene);
   (void)hipFree(c->d_chunk_ctr); (void)hipFree(c->d_chunk_ring); (void)hipFree(c->d_chunk_carry);
+  (void)hipFree(c->d_chunk_st);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -729,17 +734,18 @@ int gm_step(gm_ctx* c) {
   HIPCHK(c, launch_step(c, c->n_envs, c->n_envs, 0, dbg));
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   hipLaunchKernelGGL(gm_dispatch_order_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_cost, c->d_order, c->n_envs,
-                     c->d_chunk_ctr);
+                     c->d_chunk_ctr, c->d_chunk_st);
   HIPCHK(c, hipGetLastError());
   c->timed = true;
   return GM_OK;
 }
 
-int gm_chunk_stats(gm_ctx* c, uint32_t* out) {
+int gm_chunk_stats(gm_ctx* c, uint32_t* out, uint64_t* times) {
   if (!c || !out) return GM_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   uint32_t w[36];
-  HIPCHK(c, hipMemcpyAsync(w, c->d_chunk_ctr + 320, sizeof(w), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(w, c->d_chunk_ctr + GM_CQ_LAST, sizeof(w), hipMemcpyDeviceToHost, c->stream));
+  if (times) HIPCHK(c, hipMemcpyAsync(times, c->d_chunk_st + 8, sizeof(uint64_t) * 5, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   out[0] = std::min<uint32_t>(w[0], (uint32_t)c->n_envs);
   out[1] = w[32]; out[2] = w[33]; out[3] = w[34];

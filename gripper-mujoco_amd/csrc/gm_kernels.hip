@@ -26,6 +26,7 @@
 #include "gm_math.h"
 
 #define NT 64
+#define GM_CQ_NB 16   // priority buckets per XCD of the chunked env-step (gm_step_kernel)
 // gm_step_kernel is instantiated per finger chain length (CL = n_seg + 2) so every chain
 // recursion is unrolled into registers; GM_NSEG_LIST is the set compiled in.
 #ifndef GM_NSEG_LIST
@@ -1822,6 +1823,11 @@ struct GmPreempt {
   uint32_t n, own;
   int left, total, every;       // every = 0: never yield
   int margin;                   // percent
+  // the XCD's yielded envs: a running env also yields to the best bucket when that bucket's
+  // lower edge (cmax * b / GM_CQ_NB) exceeds its own work left by cmargin percent (< 0: off)
+  const uint32_t* bq;
+  uint32_t cmax;
+  int cmargin;
 };
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1848,15 +1854,28 @@ __device__ __noinline__ int substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS_
 #pragma nounroll
   for (; i < nsub; i++) {
     if (every > 0 && i > 0 && i % every == 0) {
+      // work left in the units of the cost array, times pre.total
+      const uint64_t left = (uint64_t)__builtin_amdgcn_readfirstlane(pre.own) *
+                            (uint64_t)(__builtin_amdgcn_readfirstlane(pre.left) - i);
+      const uint64_t total = (uint64_t)__builtin_amdgcn_readfirstlane(pre.total);
       const uint32_t fh = __builtin_amdgcn_readfirstlane(ld_agent(pre.fresh_head));
       const uint32_t n = __builtin_amdgcn_readfirstlane(pre.n);
       if (fh < n) {
         const uint32_t next = __builtin_amdgcn_readfirstlane(pre.cost[pre.order[fh]]);
-        const uint64_t left = (uint64_t)__builtin_amdgcn_readfirstlane(pre.own) *
-                              (uint64_t)(__builtin_amdgcn_readfirstlane(pre.left) - i);
         // (with a margin: a yield costs a state hand-off)
-        if (left * (uint64_t)(100 + __builtin_amdgcn_readfirstlane(pre.margin)) <
-            (uint64_t)next * (uint64_t)__builtin_amdgcn_readfirstlane(pre.total) * 100u) break;
+        if (left * (uint64_t)(100 + __builtin_amdgcn_readfirstlane(pre.margin)) < (uint64_t)next * total * 100u) break;
+      }
+      const int cm = __builtin_amdgcn_readfirstlane(pre.cmargin);
+      if (cm >= 0) {
+        const int ln = __lane_id();
+        uint32_t hb = 0, tb = 0;
+        if (ln < GM_CQ_NB) { hb = ld_agent(pre.bq + ln * 32); tb = ld_agent(pre.bq + ln * 32 + 1); }
+        const unsigned long long ne = __ballot(ln < GM_CQ_NB && hb < tb);
+        if (ne) {
+          const uint64_t b = 63 - __builtin_clzll(ne);
+          const uint64_t lower = b * (uint64_t)__builtin_amdgcn_readfirstlane(pre.cmax) / GM_CQ_NB;
+          if (left * (uint64_t)(100 + cm) < lower * total * 100u) break;
+        }
       }
     }
     // opaque per iteration: nothing derived from the lane id or the model / topology
@@ -2281,9 +2300,15 @@ __device__ __forceinline__ void store_state(const SharedT<CL>& S, GmEnvState* __
 // bit-identical to the one-shot kernel: the substeps, their order and the epilogue are the
 // same code on the same state.
 //
+// Scheduling: envs start in descending predicted cost (the previous env-step's); a running
+// env yields (at most max_yields times per env-step) when an unstarted env has clearly more
+// work than it has left, and yielded envs wait in priority buckets by predicted work left;
+// a free wave takes the larger of the best bucket's head and the next unstarted env --
+// longest-remaining-work-first at substep granularity (tools/sim_dispatch.py).
+//
 // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): an env's chunks all run on
-// the XCD that started it (each XCD has its own continuation ring, a wave serves the ring of
-// the XCD it runs on, read from HW_REG_XCC_ID), so the L2 is shared between producer and
+// the XCD that started it (each XCD has its own continuation buckets, a wave serves those
+// of the XCD it runs on, read from HW_REG_XCC_ID), so the L2 is shared between producer and
 // consumer.  Producer: plain stores of the state and carry, s_waitcnt vmcnt(0), then the
 // ring entry by an agent-scope (sc1) store.  Consumer: sc1 poll of the entry, agent-scope
 // acquire (invalidates its CU's L1) and its wait, then plain loads.
@@ -2294,18 +2319,26 @@ struct GmChunkCarry {        // what a chunk hands the next besides the hot stat
   int32_t yielded;           // yields so far this env-step (at most GmChunkQ::max_yields)
 };
 // counters (zeroed by gm_dispatch_order_kernel before every launch), one 128-B line each:
-// [x * 32 + 0] ring head of XCD x, [x * 32 + 1] its tail; [256] fresh head, [288] envs done,
-// [289] yields, [290] resumes; [320 ..] the previous launch's [256 .. 291] (diagnostics)
-#define GM_CQ_WORDS (10 * 32)
-#define GM_CQ_ALLOC (11 * 32)
+// ring r = x * GM_CQ_NB + bucket: [r * 32] its head, [r * 32 + 1] its tail; GM_CQ_FRESH the
+// next unstarted env, GM_CQ_DONE envs finished, + 1 yields, + 2 resumes; GM_CQ_LAST the
+// previous launch's [GM_CQ_FRESH ..] (36 words, diagnostics)
+#define GM_CQ_FRESH (8 * GM_CQ_NB * 32)
+#define GM_CQ_DONE (GM_CQ_FRESH + 32)
+#define GM_CQ_WORDS (GM_CQ_FRESH + 64)
+#define GM_CQ_LAST GM_CQ_WORDS
+#define GM_CQ_ALLOC (GM_CQ_WORDS + 64)
 struct GmChunkQ {
   uint32_t* ctr;             // GM_CQ_ALLOC words
-  uint64_t* ring;            // [8][cap] (predicted work left << 32) | (env + 1), 0 = empty
+  uint64_t* ring;            // [8 * GM_CQ_NB][cap] (predicted work left << 32) | (env + 1), 0 = empty
   GmChunkCarry* carry;       // [n_envs]
   int cap;                   // ring slots per XCD: n_envs + launched waves
   int chunk;                 // substeps between preemption tests
   int margin;                // yield when work left * (100 + margin) < next unstarted env's * 100
   int max_yields;            // per env per env-step
+  int cmargin;               // yield to a yielded env with cmargin percent more work left (< 0: off)
+  unsigned long long* st;    // [0] first pick, [1] first pick that found no unstarted env,
+                             // [2] last env finished (100 MHz clock), [3] wave-busy, [4] wave
+                             // polling (sums, 100 MHz ticks); [8 ..] the previous launch's
 };
 __device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2329,48 +2362,72 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
   int xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
   xcc &= 7;
-  uint32_t* head = q.ctr + xcc * 32;
-  uint32_t* tail = head + 1;
-  uint64_t* ring = q.ring + (size_t)xcc * q.cap;
-  uint32_t* fresh_head = q.ctr + 256;
-  uint32_t* n_done = q.ctr + 288;
+  uint32_t* bq = q.ctr + xcc * GM_CQ_NB * 32;                    // this XCD's bucket counters
+  uint64_t* ring = q.ring + (size_t)xcc * GM_CQ_NB * q.cap;      // and rings
+  uint32_t* fresh_head = q.ctr + GM_CQ_FRESH;
+  uint32_t* n_done = q.ctr + GM_CQ_DONE;
   const uint32_t n = (uint32_t)n_envs;
+  const uint32_t cmax = cost[order[0]] + 1u;   // bucket scale: the heaviest env's cost
+  unsigned long long busy = 0, poll = 0;
+  bool first = true, saw_empty = false;
   for (;;) {
+    const unsigned long long tw = __builtin_amdgcn_s_memrealtime();
     // take work (lane 0): a continuation queued on this XCD first, else a fresh env in
     // cost order; -1 once every env has finished its env-step
     int pick = -1, fresh = 0;
-    if (lane == 0) {
-      for (;;) {
-        // a preempted env of this XCD (its predicted work left rides in the ring entry; an
-        // entry still in flight reads 0 and counts as large) against the next unstarted env
-        const uint32_t h = ld_agent(head), fh = ld_agent(fresh_head);
-        const bool have_c = h < ld_agent(tail), have_f = fh < n;
-        bool take_c = have_c;
-        if (have_c && have_f) {
-          const uint64_t e = ld_agent64(ring + h % (uint32_t)q.cap);
-          take_c = e == 0ull || (uint32_t)(e >> 32) >= cost[order[fh]];
-        }
-        if (take_c) {
-          const uint32_t i = add_agent(head, 1u) % (uint32_t)q.cap;
-          uint64_t v;
-          while ((v = ld_agent64(ring + i)) == 0ull && ld_agent(n_done) < n) __builtin_amdgcn_s_sleep(2);
-          if (v == 0ull) break;            // everything finished while waiting
-          st_agent(ring + i, 0ull);
-          add_agent(q.ctr + 290, 1u);
-          pick = (int)(uint32_t)v - 1;
-          break;
-        }
-        if (have_f) {
-          const uint32_t i = add_agent(fresh_head, 1u);
-          if (i < n) { pick = order[i]; fresh = 1; break; }
-        }
-        if (ld_agent(n_done) >= n) break;
-        __builtin_amdgcn_s_sleep(2);
+    for (;;) {
+      // bucket occupancy, one lane per bucket; the highest non-empty bucket is the best
+      // yielded env (its exact work left rides in the entry; an entry still in flight
+      // reads 0 and counts as large)
+      uint32_t hb = 0, tb = 0;
+      if (lane < GM_CQ_NB) { hb = ld_agent(bq + lane * 32); tb = ld_agent(bq + lane * 32 + 1); }
+      const unsigned long long ne = __ballot(lane < GM_CQ_NB && hb < tb);
+      const uint32_t fh = __builtin_amdgcn_readfirstlane(ld_agent(fresh_head));
+      const bool have_f = fh < n;
+      if (!have_f && !saw_empty) {
+        saw_empty = true;
+        if (lane == 0)
+          __hip_atomic_fetch_min(q.st + 1, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      const int bsel = ne ? 63 - __builtin_clzll(ne) : -1;
+      bool take_c = bsel >= 0;
+      if (take_c && have_f) {
+        const uint32_t h = __builtin_amdgcn_readlane(hb, bsel);
+        const uint64_t e = ld_agent64(ring + (size_t)bsel * q.cap + h % (uint32_t)q.cap);
+        take_c = e == 0ull || (uint32_t)(e >> 32) >= cost[order[fh]];
+      }
+      if (take_c) {
+        if (lane == 0) {
+          uint64_t* rb = ring + (size_t)bsel * q.cap;
+          const uint32_t i = add_agent(bq + bsel * 32, 1u) % (uint32_t)q.cap;
+          uint64_t v;
+          while ((v = ld_agent64(rb + i)) == 0ull && ld_agent(n_done) < n) __builtin_amdgcn_s_sleep(2);
+          if (v != 0ull) {
+            st_agent(rb + i, 0ull);
+            add_agent(q.ctr + GM_CQ_DONE + 2, 1u);
+            pick = (int)(uint32_t)v - 1;
+          }
+        }
+        break;                             // pick < 0: everything finished while waiting
+      }
+      if (have_f) {
+        if (lane == 0) {
+          const uint32_t i = add_agent(fresh_head, 1u);
+          if (i < n) { pick = order[i]; fresh = 1; }
+        }
+        if (__builtin_amdgcn_readfirstlane(pick) >= 0) break;
+      }
+      if (__builtin_amdgcn_readfirstlane(ld_agent(n_done)) >= n) break;
+      __builtin_amdgcn_s_sleep(2);
     }
     pick = __builtin_amdgcn_readfirstlane(pick);
     fresh = __builtin_amdgcn_readfirstlane(fresh);
+    const unsigned long long tp = __builtin_amdgcn_s_memrealtime();
+    poll += tp - tw;
     if (pick < 0) break;
+    if (first && lane == 0)
+      __hip_atomic_fetch_min(q.st, tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    first = false;
     const int env = pick;
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     if (!fresh) {
@@ -2403,7 +2460,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
     const int left = cr.nsub - cr.sub_done;
     const uint32_t own = cost[env];
     const GmPreempt pre{fresh_head, order, cost, n, own, left, cr.nsub,
-                        cr.yielded < q.max_yields ? q.chunk : 0, q.margin};
+                        cr.yielded < q.max_yields ? q.chunk : 0, q.margin, bq, cmax, q.cmargin};
     const int k = substep_loop<CL, false>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
                                           (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
                                           false, left, false, pre);
@@ -2420,7 +2477,11 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
         cost[env] = (now >> 1) + (model >> 1);
       }
       store_state(S, g, lane);
-      if (lane == 0) add_agent(n_done, 1u);
+      if (lane == 0) {
+        add_agent(n_done, 1u);
+        __hip_atomic_fetch_max(q.st + 2, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      }
     } else {
       store_state(S, g, lane);
       if (lane == 0) {
@@ -2435,12 +2496,18 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       __syncthreads();
       if (lane == 0) {
         const uint64_t rem = (uint64_t)own * (uint64_t)(cr.nsub - cr.sub_done) / (uint64_t)cr.nsub;
-        add_agent(q.ctr + 289, 1u);
-        const uint32_t t = add_agent(tail, 1u) % (uint32_t)q.cap;
-        st_agent(ring + t, ((rem > 0xFFFFFFFFull ? 0xFFFFFFFFull : rem) << 32) | ((uint64_t)env + 1u));
+        add_agent(q.ctr + GM_CQ_DONE + 1, 1u);
+        const uint32_t b = rem * GM_CQ_NB / cmax < GM_CQ_NB - 1 ? (uint32_t)(rem * GM_CQ_NB / cmax) : GM_CQ_NB - 1;
+        const uint32_t t = add_agent(bq + b * 32 + 1, 1u) % (uint32_t)q.cap;
+        st_agent(ring + (size_t)b * q.cap + t, ((rem > 0xFFFFFFFFull ? 0xFFFFFFFFull : rem) << 32) | ((uint64_t)env + 1u));
       }
     }
     __syncthreads();   // LDS image reused by the next pick
+    busy += __builtin_amdgcn_s_memrealtime() - tp;
+  }
+  if (lane == 0) {
+    __hip_atomic_fetch_add(q.st + 3, busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(q.st + 4, poll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 // mode 0: action_step + obs/done/reward; mode 1: calibrate_reset settle (400 substeps,
@@ -2543,13 +2610,19 @@ __global__ __launch_bounds__(NT, 2) void gm_step_kernel(
 #ifndef GM_CAL_TU   // env-step translation unit only
 extern "C" __global__ __launch_bounds__(1024) void gm_dispatch_order_kernel(const uint32_t* __restrict__ cost,
                                                                             int32_t* __restrict__ order, int n,
-                                                                            uint32_t* __restrict__ chunk_ctr) {
+                                                                            uint32_t* __restrict__ chunk_ctr,
+                                                                            unsigned long long* __restrict__ chunk_st) {
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t cmax;
   const int t = threadIdx.x;
-  if (chunk_ctr && t < 36) chunk_ctr[320 + t] = chunk_ctr[256 + t];   // last launch's, for diagnostics
+  if (chunk_ctr && t < 36) chunk_ctr[GM_CQ_LAST + t] = chunk_ctr[GM_CQ_FRESH + t];   // last launch's, for diagnostics
   __syncthreads();
-  if (chunk_ctr && t < GM_CQ_WORDS) chunk_ctr[t] = 0;   // the chunked launch's queue counters
+  if (chunk_ctr)
+    for (int w = t; w < GM_CQ_WORDS; w += 1024) chunk_ctr[w] = 0;   // the chunked launch's queue counters
+  if (chunk_st && t < 8) {
+    chunk_st[8 + t] = chunk_st[t];
+    chunk_st[t] = (t < 2) ? ~0ull : 0ull;
+  }
   if (t < 256) cnt[t] = 0;
   if (t == 0) cmax = 1;
   __syncthreads();

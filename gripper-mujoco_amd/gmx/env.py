@@ -247,8 +247,13 @@ class BatchedGripperEnv:
     def chunk_stats(self) -> dict:
         """The last gm_step's chunked-dispatch counters (include/gripper_mi355x.h gm_chunk_stats)."""
         v = (C.c_uint32 * 6)()
-        self._check(self.lib.gm_chunk_stats(self._ctx, v))
-        return dict(started=v[0], finished=v[1], yields=v[2], resumes=v[3], every=v[4], workgroups=v[5])
+        t = (C.c_uint64 * 5)()
+        self._check(self.lib.gm_chunk_stats(self._ctx, v, t))
+        span = (t[2] - t[0]) * 1e-5 if t[2] > t[0] else 0.0   # ms
+        return dict(started=v[0], finished=v[1], yields=v[2], resumes=v[3], every=v[4], workgroups=v[5],
+                    span_ms=span, fresh_empty_ms=(t[1] - t[0]) * 1e-5 if t[1] >= t[0] and span else 0.0,
+                    busy=(t[3] / (v[5] * (t[2] - t[0]))) if span and v[5] else 0.0,
+                    poll=(t[4] / (v[5] * (t[2] - t[0]))) if span and v[5] else 0.0)
 
     # ------------------------------------------------------------ inspection
     def state(self):

@@ -509,9 +509,11 @@ int  gm_last_step_ms(gm_ctx* ctx, float* ms);
 /* The last gm_step's work queue (chunked dispatch): out[0] envs started,
  * out[1] envs finished, out[2] yields (an env handed back to its XCD's queue because an
  * unstarted env had more work left), out[3] resumptions; out[4] substeps between
- * preemption tests (0: the one-shot kernel ran), out[5] resident workgroups.
+ * preemption tests (0: the one-shot kernel ran), out[5] resident workgroups.  times (may
+ * be NULL; 100 MHz constant-clock ticks): [0] first pick, [1] first pick that found no
+ * unstarted env, [2] last env finished, [3] sum of wave-busy time, [4] sum of wave polling.
  * Synchronises the context's stream. */
-int  gm_chunk_stats(gm_ctx* ctx, uint32_t* out6);
+int  gm_chunk_stats(gm_ctx* ctx, uint32_t* out6, uint64_t* times5);
 
 /* ---- single-substep stage hooks for parity testing (GPU vs oracle) ---- */
 /* Runs exactly one MjClass::step (mj_step1 + control + mj_step2 + mj_rnePostConstraint

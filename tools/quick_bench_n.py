@@ -46,4 +46,6 @@ st = env.env_states()
 digest = hashlib.sha1(np.ascontiguousarray(st).tobytes()).hexdigest()[:12]   # bit-identity across builds
 cs = env.chunk_stats() if hasattr(env, "chunk_stats") else {}
 print(f"N={N} n={n} lib={os.environ.get('GM_LIB', 'default')} kernel ms mean {np.mean(ms):.3f} min {np.min(ms):.3f}"
-      f" state sha1 {digest} yields {cs.get('yields', '-')} resumes {cs.get('resumes', '-')}", flush=True)
+      f" state sha1 {digest} yields {cs.get('yields', '-')} resumes {cs.get('resumes', '-')}"
+      f" span {cs.get('span_ms', 0):.3f} fresh-empty {cs.get('fresh_empty_ms', 0):.3f} busy {cs.get('busy', 0):.3f}"
+      f" poll {cs.get('poll', 0):.3f}", flush=True)

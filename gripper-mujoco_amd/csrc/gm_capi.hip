@@ -63,7 +63,7 @@ struct gm_ctx {
   uint64_t* d_chunk_ring = nullptr;
   GmChunkCarry* d_chunk_carry = nullptr;
   unsigned long long* d_chunk_st = nullptr;
-  int chunk = 0, chunk_grid = 0, chunk_cap = 0, chunk_margin = 100, chunk_yields = 6, chunk_cmargin = 100;
+  int chunk = 0, chunk_grid = 0, chunk_cap = 0, chunk_margin = 50, chunk_yields = 20, chunk_cmargin = 50;
   gm_spawn_params* d_scene = nullptr;  // gm_set_scene_spawn parameters (NULL: plain spawn_object)
   int scene_tries = 0;
   GmSpawnRand spawn_rand{};            // gm_set_random_spawn (enable = 0: spawn tables)

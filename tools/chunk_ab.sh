@@ -13,7 +13,7 @@ for r in 1 2; do
   for S in "$@"; do
     IFS=: read K M Y CM <<< "$S"
     echo -n "setting=$S " >> $OUT/ab.txt
-    GM_CHUNK_SUBSTEPS=$K GM_CHUNK_MARGIN=${M:-100} GM_CHUNK_YIELDS=${Y:-6} GM_CHUNK_CMARGIN=${CM:-100} \
+    GM_CHUNK_SUBSTEPS=$K GM_CHUNK_MARGIN=${M:-50} GM_CHUNK_YIELDS=${Y:-20} GM_CHUNK_CMARGIN=${CM:-50} \
       timeout -k 10 120 python tools/quick_bench_n.py 8 4096 10 2>/dev/null >> $OUT/ab.txt
   done
 done

@@ -20,7 +20,9 @@ def rows(name):
     return [r for r in csv.DictReader(open(f)) if r['Kernel_Name'].startswith('gm_') or 'gm_step_kernel' in r['Kernel_Name']]
 
 
-for name in ("pmc_fetch", "pmc_write", "pmc_sq"):
+for name in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_lanes"):
+    if not os.path.exists(os.path.join(src, name)):
+        continue
     rs = rows(name)
     with open(os.path.join(dst, f"{tag}_{name}.csv"), "w", newline="") as f:
         w = csv.DictWriter(f, fieldnames=keep)
@@ -29,7 +31,9 @@ for name in ("pmc_fetch", "pmc_write", "pmc_sq"):
             w.writerow({k: r[k] for k in keep})
 
 n_envs = 4096
-step = lambda r: 'gm_step_kernel' in r['Kernel_Name'] and int(r['Grid_Size']) == 64 * n_envs
+# the 4096-env launches: one workgroup per env (one-shot) or per resident wave slot
+# (chunked dispatch, 2048 on MI355X); the bench's small launches (settle, C2) excluded
+step = lambda r: 'gm_step_kernel' in r['Kernel_Name'] and int(r['Grid_Size']) >= 64 * 1024
 fe = [float(r['Counter_Value']) for r in rows("pmc_fetch") if step(r)]
 wr = [float(r['Counter_Value']) for r in rows("pmc_write") if step(r)]
 fetch = sum(fe) / len(fe) * 1024 * 2
@@ -47,7 +51,7 @@ print(open(os.path.join(dst, "pmc_traffic.json")).read())
 tr = [r for r in csv.DictReader(open(os.path.join(src, "stats", "run_kernel_trace.csv")))
       if 'gm_step_kernel' in r['Kernel_Name']]
 grid = lambda r: int(r.get('Grid_Size_X') or r.get('Grid_Size') or 0)
-durs = [(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6 for r in tr if grid(r) == 64 * n_envs]
+durs = [(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6 for r in tr if grid(r) >= 64 * 1024]
 summ = {"kernel": "gm_step_kernel", "grid_envs": n_envs, "launches": len(durs),
         "avg_ms_all": sum(durs) / len(durs), "avg_ms_after_first": sum(durs[1:]) / max(len(durs) - 1, 1),
         "min_ms": min(durs), "max_ms": max(durs), "durations_ms": durs,

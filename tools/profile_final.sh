@@ -13,6 +13,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/s
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-parity --no-policy --no-c2 > $OUT/pmc_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-parity --no-policy --no-c2 > $OUT/pmc_write.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES --output-format csv -d $OUT/pmc_sq -o run -- python3 tools/pmc_step.py 4096 > $OUT/pmc_sq.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_THREAD_CYCLES_VALU --output-format csv -d $OUT/pmc_lanes -o run -- python3 tools/pmc_step.py 4096 > $OUT/pmc_lanes.log 2>&1
 timeout -k 10 200 python tools/phase_profile.py 4096 > $OUT/phase_profile.txt 2>&1
 timeout -k 10 200 python tools/tail_bench.py > $OUT/tail_bench.txt 2>&1
 echo done > $OUT/DONE

@@ -85,6 +85,12 @@ for t in range(8):
 if len(sys.argv) > 3:
     np.save(sys.argv[3], np.stack(dump))   # [step, env, (phases 0-7, total, nefc sum, mpr substeps)]
 
+# the chunked dispatch gm_step runs (the profiled steps above use the one-shot kernel)
+for t in range(3):
+    drive()
+    print("chunked dispatch:", {k: (round(v, 3) if isinstance(v, float) else v) for k, v in env.chunk_stats().items()},
+          f"kernel {env.last_step_ms():.3f} ms", flush=True)
+
 # which phases carry the spread: per-phase mean / std over envs (shader clocks per env-step)
 ph = drive(profiled=True).astype(np.float64)
 tot = ph[:, 23]

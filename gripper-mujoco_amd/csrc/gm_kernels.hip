@@ -2512,8 +2512,11 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
 }
 // mode 0: action_step + obs/done/reward; mode 1: calibrate_reset settle (400 substeps,
 // no sensors); mode 2: one full substep with diagnostics
+#ifndef GM_WPS
+#define GM_WPS 2   // waves per SIMD the register allocation is held to
+#endif
 template <int CL, bool CAL>
-__global__ __launch_bounds__(NT, 2) void gm_step_kernel(
+__global__ __launch_bounds__(NT, GM_WPS) void gm_step_kernel(
     GmEnvState* __restrict__ states, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
     const GmTopo* __restrict__ T, float* __restrict__ obs, float* __restrict__ rew,
     uint8_t* __restrict__ done, int n_envs, int mode, DebugOut dbg, const int32_t* __restrict__ order,

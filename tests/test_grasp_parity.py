@@ -225,14 +225,16 @@ def test_c3_newton_matches_converged_pgs_4096(gm, ol):
     env.close()
 
 
-@pytest.mark.parametrize("n_seg", [5, 6])
-def test_short_fingers_256(gm, ol, n_seg):
-    """N = 5, 6 segments (CL = 7, 8 builds of the step kernel) on grasp states at the
-    timestep the reference's search gives them, same bounds as the canonical batch."""
+@pytest.mark.parametrize("n_seg", [5, 6, 7, 9])
+def test_other_segment_counts_256(gm, ol, n_seg):
+    """N = 5, 6, 7, 9 segments (CL = 7, 8, 9, 11 builds of the step kernel) on grasp
+    states, same bounds as the canonical batch.  N = 5, 6 run at the timestep the
+    reference's search gives them; N = 7, 9 at a timestep inside their stable range
+    (between their neighbours' searched steps)."""
     import ctypes as C
     p = gm.ModelParams()
     gm.load_library().gm_default_model_params(C.byref(p))
-    p.n_seg, p.timestep = n_seg, {5: 6.76e-3, 6: 4.94e-3}[n_seg]
+    p.n_seg, p.timestep = n_seg, {5: 6.76e-3, 6: 4.94e-3, 7: 3.9e-3, 9: 2.6e-3}[n_seg]
     env, snaps = rollout(gm, 256, "set6_synthetic", 40 + n_seg, steps=41, snaps=(20, 40), model_params=p)
     assert env.model.nv == 3 * (n_seg + 2) + 8
     rep = [compare_step(gm, ol, env, sn) for sn in snaps]

@@ -2776,7 +2776,7 @@ extern "C" __global__ void gm_scripted_action_kernel(const GmEnvState* __restric
 // ---------------------------------------------------------------- reset + spawn
 // MjClass::spawn_object -> ObjectHandler::spawn_object (mjclass.cpp:2352-2420,
 // objecthandler.cpp:403-428): live object, pose on the ground at (x, y), z-rotation
-__device__ void spawn_object(GmEnvState& s, const GmTopo* __restrict__ T, const gm_object* __restrict__ objs,
+__device__ void spawn_object(GmEnvHot& s, const GmTopo* __restrict__ T, const gm_object* __restrict__ objs,
                              int n_objects, gm_spawn sp) {
   int oi = sp.object_index;
   if (oi < 0 || oi >= n_objects) oi = 0;
@@ -2855,7 +2855,7 @@ __device__ uint64_t uid_minstd(uint32_t& st, uint64_t a, uint64_t b) {
 // single leading {0, 1} draw for even n.  Shuffling indices permutes exactly like
 // shuffling the elements.  (n <= GM_SPAWN_MAX_XY: the pair range and its quotients fit
 // 32 bits.)
-__device__ void shuffle_minstd(uint16_t* v, int n, uint32_t& st) {
+__device__ __forceinline__ void shuffle_minstd(uint16_t* v, int n, uint32_t& st) {
   if (n <= 0) return;
   const uint64_t urngrange = 2147483645ull, urange = (uint64_t)n;
   if (urngrange / urange >= urange) {
@@ -2937,19 +2937,26 @@ __device__ __host__ inline void object_bbox(const gm_object& o, double* xyz) {
   else { xyz[0] = xyz[1] = xyz[2] = 2 * o.size[0]; }
 }
 // returns 1 and spawns on success; 0 when no candidate pose is free
-__device__ int spawn_into_scene_dev(GmEnvState& s, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
-                                    const gm_object* __restrict__ objs, int n_objects, const gm_spawn_params& p,
-                                    int index) {
+// pxy / prot: the shuffled grids' work buffers (GM_SPAWN_MAX_XY / GM_SPAWN_MAX_ROT entries):
+// LDS in the reset kernel (its one working lane would otherwise wait on a scratch round
+// trip per swap), private arrays in the thread-per-env kernel
+__device__ __forceinline__ int spawn_into_scene_dev(GmEnvHot& s, const gm_model* __restrict__ m,
+                                                    const GmTopo* __restrict__ T, const gm_object* __restrict__ objs,
+                                                    int n_objects, const gm_spawn_params& p, int index,
+                                                    uint16_t* pxy, uint16_t* prot) {
   const int num_x = (int)(((2 * p.xrange) / p.xy_increment) + 1);
   const int num_y = (int)(((2 * p.yrange) / p.xy_increment) + 1);
   const int num_r = (int)(((2 * p.rotrange) / p.rot_increment) + 1);
   const int nxy = num_x * num_y;
   if (num_x < 1 || num_y < 1 || num_r < 1 || nxy > GM_SPAWN_MAX_XY || num_r > GM_SPAWN_MAX_ROT) return 0;
-  uint16_t pxy[GM_SPAWN_MAX_XY], prot[GM_SPAWN_MAX_ROT];
   for (int i = 0; i < nxy; i++) pxy[i] = (uint16_t)i;
   for (int i = 0; i < num_r; i++) prot[i] = (uint16_t)i;
-  if (nxy > 1) shuffle_minstd(pxy, nxy, s.rng);
-  if (num_r > 1) shuffle_minstd(prot, num_r, s.rng);
+  {
+    uint32_t rng = s.rng;   // in a register through both shuffles, not the env's HBM record
+    if (nxy > 1) shuffle_minstd(pxy, nxy, rng);
+    if (num_r > 1) shuffle_minstd(prot, num_r, rng);
+    s.rng = rng;
+  }
   // object footprint
   int oi = index;
   if (oi < 0 || oi >= n_objects) oi = 0;
@@ -3005,7 +3012,8 @@ extern "C" __global__ void gm_spawn_into_scene_kernel(GmEnvState* __restrict__ s
   if (env >= n_envs) return;
   if (mask && !mask[env]) { if (ok) ok[env] = 0; return; }
   const gm_spawn_params p = params[n_params == 1 ? 0 : env];
-  const int r = spawn_into_scene_dev(states[env], m, T, objs, n_objects, p, p.index);
+  uint16_t pxy[GM_SPAWN_MAX_XY], prot[GM_SPAWN_MAX_ROT];
+  const int r = spawn_into_scene_dev(states[env], m, T, objs, n_objects, p, p.index, pxy, prot);
   if (ok) ok[env] = (uint8_t)r;
 }
 #endif
@@ -3035,86 +3043,103 @@ extern "C" __global__ __launch_bounds__(64) void gm_reset_kernel(
     const GmTopo* __restrict__ T, const double* __restrict__ eq_qpos, const uint8_t* __restrict__ mask,
     const gm_spawn* __restrict__ spawn, const gm_object* __restrict__ objs, int n_objects, int n_envs,
     const gm_spawn_params* __restrict__ scene, int scene_tries, float* __restrict__ obs, GmSpawnRand sr) {
+  __shared__ uint16_t sh_pxy[GM_SPAWN_MAX_XY], sh_prot[GM_SPAWN_MAX_ROT];   // spawn grid shuffles
   const int env = blockIdx.x;
   if (env >= n_envs) return;
   if (mask && !mask[env]) return;
-  GmEnvState& s = states[env];
+  // the new record's hot part is built in LDS (lane 0's serial reset reads back what it
+  // wrote many times over) and stored to HBM in one coalesced sweep; the sensor windows
+  // are cleared in place
+  __shared__ uint4 hot_words[GM_HOT_WORDS / 4];
+  GmEnvHot& s = *reinterpret_cast<GmEnvHot*>(hot_words);
+  GmEnvState& rec = states[env];
   // keep the per-env RNG stream and the function-static stepper flags (quirk)
-  const uint32_t rng = s.rng;
-  const int ox = s.old_x, oy = s.old_y, oz = s.old_z;
-  const int32_t episode = s.episode + 1;
-  __syncthreads();   // every lane has read them before the record is cleared
+  const uint32_t rng = rec.rng;
+  const int ox = rec.old_x, oy = rec.old_y, oz = rec.old_z;
+  const int32_t episode = rec.episode + 1;
   {
-    static_assert(sizeof(GmEnvState) % 16 == 0, "GmEnvState is cleared in 16-byte words");
-    uint4* w = reinterpret_cast<uint4*>(&s);
-    for (int i = threadIdx.x; i < GM_STATE_WORDS / 4; i += 64) w[i] = make_uint4(0u, 0u, 0u, 0u);
+    static_assert(sizeof(GmEnvState) % 16 == 0 && sizeof(GmEnvHot) % 16 == 0, "records move in 16-byte words");
+    for (int i = threadIdx.x; i < GM_HOT_WORDS / 4; i += 64) hot_words[i] = make_uint4(0u, 0u, 0u, 0u);
+    uint4* w = reinterpret_cast<uint4*>(&rec);
+    for (int i = GM_HOT_WORDS / 4 + threadIdx.x; i < GM_STATE_WORDS / 4; i += 64) w[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  s.rng = rng; s.old_x = ox; s.old_y = oy; s.old_z = oz;
-  s.episode = episode;
-  g_reset(s.end); g_reset(s.next);
-  for (int k = 0; k < GM_MAX_QPOS; k++) s.qpos[k] = m->qpos0[k];
-  s.time = 0; s.last_step_time = 0;
-  s.dt = m->timestep;
-  for (int d = 0; d < T->nv; d++) {
-    bool motor = (d == m->dof_base || d == m->dof_palm);
-    for (int f = 0; f < 3; f++) motor = motor || d == m->dof_pris[f] || d == m->dof_rev[f];
-    if (motor) s.qpos[d] = eq_qpos[d];
+  if (threadIdx.x == 0) {   // the reference's serial reset on lane 0
+    s.rng = rng; s.old_x = ox; s.old_y = oy; s.old_z = oz;
+    s.episode = episode;
+    g_reset(s.end); g_reset(s.next);
+    for (int k = 0; k < GM_MAX_QPOS; k++) s.qpos[k] = m->qpos0[k];
+    s.time = 0; s.last_step_time = 0;
+    s.dt = m->timestep;
+    for (int d = 0; d < T->nv; d++) {
+      bool motor = (d == m->dof_base || d == m->dof_palm);
+      for (int f = 0; f < 3; f++) motor = motor || d == m->dof_pris[f] || d == m->dof_rev[f];
+      if (motor) s.qpos[d] = eq_qpos[d];
+    }
+    for (int k = 0; k < T->nlock; k++) { s.lock_active[k] = 1; s.lock_q[k] = m->qpos0[m->lock_dof[k]]; }
+    for (int st = 0; st < GM_NSTREAM; st++) s.ring_i[st] = -1;
+    // apply_noise_params: mean draws, SS order then the state sensors again
+    {
+      const gm_settings& st = C->s;
+      const gm_sensor* ss[SL_N] = {&st.motor_state_sensor, &st.base_state_sensor_Z, &st.base_state_sensor_XY,
+                                   &st.base_state_sensor_yaw, &st.bending_gauge, &st.axial_gauge, &st.palm_sensor,
+                                   &st.wrist_sensor_XY, &st.wrist_sensor_Z, &st.cartesian_contacts_XYZ};
+      uint32_t g = s.rng;   // the draws below run on a register copy of the stream
+      for (int k = 0; k < SL_N; k++)
+        for (int i = 0; i < 3; i++) {
+          s.rand_mu[k][i] = ss[k]->noise_mu * (2 * unif01(g) - 1);
+        }
+      int order[5] = {SL_MOTOR, SL_BASEXY, SL_BASEZ, SL_YAW, SL_CART};
+      for (int k = 0; k < 5; k++)
+        for (int i = 0; i < 3; i++) {
+          s.rand_mu[order[k]][i] = ss[order[k]]->noise_mu * (2 * unif01(g) - 1);
+        }
+      s.rng = g;
+    }
+    {
+      double size = C->s.base_position_noise;
+      uint32_t g = s.rng;
+      double u = canon_d(g);
+      s.rng = g;
+      double z = u * (size - (-size)) + (-size);
+      s.base[2] = z;
+      if (s.base[2] > C->base_max[2]) s.base[2] = C->base_max[2];
+      if (s.base[2] < C->base_min[2]) s.base[2] = C->base_min[2];
+      s.qpos[m->dof_base] = s.base[2] + eq_qpos[m->dof_base];
+    }
+    gm_spawn sp = spawn ? spawn[env] : gm_spawn{0, 0.0, 0.0, 0.0};
+    if (sr.enable && !spawn) {
+      // MjEnv._spawn_object's generator draws: object index, then the "old method" pose
+      // (integer mm offsets, one of {0, 60, 120} deg plus integer-degree noise)
+      const int64_t gid = sr.env_offset + env;
+      const int nm = sr.position_noise_mm, nd = sr.rotation_noise_deg;
+      sp.object_index = gm_spawn_int(sr.seed, gid, episode, 0, 0, n_objects - 1);
+      sp.x = gm_spawn_int(sr.seed, gid, episode, 1, -nm, nm) * 1e-3;
+      sp.y = gm_spawn_int(sr.seed, gid, episode, 2, -nm, nm) * 1e-3;
+      const int noise_deg = gm_spawn_int(sr.seed, gid, episode, 3, -nd, nd);
+      const int opt = gm_spawn_int(sr.seed, gid, episode, 4, 0, 2);
+      sp.zrot = (60 * opt + noise_deg) * (M_PI / 180.0);
+    }
+    bool placed = false;
+    if (scene) {
+      // MjEnv._spawn_object (MjEnv.py:1177-1267): spawn_into_scene up to scene_tries times,
+      // then the "old method" pose from the spawn table
+      for (int t = 0; t < scene_tries && !placed; t++)
+        placed = spawn_into_scene_dev(s, m, T, objs, n_objects, *scene, sp.object_index, sh_pxy, sh_prot);
+    }
+    if (!placed) spawn_object(s, T, objs, n_objects, sp);
+    s.done = 0;
+    s.reward = 0;
   }
-  for (int k = 0; k < T->nlock; k++) { s.lock_active[k] = 1; s.lock_q[k] = m->qpos0[m->lock_dof[k]]; }
-  for (int st = 0; st < GM_NSTREAM; st++) s.ring_i[st] = -1;
-  // apply_noise_params: mean draws, SS order then the state sensors again
-  {
-    const gm_settings& st = C->s;
-    const gm_sensor* ss[SL_N] = {&st.motor_state_sensor, &st.base_state_sensor_Z, &st.base_state_sensor_XY,
-                                 &st.base_state_sensor_yaw, &st.bending_gauge, &st.axial_gauge, &st.palm_sensor,
-                                 &st.wrist_sensor_XY, &st.wrist_sensor_Z, &st.cartesian_contacts_XYZ};
-    for (int k = 0; k < SL_N; k++)
-      for (int i = 0; i < 3; i++) {
-        s.rand_mu[k][i] = ss[k]->noise_mu * (2 * unif01(s.rng) - 1);
-      }
-    int order[5] = {SL_MOTOR, SL_BASEXY, SL_BASEZ, SL_YAW, SL_CART};
-    for (int k = 0; k < 5; k++)
-      for (int i = 0; i < 3; i++) {
-        s.rand_mu[order[k]][i] = ss[order[k]]->noise_mu * (2 * unif01(s.rng) - 1);
-      }
-  }
-  {
-    double size = C->s.base_position_noise;
-    double u = canon_d(s.rng);
-    double z = u * (size - (-size)) + (-size);
-    s.base[2] = z;
-    if (s.base[2] > C->base_max[2]) s.base[2] = C->base_max[2];
-    if (s.base[2] < C->base_min[2]) s.base[2] = C->base_min[2];
-    s.qpos[m->dof_base] = s.base[2] + eq_qpos[m->dof_base];
-  }
-  gm_spawn sp = spawn ? spawn[env] : gm_spawn{0, 0.0, 0.0, 0.0};
-  if (sr.enable && !spawn) {
-    // MjEnv._spawn_object's generator draws: object index, then the "old method" pose
-    // (integer mm offsets, one of {0, 60, 120} deg plus integer-degree noise)
-    const int64_t gid = sr.env_offset + env;
-    const int nm = sr.position_noise_mm, nd = sr.rotation_noise_deg;
-    sp.object_index = gm_spawn_int(sr.seed, gid, episode, 0, 0, n_objects - 1);
-    sp.x = gm_spawn_int(sr.seed, gid, episode, 1, -nm, nm) * 1e-3;
-    sp.y = gm_spawn_int(sr.seed, gid, episode, 2, -nm, nm) * 1e-3;
-    const int noise_deg = gm_spawn_int(sr.seed, gid, episode, 3, -nd, nd);
-    const int opt = gm_spawn_int(sr.seed, gid, episode, 4, 0, 2);
-    sp.zrot = (60 * opt + noise_deg) * (M_PI / 180.0);
-  }
-  bool placed = false;
-  if (scene) {
-    // MjEnv._spawn_object (MjEnv.py:1177-1267): spawn_into_scene up to scene_tries times,
-    // then the "old method" pose from the spawn table
-    for (int t = 0; t < scene_tries && !placed; t++)
-      placed = spawn_into_scene_dev(s, m, T, objs, n_objects, *scene, sp.object_index);
-  }
-  if (!placed) spawn_object(s, T, objs, n_objects, sp);
   // MjEnv.reset returns _next_observation() of the fresh episode (MjEnv.py:2222-2263):
-  // the observation buffer holds the reset env's sensor windows, not the last episode's
-  if (obs) get_obs(s, s.ring, C, obs + (size_t)env * C->n_obs);
-  s.done = 0;
-  s.reward = 0;
+  // the observation buffer holds the reset env's sensor windows, not the last episode's;
+  // sampled one stream per lane as in the env-step epilogue
+  __syncthreads();
+  {
+    uint4* w = reinterpret_cast<uint4*>(&rec);
+    for (int i = threadIdx.x; i < GM_HOT_WORDS / 4; i += 64) w[i] = hot_words[i];
+  }
+  if (obs) get_obs_lanes(s, rec.ring, C, obs + (size_t)env * C->n_obs, threadIdx.x);
 }
 #endif
 

@@ -2639,9 +2639,24 @@ extern "C" __global__ __launch_bounds__(1024) void gm_dispatch_order_kernel(cons
     atomicAdd(&cnt[b], 1u);
   }
   __syncthreads();
-  if (t == 0) {
-    uint32_t acc = 0;
-    for (int b = 0; b < 256; b++) { const uint32_t c = cnt[b]; cnt[b] = acc; acc += c; }
+  {
+    // exclusive prefix over the 256 buckets: shuffle scans in the first four waves, then
+    // each wave's offset from the wave totals (a serial loop on one thread took ~10 us)
+    __shared__ uint32_t wsum[4];
+    const uint32_t v = (t < 256) ? cnt[t] : 0u;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o);
+      if ((t & 63) >= o) inc += u;
+    }
+    if (t < 256 && (t & 63) == 63) wsum[t >> 6] = inc;
+    __syncthreads();
+    if (t < 256) {
+      uint32_t base = 0;
+      for (int w = 0; w < (t >> 6); w++) base += wsum[w];
+      cnt[t] = base + inc - v;
+    }
   }
   __syncthreads();
   for (int i = t; i < n; i += 1024) {

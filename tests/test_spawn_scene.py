@@ -182,28 +182,54 @@ def test_gpu_spawn_into_scene_matches_oracle(world):
     env.close()
 
 
+def grid_params(gm, index, grid):
+    """MjEnv's spawn params, or the largest grids the reset kernel's LDS shuffle buffers
+    hold (31 x 31 = 961 of GM_SPAWN_MAX_XY = 1024 xy points, 181 of GM_SPAWN_MAX_ROT = 256
+    rotations)."""
+    p = mjenv_params(gm, index)
+    if grid == "max":
+        p.xrange = p.yrange = 15e-3
+        p.xy_increment = 1e-3
+        p.rot_increment = np.pi / 180.0
+    return p
+
+
 @pytest.mark.gpu
-def test_gpu_reset_with_scene_spawn_matches_oracle(world):
+@pytest.mark.parametrize("grid", ["mjenv", "max"])
+def test_gpu_reset_with_scene_spawn_matches_oracle(world, grid):
     """gm_set_scene_spawn: resets place objects the MjEnv._spawn_object way
-    (MjEnv.py:1177-1267) on the device -- reset, then spawn_into_scene(spawn[e].index)."""
+    (MjEnv.py:1177-1267) on the device -- reset, then spawn_into_scene(spawn[e].index) --
+    pose for pose, and leave the RNG stream where the oracle's is (sensor noise on: the
+    next env-step's observations agree)."""
     if not gpu_available():
         pytest.skip("no GPU")
     gm, model, cfg, objs = world
     n = 32
-    s = gm.canonical_settings(noise=False, seed=12)
+    s = gm.canonical_settings(noise=True, seed=12)
     env = gm.BatchedGripperEnv(n, object_set="set6_synthetic", settings=s, seed=12)
-    p = mjenv_params(gm, 0)
+    p = grid_params(gm, 0, grid)
+    if grid == "max":
+        nxy = int(2 * p.xrange / p.xy_increment + 1) * int(2 * p.yrange / p.xy_increment + 1)
+        nr = int(2 * p.rotrange / p.rot_increment + 1)
+        assert 900 < nxy <= 1024 and 150 < nr <= 256, (nxy, nr)
     env.set_scene_spawn(p, max_tries=3)
     sp = env.make_spawn()
     env.reset(spawn=sp)
     q, _, _ = env.state()
     qa = env.model.nq - 7
+    oracles = []
     for e in range(n):
         o = oracle_lib.OracleEnv(env.model, env.cfg, env.objects, env_id=e)
         o.reset(sp[e])
-        pe = mjenv_params(gm, sp[e].object_index)
+        pe = grid_params(gm, sp[e].object_index, grid)
         assert o.spawn_into_scene(pe)
         qo, _, _ = o.state()
         np.testing.assert_array_equal(q[e][qa:qa + 7], qo[qa:qa + 7], err_msg=f"env {e}")
+        oracles.append(o)
+    a = np.zeros((n, env.n_actions), dtype=np.float32)
+    obs, _, _, _ = env.step(a)
+    for e in range(0, n, 4):
+        ro, _, _ = oracles[e].step(a[e])
+        np.testing.assert_allclose(obs[e], ro, rtol=1e-4, atol=1e-4, err_msg=f"env {e}")
     env.set_scene_spawn(None)
     env.close()

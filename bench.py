@@ -169,6 +169,117 @@ def c2_line(gmx, torch, dev, stream, steps: int, seed: int, env_offset: int):
                                                                    "scripted grasp mix"}
 
 
+def c3_random_line(gmx, torch, dev, stream, steps: int, seed: int, env_offset: int, n: int):
+    """C3 with synthetic random actions (BASELINE.json north_star: "throughput on synthetic
+    random-action rollouts"): every env draws U[-1,1]^4 each step from one device generator
+    seeded 1234 (TrainDQN.profile's seed, TrainDQN.py:2520), written straight into the
+    context's action buffer; same set6 objects, scene spawn, auto-reset and steady-state
+    pre-roll as the scripted headline."""
+    import ctypes
+    s = gmx.canonical_settings(seed=seed)
+    env = gmx.BatchedGripperEnv(n, object_set="set6_synthetic", settings=s, seed=seed, env_offset=env_offset,
+                                device=dev.index)
+    env.set_stream(stream.cuda_stream)
+    env.set_scene_spawn(mjenv_spawn_params(gmx), max_tries=3)
+    env.reset()
+    returns = torch.full((n,), float("nan"), device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    act = torch.empty((n, env.n_actions), device=dev, dtype=torch.float32)
+
+    def drive():
+        act.uniform_(-1.0, 1.0, generator=g)
+        env.lib.gm_set_action(env.ctx, ctypes.c_void_p(act.data_ptr()), 1)
+        env.lib.gm_step(env.ctx)
+        env.autoreset_device(0, returns.data_ptr(), max_episode_steps=MAX_EP)
+
+    t_start = gmx.spawn_int(seed, env_offset + np.arange(n), 0, 99, 0, MAX_EP - 1)
+    for t in range(MAX_EP):
+        m = (t_start == t)
+        if m.any():
+            env.lib.gm_reset(env.ctx, np.ascontiguousarray(m.astype(np.uint8)).ctypes.data_as(
+                ctypes.POINTER(ctypes.c_uint8)), None)
+        drive()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        drive()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    caps = int(gmx.env_state_view(env.env_states())["newton_caps"].sum())
+    env.close()
+    return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "envs": n, "steps": steps,
+            "ms_per_step": round(el / steps * 1e3, 3), "newton_cap_hits": caps,
+            "workload": "C3 with random actions U[-1,1]^4 (device generator, seed 1234), set6_synthetic, scene "
+                        "spawn, auto-reset, steady state after a staggered pre-roll"}
+
+
+def c1_line(gmx, seed: int, n_steps: int = 200):
+    """C1 (BASELINE.json configs[0]): 1 env, one 200-step random-action episode, actions
+    U[-1,1]^4 from np.random.default_rng(1234) (TrainDQN.py:2520).  Device: the mjpy.bind
+    facade in MjEnv.step's call order (set_continous_action per index, action_step,
+    get_observation_numpy, is_done, reward; MjEnv.py:585-637); CPU: the fp64 oracle on one
+    core, the same actions from the same reset.  set1_nocuboid_525 is absent, so the
+    synthetic set1 (box, cylinder, sphere) stands in."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib
+    from mjpy.bind import MjClass
+    acts = np.random.default_rng(1234).uniform(-1, 1, size=(n_steps, 4)).astype(np.float32)
+    mj = MjClass()
+    mj.set = gmx.canonical_settings(seed=seed)
+    mj.object_set_name = "set1_synthetic"
+    mj.reset()
+    na = mj.get_n_actions()
+    env = mj._env
+    o = oracle_lib.OracleEnv(env.model, env.cfg, env.objects, env_id=0)
+    sp = gmx.Spawn()
+    sp.object_index, sp.x, sp.y, sp.zrot = 0, 0.0, 0.0, 0.0
+    o.reset(sp)
+    obs_d = []
+    t0 = time.perf_counter()
+    for t in range(n_steps):
+        for i in range(na):
+            mj.set_continous_action(i, float(acts[t, i]))
+        mj.action_step()
+        obs_d.append(mj.get_observation_numpy())
+        mj.is_done()
+        mj.reward()
+    dev_s = time.perf_counter() - t0
+    obs_o = []
+    t0 = time.perf_counter()
+    for t in range(n_steps):
+        ob, _, _ = o.step(acts[t, :na])
+        obs_o.append(ob)
+    cpu_s = time.perf_counter() - t0
+    a = np.asarray(obs_d, dtype=np.float64)
+    b = np.asarray(obs_o, dtype=np.float64)
+    d = np.abs(a - b)
+    big = np.abs(b) >= 1e-3
+    rel = float((d[big] / np.abs(b[big])).max(initial=0.0))
+    mj._drop()
+    return {"device": {"value": round(n_steps / dev_s, 1), "unit": "env-steps/s", "ms_per_step": round(dev_s / n_steps * 1e3, 3),
+                       "path": "mjpy.bind.MjClass facade (one env, host round trip per call, as MjEnv drives it)"},
+            "cpu_oracle_1_core": {"value": round(n_steps / cpu_s, 1), "unit": "env-steps/s", "cores": 1, "kind": "port"},
+            "steps": n_steps, "actions": "np.random.default_rng(1234).uniform(-1, 1, (200, 4))",
+            "object_set": "set1_synthetic",
+            "obs_max_rel_err_over_episode": rel,
+            "obs_max_abs_err_small_over_episode": float(np.where(big, 0.0, d).max(initial=0.0))}
+
+
+def host_cpu_quota():
+    """CPUs this process may use: its affinity mask and the cgroup v2 CPU quota (cpu.max)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return aff, quota
+
+
 def host_cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -193,8 +304,13 @@ def cpu_baseline(gmx, n_envs: int, n_steps: int, n_threads: int):
     objs = gmx.make_object_set("set6_synthetic", 1234)
     t = time.time()
     v = oracle_lib.bench(model, cfg, objs, n_envs, n_steps, seed=1234, n_threads=n_threads, scripted=True)
+    aff, quota = host_cpu_quota()
     return {"value": round(v, 2), "unit": "env-steps/s", "cores": n_threads, "kind": "port",
             "cpu_model": host_cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+            "cores_note": "the GPU box gives a 1-GPU job a share of 16 host CPUs (OMP_NUM_THREADS / MAX_JOBS are "
+                          "16 there and worker pools must stay within it); the other visible CPUs belong to "
+                          "other jobs, so 16 threads is every core this job may use",
             "sample": f"fp64 C oracle (oracle/oracle.c, gcc -O2 -mavx), {n_threads} thread(s), {n_envs} envs x "
                       f"{n_steps} env-steps of the C3 workload (set6_synthetic, scripted grasp mix, resets at "
                       f"done / 250 steps), {time.time() - t:.1f} s wall"}
@@ -303,6 +419,8 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-policy", action="store_true", help="skip the C5 on-device DQN rollout line item")
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 (256 envs, one cylinder) line item")
+    ap.add_argument("--no-random", action="store_true", help="skip the C3 random-action line item")
+    ap.add_argument("--no-c1", action="store_true", help="skip the C1 (1 env, 200 random steps) line item")
     ap.add_argument("--no-preroll", dest="preroll", action="store_false",
                     help="skip the steady-state pre-roll (profiling runs only; the headline needs it)")
     args = ap.parse_args()
@@ -380,6 +498,9 @@ def main():
               "max_iterations_in_env_step": int(ph[:, env.PH_NEWTON].max()),
               "line_search_evals_per_solve": round(ph[:, env.PH_LS].sum() / n_solves, 4),
               "rows_per_solve": round(ph[:, env.PH_NEFC].sum() / n_solves, 3),
+              # solves that hit GM_NEWTON_MAXIT or a line search that hit GM_NEWTON_MAXLS,
+              # over every substep this batch ran (pre-roll, warmup, timed, probes)
+              "newton_cap_hits": int(gmx.env_state_view(env.env_states())["newton_caps"].sum()),
               "states": "the batch after the timed window, one profiled env-step"}
 
     if rank == 0:
@@ -393,6 +514,7 @@ def main():
                 "kernel": "gm_step_kernel", "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "traffic_source": traffic_src,
+                "traffic_measured_in_this_run": False,   # PMC counters need their own rocprofv3 pass
                 # the same roofline with the per-substep bytes at the batch's measured mean
                 # contact count instead of SURVEY.md 8d's nominal 12
                 "achieved_at_measured_ncon": round(n * S * Bm["bytes"] / kern_avg_s / 1e9, 2),
@@ -403,6 +525,8 @@ def main():
             cpu = cpu_baseline(gmx, args.cpu_envs * args.cpu_threads // 4, args.cpu_steps, args.cpu_threads)
             cpu["single_thread"] = cpu_baseline(gmx, args.cpu_envs, args.cpu_steps, 1)["value"]
         c2 = None if (args.no_c2 or world > 1) else c2_line(gmx, torch, dev, stream, K, args.seed, first_env)
+        c3r = None if (args.no_random or world > 1) else c3_random_line(gmx, torch, dev, stream, K, args.seed, first_env, n)
+        c1 = None if (args.no_c1 or world > 1) else c1_line(gmx, args.seed)
         c5 = None if (args.no_policy or world > 1) else policy_rollout(gmx, torch, dev, stream, n, max(3, K // 2), args.seed,
                                                         first_env)
         out = headline(world, n, K, W, elapsed, episodes)
@@ -428,6 +552,8 @@ def main():
             "cpu_baseline": cpu,
             "obs_max_rel_err": parity,
             "c2_single_cylinder_256": c2,
+            "c3_random_actions": c3r,
+            "c1_single_env_200_steps": c1,
             "c5_device_policy_rollout": c5,
             "overflow_envs": overflow, "finite": finite,
         })

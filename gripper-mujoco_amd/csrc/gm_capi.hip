@@ -252,12 +252,21 @@ int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
     if (!with_obj && !with_gnd) { err = "gripper self-collision pairs are not supported"; return GM_E_RANGE; }
     const int g = with_obj ? (a == m.geom_obj ? bg : a) : (a == m.geom_ground ? bg : a);
     const int b = m.geom_body[g];
+    bool assigned = false;
     for (int l = 0; l < 64; l++) {
       if (T.lane_body[l] != b || l == T.lane_obj) continue;
       int32_t* slot = with_obj ? T.lane_opair[l] : T.lane_gpair[l];
       if (slot[0] < 0) slot[0] = pr;
       else if (slot[1] < 0) slot[1] = pr;
       else { err = "a body has more than two object (or ground) pairs"; return GM_E_RANGE; }
+      assigned = true;
+    }
+    // the Newton Hessian composites reach a contact only through its gripper body's scan
+    // lane: a pair on a body without one would be solved with an inconsistent Hessian
+    if (!assigned) {
+      err = "contact pair " + std::to_string(pr) + " is on body " + std::to_string(b) +
+            ", which has no scan lane (fingers, palm); the solver cannot take it";
+      return GM_E_RANGE;
     }
   }
   return GM_OK;
@@ -329,8 +338,10 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   HIPCHK(c, hipMalloc(&c->d_mask, (size_t)n_envs));
   HIPCHK(c, hipMalloc(&c->d_spawn, sizeof(gm_spawn) * (size_t)n_envs));
   HIPCHK(c, hipMalloc(&c->d_order, sizeof(int32_t) * (size_t)n_envs));
-  HIPCHK(c, hipMalloc(&c->d_cost, sizeof(uint32_t) * (size_t)n_envs));
-  HIPCHK(c, hipMemsetAsync(c->d_cost, 0, sizeof(uint32_t) * (size_t)n_envs, c->stream));
+  // two halves: [0, n) the costs the current launch is ordered and scheduled by (read-only
+  // during it), [n, 2n) the costs it records; gm_dispatch_order_kernel moves them over
+  HIPCHK(c, hipMalloc(&c->d_cost, sizeof(uint32_t) * 2 * (size_t)n_envs));
+  HIPCHK(c, hipMemsetAsync(c->d_cost, 0, sizeof(uint32_t) * 2 * (size_t)n_envs, c->stream));
   {
     // chunked env-step: as many workgroups as wave slots are resident (occupancy query),
     // GM_CHUNK_SUBSTEPS substeps per chunk (default 8; 0 selects the one-shot kernel)

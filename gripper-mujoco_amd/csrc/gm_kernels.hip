@@ -2324,6 +2324,7 @@ struct GmChunkCarry {        // what a chunk hands the next besides the hot stat
 // previous launch's [GM_CQ_FRESH ..] (36 words, diagnostics)
 #define GM_CQ_FRESH (8 * GM_CQ_NB * 32)
 #define GM_CQ_DONE (GM_CQ_FRESH + 32)
+#define GM_CQ_CMAX (GM_CQ_DONE + 3)   // this launch's bucket scale (written by the order kernel)
 #define GM_CQ_WORDS (GM_CQ_FRESH + 64)
 #define GM_CQ_LAST GM_CQ_WORDS
 #define GM_CQ_ALLOC (GM_CQ_WORDS + 64)
@@ -2367,7 +2368,9 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
   uint32_t* fresh_head = q.ctr + GM_CQ_FRESH;
   uint32_t* n_done = q.ctr + GM_CQ_DONE;
   const uint32_t n = (uint32_t)n_envs;
-  const uint32_t cmax = cost[order[0]] + 1u;   // bucket scale: the heaviest env's cost
+  // bucket scale: the heaviest env's last cost + 1, snapshot by gm_dispatch_order_kernel, so
+  // every wave of the launch buckets alike (costs of this launch go to the second half)
+  const uint32_t cmax = q.ctr[GM_CQ_CMAX];
   unsigned long long busy = 0, poll = 0;
   bool first = true, saw_empty = false;
   for (;;) {
@@ -2401,7 +2404,10 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
           uint64_t* rb = ring + (size_t)bsel * q.cap;
           const uint32_t i = add_agent(bq + bsel * 32, 1u) % (uint32_t)q.cap;
           uint64_t v;
-          while ((v = ld_agent64(rb + i)) == 0ull && ld_agent(n_done) < n) __builtin_amdgcn_s_sleep(2);
+          // acquire: pairs with the producer's release store of this entry
+          while ((v = __hip_atomic_load(rb + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0ull &&
+                 ld_agent(n_done) < n)
+            __builtin_amdgcn_s_sleep(2);
           if (v != 0ull) {
             st_agent(rb + i, 0ull);
             add_agent(q.ctr + GM_CQ_DONE + 2, 1u);
@@ -2431,9 +2437,9 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
     const int env = pick;
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     if (!fresh) {
-      // the previous chunk's stores (another CU of this XCD) through this CU's L1
+      // lane 0's acquire load saw the entry; the fence extends that acquire to the whole
+      // wave's loads of the env's state (another CU of this XCD stored it) below
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     GmEnvState* g = states + env;
     load_state(S, g, lane);
@@ -2474,7 +2480,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
         const uint32_t now = cr.clk + (uint32_t)((__builtin_amdgcn_s_memtime() - t_start) >> 6);
         const uint32_t model = 14000u + 19u * (uint32_t)S.work_nefc + 188u * (uint32_t)S.work_mpr +
                                940u * (uint32_t)S.work_newton;
-        cost[env] = (now >> 1) + (model >> 1);
+        cost[n + env] = (now >> 1) + (model >> 1);   // recorded for the next launch's order
       }
       store_state(S, g, lane);
       if (lane == 0) {
@@ -2491,15 +2497,18 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
         cr.clk += (uint32_t)((__builtin_amdgcn_s_memtime() - t_start) >> 6);
         q.carry[env] = cr;
       }
-      // every lane's stores have reached the L2 before the env is handed on
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // the workgroup barrier orders every lane's state / carry stores before lane 0's
+      // release store of the ring entry, which publishes them at agent scope (the consumer's
+      // acquire pairs with it)
       __syncthreads();
       if (lane == 0) {
         const uint64_t rem = (uint64_t)own * (uint64_t)(cr.nsub - cr.sub_done) / (uint64_t)cr.nsub;
         add_agent(q.ctr + GM_CQ_DONE + 1, 1u);
         const uint32_t b = rem * GM_CQ_NB / cmax < GM_CQ_NB - 1 ? (uint32_t)(rem * GM_CQ_NB / cmax) : GM_CQ_NB - 1;
         const uint32_t t = add_agent(bq + b * 32 + 1, 1u) % (uint32_t)q.cap;
-        st_agent(ring + (size_t)b * q.cap + t, ((rem > 0xFFFFFFFFull ? 0xFFFFFFFFull : rem) << 32) | ((uint64_t)env + 1u));
+        __hip_atomic_store(ring + (size_t)b * q.cap + t,
+                           ((rem > 0xFFFFFFFFull ? 0xFFFFFFFFull : rem) << 32) | ((uint64_t)env + 1u), __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     __syncthreads();   // LDS image reused by the next pick
@@ -2600,7 +2609,7 @@ __global__ __launch_bounds__(NT, GM_WPS) void gm_step_kernel(
     const uint32_t now = (uint32_t)((__builtin_amdgcn_s_memtime() - t_start) >> 6);
     const uint32_t model = 14000u + 19u * (uint32_t)S.work_nefc + 188u * (uint32_t)S.work_mpr +
                            940u * (uint32_t)S.work_newton;
-    cost[env] = (now >> 1) + (model >> 1);
+    cost[n_envs + env] = (now >> 1) + (model >> 1);   // recorded for the next launch's order
   }
   store_state(S, states + env, lane);
 }
@@ -2611,7 +2620,7 @@ __global__ __launch_bounds__(NT, GM_WPS) void gm_step_kernel(
 // One 1024-thread workgroup; the order only changes which env a workgroup slot runs
 // first, never any result.
 #ifndef GM_CAL_TU   // env-step translation unit only
-extern "C" __global__ __launch_bounds__(1024) void gm_dispatch_order_kernel(const uint32_t* __restrict__ cost,
+extern "C" __global__ __launch_bounds__(1024) void gm_dispatch_order_kernel(uint32_t* __restrict__ cost,
                                                                             int32_t* __restrict__ order, int n,
                                                                             uint32_t* __restrict__ chunk_ctr,
                                                                             unsigned long long* __restrict__ chunk_st) {
@@ -2630,10 +2639,15 @@ extern "C" __global__ __launch_bounds__(1024) void gm_dispatch_order_kernel(cons
   if (t == 0) cmax = 1;
   __syncthreads();
   uint32_t m = 1;
-  for (int i = t; i < n; i += 1024) m = max(m, cost[i]);
+  for (int i = t; i < n; i += 1024) {
+    const uint32_t c = cost[n + i];   // the costs the last launch recorded become current
+    cost[i] = c;
+    m = max(m, c);
+  }
   atomicMax(&cmax, m);
   __syncthreads();
   const uint64_t cm = (uint64_t)cmax + 1;
+  if (chunk_ctr && t == 0) chunk_ctr[GM_CQ_CMAX] = (uint32_t)cm;
   for (int i = t; i < n; i += 1024) {
     const int b = 255 - (int)(((uint64_t)cost[i] * 256) / cm);
     atomicAdd(&cnt[b], 1u);
@@ -3072,6 +3086,7 @@ extern "C" __global__ __launch_bounds__(64) void gm_reset_kernel(
   const uint32_t rng = rec.rng;
   const int ox = rec.old_x, oy = rec.old_y, oz = rec.old_z;
   const int32_t episode = rec.episode + 1;
+  const int32_t newton_caps = rec.newton_caps;   // solver diagnostics survive resets
   {
     static_assert(sizeof(GmEnvState) % 16 == 0 && sizeof(GmEnvHot) % 16 == 0, "records move in 16-byte words");
     for (int i = threadIdx.x; i < GM_HOT_WORDS / 4; i += 64) hot_words[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -3082,6 +3097,7 @@ extern "C" __global__ __launch_bounds__(64) void gm_reset_kernel(
   if (threadIdx.x == 0) {   // the reference's serial reset on lane 0
     s.rng = rng; s.old_x = ox; s.old_y = oy; s.old_z = oz;
     s.episode = episode;
+    s.newton_caps = newton_caps;
     g_reset(s.end); g_reset(s.next);
     for (int k = 0; k < GM_MAX_QPOS; k++) s.qpos[k] = m->qpos0[k];
     s.time = 0; s.last_step_time = 0;

@@ -1039,6 +1039,8 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
   __syncthreads();
   PH(12);
   int it = 0, nls = 0;
+  bool capped = true;   // no Newton point accepted within GM_NEWTON_MAXIT iterations
+  bool ls_cap = false;  // a line search ran GM_NEWTON_MAXLS evaluations without settling
   for (it = 0; it < GM_NEWTON_MAXIT; it++) {
     bool act[4];
 #pragma unroll
@@ -1057,6 +1059,7 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
       for (int e = 0; e < 4; e++) jq[e] = jx[e];
       jql = jxl;
       it++;
+      capped = false;
       break;
     }
     // exact line search along d = x - q (d overwrites x); H~ q formed when first needed
@@ -1075,7 +1078,8 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
     real alpha = 1.0, lo = 0.0, hi = 0.0;
     bool hi_set = false, newton = false, have_prev = false;
     unsigned prev = 0;
-    for (int ls = 0; ls < GM_NEWTON_MAXLS; ls++) {
+    int ls = 0;
+    for (; ls < GM_NEWTON_MAXLS; ls++) {
       nls++;
       unsigned pat = 0;
       real tg[4], th[4];
@@ -1103,6 +1107,7 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
       have_prev = true;
       alpha = an;
     }
+    ls_cap = ls_cap || ls == GM_NEWTON_MAXLS;   // wave-uniform: every exit test above is
     if (lane < nv) {
       S.qacc[lane] = S.qacc[lane] + alpha * S.xs[lane];
       S.Ma[lane] = S.Ma[lane] + alpha * S.Mv[lane];
@@ -1131,6 +1136,7 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
   if (lane == 0) {
     S.work_nefc += nl + 4 * ncon;
     S.work_newton += it;
+    if (capped || ls_cap) S.s.newton_caps += 1;   // (the oracle counts the same, physics.c newton_solve)
     if (prof) { S.tph[28] += nl + 4 * ncon; S.tph[30] += it; S.tph[31] += nls; }
   }
   __syncthreads();

@@ -91,10 +91,11 @@ struct GmGrip {            // luke::Gripper (gripper.h:11-198)
   int32_t cal_steps;             /* calibration launch: substeps to run */             \
   int32_t badqacc;               /* mjWARN_BADQACC: non-finite or |qacc| > 1e10 seen */ \
   int32_t episode;               /* resets since gm_create (keys the spawn draws) */   \
+  int32_t newton_caps;           /* constraint solves that hit GM_NEWTON_MAXIT / _MAXLS */ \
   int32_t pad_end[GM_HOT_PAD];
 
 // pad words so the hot part is a multiple of 16 B (see GM_STATE_WORDS below)
-#define GM_HOT_PAD 2
+#define GM_HOT_PAD 1
 struct GmEnvHot { GM_ENV_HOT_FIELDS };
 
 // The sensor windows (SlidingWindow, mjclass.h:155-241) are the state's tail: GM_RING

@@ -358,7 +358,7 @@ def env_state_dtype():
         ("old_x", "i4"), ("old_y", "i4"), ("old_z", "i4"), ("num_action_steps", "i4"),
         ("termination_signal_sent", "i4"), ("extra_substeps", "i4"), ("obj_type", "i4"), ("obj_index", "i4"),
         ("done", "i4"), ("overflow", "i4"), ("rng", "u4"), ("cal_steps", "i4"), ("badqacc", "i4"),
-        ("episode", "i4"), ("pad_end", "i4", 2),
+        ("episode", "i4"), ("newton_caps", "i4"), ("pad_end", "i4", 1),
         # the sensor windows follow the part the step kernel stages into LDS (GmEnvHot)
         ("ring", "f4", (37, GM_RING))], align=True)
 

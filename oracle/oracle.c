@@ -147,7 +147,8 @@ static int g_step_to(grip_t* g, const grip_t* t, int num) {
   return fin;
 }
 
-/* golden driver, op codes documented in tests/golden/make_gripper_golden.sh */
+/* golden driver: op 0 set_xyz_m_rad, 1 set_xyz_m (both relative to end), 2 next.step_to(end, a),
+ * 3 reset -- the ops of oracle/ref_golden_driver.cpp, fixtures by tests/golden/make_golden.py */
 int or_grip_step_sequence(const double* cmds, int n, double* out) {
   grip_t end, next;
   g_reset(&end); g_reset(&next);
@@ -331,6 +332,7 @@ struct or_env {
   /* calibration (curve_validation tip load, mjWARN_BADQACC) */
   double tip_force;
   int badqacc;
+  int newton_caps;                 /* solves that hit GM_NEWTON_MAXIT / _MAXLS (GmEnvState::newton_caps) */
 };
 
 size_t or_sizeof(void) { return sizeof(or_env); }
@@ -1510,7 +1512,7 @@ or_env* or_create(const gm_model* m, const gm_config* c, const gm_object* object
   e->weld_locks = g_weld_locks;
   e->rng = lcg_seed((uint64_t)c->s.random_seed + (uint64_t)env_id * 1000003ull);
   /* settle with the first object parked at the keyframe pose */
-  topo_init(e);
+  if (topo_init(e) != 0) { free(e); return NULL; }
   if (e->nobj > 0) { apply_object(&e->m, &e->objs[0]); object_invweight(e); }
   settle(e);
   e->old_x = e->old_y = e->old_z = 0;
@@ -1670,6 +1672,7 @@ int or_import_state(or_env* e, const void* state) {
   e->rng = s->rng;
   e->tip_force = s->tip_force;
   e->badqacc = s->badqacc;
+  e->newton_caps = s->newton_caps;
   e->last_done = s->done;
   e->last_reward = s->reward;
   e->episode = s->episode;
@@ -1728,6 +1731,7 @@ void or_export_state(const or_env* e, void* state) {
   s->overflow = e->overflow;
   s->rng = e->rng;
   s->badqacc = e->badqacc;
+  s->newton_caps = e->newton_caps;
   s->done = e->last_done;
   s->reward = e->last_reward;
   s->episode = e->episode;

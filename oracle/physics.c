@@ -17,7 +17,7 @@
 /* ---------------------------------------------------------------- topology
  * The canonical gripper tree as the device lays it out (gm_capi.hip build_topo): finger f
  * chain position p (1..CL) on scan lane 16 f + p, base on lane 48, palm 49, object 50. */
-static void topo_init(or_env* e) {
+static int topo_init(or_env* e) {   /* 0, or -1: a contact pair the solver cannot take */
   const gm_model* m = &e->m;
   otopo* T = &e->T;
   memset(T, 0, sizeof(*T));
@@ -91,12 +91,18 @@ static void topo_init(or_env* e) {
     else if (with_gnd && !with_obj) g = (a == m->geom_ground) ? bgeom : a;
     if (g < 0) continue;
     const int b = m->geom_body[g];
+    int assigned = 0;
     for (int l = 0; l < 64; l++) {
       if (T->lane_body[l] != b || l == 50) continue;
       int* slot = with_obj ? T->lane_opair[l] : T->lane_gpair[l];
       if (slot[0] < 0) slot[0] = pr; else slot[1] = pr;
+      assigned = 1;
     }
+    /* gm_capi.hip build_topo rejects the same: the Hessian composites reach a contact only
+     * through its gripper body's scan lane */
+    if (!assigned) return -1;
   }
+  return 0;
 }
 
 /* ---------------------------------------------------------------- small helpers */
@@ -1674,7 +1680,7 @@ static void newton_solve(or_env* e) {
   int act[NE], actx[NE];
   for (int i = 0; i < nv; i++) q[i] = e->qacc_warm[i];
   rows_jar(e, q, jq);
-  int it = 0;
+  int it = 0, capped = 1, ls_cap = 0;
   e->stat_ls = 0;
   for (it = 0; it < GM_NEWTON_MAXIT; it++) {
     for (int r = 0; r < nefc; r++) act[r] = row_active(e, r, jq[r]);
@@ -1688,6 +1694,7 @@ static void newton_solve(or_env* e) {
       for (int i = 0; i < nv; i++) q[i] = xv[i];
       for (int r = 0; r < nefc; r++) jq[r] = jx[r];
       it++;
+      capped = 0;
       break;
     }
     /* exact line search along d = x - q.  H~ q is formed here, when first needed: the
@@ -1704,7 +1711,8 @@ static void newton_solve(or_env* e) {
     double alpha = 1.0, lo = 0.0, hi = 0.0;
     int hi_set = 0, newton = 0, have_prev = 0;
     int prev[NE];
-    for (int ls = 0; ls < GM_NEWTON_MAXLS; ls++) {
+    int ls = 0;
+    for (; ls < GM_NEWTON_MAXLS; ls++) {
       e->stat_ls++;
       int pat[NE], same_piece = 1;
       for (int r = 0; r < nefc; r++) {
@@ -1728,10 +1736,14 @@ static void newton_solve(or_env* e) {
       have_prev = 1;
       alpha = an;
     }
+    if (ls == GM_NEWTON_MAXLS) ls_cap = 1;
     for (int i = 0; i < nv; i++) { q[i] = q[i] + alpha * d[i]; Ma[i] = Ma[i] + alpha * Mv[i]; }
     for (int r = 0; r < nefc; r++) jq[r] = jq[r] + alpha * dj[r];
   }
   e->stat_it = it;
+  /* a solve that ran out of iterations, or a line search out of evaluations, is counted
+   * (GmEnvState::newton_caps; the device counts the same) */
+  if (capped || ls_cap) e->newton_caps += 1;
   /* constraint forces at the solution, contact-frame forces (mj_contactForce, pyramid) */
   for (int r = 0; r < nefc; r++) {
     const double j = jq[r];

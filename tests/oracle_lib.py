@@ -17,8 +17,16 @@ ORACLE_DIR = os.path.join(REPO, "oracle")
 ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
 
 
+# every source the oracle is compiled from (oracle/Makefile's liboracle.so prerequisites)
+ORACLE_DEPS = [os.path.join(ORACLE_DIR, f) for f in ("oracle.c", "physics.c", "oracle.h", "Makefile")] + \
+    [os.path.join(REPO, "gripper-mujoco_amd", "csrc", f) for f in ("gm_math.h", "gm_state.h")] + \
+    [os.path.join(REPO, "include", f) for f in ("gripper_mi355x.h", "gm_settings.def")]
+
+
 def build_oracle():
-    if not os.path.exists(ORACLE_LIB) or os.path.getmtime(ORACLE_LIB) < os.path.getmtime(os.path.join(ORACLE_DIR, "oracle.c")):
+    stale = not os.path.exists(ORACLE_LIB) or any(
+        os.path.exists(d) and os.path.getmtime(d) > os.path.getmtime(ORACLE_LIB) for d in ORACLE_DEPS)
+    if stale:
         subprocess.run(["make", "-s", "-C", ORACLE_DIR, os.path.join(ORACLE_DIR, "liboracle.so")], check=True)
     return ORACLE_LIB
 

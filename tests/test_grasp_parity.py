@@ -84,7 +84,7 @@ def compare_step(gm, ol, env, snap):
         f"(envs {bad_obs[:8]})")
     np.testing.assert_array_equal(snap["done"].astype(np.uint8), done_o, err_msg=f"done flags, step {snap['k']}")
     for f in ("bev_row", "bev_abs", "lev_row", "lev_abs", "num_action_steps", "old_x", "old_y", "old_z",
-              "lock_active", "rng", "ring_i"):
+              "lock_active", "rng", "ring_i", "newton_caps"):
         np.testing.assert_array_equal(dv[f], ov[f], err_msg=f"{f}, step {snap['k']}")
     for g in ("end", "next"):
         for f in ("sx", "sy", "sz"):
@@ -167,6 +167,9 @@ def test_c3_grasp_states_4096(gm, ol):
     assert sum(r["done"] for r in rep) > 0, "no env reached done == 1"
     assert sum(s["n_big"] for s in sub) > 0, "no constraint problem with nefc > 32 was checked"
     assert sum(s["n_boxbox_manifold_envs"] for s in sub) > 100, "too few multi-point box-box grasps were checked"
+    # every constraint solve of the rollout converged: no Newton solve ran out of
+    # iterations (GM_NEWTON_MAXIT) and no line search out of evaluations (GM_NEWTON_MAXLS)
+    assert int(last["newton_caps"].sum()) == 0, f"{int((last['newton_caps'] > 0).sum())} envs hit a solver cap"
 
 
 def test_c2_single_cylinder_256(gm, ol):

@@ -183,19 +183,31 @@ def test_gpu_spawn_into_scene_matches_oracle(world):
 
 
 def grid_params(gm, index, grid):
-    """MjEnv's spawn params, or the largest grids the reset kernel's LDS shuffle buffers
-    hold (31 x 31 = 961 of GM_SPAWN_MAX_XY = 1024 xy points, 181 of GM_SPAWN_MAX_ROT = 256
-    rotations)."""
+    """MjEnv's spawn params; large grids (31 x 31 = 961 xy points, 181 rotations); or grids
+    at exactly the reset kernel's LDS shuffle-buffer capacity, where an off-by-one would
+    overrun them (32 x 32 = GM_SPAWN_MAX_XY = 1024 xy points, GM_SPAWN_MAX_ROT = 256
+    rotations: an even count, so the shuffle's leading single swap runs at the bound)."""
     p = mjenv_params(gm, index)
     if grid == "max":
         p.xrange = p.yrange = 15e-3
         p.xy_increment = 1e-3
         p.rot_increment = np.pi / 180.0
+    elif grid == "exact":
+        p.xrange = p.yrange = 15.7e-3
+        p.xy_increment = 1e-3
+        p.rot_increment = np.pi / 255.3
     return p
 
 
+def grid_counts(p):
+    """spawn_into_scene's grid sizes, truncated as the device and the oracle do (double)"""
+    nx = int(2 * p.xrange / p.xy_increment + 1)
+    ny = int(2 * p.yrange / p.xy_increment + 1)
+    return nx * ny, int(2 * p.rotrange / p.rot_increment + 1)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("grid", ["mjenv", "max"])
+@pytest.mark.parametrize("grid", ["mjenv", "max", "exact"])
 def test_gpu_reset_with_scene_spawn_matches_oracle(world, grid):
     """gm_set_scene_spawn: resets place objects the MjEnv._spawn_object way
     (MjEnv.py:1177-1267) on the device -- reset, then spawn_into_scene(spawn[e].index) --
@@ -208,10 +220,11 @@ def test_gpu_reset_with_scene_spawn_matches_oracle(world, grid):
     s = gm.canonical_settings(noise=True, seed=12)
     env = gm.BatchedGripperEnv(n, object_set="set6_synthetic", settings=s, seed=12)
     p = grid_params(gm, 0, grid)
+    nxy, nr = grid_counts(p)
     if grid == "max":
-        nxy = int(2 * p.xrange / p.xy_increment + 1) * int(2 * p.yrange / p.xy_increment + 1)
-        nr = int(2 * p.rotrange / p.rot_increment + 1)
         assert 900 < nxy <= 1024 and 150 < nr <= 256, (nxy, nr)
+    elif grid == "exact":
+        assert (nxy, nr) == (1024, 256), (nxy, nr)
     env.set_scene_spawn(p, max_tries=3)
     sp = env.make_spawn()
     env.reset(spawn=sp)

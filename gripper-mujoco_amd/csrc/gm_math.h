@@ -19,6 +19,13 @@
 #define GM_MATH_FN static inline
 #endif
 
+#if defined(GM_LIBM_TRIG) && !defined(__HIPCC__)
+/* the oracle's libm variant (oracle/Makefile liboracle_libm.so, test infrastructure):
+ * glibc's own sin / cos, to show the shared kernel below is not what makes device and
+ * oracle agree (tests/test_physics_independent.py) */
+#include <math.h>
+GM_MATH_FN void gm_sincos(double x, double* s, double* c) { *s = sin(x); *c = cos(x); }
+#else
 GM_MATH_FN void gm_sincos(double x, double* s, double* c) {
   const double invpio2 = 6.36619772367581382433e-01;
   const double pio2_1 = 1.57079632673412561417e+00;   /* first 33 bits of pi/2 */
@@ -46,6 +53,7 @@ GM_MATH_FN void gm_sincos(double x, double* s, double* c) {
     default: *s = -cs; *c = sn; break;
   }
 }
+#endif
 
 GM_MATH_FN double gm_sin(double x) { double s, c; gm_sincos(x, &s, &c); return s; }
 GM_MATH_FN double gm_cos(double x) { double s, c; gm_sincos(x, &s, &c); return c; }

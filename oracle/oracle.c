@@ -1596,6 +1596,79 @@ void or_debug_substep(or_env* e, int32_t* ncon, double* contact, double* efc_for
   if (obj_wrench) or_object_net_wrench(e, obj_wrench);
 }
 
+/* ---- hooks for the independent physics checks (tests/test_physics_independent.py) ----
+ * or_dynamics: the engine's kinematics, joint-space inertia and bias at the env's current
+ * state -- body poses, the dense smooth matrix H~ (M + armature + h (D + Kd) + h^2 Kp, from
+ * the tree blocks), its diagonal additions, and qfrc_bias (RNE: Coriolis, centrifugal,
+ * gravity); the test compares them with a natural-order Jacobian formulation. */
+void or_dynamics(or_env* e, double* xpos, double* xquat, double* H, double* add, double* bias) {
+  const gm_model* m = &e->m;
+  extern int g_explicit_pd;
+  fk(e);
+  crb_rne(e);
+  mass_and_forces(e);
+  const int nv = m->nv;
+  if (xpos) for (int b = 0; b < m->nbody; b++) for (int k = 0; k < 3; k++) xpos[3 * b + k] = e->xpos[b][k];
+  if (xquat) for (int b = 0; b < m->nbody; b++) for (int k = 0; k < 4; k++) xquat[4 * b + k] = e->xquat[b][k];
+  if (H) {
+    static double Hd[NV][NV];
+    dense_H(e, Hd);
+    for (int i = 0; i < nv; i++) for (int j = 0; j < nv; j++) H[i * nv + j] = Hd[i][j];
+  }
+  for (int d = 0; d < nv; d++) {
+    const double h = m->timestep;
+    double a = e->T.dof_arm[d] + h * e->T.dof_dsum[d];
+    a += h * h * e->T.dof_ksum[d];
+    if (g_explicit_pd) a = e->T.dof_arm[d] + h * e->T.dof_damp[d];
+    if (add) add[d] = a;
+    if (bias) bias[d] = dot6(e->cdof[d], e->cfrc[m->dof_body[d]]);
+  }
+}
+/* or_collide: the engine's narrowphase for one canonical pair (geom1 type <= geom2 type),
+ * geoms given by type, size, centre and row-major rotation; up to 8 contacts as
+ * [dist, pos[3], normal[3]] (normal from geom1 to geom2); returns the count. */
+int or_collide(int type1, const double* size1, const double* c1, const double* R1, int type2, const double* size2,
+               const double* c2, const double* R2, double mpr_tol, int mpr_it, double* out) {
+  geomv_t A, B;
+  A.type = type1; B.type = type2;
+  for (int k = 0; k < 3; k++) { A.size[k] = size1[k]; A.c[k] = c1[k]; B.size[k] = size2[k]; B.c[k] = c2[k]; }
+  for (int k = 0; k < 9; k++) { A.R[k] = R1[k]; B.R[k] = R2[k]; }
+  A.rbound = B.rbound = 1e9; A.friction = B.friction = 1.0;
+  hit_t hs[8];
+  int n = 0;
+  hit_t h;
+  if (A.type == GM_GEOM_PLANE) {
+    if (B.type == GM_GEOM_SPHERE) { if (plane_sphere(&A, &B, &h)) hs[n++] = h; }
+    else if (B.type == GM_GEOM_BOX) {
+      for (int i = 0; i < 8 && n < 4; i++) if (plane_box_point(&A, &B, i, &h)) hs[n++] = h;
+    } else if (B.type == GM_GEOM_CYLINDER) {
+      cylframe_t cf;
+      cyl_frame(&A, &B, &cf);
+      for (int i = 0; i < 8 && n < 4; i++) if (plane_cyl_point(&A, &B, &cf, i, &h)) hs[n++] = h;
+    }
+  } else if (A.type == GM_GEOM_SPHERE && B.type == GM_GEOM_BOX) {
+    if (sphere_box(&A, &B, &h)) hs[n++] = h;
+  } else if (A.type == GM_GEOM_BOX && B.type == GM_GEOM_BOX) {
+    bbox_t S;
+    bb_setup(&A, &B, &S);
+    if (S.kind == 1) {
+      for (int i = 0; i < BB_NCAND && n < 8; i++) {
+        double P[3], depth;
+        if (bb_face_cand(&S, i, P, &depth)) { bb_face_hit(&S, P, depth, &h); hs[n++] = h; }
+      }
+    } else if (S.kind == 2) {
+      if (bb_edge_hit(&S, &h)) hs[n++] = h;
+    }
+  } else {
+    if (mpr(&A, &B, mpr_tol, mpr_it, &h) && h.dist < 0) hs[n++] = h;
+  }
+  for (int i = 0; i < n; i++) {
+    out[7 * i] = hs[i].dist;
+    for (int k = 0; k < 3; k++) { out[7 * i + 1 + k] = hs[i].pos[k]; out[7 * i + 4 + k] = hs[i].n[k]; }
+  }
+  return n;
+}
+
 /* =====================================================================
  * fp64 state hand-off with the device (GmEnvState, gripper-mujoco_amd/csrc/gm_state.h):
  * the parity tests snapshot the device state at any point of an episode and run the

@@ -55,6 +55,11 @@ void  or_get_eq(const or_env* e, double* eq_qpos);                 /* settled eq
 void  or_debug_substep(or_env* e, int32_t* ncon, double* contact, double* efc_force, double* qacc,
                        double* obj_wrench);
 void  or_object_net_wrench(const or_env* e, double* out);
+/* independent-check hooks: kinematics / H~ / bias at the current state, one narrowphase call */
+void  or_dynamics(or_env* e, double* xpos, double* xquat, double* H, double* add, double* bias);
+int   or_collide(int type1, const double* size1, const double* c1, const double* R1, int type2,
+                 const double* size2, const double* c2, const double* R2, double mpr_tol, int mpr_it,
+                 double* out);
 
 /* fp64 state hand-off with the device's GmEnvState (gripper-mujoco_amd/csrc/gm_state.h) */
 size_t or_state_size(void);

@@ -38,7 +38,27 @@ def lib():
     global _lib
     if _lib is None:
         build_oracle()
-        L = C.CDLL(ORACLE_LIB)
+        _lib = load(ORACLE_LIB)
+    return _lib
+
+
+ORACLE_LIBM = os.path.join(ORACLE_DIR, "liboracle_libm.so")
+
+
+def lib_libm():
+    """The same oracle built with glibc's sin / cos in place of gm_math.h's shared kernel
+    (oracle/Makefile liboracle_libm.so; -DGM_LIBM_TRIG): an independent check that the
+    shared trigonometry is not what makes device and oracle agree."""
+    stale = not os.path.exists(ORACLE_LIBM) or any(
+        os.path.exists(d) and os.path.getmtime(d) > os.path.getmtime(ORACLE_LIBM) for d in ORACLE_DEPS)
+    if stale:
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR, ORACLE_LIBM], check=True)
+    return load(ORACLE_LIBM)
+
+
+def load(path):
+    if True:
+        L = C.CDLL(path)
         vp, i32, f32p, f64p, i32p = C.c_void_p, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_double), C.POINTER(C.c_int32)
         sig = {
             "or_create": (vp, [vp, vp, vp, i32, C.c_int64]),
@@ -80,13 +100,14 @@ def lib():
             "or_set_default_solver": (None, [i32]),
             "or_set_default_weld_locks": (None, [i32]),
             "or_set_solver": (None, [vp, i32]),
+            "or_dynamics": (None, [vp, f64p, f64p, f64p, f64p, f64p]),
+            "or_collide": (i32, [i32, f64p, f64p, f64p, i32, f64p, f64p, f64p, C.c_double, i32, f64p]),
         }
         for n, (r, a) in sig.items():
             f = getattr(L, n)
             f.restype = r
             f.argtypes = a
-        _lib = L
-    return _lib
+    return L
 
 
 def _f32(a):

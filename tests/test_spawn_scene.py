@@ -193,7 +193,7 @@ def grid_params(gm, index, grid):
         p.xy_increment = 1e-3
         p.rot_increment = np.pi / 180.0
     elif grid == "exact":
-        p.xrange = p.yrange = 15.7e-3
+        p.xrange = p.yrange = 15.5e-3   # 2 r / inc + 1 = 32.0 exactly (the host check bounds the product)
         p.xy_increment = 1e-3
         p.rot_increment = np.pi / 255.3
     return p

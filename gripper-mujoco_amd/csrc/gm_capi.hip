@@ -172,13 +172,16 @@ int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
     if (d == m.dof_palm) { kp = m.kp_gripper[2]; kd = m.kd_gripper[2]; tgt = 3; }
     if (d == m.dof_base) { kp = m.kp_base[2]; kd = m.kd_base[2]; tgt = 4; }
     const bool free = m.jnt_type[j] == GM_JNT_FREE;
-    // joint springs are explicit (qfrc_passive), joint damping and the PD gains implicit
-    double add = m.jnt_armature[j] + m.timestep * (m.jnt_damping[j] + kd);
-    if (!free) add += m.timestep * m.timestep * kp;
+    // the constraint solve's matrix: M + armature under MuJoCo's actuator order (the PD
+    // forces explicit, the joint damping implicit in the Euler step, integrate); with the
+    // folded scheme also h (damping + kd) + h^2 kp.  Joint springs are explicit either way.
+    const bool mj = m.mujoco_actuators != 0;
+    double add = m.jnt_armature[j] + (mj ? 0.0 : m.timestep * (m.jnt_damping[j] + kd));
+    if (!free && !mj) add += m.timestep * m.timestep * kp;
     T.dof_add[d] = add;
     T.dof_arm[d] = m.jnt_armature[j];
-    T.dof_dsum[d] = m.jnt_damping[j] + kd;
-    T.dof_ksum[d] = free ? 0.0 : kp;
+    T.dof_dsum[d] = mj ? 0.0 : m.jnt_damping[j] + kd;
+    T.dof_ksum[d] = (free || mj) ? 0.0 : kp;
     T.dof_stiff[d] = free ? 0.0 : m.jnt_stiffness[j];
     T.dof_damp[d] = m.jnt_damping[j];
     T.dof_kp[d] = kp; T.dof_kd[d] = kd; T.dof_target[d] = tgt;

@@ -342,10 +342,20 @@ void gm_default_model_params(gm_model_params* p) {
   p->timestep = 3.187e-3;
   p->pgs_iterations = 24;
   p->collision_half_thickness = 1.5e-3;
-  p->segment_damping = 0.24;
-  p->segment_damping_power = 1.0;
+  // with MuJoCo 2.1.5's actuator order (below) the segment damping law 0.16 N^-0.85
+  // reproduces the reference's stable timesteps at inertia x50 within 7 % (DESIGN.md
+  // section 2, tests/test_calibration.py); the revolute motor's reflected inertia 0.01 kg m^2
+  // keeps its explicit kd = 1 stable (h kd / a < 2 up to the search's 20 ms ceiling)
+  p->segment_damping = 0.16;
+  p->segment_damping_power = 0.85;
   p->segment_armature = 0.0;
   p->segment_armature_power = 0.0;
+  p->mujoco_actuators = 1;
+  p->pad_params = 0;
+  p->actuator_armature[0] = 0.0;     // prismatic (finger_f_prismatic_joint)
+  p->actuator_armature[1] = 0.01;    // revolute (finger_f_revolute_joint)
+  p->actuator_armature[2] = 0.0;     // palm
+  p->actuator_armature[3] = 0.0;     // base Z
 }
 
 int gm_build_model(const gm_model_params* p, gm_model* m) {
@@ -365,6 +375,7 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
   m->hook_angle_degrees = p->hook_angle_degrees;
   m->fingertip_clearance = p->fingertip_clearance;
   m->fixed_first_segment = 1;   // links 2..N+1 carry the N joints (myfunctions.cpp:650-660)
+  m->mujoco_actuators = p->mujoco_actuators ? 1 : 0;
   gm_derive_model_constants(m);
   const double Ls = m->segment_length;
   const double EI = m->finger_EI;
@@ -404,7 +415,7 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
     double ipos[3] = {0, 0, 0.03};
     m->body_base = B.add_body(0, GM_GRP_BASE, pos, id4, 0.5, ipos, in);
     double ax[3] = {0, 0, -1};
-    m->dof_base = B.add_joint(m->body_base, GM_JNT_SLIDE, ax, 0, 0, 0, -1);
+    m->dof_base = B.add_joint(m->body_base, GM_JNT_SLIDE, ax, 0, 0, p->actuator_armature[3], -1);
   }
 
   const double ht = std::max(p->collision_half_thickness, 0.5 * p->finger_thickness);
@@ -419,12 +430,12 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
     return (N * EI) / p->finger_length;
   };
 
-  // segment hinge damping (the MJCF's value is absent): 0.24 / N N m s / rad, i.e. in
-  // proportion to the segment length.  With the springs explicit and the damping implicit
-  // (MuJoCo 2.1.5 Euler), this makes find_highest_stable_timestep reproduce the reference's
-  // own measured stable timesteps (rl/juypter/thesis_plots/mujoco_timesteps.csv, the
-  // t = 0.9 mm, w = 28 mm, inertia x50 column) within a few percent for N = 5..10
-  // (tests/test_calibration.py).
+  // segment hinge damping (the MJCF's value is absent): segment_damping N^-power N m s / rad
+  // (default 0.16 N^-0.85).  With the springs explicit and the damping implicit (MuJoCo
+  // 2.1.5 Euler), this makes find_highest_stable_timestep reproduce the reference's own
+  // measured stable timesteps (rl/juypter/thesis_plots/mujoco_timesteps.csv, the inertia
+  // x50 columns) within a few percent for N = 5..10 (tests/test_calibration.py, DESIGN.md
+  // section 2).
   const double seg_damping = p->segment_damping * std::pow((double)N, -p->segment_damping_power);
   const double seg_armature = p->segment_armature * std::pow((double)N, -p->segment_armature_power);
 
@@ -435,7 +446,7 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
     // intermediate carriage: prismatic "finger_f_prismatic_joint" along r (q = radius x)
     double in_int[3] = {2e-5, 2e-5, 2e-5};
     int bint = B.add_body(m->body_base, GM_GRP_FINGER0 + f, zero3, id4, 0.05, zero3, in_int);
-    m->dof_pris[f] = B.add_joint(bint, GM_JNT_SLIDE, r, 0, 5.0, 0, m->dof_base);
+    m->dof_pris[f] = B.add_joint(bint, GM_JNT_SLIDE, r, 0, 5.0, p->actuator_armature[0], m->dof_base);
     // finger body frame: x down the finger, y radially outward, z = x cross y
     double xb[3] = {0, 0, -1};
     double yb[3] = {r[0], r[1], r[2]};
@@ -457,7 +468,7 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
     int bf = B.add_body(bint, GM_GRP_FINGER0 + f, zero3, qf, mseg, ipos_seg, in_seg);
     m->body_finger[f] = bf;
     double axr[3] = {0, 0, -1};
-    m->dof_rev[f] = B.add_joint(bf, GM_JNT_HINGE, axr, 0, 0.0, 0, m->dof_pris[f]);
+    m->dof_rev[f] = B.add_joint(bf, GM_JNT_HINGE, axr, 0, 0.0, p->actuator_armature[1], m->dof_pris[f]);
     double gpos[3] = {0.5 * Ls, 0, 0};
     double gsz[3] = {0.5 * Ls, ht, hw};
     B.add_geom(bf, GM_GEOM_BOX, GM_CLS_FINGER1 + f, gpos, id4, gsz, 1.0);
@@ -515,7 +526,7 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
     box_inertia(0.1, 0.03, 0.03, 0.004, in);
     m->body_palm = B.add_body(m->body_base, GM_GRP_PALM, zero3, id4, 0.1, zero3, in);
     double ax[3] = {0, 0, -1};
-    m->dof_palm = B.add_joint(m->body_palm, GM_JNT_SLIDE, ax, 0, 10.0, 0, m->dof_base);
+    m->dof_palm = B.add_joint(m->body_palm, GM_JNT_SLIDE, ax, 0, 10.0, p->actuator_armature[2], m->dof_base);
     double gpos[3] = {0, 0, -(p->finger_length - 165e-3)};
     double gsz[3] = {0.03, 0.03, 0.004};
     B.add_geom(m->body_palm, GM_GEOM_BOX, GM_CLS_PALM, gpos, id4, gsz, 1.0);

@@ -1295,7 +1295,11 @@ __device__ __forceinline__ void integrate(SharedT<CL>& S, const gm_model* __rest
     const bool bad = lane < T->nv && !(fabs(S.qacc[lane]) <= 1e10);
     if (__ballot(bad) != 0ull && lane == 0) S.s.badqacc = 1;
   }
-  if (lane < T->nv) S.s.qvel[lane] += h * S.qacc[lane];
+  // mj_Euler: under MuJoCo's actuator order the joint damping is implicit here
+  // (euler_damping: qacc_e = (M + h D)^-1 (qfrc_smooth + qfrc_constraint) into S.xs)
+  const bool mj = m->mujoco_actuators != 0;
+  if (mj) euler_damping<CL>(S, T, h, lane);
+  if (lane < T->nv) S.s.qvel[lane] += h * (mj ? S.xs[lane] : S.qacc[lane]);
   __syncthreads();
   if (lane < T->nv && lane < T->dof_obj) {
     S.s.qpos[lane] += h * S.s.qvel[lane];   // slides/hinges: qposadr == dofadr before the object

@@ -277,6 +277,23 @@ int64_t gm_model_to_mjcf(const gm_model* m, char* buf, int64_t cap) {
     if (m->body_parent[b] == 0) write_body(w, m, nm, b);
   w.depth--;
   w.line("</worldbody>");
+  // the reference's motors (luke::control writes ctrl[n + i], myfunctions.cpp:1912-2057):
+  // MJCF <motor> actuators on the 8 actuated joints select MuJoCo's explicit actuator path
+  if (m->mujoco_actuators) {
+    w.line("<actuator>");
+    w.depth++;
+    for (int f = 0; f < 3; f++) {
+      const int jp = m->body_jnt[m->dof_body[m->dof_pris[f]]], jr = m->body_jnt[m->dof_body[m->dof_rev[f]]];
+      w.line("<motor name=\"" + nm.joint[jp] + "_motor\" joint=\"" + nm.joint[jp] + "\" gear=\"1\"/>");
+      w.line("<motor name=\"" + nm.joint[jr] + "_motor\" joint=\"" + nm.joint[jr] + "\" gear=\"1\"/>");
+    }
+    for (int d : {m->dof_palm, m->dof_base}) {
+      const int j = m->body_jnt[m->dof_body[d]];
+      w.line("<motor name=\"" + nm.joint[j] + "_motor\" joint=\"" + nm.joint[j] + "\" gear=\"1\"/>");
+    }
+    w.depth--;
+    w.line("</actuator>");
+  }
   w.line("<contact>");
   w.depth++;
   for (int p = 0; p < m->npair; p++)
@@ -351,6 +368,9 @@ int gm_model_from_mjcf(const char* xml, gm_model* out, char* err, int err_cap) {
     else if (x.tag == "contact") contact = &x;
     else if (x.tag == "equality") equality = &x;
     else if (x.tag == "keyframe") keyframe = &x;
+    else if (x.tag == "actuator") {
+      for (auto& a : x.kids) if (a->tag == "motor") m->mujoco_actuators = 1;
+    }
   }
   if (!world) return fail("no <worldbody>");
   // body tree, depth-first in document order (MuJoCo's compiler order)

@@ -1141,3 +1141,108 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
   }
   __syncthreads();
 }
+
+// ------------------------------------------------------------ mj_Euler's implicit damping
+// MuJoCo 2.1.5's actuator order (gm_model::mujoco_actuators): the PD forces are explicit
+// (mass_and_forces), the constraint solve runs on M + armature, and mj_Euler integrates
+// qacc_e = (M + h D)^-1 (qfrc_smooth + qfrc_constraint) = qacc - (M + h D)^-1 (h D qacc)
+// (M qacc = qfrc_smooth + qfrc_constraint at the solve's optimum).  The gripper's M + h D on
+// the factor lanes: each finger chain block leaf-first on its DPP row with the base as the
+// single border column (row_newbcast pivots, as newton_point with a one-wide border), the
+// palm one pivot, the base pivot after the wave-summed Schur complement; the object has no
+// damping and no coupling to the gripper in M, so its rows take no correction.  qacc_e goes
+// to S.xs (free after the solve); oracle/physics.c euler_damping restates it lane for lane.
+template <int CL>
+__device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __restrict__ T, real h, int lane) {
+  const int rowf = lane >> 4, p = lane & 15;
+  const bool chainrow = rowf < 3 && p >= 1 && p <= CL;
+  const bool palm = lane == GM_LANE_PALM_F, base = lane == 48;
+  real L[CL + 1], lb = 0.0, y = 0.0, bb = 0.0;
+#pragma unroll
+  for (int j = 0; j <= CL; j++) L[j] = 0.0;
+  if (chainrow) {
+    const real* H = S.Hf[rowf];
+    const int d = T->dof_f0[rowf] + p - 1;
+    const real hd = h * T->dof_damp[d];
+#pragma unroll
+    for (int j = 1; j <= CL; j++) L[j] = (j <= p) ? H[TRI(p, j)] : 0.0;
+#pragma unroll
+    for (int j = 1; j <= CL; j++) L[j] = (j == p) ? L[j] + hd : L[j];
+    lb = H[TRI(p, 0)];
+    y = hd * S.qacc[d];
+  } else if (palm) {
+    const int d = T->dof_palm;
+    const real hd = h * T->dof_damp[d];
+    L[1] = S.Hp[TRI(1, 1)] + hd;
+    lb = S.Hp[TRI(1, 0)];
+    y = hd * S.qacc[d];
+  } else if (base) {
+    const int d = T->dof_base;
+    const real hd = h * T->dof_damp[d];
+    bb = S.Hbb + hd;
+    y = hd * S.qacc[d];
+  }
+  real invd = 1.0, ub = 0.0;
+  if (lane < 48) {
+#pragma unroll
+    for (int k = CL; k >= 1; k--) {
+      const real ihk = rcp_n(row_bcast(L[k], k));
+      real hk[CL + 1];
+#pragma unroll
+      for (int j = 1; j < k; j++) hk[j] = row_bcast(L[j], k);
+      const real hkb = row_bcast(lb, k);
+      const bool upd = p >= 1 && p < k, piv = p == k;
+      real Hpk = 0.0;
+#pragma unroll
+      for (int j = 1; j < k; j++) Hpk = (p == j) ? hk[j] : Hpk;
+      const real a = Hpk * ihk;
+      const real aa = upd ? a : 0.0;
+      const real sc = piv ? ihk : 1.0;
+      ub = piv ? lb : ub;
+#pragma unroll
+      for (int j = 1; j < k; j++) L[j] = (L[j] - hk[j] * aa) * sc;
+      lb = (lb - hkb * aa) * sc;
+      L[k] = upd ? a : L[k];
+      invd = piv ? ihk : invd;
+    }
+  } else if (palm) {
+    const real ih = rcp_n(L[1]);
+    ub = lb;
+    lb = lb * ih;
+    invd = ih;
+  }
+  const bool part = chainrow || palm;
+  const real sch = wave_sum(part ? lb * ub : 0.0);
+  // forward over the chains, leaf first
+  if (lane < 48) {
+#pragma unroll
+    for (int k = CL; k >= 1; k--) {
+      const real yk = row_bcast(y, k);
+      const real Lc = (p >= 1 && p < k) ? L[k] : 0.0;
+      y = y - Lc * yk;
+    }
+  }
+  const real fs = wave_sum(part ? lb * y : 0.0);
+  const real xb = readlane_real((y - fs) * rcp_n(bb - sch), 48);
+  // back substitution: D^-1, the border column, then the chains root -> leaf
+  y = y * invd;
+  y = y - lb * xb;
+  if (lane < 48) {
+#pragma unroll
+    for (int j = 1; j < CL; j++) {
+      const real xj = row_bcast(y, j);
+      const real Lr = (j < p) ? L[j] : 0.0;
+      y = y - Lr * xj;
+    }
+  }
+  if (chainrow) {
+    const int d = T->dof_f0[rowf] + p - 1;
+    S.xs[d] = S.qacc[d] - y;
+  } else if (palm) {
+    S.xs[T->dof_palm] = S.qacc[T->dof_palm] - y;
+  } else if (base) {
+    S.xs[T->dof_base] = S.qacc[T->dof_base] - xb;
+  }
+  if (lane < 6) S.xs[T->dof_obj + lane] = S.qacc[T->dof_obj + lane];
+  __syncthreads();
+}

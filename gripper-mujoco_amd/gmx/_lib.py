@@ -104,7 +104,8 @@ class ModelParams(C.Structure):
                 ("timestep", C.c_double), ("pgs_iterations", C.c_int32),
                 ("collision_half_thickness", C.c_double), ("segment_damping", C.c_double),
                 ("segment_damping_power", C.c_double), ("segment_armature", C.c_double),
-                ("segment_armature_power", C.c_double)]
+                ("segment_armature_power", C.c_double), ("mujoco_actuators", C.c_int32), ("pad_params", C.c_int32),
+                ("actuator_armature", C.c_double * 4)]
 
 
 class Object(C.Structure):

@@ -199,6 +199,15 @@ typedef struct gm_model_params {      /* numerics the MJCF would carry (myfuncti
   double  segment_damping_power;
   double  segment_armature;
   double  segment_armature_power;
+  /* actuators (the reference writes ctrl to MJCF motors, luke::control myfunctions.cpp:1912-2057):
+   * 1 = MuJoCo 2.1.5's order -- the PD forces explicit between mj_step1 and mj_step2, the
+   * constraint solve on M + armature, joint damping implicit in mj_Euler; 0 = the PD gains
+   * and joint damping folded implicitly into the solve's matrix (rounds 1-3) */
+  int32_t mujoco_actuators;
+  int32_t pad_params;
+  /* armature of the actuated joints (prismatic, revolute, palm, base): the motors'
+   * reflected inertia the absent MJCF would carry (invented; DESIGN.md "Model spec") */
+  double  actuator_armature[4];
 } gm_model_params;
 
 typedef struct gm_model {
@@ -279,6 +288,9 @@ typedef struct gm_model {
    * bending direction at the keyframe (world frame, radially outward) */
   int32_t body_tip[3];
   double  tip_dir[3][3];
+  /* gm_model_params.mujoco_actuators */
+  int32_t mujoco_actuators;
+  int32_t pad_model;
 } gm_model;
 
 /* one graspable object (a synthetic object-set entry) */

@@ -1487,10 +1487,6 @@ void or_set_default_solver(int pgs_sweeps) { g_solver_pgs = pgs_sweeps; }
  * two bodies (myfunctions.cpp:1177-1279) instead of the engine's 1-row joint locks */
 static int g_weld_locks = 0;
 void or_set_default_weld_locks(int on) { g_weld_locks = on; }
-/* test variant: MuJoCo 2.1.5's actuator path -- the PD forces explicit, only joint
- * damping implicit in the Euler step (the engine folds kp, kd into H~) */
-int g_explicit_pd = 0;
-void or_set_explicit_pd(int on) { g_explicit_pd = on; }
 void or_set_solver(or_env* e, int pgs_sweeps) { e->solver_pgs = pgs_sweeps; }
 /* solver statistics since creation: solves, Newton iterations, line-search evaluations,
  * max iterations, max contacts generated, constraint rows */
@@ -1603,7 +1599,6 @@ void or_debug_substep(or_env* e, int32_t* ncon, double* contact, double* efc_for
  * gravity); the test compares them with a natural-order Jacobian formulation. */
 void or_dynamics(or_env* e, double* xpos, double* xquat, double* H, double* add, double* bias) {
   const gm_model* m = &e->m;
-  extern int g_explicit_pd;
   fk(e);
   crb_rne(e);
   mass_and_forces(e);
@@ -1619,7 +1614,6 @@ void or_dynamics(or_env* e, double* xpos, double* xquat, double* H, double* add,
     const double h = m->timestep;
     double a = e->T.dof_arm[d] + h * e->T.dof_dsum[d];
     a += h * h * e->T.dof_ksum[d];
-    if (g_explicit_pd) a = e->T.dof_arm[d] + h * e->T.dof_damp[d];
     if (add) add[d] = a;
     if (bias) bias[d] = dot6(e->cdof[d], e->cfrc[m->dof_body[d]]);
   }

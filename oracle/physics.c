@@ -68,8 +68,9 @@ static int topo_init(or_env* e) {   /* 0, or -1: a contact pair the solver canno
     T->dof_grp[d] = m->body_group[b];
     T->dof_p[d] = (m->body_group[b] == GM_GRP_OBJECT) ? d - m->dof_obj : T->body_cpos[b];
     T->dof_arm[d] = m->jnt_armature[j];
-    T->dof_dsum[d] = m->jnt_damping[j] + kd;
-    T->dof_ksum[d] = fr ? 0.0 : kp;
+    /* MuJoCo's actuator order (mujoco_actuators): the solve's matrix is M + armature */
+    T->dof_dsum[d] = m->mujoco_actuators ? 0.0 : m->jnt_damping[j] + kd;
+    T->dof_ksum[d] = (fr || m->mujoco_actuators) ? 0.0 : kp;
     T->dof_stiff[d] = fr ? 0.0 : m->jnt_stiffness[j];
     T->dof_damp[d] = m->jnt_damping[j];
     T->dof_kp[d] = kp; T->dof_kd[d] = kd; T->dof_target[d] = tgt;
@@ -434,10 +435,8 @@ static void mass_and_forces(or_env* e) {
     const int b = m->dof_body[d];
     const int c = T->dof_grp[d];
     const int p = T->dof_p[d];
-    extern int g_explicit_pd;
     double add = T->dof_arm[d] + h * T->dof_dsum[d];
     add += h * h * T->dof_ksum[d];
-    if (g_explicit_pd) add = T->dof_arm[d] + h * T->dof_damp[d];
     const double* cd = e->cdof[d];
     double F[6];
     inert_mul(F, e->Ic[b], cd);
@@ -1860,6 +1859,118 @@ static void ref_pgs_solve(or_env* e, int sweeps) {
  * one physics substep: before_step + step + after_step (physics part),
  * myfunctions.cpp:1864-1908 -> mj_step1 / control / mj_step2 (the engine spec)
  * ===================================================================== */
+/* MuJoCo 2.1.5 mj_Euler's implicit joint damping (mujoco_actuators): qacc_e =
+ * (M + h D)^-1 (qfrc_smooth + qfrc_constraint) = qacc - (M + h D)^-1 (h D qacc), qacc the
+ * solve's (M qacc = qfrc_smooth + qfrc_constraint at its optimum).  The system on the
+ * device's lanes (gm_newton.hip euler_damping): each finger chain block leaf-first LDL^T
+ * on its DPP row with the base as the one border column, the palm one pivot, the base
+ * pivot after the wave-summed Schur complement; the object (no damping, decoupled from the
+ * gripper in M) takes no correction. */
+static void euler_damping(const or_env* e, double* qe) {
+  const gm_model* m = &e->m;
+  const otopo* T = &e->T;
+  const int CL = T->CL;
+  const double h = m->timestep;
+  double L[64][GM_CHAIN + 1], lb[64], ub[64], invd[64], y[64], lane_v[64];
+  for (int l = 0; l < 64; l++) {
+    for (int j = 0; j <= CL; j++) L[l][j] = 0.0;
+    lb[l] = 0.0; ub[l] = 0.0; invd[l] = 1.0; y[l] = 0.0;
+  }
+  for (int f = 0; f < 3; f++)
+    for (int p = 1; p <= CL; p++) {
+      const int l = 16 * f + p, d = T->dof_f0[f] + p - 1;
+      const double hd = h * T->dof_damp[d];
+      for (int j = 1; j <= p; j++) L[l][j] = e->Hf[f][TRI(p, j)];
+      L[l][p] = L[l][p] + hd;
+      lb[l] = e->Hf[f][TRI(p, 0)];
+      y[l] = hd * e->qacc[d];
+    }
+  const int lp = 56, lbase = 48;
+  {
+    const double hd = h * T->dof_damp[m->dof_palm];
+    L[lp][1] = e->Hp[TRI(1, 1)] + hd;
+    lb[lp] = e->Hp[TRI(1, 0)];
+    y[lp] = hd * e->qacc[m->dof_palm];
+  }
+  const double hdb = h * T->dof_damp[m->dof_base];
+  const double bb = e->Hbb + hdb;
+  y[lbase] = hdb * e->qacc[m->dof_base];
+  /* chain factor, pivots CL .. 1, every lane of rows 0..2 in lock step */
+  for (int k = CL; k >= 1; k--) {
+    double hk[3][GM_CHAIN + 1], hkb[3], ihk[3];
+    for (int f = 0; f < 3; f++) {
+      const int lk = 16 * f + k;
+      ihk[f] = 1.0 / L[lk][k];
+      for (int j = 1; j < k; j++) hk[f][j] = L[lk][j];
+      hkb[f] = lb[lk];
+    }
+    for (int l = 0; l < 48; l++) {
+      const int f = l >> 4, p = l & 15;
+      const int upd = p >= 1 && p < k, piv = p == k;
+      double Hpk = 0.0;
+      for (int j = 1; j < k; j++) Hpk = (p == j) ? hk[f][j] : Hpk;
+      const double a = Hpk * ihk[f];
+      const double aa = upd ? a : 0.0;
+      const double sc = piv ? ihk[f] : 1.0;
+      if (piv) ub[l] = lb[l];
+      for (int j = 1; j < k; j++) L[l][j] = (L[l][j] - hk[f][j] * aa) * sc;
+      lb[l] = (lb[l] - hkb[f] * aa) * sc;
+      L[l][k] = upd ? a : L[l][k];
+      if (piv) invd[l] = ihk[f];
+    }
+  }
+  {
+    const double ih = 1.0 / L[lp][1];
+    ub[lp] = lb[lp];
+    lb[lp] = lb[lp] * ih;
+    invd[lp] = ih;
+  }
+  /* Schur complement of the base: the wave sum of lb ub over the chain rows and the palm */
+  for (int l = 0; l < 64; l++) {
+    const int f = l >> 4, p = l & 15;
+    const int part = (f < 3 && p >= 1 && p <= CL) || l == lp;
+    lane_v[l] = part ? lb[l] * ub[l] : 0.0;
+  }
+  const double sch = butterfly64(lane_v);
+  /* forward over the chains (leaf first) */
+  for (int k = CL; k >= 1; k--)
+    for (int f = 0; f < 3; f++) {
+      const double yk = y[16 * f + k];
+      for (int p = 1; p <= CL; p++) {
+        const double Lc = (p < k) ? L[16 * f + p][k] : 0.0;
+        y[16 * f + p] = y[16 * f + p] - Lc * yk;
+      }
+    }
+  for (int l = 0; l < 64; l++) {
+    const int f = l >> 4, p = l & 15;
+    const int part = (f < 3 && p >= 1 && p <= CL) || l == lp;
+    lane_v[l] = part ? lb[l] * y[l] : 0.0;
+  }
+  const double fs = butterfly64(lane_v);
+  const double xb = (y[lbase] - fs) * (1.0 / (bb - sch));
+  /* back substitution: D^-1, the border, then the chains root -> leaf */
+  for (int f = 0; f < 3; f++) {
+    for (int p = 1; p <= CL; p++) {
+      const int l = 16 * f + p;
+      y[l] = y[l] * invd[l];
+      y[l] = y[l] - lb[l] * xb;
+    }
+    for (int j = 1; j < CL; j++) {
+      const double xj = y[16 * f + j];
+      for (int p = 1; p <= CL; p++) {
+        const double Lr = (j < p) ? L[16 * f + p][j] : 0.0;
+        y[16 * f + p] = y[16 * f + p] - Lr * xj;
+      }
+    }
+  }
+  y[lp] = y[lp] * invd[lp] - lb[lp] * xb;
+  for (int d = 0; d < m->nv; d++) qe[d] = e->qacc[d];
+  for (int f = 0; f < 3; f++)
+    for (int p = 1; p <= CL; p++) qe[T->dof_f0[f] + p - 1] = e->qacc[T->dof_f0[f] + p - 1] - y[16 * f + p];
+  qe[m->dof_palm] = e->qacc[m->dof_palm] - y[lp];
+  qe[m->dof_base] = e->qacc[m->dof_base] - xb;
+}
+
 static void physics_substep(or_env* e) {
   const gm_model* m = &e->m;
   const double h = m->timestep;
@@ -1879,8 +1990,13 @@ static void physics_substep(or_env* e) {
   e->stat_nefc_sum += e->nefc;
   /* mj_checkAcc -> mjWARN_BADQACC (is_sim_unstable, myfunctions.cpp:4233-4242) */
   for (int d = 0; d < m->nv; d++) if (!(fabs(e->qacc[d]) <= 1e10)) e->badqacc = 1;
-  /* semi-implicit Euler (mj_Euler) */
-  for (int d = 0; d < m->nv; d++) e->qvel[d] += h * e->qacc[d];
+  /* semi-implicit Euler (mj_Euler): with MuJoCo's actuator order the joint damping is
+   * implicit here, qacc_e = (M + h D)^-1 (qfrc_smooth + qfrc_constraint) (euler_damping);
+   * the folded scheme integrates the solve's qacc directly */
+  double qe[NV];
+  if (m->mujoco_actuators) euler_damping(e, qe);
+  else for (int d = 0; d < m->nv; d++) qe[d] = e->qacc[d];
+  for (int d = 0; d < m->nv; d++) e->qvel[d] += h * qe[d];
   for (int d = 0; d < m->dof_obj; d++) e->qpos[d] += h * e->qvel[d];
   {
     const int qa = m->dof_obj, da = m->dof_obj;

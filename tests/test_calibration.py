@@ -192,11 +192,14 @@ def test_gpu_timestep_search_matches_oracle_over_segments(world):
         assert tr_d == tr_o and ms_d == ms_o, n
 
 
-# Stated bands over the whole CSV (4 inertia scalings x 3 (t, w) x N = 5..10): the
-# engine's stable timestep depends on the inertia scaling much less than MuJoCo's did
-# (its proximal-hinge mode is damping-limited; tools/fit_timesteps.py and DESIGN.md
-# section 2 record the fits tried), so the low-scaling columns sit high and x100 low.
-CSV_BANDS = {1.0: (0.95, 2.75), 10.0: (0.95, 1.80), 50.0: (0.92, 1.08), 100.0: (0.70, 1.00)}
+# Stated bands over the whole CSV (4 inertia scalings x 3 (t, w) x N = 5..10).  Only the
+# baselines' x50 column is pinned (within 8 %, the test above).  The engine's stable step
+# barely depends on the inertia scaling: with the segment damping implicit in mj_Euler the
+# limiting proximal-hinge mode is damping-limited (h < 2 c / k, independent of the mass),
+# where MuJoCo's moved 2.9x from x1 to x100 -- the absent MJCF's inertia distribution
+# (tools/fit_timesteps.py).  So the low-scaling columns sit high and
+# x100 low, measured under MuJoCo's actuator order (the default model):
+CSV_BANDS = {1.0: (2.0, 3.5), 10.0: (1.45, 2.25), 50.0: (0.92, 1.08), 100.0: (0.70, 0.87)}
 
 
 def test_timestep_search_all_72_points_within_stated_bands(world):
@@ -215,20 +218,17 @@ def test_timestep_search_all_72_points_within_stated_bands(world):
         lo, hi = CSV_BANDS[s]
         assert lo <= ms / ref <= hi, f"N={n} t={t} w={w} x{s:g}: {ms:.3f} ms vs reference {ref:.3f} ms"
         got[(n, t, w, s)] = ms
-    # the reference's orderings hold: more inertia scaling -> larger stable step, more
-    # segments -> smaller
+    # the reference's ordering in N holds everywhere (more segments -> smaller stable
+    # step); its ordering in the inertia scaling does not (the damping-limited mode above)
     for (n, t, w, s), ms in got.items():
-        for s2 in (10.0, 50.0, 100.0):
-            if s2 > s:
-                assert got[(n, t, w, s2)] >= ms, (n, t, w, s, s2)
         if n < 10:
             assert got[(n + 1, t, w, s)] < ms, (n, t, w, s)
 
 
 # validate_curve_under_force's retry branch (mjclass.cpp:4073-4090), forced: at a 4.8 ms
-# model step with a 10x saturation load the loaded 50 s settle reaches mjWARN_BADQACC, the
+# model step with a 50x saturation load the loaded 50 s settle reaches mjWARN_BADQACC, the
 # run is repeated at 0.8x the step and settles.
-RETRY_DT, RETRY_SAT = 4.8e-3, 10.0
+RETRY_DT, RETRY_SAT = 4.8e-3, 50.0
 
 
 def retry_world(gm):
@@ -274,19 +274,37 @@ def test_gpu_gauge_calibration_retry_matches_oracle(world):
     assert dev.bending_normalise == pytest.approx(ref.bending_normalise, rel=1e-4)
 
 
-def test_explicit_pd_is_unstable_so_the_engine_integrates_it_implicitly(world):
-    """MuJoCo 2.1.5's actuator path keeps the PD forces explicit (only joint damping is
-    implicit).  With this model that is unstable at every timestep the search tries, down
-    to 50 us (oracle variant or_set_explicit_pd), which is why the engine folds kp and kd
-    into H~; the engine's own search finds the reference's 4.3 ms."""
+def model_search_ms(gm, n_seg, **overrides):
+    """search_ms at t 0.9 mm, w 28 mm, inertia x50 with gm_model_params overrides"""
     import ctypes as C
+    p = gm.ModelParams()
+    gm.load_library().gm_default_model_params(C.byref(p))
+    p.n_seg, p.finger_thickness, p.finger_width = n_seg, 0.9e-3, 28e-3
+    p.segment_inertia_scaling, p.timestep = 50.0, 1.0e-3
+    for k, v in overrides.items():
+        if k == "revolute_armature":
+            p.actuator_armature[1] = v
+        else:
+            setattr(p, k, v)
+    model = gm.ModelBlob(p)
+    cfg = gm.ConfigBlob(gm.canonical_settings(noise=False, seed=1), model)
+    cal, trace = oracle_lib.calibrate(model, cfg, gm.make_object_set("set1_synthetic", 1), 1)
+    return cal.search_timestep * 1e3, trace
+
+
+def test_mujoco_actuator_order_needs_the_revolute_motor_inertia(world):
+    """MuJoCo 2.1.5's actuator path (the default, gm_model_params.mujoco_actuators): the
+    PD forces explicit, the constraint solve on M + armature, the joint damping implicit
+    in mj_Euler.  The revolute motor's explicit kd = 1 on the bare finger link (~1.5e-5
+    kg m^2) is unstable at every timestep the search tries, down to 50 us; the motor's
+    reflected inertia (actuator armature 0.01 kg m^2, DESIGN.md "Model spec") makes the
+    explicit path stable and the search lands on the reference's 4.3 ms."""
     gm = world[0]
-    L = oracle_lib.lib()
-    L.or_set_explicit_pd.argtypes = [C.c_int]
-    try:
-        L.or_set_explicit_pd(1)
-        with pytest.raises(RuntimeError):
-            search_ms(gm, 8, 0.9, 28.0, 50.0)
-    finally:
-        L.or_set_explicit_pd(0)
-    assert search_ms(gm, 8, 0.9, 28.0, 50.0)[0] == pytest.approx(4.3, rel=0.08)
+    with pytest.raises(RuntimeError):
+        model_search_ms(gm, 8, revolute_armature=0.0)
+    assert model_search_ms(gm, 8)[0] == pytest.approx(4.3, rel=0.08)
+    # the rounds-1-3 scheme (PD gains and joint damping folded into the solve's matrix,
+    # the r03 damping law) stays available and stable
+    ms, _ = model_search_ms(gm, 8, mujoco_actuators=0, revolute_armature=0.0, segment_damping=0.24,
+                            segment_damping_power=1.0)
+    assert ms == pytest.approx(4.35, rel=0.08)

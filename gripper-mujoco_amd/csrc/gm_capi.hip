@@ -16,6 +16,7 @@
 #include <map>
 #include <string>
 #include <vector>
+#include <mutex>
 
 #include "gm_kernels.hip"
 #include "gm_policy.hip"
@@ -277,6 +278,14 @@ int build_topo(const gm_model& m, GmTopo& T, std::string& err) {
 
 }  // namespace
 
+namespace {
+// the process-wide settle cache of gm_set_settle_cache (calibrate_reset's first_call)
+std::mutex g_settle_mu;
+bool g_settle_cache_on = false, g_settle_valid = false;
+int g_settle_nseg = -1;
+double g_settle_eq[GM_MAX_QPOS];
+}  // namespace
+
 extern "C" {
 
 const char* gm_version(void) { return "gripper-mi355x 0.1 (gfx950, one-wave-per-env fused env-step)"; }
@@ -385,11 +394,32 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   HIPCHK(c, hipMemcpyAsync(c->d_cfg, &c->cfg, sizeof(gm_config), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->d_topo, &c->topo, sizeof(GmTopo), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->d_objs, objects, sizeof(gm_object) * (size_t)n_objects, hipMemcpyHostToDevice, c->stream));
-  // one-time calibrate_reset settle (myfunctions.cpp:1470-1505) on env 0
-  hipLaunchKernelGGL(gm_settle_init_kernel, dim3(1), dim3(1), 0, c->stream, c->d_state, c->d_model, c->d_topo, c->d_objs);
-  DebugOut dbg{nullptr, nullptr, nullptr, nullptr, nullptr};
-  HIPCHK(c, launch_step(c, 1, 1, 1, dbg));
-  HIPCHK(c, hipMemcpyAsync(c->d_eq, reinterpret_cast<char*>(c->d_state) + offsetof(GmEnvHot, qpos), sizeof(double) * GM_MAX_QPOS, hipMemcpyDeviceToDevice, c->stream));
+  // one-time calibrate_reset settle (myfunctions.cpp:1470-1505) on env 0 -- per context, or,
+  // with gm_set_settle_cache(1), once per process as the reference's function-static
+  // first_call does (myfunctions.cpp:1447): later contexts with the same joint count reuse
+  // the first settle's equilibrium whatever else changed
+  bool from_cache = false;
+  {
+    std::lock_guard<std::mutex> lk(g_settle_mu);
+    if (g_settle_cache_on && g_settle_valid && g_settle_nseg == c->model.n_seg) {
+      HIPCHK(c, hipMemcpyAsync(c->d_eq, g_settle_eq, sizeof(double) * GM_MAX_QPOS, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      from_cache = true;
+    }
+  }
+  if (!from_cache) {
+    hipLaunchKernelGGL(gm_settle_init_kernel, dim3(1), dim3(1), 0, c->stream, c->d_state, c->d_model, c->d_topo, c->d_objs);
+    DebugOut dbg{nullptr, nullptr, nullptr, nullptr, nullptr};
+    HIPCHK(c, launch_step(c, 1, 1, 1, dbg));
+    HIPCHK(c, hipMemcpyAsync(c->d_eq, reinterpret_cast<char*>(c->d_state) + offsetof(GmEnvHot, qpos), sizeof(double) * GM_MAX_QPOS, hipMemcpyDeviceToDevice, c->stream));
+    std::lock_guard<std::mutex> lk(g_settle_mu);
+    if (g_settle_cache_on && !g_settle_valid) {
+      HIPCHK(c, hipMemcpyAsync(g_settle_eq, c->d_eq, sizeof(double) * GM_MAX_QPOS, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      g_settle_valid = true;
+      g_settle_nseg = c->model.n_seg;
+    }
+  }
   int threads = 256, blocks = (n_envs + threads - 1) / threads;
   hipLaunchKernelGGL(gm_init_envs_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, cfg->s.random_seed,
                      (long long)env_offset, n_envs, c->model.timestep);
@@ -564,6 +594,12 @@ int gm_set_random_spawn(gm_ctx* c, int enable, uint64_t seed, int position_noise
   return GM_OK;
 }
 
+void gm_set_settle_cache(int on) {
+  std::lock_guard<std::mutex> lk(g_settle_mu);
+  g_settle_cache_on = on != 0;
+  g_settle_valid = false;        // first_call = true: the next context settles and is kept
+}
+
 // ---------------------------------------------------------------- calibration
 namespace {
 uint32_t fbits(float x) { uint32_t u; std::memcpy(&u, &x, 4); return u; }
@@ -590,7 +626,7 @@ struct CalCtx {
   // reset the first n envs (object 0 at the origin, as MjClass::reset leaves the scene),
   // give env i timestep dt[i], steps[i] substeps and the tip load, run them, read BADQACC
   int run(const std::vector<double>& dt, const std::vector<int32_t>& steps, double tip, std::vector<uint8_t>& bad,
-          bool reset = true) {
+          bool reset = true, int32_t* ran0 = nullptr) {
     const int n = (int)dt.size();
     if (n == 0) return GM_OK;
     if (reset) {
@@ -606,6 +642,9 @@ struct CalCtx {
     HIPCHK(c, gm_cal_launch_read(c->stream, c->d_state, d_bad, n));
     bad.assign(n, 0);
     HIPCHK(c, hipMemcpyAsync(bad.data(), d_bad, n, hipMemcpyDeviceToHost, c->stream));
+    if (ran0)   // substeps env 0 made (GmEnvState::cal_steps after the run)
+      HIPCHK(c, hipMemcpyAsync(ran0, reinterpret_cast<char*>(c->d_state) + offsetof(GmEnvHot, cal_steps), sizeof(int32_t),
+                               hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return GM_OK;
   }
@@ -709,8 +748,12 @@ int gm_calibrate(const gm_model* model, const gm_config* cfg, const gm_object* o
     const int steps_to_make = (int)(time_to_settle / tsd);
     int repeats_done = 1;
     bool first = true;
+    const bool ref_retry = (what & GM_CAL_REFERENCE_RETRY) != 0;
+    int left = steps_to_make;            // the reference's loop index resumes after a retry
+    double tip = (double)bend_gauge_normalise;
     while (true) {
-      rc = k.run({tsd}, {steps_to_make}, (double)bend_gauge_normalise, bad, !first);
+      int32_t ran = 0;
+      rc = k.run({tsd}, {ref_retry ? left : steps_to_make}, tip, bad, !first, &ran);
       if (rc != GM_OK) return rc;
       first = false;
       if (bad[0]) {
@@ -719,6 +762,17 @@ int gm_calibrate(const gm_model* model, const gm_config* cfg, const gm_object* o
         if (repeats_done > 5) {
           fprintf(stderr, "gm_calibrate: curve validation unstable\n");
           return GM_E_RANGE;
+        }
+        if (ref_retry) {
+          // reset() wiped the segment forces; `continue` resumes the step loop after the
+          // unstable step, at the new timestep, unloaded
+          tip = 0.0;
+          left -= ran;
+          if (left <= 0) {   // the unstable step was the last: only the reset remains
+            rc = k.run({tsd}, {0}, 0.0, bad, true);
+            if (rc != GM_OK) return rc;
+            break;
+          }
         }
         continue;
       }

@@ -2562,8 +2562,12 @@ __global__ __launch_bounds__(NT, GM_WPS) void gm_step_kernel(
   const int nsub = settle ? 400 : calib ? S.s.cal_steps : (mode == 2) ? 1 : C->sim_steps_per_action + S.s.extra_substeps;
   // a calibration run starts from a reset's mj_forward pose
   if (calib && lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
-  substep_loop<CL, CAL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m, (const GM_AS_GLOBAL GmTopo*)T,
-                        (const GM_AS_GLOBAL gm_config*)C, lane, prof, nsub, settle, GmPreempt{});
+  const int ran = substep_loop<CL, CAL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
+                                        (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane, prof,
+                                        nsub, settle, GmPreempt{});
+  // a calibration run reports the substeps it made (the unstable one included: the loop
+  // stops right after it, as the reference's retry resumes after it)
+  if (calib && lane == 0) S.s.cal_steps = S.s.badqacc ? ran + 1 : ran;
   if (settle || calib) {
     store_state(S, states + env, lane);
     return;

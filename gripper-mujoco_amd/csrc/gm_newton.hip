@@ -1149,15 +1149,17 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
 // (M qacc = qfrc_smooth + qfrc_constraint at the solve's optimum).  The gripper's M + h D on
 // the factor lanes: each finger chain block leaf-first on its DPP row with the base as the
 // single border column (row_newbcast pivots, as newton_point with a one-wide border), the
-// palm one pivot, the base pivot after the wave-summed Schur complement; the object has no
-// damping and no coupling to the gripper in M, so its rows take no correction.  qacc_e goes
-// to S.xs (free after the solve); oracle/physics.c euler_damping restates it lane for lane.
+// palm one pivot; the base pivot's two sums (Schur complement sum lb ub, forward sum lb y)
+// are one two-value segmented scan per DPP row plus the three row totals and the palm read
+// back as scalars, so the base solve is computed wave-uniformly.  The object has no damping
+// and no coupling to the gripper in M: its rows take no correction.  qacc_e goes to S.xs
+// (free after the solve); oracle/physics.c euler_damping restates it lane for lane.
 template <int CL>
 __device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __restrict__ T, real h, int lane) {
   const int rowf = lane >> 4, p = lane & 15;
   const bool chainrow = rowf < 3 && p >= 1 && p <= CL;
-  const bool palm = lane == GM_LANE_PALM_F, base = lane == 48;
-  real L[CL + 1], lb = 0.0, y = 0.0, bb = 0.0;
+  const bool palm = lane == GM_LANE_PALM_F;
+  real L[CL + 1], lb = 0.0, y = 0.0;
 #pragma unroll
   for (int j = 0; j <= CL; j++) L[j] = 0.0;
   if (chainrow) {
@@ -1176,12 +1178,12 @@ __device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __re
     L[1] = S.Hp[TRI(1, 1)] + hd;
     lb = S.Hp[TRI(1, 0)];
     y = hd * S.qacc[d];
-  } else if (base) {
-    const int d = T->dof_base;
-    const real hd = h * T->dof_damp[d];
-    bb = S.Hbb + hd;
-    y = hd * S.qacc[d];
   }
+  // the base row (wave-uniform: one scalar dof)
+  const int db = T->dof_base;
+  const real hdb = h * T->dof_damp[db];
+  const real bb = S.Hbb + hdb;
+  const real yb0 = hdb * S.qacc[db];
   real invd = 1.0, ub = 0.0;
   if (lane < 48) {
 #pragma unroll
@@ -1205,25 +1207,32 @@ __device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __re
       L[k] = upd ? a : L[k];
       invd = piv ? ihk : invd;
     }
-  } else if (palm) {
-    const real ih = rcp_n(L[1]);
-    ub = lb;
-    lb = lb * ih;
-    invd = ih;
-  }
-  const bool part = chainrow || palm;
-  const real sch = wave_sum(part ? lb * ub : 0.0);
-  // forward over the chains, leaf first
-  if (lane < 48) {
+    // forward over the chains, leaf first
 #pragma unroll
     for (int k = CL; k >= 1; k--) {
       const real yk = row_bcast(y, k);
       const real Lc = (p >= 1 && p < k) ? L[k] : 0.0;
       y = y - Lc * yk;
     }
+  } else if (palm) {
+    const real ih = rcp_n(L[1]);
+    ub = lb;
+    lb = lb * ih;
+    invd = ih;
   }
-  const real fs = wave_sum(part ? lb * y : 0.0);
-  const real xb = readlane_real((y - fs) * rcp_n(bb - sch), 48);
+  // base sums: per DPP row an inclusive scan of (lb ub, lb y) (lane 15 of the row holds the
+  // row total; lanes outside the chain hold zeros), then rows 0, 1, 2 and the palm in order
+  const bool part = chainrow || palm;
+  real s1 = part ? lb * ub : 0.0, s2 = part ? lb * y : 0.0;
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) {
+    const real t1 = row_shr(s1, off), t2 = row_shr(s2, off);
+    s1 += t1;
+    s2 += t2;
+  }
+  const real sch = ((readlane_real(s1, 15) + readlane_real(s1, 31)) + readlane_real(s1, 47)) + readlane_real(s1, 56);
+  const real fs = ((readlane_real(s2, 15) + readlane_real(s2, 31)) + readlane_real(s2, 47)) + readlane_real(s2, 56);
+  const real xb = (yb0 - fs) * rcp_n(bb - sch);
   // back substitution: D^-1, the border column, then the chains root -> leaf
   y = y * invd;
   y = y - lb * xb;
@@ -1240,9 +1249,10 @@ __device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __re
     S.xs[d] = S.qacc[d] - y;
   } else if (palm) {
     S.xs[T->dof_palm] = S.qacc[T->dof_palm] - y;
-  } else if (base) {
-    S.xs[T->dof_base] = S.qacc[T->dof_base] - xb;
+  } else if (lane == 48) {
+    S.xs[db] = S.qacc[db] - xb;
+  } else if (lane >= 57 && lane < 63) {
+    S.xs[T->dof_obj + lane - 57] = S.qacc[T->dof_obj + lane - 57];
   }
-  if (lane < 6) S.xs[T->dof_obj + lane] = S.qacc[T->dof_obj + lane];
   __syncthreads();
 }

@@ -140,7 +140,7 @@ class Calibration(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
-CAL_TIMESTEP, CAL_GAUGES = 1, 2
+CAL_TIMESTEP, CAL_GAUGES, CAL_REFERENCE_RETRY = 1, 2, 4
 
 
 def calibrate(model, cfg, objects, what: int = CAL_TIMESTEP | CAL_GAUGES, device: int = 0):
@@ -254,6 +254,7 @@ def _declare(lib):
         "gm_spawn_into_scene": (i32, [vp, u8p, vp, i32, u8p]),
         "gm_set_scene_spawn": (i32, [vp, vp, i32]),
         "gm_calibrate": (i32, [vp, vp, vp, i32, i32, i32, vp, vp, vp, i32]),
+        "gm_set_settle_cache": (None, [i32]),
         "gm_autoreset": (i32, [vp, i32, vp, i32, vp]),
         "gm_set_random_spawn": (i32, [vp, i32, C.c_uint64, i32, i32]),
         "gm_scripted_actions": (i32, [vp, C.c_uint64, C.c_float, vp, i32]),

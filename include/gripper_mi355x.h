@@ -387,8 +387,20 @@ typedef struct gm_calibration {
   float   wrist_Z_offset;             /* mjclass.cpp:4659: userdata[2] is never written, 0  */
   int32_t gauge_retries;              /* 0.8x timestep retries of the tip-load run          */
 } gm_calibration;
+/* calibrate_reset's first-call settle as the reference scopes it (myfunctions.cpp:1441-1519:
+ * a function-static first_call, so the 400-substep settle runs once per PROCESS and later
+ * models with the same joint count reuse its equilibrium even when their timestep or finger
+ * stiffness differ).  on = 1: contexts created from now on share one settle (the first one
+ * made after the call); 0 (default): every context settles its own model. */
+void gm_set_settle_cache(int on);
+
 #define GM_CAL_TIMESTEP 1
 #define GM_CAL_GAUGES   2
+/* validate_curve_under_force's retry as the reference runs it (mjclass.cpp:4073-4090): on
+ * instability the timestep drops to 0.8x, reset() wipes the tip load, and `continue` resumes
+ * the step loop -- the remaining steps run unloaded from the reset pose.  Without the flag
+ * the whole loaded settle is rerun at the reduced step (the engine's default). */
+#define GM_CAL_REFERENCE_RETRY 4
 #define GM_CAL_MAX_TRACE 256
 
 /* Batched calibration on `device`: every candidate timestep of the search is simulated

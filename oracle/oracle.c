@@ -1119,7 +1119,43 @@ static int is_motor_or_base_dof(const gm_model* m, int d) {
   return 0;
 }
 /* first-call settle of calibrate_reset (400 substeps, no sensors) */
+/* calibrate_reset's function-static first_call (myfunctions.cpp:1447), as a switch: with
+ * the cache on, the first env created settles and every later env with the same segment
+ * count takes that equilibrium (or_set_settle_cache; gm_set_settle_cache on the device) */
+static pthread_mutex_t g_settle_mu = PTHREAD_MUTEX_INITIALIZER;
+static int g_settle_cache_on = 0, g_settle_valid = 0, g_settle_nseg = -1;
+static double g_settle_eq[NQ];
+void or_set_settle_cache(int on) {
+  pthread_mutex_lock(&g_settle_mu);
+  g_settle_cache_on = on != 0;
+  g_settle_valid = 0;
+  pthread_mutex_unlock(&g_settle_mu);
+}
+static void settle_uncached(or_env* e);
 static void settle(or_env* e) {
+  pthread_mutex_lock(&g_settle_mu);
+  if (g_settle_cache_on && g_settle_valid && g_settle_nseg == e->m.n_seg) {
+    for (int i = 0; i < NQ; i++) e->eq_q[i] = g_settle_eq[i];
+    /* the settle's side effects on the env (targets home, locks off, keyframe) */
+    g_reset(&e->end); g_reset(&e->next);
+    for (int k = 0; k < 6; k++) e->base[k] = 0;
+    for (int k = 0; k < GM_MAX_LOCK; k++) { e->lock_active[k] = 0; e->lock_q[k] = 0; }
+    e->old_x = e->old_y = e->old_z = 1;
+    keyframe_state(e);
+    pthread_mutex_unlock(&g_settle_mu);
+    return;
+  }
+  pthread_mutex_unlock(&g_settle_mu);
+  settle_uncached(e);
+  pthread_mutex_lock(&g_settle_mu);
+  if (g_settle_cache_on && !g_settle_valid) {
+    for (int i = 0; i < NQ; i++) g_settle_eq[i] = e->eq_q[i];
+    g_settle_valid = 1;
+    g_settle_nseg = e->m.n_seg;
+  }
+  pthread_mutex_unlock(&g_settle_mu);
+}
+static void settle_uncached(or_env* e) {
   g_reset(&e->end); g_reset(&e->next);
   for (int k = 0; k < 6; k++) e->base[k] = 0;
   for (int k = 0; k < GM_MAX_LOCK; k++) { e->lock_active[k] = 0; e->lock_q[k] = 0; }
@@ -1374,11 +1410,14 @@ static float yield_point_load(const gm_model* m) {      /* myfunctions.cpp:3587-
 }
 /* n substeps of MjClass::step (before_step / resolve_segment_forces / step / after_step /
  * monitor_sensors); stops at the first BADQACC like the reference's break */
+static __thread int cal_ran;   /* substeps the last cal_steps made (the unstable one included) */
 static int cal_steps(or_env* e, int n) {
   /* a run starts from the reset's mj_forward pose */
   memcpy(e->qpos_pre, e->qpos, sizeof(e->qpos));
   e->badqacc = 0;
+  cal_ran = 0;
   for (int i = 0; i < n; i++) {
+    cal_ran = i + 1;
     if (e->tip_force != 0.0) {
       /* apply_segment_force locks the prismatic motors every step (set_constraint,
        * myfunctions.cpp:1679-1685), anchored at the last mj_step1 pose */
@@ -1451,15 +1490,25 @@ int or_calibrate(const gm_model* m, const gm_config* c, const gm_object* objects
     float time_to_settle = 50;
     int steps_to_make = time_to_settle / ts;
     int repeats_done = 1;
+    const int ref_retry = (what & GM_CAL_REFERENCE_RETRY) != 0;
+    int left = steps_to_make;
+    double tip = bend_gauge_normalise;
     while (1) {
-      e->tip_force = bend_gauge_normalise;
-      if (cal_steps(e, steps_to_make)) {
+      e->tip_force = tip;
+      if (cal_steps(e, ref_retry ? left : steps_to_make)) {
         ts *= 0.8;
         e->tip_force = 0;
         or_reset(e, &sp);
         e->m.timestep = ts;
         repeats_done += 1;
         if (repeats_done > 5) { or_destroy(e); return -3; }
+        if (ref_retry) {
+          /* validate_curve_under_force (mjclass.cpp:4073-4090): reset() wiped the segment
+           * forces and `continue` resumes the step loop after the unstable step, unloaded */
+          tip = 0.0;
+          left -= cal_ran;
+          if (left <= 0) break;
+        }
         continue;
       }
       break;

@@ -49,6 +49,7 @@ void  or_get_target(const or_env* e, double* end_xyzth, int32_t* end_steps, int3
 void  or_get_event_rows(const or_env* e, int32_t* rows, int32_t* abs_counts, float* last_values);
 int   or_overflow(const or_env* e);
 void  or_get_eq(const or_env* e, double* eq_qpos);                 /* settled equilibrium */
+void  or_set_settle_cache(int on);            /* calibrate_reset's process-wide first_call settle */
 
 /* one physics substep, with diagnostics (same layout as gm_debug_substep, fp64);
  * obj_wrench: the live object's cfrc_ext [force; torque about its centre of mass] */

@@ -1871,7 +1871,7 @@ static void euler_damping(const or_env* e, double* qe) {
   const otopo* T = &e->T;
   const int CL = T->CL;
   const double h = m->timestep;
-  double L[64][GM_CHAIN + 1], lb[64], ub[64], invd[64], y[64], lane_v[64];
+  double L[64][GM_CHAIN + 1], lb[64], ub[64], invd[64], y[64];
   for (int l = 0; l < 64; l++) {
     for (int j = 0; j <= CL; j++) L[l][j] = 0.0;
     lb[l] = 0.0; ub[l] = 0.0; invd[l] = 1.0; y[l] = 0.0;
@@ -1925,13 +1925,6 @@ static void euler_damping(const or_env* e, double* qe) {
     lb[lp] = lb[lp] * ih;
     invd[lp] = ih;
   }
-  /* Schur complement of the base: the wave sum of lb ub over the chain rows and the palm */
-  for (int l = 0; l < 64; l++) {
-    const int f = l >> 4, p = l & 15;
-    const int part = (f < 3 && p >= 1 && p <= CL) || l == lp;
-    lane_v[l] = part ? lb[l] * ub[l] : 0.0;
-  }
-  const double sch = butterfly64(lane_v);
   /* forward over the chains (leaf first) */
   for (int k = CL; k >= 1; k--)
     for (int f = 0; f < 3; f++) {
@@ -1941,12 +1934,26 @@ static void euler_damping(const or_env* e, double* qe) {
         y[16 * f + p] = y[16 * f + p] - Lc * yk;
       }
     }
+  /* the base's two sums: per DPP row an inclusive Hillis-Steele scan of (lb ub, lb y) (the
+   * row total lands on lane 15), then rows 0, 1, 2 and the palm in that order */
+  double s1[64], s2[64];
   for (int l = 0; l < 64; l++) {
     const int f = l >> 4, p = l & 15;
     const int part = (f < 3 && p >= 1 && p <= CL) || l == lp;
-    lane_v[l] = part ? lb[l] * y[l] : 0.0;
+    s1[l] = part ? lb[l] * ub[l] : 0.0;
+    s2[l] = part ? lb[l] * y[l] : 0.0;
   }
-  const double fs = butterfly64(lane_v);
+  for (int off = 1; off < 16; off <<= 1) {
+    double o1[64], o2[64];
+    memcpy(o1, s1, sizeof(o1)); memcpy(o2, s2, sizeof(o2));
+    for (int l = 0; l < 64; l++) {
+      const int pos = l & 15, row = l & ~15;
+      s1[l] = o1[l] + rshr(o1 + row, pos, off);
+      s2[l] = o2[l] + rshr(o2 + row, pos, off);
+    }
+  }
+  const double sch = ((s1[15] + s1[31]) + s1[47]) + s1[lp];
+  const double fs = ((s2[15] + s2[31]) + s2[47]) + s2[lp];
   const double xb = (y[lbase] - fs) * (1.0 / (bb - sch));
   /* back substitution: D^-1, the border, then the chains root -> leaf */
   for (int f = 0; f < 3; f++) {

@@ -101,6 +101,7 @@ def load(path):
             "or_set_default_weld_locks": (None, [i32]),
             "or_set_solver": (None, [vp, i32]),
             "or_dynamics": (None, [vp, f64p, f64p, f64p, f64p, f64p]),
+            "or_set_settle_cache": (None, [i32]),
             "or_collide": (i32, [i32, f64p, f64p, f64p, i32, f64p, f64p, f64p, C.c_double, i32, f64p]),
         }
         for n, (r, a) in sig.items():

@@ -308,3 +308,100 @@ def test_mujoco_actuator_order_needs_the_revolute_motor_inertia(world):
     ms, _ = model_search_ms(gm, 8, mujoco_actuators=0, revolute_armature=0.0, segment_damping=0.24,
                             segment_damping_power=1.0)
     assert ms == pytest.approx(4.35, rel=0.08)
+
+
+def test_gauge_calibration_reference_retry_on_the_oracle(world):
+    """GM_CAL_REFERENCE_RETRY: validate_curve_under_force's retry as the reference runs it
+    (mjclass.cpp:4073-4090) -- after the unstable step reset() wipes the tip load and the
+    step loop resumes at 0.8x the timestep, so the remaining steps run unloaded from the
+    reset pose and the gauge reads an (almost) unloaded finger: a normalisation far below
+    the engine's default retry (which reruns the loaded settle)."""
+    gm = world[0]
+    model, cfg, objs, _ = retry_world(gm)
+    fixed, _ = oracle_lib.calibrate(model, cfg, objs, gm.CAL_GAUGES)
+    ref, _ = oracle_lib.calibrate(model, cfg, objs, gm.CAL_GAUGES | gm.CAL_REFERENCE_RETRY)
+    assert fixed.gauge_retries == ref.gauge_retries == 1
+    assert ref.timestep == fixed.timestep == pytest.approx(0.8 * RETRY_DT, rel=1e-12)
+    assert abs(ref.bending_normalise) < 0.2 * abs(fixed.bending_normalise), (ref.bending_normalise,
+                                                                            fixed.bending_normalise)
+
+
+@pytest.mark.gpu
+def test_gpu_gauge_calibration_reference_retry_matches_oracle(world):
+    if not gpu_available():
+        pytest.skip("no GPU")
+    gm = world[0]
+    model, cfg, objs, _ = retry_world(gm)
+    what = gm.CAL_GAUGES | gm.CAL_REFERENCE_RETRY
+    dev, _ = gm.calibrate(model, cfg, objs, what=what)
+    ref, _ = oracle_lib.calibrate(model, cfg, objs, what)
+    assert dev.gauge_retries == ref.gauge_retries == 1
+    assert dev.timestep == ref.timestep
+    assert dev.bending_normalise == pytest.approx(ref.bending_normalise, rel=1e-4, abs=1e-6)
+
+
+def thick_model(gm):
+    import ctypes as C
+    p = gm.ModelParams()
+    gm.load_library().gm_default_model_params(C.byref(p))
+    p.finger_thickness = 1.0e-3          # stiffer fingers: a different equilibrium
+    return gm.ModelBlob(p)
+
+
+def test_settle_cache_first_call_quirk_on_the_oracle(world):
+    """calibrate_reset's function-static first_call (myfunctions.cpp:1441-1519): with the
+    process-wide cache on (or_set_settle_cache) the first env's 400-substep settle is reused
+    by a later env whose model has the same joint count but stiffer fingers; with it off
+    each env settles its own model."""
+    gm = world[0]
+    model = gm.ModelBlob()
+    objs = gm.make_object_set("set1_synthetic", 1)
+    cfg = gm.ConfigBlob(gm.canonical_settings(noise=False, seed=1), model)
+    m2 = thick_model(gm)
+    cfg2 = gm.ConfigBlob(gm.canonical_settings(noise=False, seed=1), m2)
+    L = oracle_lib.lib()
+    try:
+        L.or_set_settle_cache(1)
+        a = oracle_lib.OracleEnv(model, cfg, objs, 0)
+        b = oracle_lib.OracleEnv(m2, cfg2, objs, 0)
+        ea, eb = a.eq(), b.eq()
+        np.testing.assert_array_equal(ea, eb)
+    finally:
+        L.or_set_settle_cache(0)
+    c = oracle_lib.OracleEnv(m2, cfg2, objs, 0)
+    assert np.abs(c.eq() - ea).max() > 1e-6
+
+
+@pytest.mark.gpu
+def test_gpu_settle_cache_first_call_quirk_matches_oracle(world):
+    """gm_set_settle_cache(1): the device shares the first context's settle the same way;
+    the later context's reset state equals the oracle's under the same switch."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    gm = world[0]
+    objs_name = "set1_synthetic"
+    m1 = gm.ModelBlob()
+    m2 = thick_model(gm)
+    s = gm.canonical_settings(noise=False, seed=1)
+    lib = gm.load_library()
+    L = oracle_lib.lib()
+    try:
+        lib.gm_set_settle_cache(1)
+        L.or_set_settle_cache(1)
+        e1 = gm.BatchedGripperEnv(2, object_set=objs_name, settings=s, seed=1, model_blob=m1)
+        o1 = oracle_lib.OracleEnv(m1, e1.cfg, e1.objects, 0)
+        e2 = gm.BatchedGripperEnv(2, object_set=objs_name, settings=s, seed=1, model_blob=m2)
+        o2 = oracle_lib.OracleEnv(m2, e2.cfg, e2.objects, 0)
+        sp = e2.make_spawn(idx=0, x=0.0, y=0.0, rot=0.0)
+        obs = e2.reset(spawn=sp)
+        o2.reset(sp[0])
+        q, _, _ = e2.state()
+        qo, _, _ = o2.state()
+        np.testing.assert_allclose(q[0], qo, rtol=0, atol=1e-12)
+        np.testing.assert_allclose(obs[0], o2.observation(), rtol=1e-5, atol=1e-6)
+        # the shared equilibrium: the stiff model reset to the first model's settled pose
+        np.testing.assert_allclose(o2.eq(), o1.eq(), rtol=0, atol=0)
+        e1.close(); e2.close()
+    finally:
+        lib.gm_set_settle_cache(0)
+        L.or_set_settle_cache(0)

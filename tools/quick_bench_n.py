@@ -17,6 +17,11 @@ p = gmx.ModelParams()
 gmx.load_library().gm_default_model_params(C.byref(p))
 p.n_seg = N
 p.timestep = 3.187e-3 if N <= 8 else 2.2e-3
+if os.environ.get("GM_MJ") is not None:       # 0: the folded actuator scheme (r01-r03 physics)
+    p.mujoco_actuators = int(os.environ["GM_MJ"])
+    if p.mujoco_actuators == 0:
+        p.actuator_armature[1] = 0.0
+        p.segment_damping, p.segment_damping_power = 0.24, 1.0
 env = gmx.BatchedGripperEnv(n, object_set="set6_synthetic", settings=gmx.canonical_settings(seed=seed), seed=seed,
                             model_params=p)
 env.set_scene_spawn(bench.mjenv_spawn_params(gmx), max_tries=3)

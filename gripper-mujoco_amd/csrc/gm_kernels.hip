@@ -26,7 +26,15 @@
 #include "gm_math.h"
 
 #define NT 64
-#define GM_CQ_NB 16   // priority buckets per XCD of the chunked env-step (gm_step_kernel)
+// Phase boundary inside one env's physics.  Every kernel that runs the substep is launched
+// with one 64-lane wavefront per workgroup (NT), and a wave's LDS operations complete in
+// issue order, so a lane's read issued after another lane's write sees it: the boundary
+// only has to stop the compiler moving LDS accesses across it.  __syncthreads' workgroup
+// fence is lowered to an s_waitcnt lgkmcnt(0) drain at every boundary (the substep loop
+// had ~430 of them), stalling the wave on loads whose results it does not yet need.
+#define GM_WAVE_SYNC() do { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); \
+                            __builtin_amdgcn_wave_barrier(); } while (0)
+#define GM_CQ_NB 16  // priority buckets per XCD of the chunked env-step (gm_step_kernel)
 // gm_step_kernel is instantiated per finger chain length (CL = n_seg + 2) so every chain
 // recursion is unrolled into registers; GM_NSEG_LIST is the set compiled in.
 #ifndef GM_NSEG_LIST
@@ -312,7 +320,7 @@ __device__ __forceinline__ void kinematics(SharedT<CL>& S, const gm_model* __res
       }
     }
   }
-#if defined(GM_PHASE_SPLIT_PGS) || defined(GM_PHASE_SPLIT_COLL)
+#if defined(GM_PHASE_SPLIT_PGS) || defined(GM_PHASE_SPLIT_COLL) || defined(GM_PHASE_SPLIT_SETUP)
   PH(0);
 #else
   PH(15);
@@ -373,8 +381,8 @@ __device__ __forceinline__ void kinematics(SharedT<CL>& S, const gm_model* __res
       for (int k = 0; k < 4; k++) S.xquat[b][k] = q[k];
     }
   }
-  __syncthreads();
-#if defined(GM_PHASE_SPLIT_PGS) || defined(GM_PHASE_SPLIT_COLL)
+  GM_WAVE_SYNC();
+#if defined(GM_PHASE_SPLIT_PGS) || defined(GM_PHASE_SPLIT_COLL) || defined(GM_PHASE_SPLIT_SETUP)
   PH(0);
 #else
   PH(16);
@@ -443,7 +451,7 @@ __device__ __forceinline__ void kinematics(SharedT<CL>& S, const gm_model* __res
       }
     }
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
 }
 
 // ============================================================ CRB + RNE
@@ -620,7 +628,7 @@ __device__ __forceinline__ void crb_rne(SharedT<CL>& S, const gm_model* __restri
     }
     body_force(S, b, cvel, cacc);
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
   PH(17);
   // base body: its own inertia / force plus the four chain roots
   if (lane == 0) {
@@ -643,7 +651,7 @@ __device__ __forceinline__ void crb_rne(SharedT<CL>& S, const gm_model* __restri
 #pragma unroll
     for (int k = 0; k < 6; k++) S.cfrc[bb][k] = fb[k];
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
 }
 
 // ============================================================ mass matrix rows + forces
@@ -731,7 +739,7 @@ __device__ __forceinline__ void mass_and_forces(SharedT<CL>& S, const gm_model* 
     }
     S.frc[d] = frc;
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
 }
 
 // ============================================================ collision
@@ -1269,7 +1277,7 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
   // make_frame builds them; the rest of the frame is implied by the two
   static_assert(GM_MAX_CON <= NT, "contact frames: one lane per contact");
   const int ncon = written < GM_MAX_CON ? written : GM_MAX_CON;
-  __syncthreads();
+  GM_WAVE_SYNC();
   if (lane < ncon) {
     real* C = S.con[lane];
     const real n[3] = {C[4], C[5], C[6]};
@@ -1282,7 +1290,7 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
     S.ncon = ncon;
     S.overflow = written > GM_MAX_CON;
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
 }
 
 // ============================================================ integrate
@@ -1300,7 +1308,7 @@ __device__ __forceinline__ void integrate(SharedT<CL>& S, const gm_model* __rest
   const bool mj = m->mujoco_actuators != 0;
   if (mj) euler_damping<CL>(S, T, h, lane);
   if (lane < T->nv) S.s.qvel[lane] += h * (mj ? S.xs[lane] : S.qacc[lane]);
-  __syncthreads();
+  GM_WAVE_SYNC();
   if (lane < T->nv && lane < T->dof_obj) {
     S.s.qpos[lane] += h * S.s.qvel[lane];   // slides/hinges: qposadr == dofadr before the object
   }
@@ -1321,7 +1329,7 @@ __device__ __forceinline__ void integrate(SharedT<CL>& S, const gm_model* __rest
     quatnorm(q);
     S.s.time += h;
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
 }
 
 }  // namespace gmf
@@ -1459,7 +1467,7 @@ GM_EPI_ATTR void update_all(SharedT<CL>& S, const gm_model* __restrict__ m, cons
     real mag = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
     if (mag < 1e-6) for (int k = 0; k < 6; k++) s.qvel[T->dof_obj + k] = 0;
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
 }
 
 // ---- RNG: minstd_rand0 + generate_canonical (libstdc++), per-env stream ----
@@ -1713,10 +1721,10 @@ GM_EPI_ATTR void monitor_sensors(SharedT<CL>& S, const gm_model* __restrict__ m,
   // (per-env LDS fields, no function-scope __shared__: substep_loop and monitor_sensors are
   // reached from two kernels, and such variables would cost a per-kernel offset lookup)
   if (lane == 0) S.bend_ready = s_ready(S.s, C->s.bending_gauge, SL_BEND);
-  __syncthreads();
+  GM_WAVE_SYNC();
   const int bend_ready = S.bend_ready;
   if (bend_ready && lane < 3) S.gauge_tmp[lane] = gauge_reading<CL - 2>(m, &S.s.qpos[T->dof_f0[lane] + 2]);
-  __syncthreads();
+  GM_WAVE_SYNC();
   if (lane == 0) {
     GmEnvHot& s = S.s;
   RingRef R = S.gs->ring;
@@ -1755,7 +1763,7 @@ GM_EPI_ATTR void monitor_sensors(SharedT<CL>& S, const gm_model* __restrict__ m,
       ring_add(s, R, ST_WZ, z);
     }
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
 }
 
 // ============================================================ one full substep
@@ -1853,7 +1861,7 @@ __device__ __noinline__ int substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS_
   (void)lane_in;
   const int every = CAL ? 0 : __builtin_amdgcn_readfirstlane(pre.every);
   if (__lane_id() == 0) S.next_read = (settle || CAL) ? 0.0 : next_sensor_read(S.s, C->s);
-  __syncthreads();
+  GM_WAVE_SYNC();
   int i = 0;
 #pragma nounroll
   for (; i < nsub; i++) {
@@ -1909,7 +1917,7 @@ __device__ __noinline__ int substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS_
       monitor_call<CL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)(uintptr_t)m,
                        (const GM_AS_GLOBAL gm_config*)(uintptr_t)C, (const GM_AS_GLOBAL GmTopo*)(uintptr_t)T, __lane_id());
       if (__lane_id() == 0) S.next_read = next_sensor_read(S.s, C->s);
-      __syncthreads();
+      GM_WAVE_SYNC();
     }
     PH(10);
     if (CAL && S.s.badqacc) break;
@@ -2265,7 +2273,7 @@ __device__ __forceinline__ void env_step_epilogue(SharedT<CL>& S, const gm_model
     PH(19);
     S.s.num_action_steps += 1;
   }
-  __syncthreads();   // lane 0's window appends (HBM) and indices (LDS) before the samplers
+  GM_WAVE_SYNC();   // lane 0's window appends (HBM) and indices (LDS) before the samplers
   get_obs_lanes(S.s, S.gs->ring, C, obs + (size_t)env * C->n_obs, lane);
   PH(20);
   if (lane == 0) {

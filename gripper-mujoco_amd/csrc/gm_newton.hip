@@ -242,23 +242,35 @@ __device__ __forceinline__ int bb_edge_hit(const BBox& S, const real* ea, const 
 }
 
 // ------------------------------------------------------------ constraint rows
+// the solimp sigmoid's general power (cold on the canonical model): one pow pair serves
+// both halves; outlined so the inlined fast path stays small
+__device__ __noinline__ real impedance_pow(real x, real mid, real pw) {
+  const bool lo = x <= mid;
+  const real t = pow(lo ? x : 1 - x, pw) / pow(lo ? mid : 1 - mid, pw - 1);
+  return lo ? t : 1 - t;
+}
+// mj_makeImpedance's sigmoid, branch-free in the data (the branches left test model
+// constants, wave-uniform): the same values as the early-return form, so several calls can
+// interleave their dependency chains
 __device__ __forceinline__ real impedance(const gm_model* __restrict__ m, real r) {
   const real dmin = m->solimp[0], dmax = m->solimp[1], width = m->solimp[2];
   const real mid = m->solimp[3], pw = m->solimp[4];
   if (dmin == dmax || width <= 1e-15) return dmin;
   const real x = div_n(fabs(r), width);
-  if (x >= 1) return dmax;
-  if (x <= 0) return dmin;
   real y;
-  if (pw == 1) y = x;
-  else if (pw == 2) y = (x <= mid) ? div_n(x * x, mid) : 1 - div_n((1 - x) * (1 - x), 1 - mid);   // MuJoCo's default power
-  else {
-    // general power (cold): one pow pair serves both halves of the sigmoid
+  if (pw == 2) {   // MuJoCo's default power
     const bool lo = x <= mid;
-    const real t = pow(lo ? x : 1 - x, pw) / pow(lo ? mid : 1 - mid, pw - 1);
-    y = lo ? t : 1 - t;
+    const real q = div_n(lo ? x * x : (1 - x) * (1 - x), lo ? mid : 1 - mid);
+    y = lo ? q : 1 - q;
+  } else if (pw == 1) {
+    y = x;
+  } else {
+    y = impedance_pow(x, mid, pw);
   }
-  return dmin + y * (dmax - dmin);
+  real imp = dmin + y * (dmax - dmin);
+  imp = (x >= 1) ? dmax : imp;
+  imp = (x <= 0) ? dmin : imp;
+  return imp;
 }
 
 // spatial velocity [angular; linear at the world origin] of every body for NVEC dof
@@ -322,7 +334,7 @@ __device__ void body_vel(SharedT<CL>& S, const real* const* v, real (*const* V)[
 #pragma unroll
       for (int k = 0; k < 6; k++) V[n][0][k] = 0.0;
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
 }
 
 // J v of contact c's 4 pyramid edges from the body velocities V (n + mu t1, n - mu t1,
@@ -427,7 +439,7 @@ __device__ void smooth_matvec(SharedT<CL>& S, const GmTopo* __restrict__ T, cons
     }
     out[d] = acc;
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
 }
 
 // ------------------------------------------------------------ Newton solve
@@ -444,45 +456,65 @@ struct RowsT {
 // tran + mu^2 tran, tran = the two bodies' invweight0), reference accelerations
 template <int CL, bool CAL>
 __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
-                                 int lane, RowsT& R, real* jq, real& jql, bool& obj_only) {
+                                 int lane, RowsT& R, real* jq, real& jql, bool& obj_only, bool prof = false) {
+  unsigned long long t0 = prof ? clock64() : 0;
+  (void)t0;
   const real h = CAL ? S.s.dt : m->timestep;
   real tc = m->solref[0];
   if (tc < 2 * h) tc = 2 * h;
   const real dr = m->solref[1], dmax = m->solimp[1];
   const real K = rcp_n(dmax * dmax * tc * tc * dr * dr);
   const real Bd = div_n(2.0, dmax * tc);
-  // lock rows: the lane-th active lock
-  int nl = 0;
-  for (int k = 0; k < T->nlock; k++) nl += S.s.lock_active[k] ? 1 : 0;
+  // lock rows: row r (lane r) is the r-th active lock.  The lock behind each row is picked
+  // branch-free from the (wave-uniform) active flags and its constants from uniform scalar
+  // loads, and the weld's per-axis rows are evaluated side by side: no divergent search
+  // loop, no per-lane global loads, three independent dependency chains instead of one.
+  int nl = 0, k = 0, d = 0;
+  real tran = 0.0;
+#pragma unroll
+  for (int kk = 0; kk < GM_MAX_LOCK; kk++) {
+    const bool act = kk < T->nlock && S.s.lock_active[kk];
+    const bool mine = act && nl == lane;
+    k = mine ? kk : k;
+    d = mine ? m->lock_dof[kk] : d;
+    tran = mine ? T->lock_tran[kk] : tran;
+    nl += act ? 1 : 0;
+  }
   R.lD = 0; R.laref = 0; R.ldof = 0;
   if (lane < nl) {
-    int k = 0, cntl = -1;
-    for (k = 0; k < T->nlock; k++) { if (S.s.lock_active[k]) cntl++; if (cntl == lane) break; }
-    const int d = m->lock_dof[k];
     const real pos = S.s.qpos[d] - S.s.lock_q[k];
     const real vel = S.s.qvel[d];
     // the reference's weld on a slide as one row on the dof (oracle constraint_setup):
     // per world axis r the weld row a_r qdot with its own impedance and the weld's
-    // regulariser, summed: D = sum D_r a_r^2, D aref = sum D_r a_r aref_r
-    const real tran = T->lock_tran[k];
-    real De = 0.0, Dar = 0.0;
-#pragma unroll 1   // one inlined impedance, not three
+    // regulariser, summed in axis order: D = sum D_r a_r^2, D aref = sum D_r a_r aref_r
+    real Da[3], ar[3], av[3];
+    bool on[3];
+#pragma unroll
     for (int r = 0; r < 3; r++) {
       const real a = S.cdof[d][3 + r];
-      if (a == 0.0) continue;
+      av[r] = a;
+      on[r] = a != 0.0;
       const real pr = a * pos, vr = a * vel;
       const real imp = impedance(m, pr);
       real Rr = div_n(1 - imp, imp) * tran;
       if (Rr < 1e-15) Rr = 1e-15;
-      const real Da = rcp_n(Rr) * a;
-      De = De + Da * a;
-      Dar = Dar + Da * (-Bd * vr - K * imp * pr);
+      Da[r] = rcp_n(Rr) * a;
+      ar[r] = -Bd * vr - K * imp * pr;
+    }
+    real De = 0.0, Dar = 0.0;
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      De = on[r] ? De + Da[r] * av[r] : De;
+      Dar = on[r] ? Dar + Da[r] * ar[r] : Dar;
     }
     R.lD = De;
     R.laref = div_n(Dar, De);
     R.ldof = d;
   }
   if (lane == 0) { S.nl = nl; S.nefc = nl + 4 * S.ncon; }
+#ifdef GM_PHASE_SPLIT_SETUP
+  PH(15);   // developer split: lock rows
+#endif
   // body velocities at qvel (reference accelerations) and at the warm start (the first
   // iterate's J q - aref), one fused pass
   {
@@ -496,6 +528,9 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
     obj_only = __ballot(!og) == 0ull;
     body_vel<CL, 2>(S, vv, VV, m, T, lane, obj_only);
   }
+#ifdef GM_PHASE_SPLIT_SETUP
+  PH(16);   // developer split: the two velocity scans
+#endif
   jql = (lane < nl) ? S.s.qacc_warm[R.ldof] - R.laref : 0.0;
 #pragma unroll
   for (int e = 0; e < 4; e++) jq[e] = 0.0;
@@ -523,7 +558,10 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
       jq[e] = jv[e] - R.caref[e];
     }
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
+#ifdef GM_PHASE_SPLIT_SETUP
+  PH(11);   // developer split: the contact rows
+#endif
 }
 
 // J v - aref for every row at the dof vector v (LDS); into jr (contact) / jl (lock)
@@ -589,7 +627,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     for (int k = 0; k < 6; k++) qf[k] = Q[k];
     qf[6] = F[0]; qf[7] = F[1]; qf[8] = F[2];
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
   // ---- scan lanes: the body's contacts with the object.  Contacts of gripper bodies with
   // the ground (rare) are added in a second pass below, so the common path keeps one
   // 27-value composite per lane in registers instead of two.
@@ -682,7 +720,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
       for (int k = 0; k < 6; k++) st[42 + k] = Fo[k];
     }
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
   // ---- base composites (the four roots in order) and the object's totals
   if (lane < 27) {
     const int k = lane < 21 ? lane : 42 + lane - 21;
@@ -691,12 +729,12 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     for (int c = 0; c < 4; c++) acc += S.st.root[c][k];
     S.st.comp[k] = acc;
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
   if (lane < 27) {
     // Koo = KBo + Kgo (21), Fobj = Fgo - FBo (6)
     S.st.oo[lane] = (lane < 21) ? S.st.comp[lane] + S.go[lane] : S.go[lane] - S.st.comp[42 + lane - 21];
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
   PH(4);
   // ---- H and rhs on the factor lanes
   real h[CL + 1], hb[7], rhs = 0;
@@ -817,7 +855,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
 #pragma unroll
       for (int k = 0; k < 6; k++) st[48 + k] = Fg[k];
     }
-    __syncthreads();
+    GM_WAVE_SYNC();
     const bool chainrow = rowf < 3 && p >= 1 && p <= CL;
     if (lane == GM_LANE_PALM_F) {
 #pragma unroll
@@ -863,7 +901,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
       rhs += lR;
     }
   }
-  __syncthreads();   // the stage is read; the factor's transfers reuse the union
+  GM_WAVE_SYNC();   // the stage is read; the factor's transfers reuse the union
   PH(7);
   // ---- factor: finger chains (rows 0..2), pivots CL .. 1
   real invd = 1.0;
@@ -914,7 +952,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     for (int j = 0; j < 7; j++)
       if (j <= i) S.fs.bbx[i * (i + 1) / 2 + j] = hb[j];
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
   // Schur complements: one lane per border entry (i, j), elimination order
   if (lane < 28) {
     int i = 0;
@@ -931,7 +969,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     v = (((v - acc[0]) - acc[1]) - acc[2]) - S.fs.plb[i] * S.fs.plb[7 + j];
     S.fs.bbx[lane] = v;
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
   const int bi = lane - 48;
   const bool border = lane >= 48 && lane < 55;
   if (border) {
@@ -972,7 +1010,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
   } else if (lane == GM_LANE_PALM_F) {
     S.fs.ypalm = y;
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
   if (border) {
     real acc[3] = {0.0, 0.0, 0.0};
 #pragma unroll
@@ -1017,7 +1055,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
   } else if (border) {
     S.xs[bi == 0 ? T->dof_base : T->dof_obj + bi - 1] = y;
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
   PH(24);
 }
 
@@ -1031,12 +1069,15 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
   RowsT R;
   real jq[4], jql;
   bool obj_only;
-  constraint_setup<CL, CAL>(S, m, T, lane, R, jq, jql, obj_only);
+  constraint_setup<CL, CAL>(S, m, T, lane, R, jq, jql, obj_only, prof);
+#ifdef GM_PHASE_SPLIT_SETUP
+  if (prof) t0 = clock64();   // the split phases above were charged inside; the rest: contact rows
+#endif
   PH(11);
   const int ncon = S.ncon, nl = S.nl, nv = T->nv;
   const bool clane = lane < ncon;
   if (lane < nv) S.qacc[lane] = S.s.qacc_warm[lane];
-  __syncthreads();
+  GM_WAVE_SYNC();
   PH(12);
   int it = 0, nls = 0;
   bool capped = true;   // no Newton point accepted within GM_NEWTON_MAXIT iterations
@@ -1066,7 +1107,7 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
     // (only iteration 0 reaches here with q unchanged: the oracle does the same)
     if (it == 0) smooth_matvec<CL>(S, T, S.qacc, S.Ma, lane);
     if (lane < nv) S.xs[lane] = S.xs[lane] - S.qacc[lane];
-    __syncthreads();
+    GM_WAVE_SYNC();
     smooth_matvec<CL>(S, T, S.xs, S.Mv, lane);
     const real dd = lane < nv ? S.xs[lane] : 0.0;
     const real g0 = wave_sum(lane < nv ? dd * (S.Ma[lane] - S.frc[lane]) : 0.0);
@@ -1115,7 +1156,7 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
 #pragma unroll
     for (int e = 0; e < 4; e++) jq[e] = jq[e] + alpha * dj[e];
     jql = jql + alpha * djl;
-    __syncthreads();
+    GM_WAVE_SYNC();
   }
   PH(13);
   // constraint forces at the solution and the contact-frame forces (mj_contactForce)
@@ -1139,7 +1180,7 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
     if (capped || ls_cap) S.s.newton_caps += 1;   // (the oracle counts the same, physics.c newton_solve)
     if (prof) { S.tph[28] += nl + 4 * ncon; S.tph[30] += it; S.tph[31] += nls; }
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
 }
 
 // ------------------------------------------------------------ mj_Euler's implicit damping
@@ -1254,5 +1295,5 @@ __device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __re
   } else if (lane >= 57 && lane < 63) {
     S.xs[T->dof_obj + lane - 57] = S.qacc[T->dof_obj + lane - 57];
   }
-  __syncthreads();
+  GM_WAVE_SYNC();
 }

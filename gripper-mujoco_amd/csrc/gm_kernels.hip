@@ -30,10 +30,18 @@
 // with one 64-lane wavefront per workgroup (NT), and a wave's LDS operations complete in
 // issue order, so a lane's read issued after another lane's write sees it: the boundary
 // only has to stop the compiler moving LDS accesses across it.  __syncthreads' workgroup
-// fence is lowered to an s_waitcnt lgkmcnt(0) drain at every boundary (the substep loop
-// had ~430 of them), stalling the wave on loads whose results it does not yet need.
+// fence is lowered to an s_waitcnt lgkmcnt(0) drain at every boundary, stalling the wave
+// on loads whose results it does not yet need.
 #define GM_WAVE_SYNC() do { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); \
                             __builtin_amdgcn_wave_barrier(); } while (0)
+// The lane id, opaque to the compiler: each phase derives its lane predicates (chain row,
+// border, contact lane, ...) from its own copy, so they are recomputed per phase instead of
+// being computed once per substep and held live (in spilled SGPR pairs) across all of them.
+__device__ __forceinline__ int fresh_lane() {
+  int lane;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  return lane;
+}
 #define GM_CQ_NB 16  // priority buckets per XCD of the chunked env-step (gm_step_kernel)
 // gm_step_kernel is instantiated per finger chain length (CL = n_seg + 2) so every chain
 // recursion is unrolled into registers; GM_NSEG_LIST is the set compiled in.
@@ -123,6 +131,16 @@ struct __align__(16) SharedT {
 
 // per-phase shader-clock accounting (gm_step_profiled); needs `prof`, `lane`, `t0` in scope
 #define PH(k) do { if (__builtin_expect(prof, 0)) { unsigned long long t_ = clock64(); if (lane == 0) S.tph[k] += t_ - t0; t0 = t_; } } while (0)
+// developer split of the narrowphase (GM_PHASE_SPLIT_NARROW builds): each collider branch
+// charges its own clocks to slot k from its first active lane (the branches are divergent)
+#ifdef GM_PHASE_SPLIT_NARROW
+#define NB_BEGIN() const unsigned long long tb_ = prof ? clock64() : 0
+#define NB_END(k) do { if (prof) { const unsigned long long te_ = clock64(); \
+    if (lane == (int)__builtin_ctzll(__ballot(1))) S.tph[k] += te_ - tb_; } } while (0)
+#else
+#define NB_BEGIN() do { } while (0)
+#define NB_END(k) do { } while (0)
+#endif
 
 // ------------------------------------------------------------ small math
 // Correctly rounded fp64 sqrt, reciprocal and quotient on the compiler's own expansions
@@ -297,30 +315,27 @@ __device__ __forceinline__ void kinematics(SharedT<CL>& S, const gm_model* __res
   //    hinge  p = bpos,                    quat = bquat (x) (cos q/2, axis sin q/2)
   // every constant below is one load from the lane's flattened GmTopo entry (identity
   // transform and no joint on lanes without a body)
-  real lp[3], lq[4];
+  real lp[3], lq[4], ax[3] = {0, 0, 0};
   const int b = T->lane_body[lane];   // scan-lane layout (GmTopo::lane_body)
+  const int type = T->kl_type[lane];
   ld3(lp, T->kl_pos[lane]);
   ld4(lq, T->kl_quat[lane]);
-  {
-    const int type = T->kl_type[lane];
-    if (type >= 0) {
-      const real qv = S.s.qpos[T->kl_qadr[lane]];
-      real ax[3];
-      ld3(ax, T->kl_axis[lane]);
-      if (type == GM_JNT_SLIDE) {
-        real R[9], wa[3];
-        quat2mat(R, lq);
-        mulmv3(wa, R, ax);
-        lp[0] += wa[0] * qv; lp[1] += wa[1] * qv; lp[2] += wa[2] * qv;
-      } else if (type == GM_JNT_HINGE) {
-        real sn, cs;
-        gm_sincos(0.5 * qv, &sn, &cs);   // shared with the oracle (gm_math.h)
-        const real ql[4] = {cs, ax[0] * sn, ax[1] * sn, ax[2] * sn};
-        quatmul(lq, lq, ql);
-      }
+  if (type >= 0) {
+    const real qv = S.s.qpos[T->kl_qadr[lane]];
+    ld3(ax, T->kl_axis[lane]);
+    if (type == GM_JNT_SLIDE) {
+      real R[9], wa[3];
+      quat2mat(R, lq);
+      mulmv3(wa, R, ax);
+      lp[0] += wa[0] * qv; lp[1] += wa[1] * qv; lp[2] += wa[2] * qv;
+    } else if (type == GM_JNT_HINGE) {
+      real sn, cs;
+      gm_sincos(0.5 * qv, &sn, &cs);   // shared with the oracle (gm_math.h)
+      const real ql[4] = {cs, ax[0] * sn, ax[1] * sn, ax[2] * sn};
+      quatmul(lq, lq, ql);
     }
   }
-#if defined(GM_PHASE_SPLIT_PGS) || defined(GM_PHASE_SPLIT_COLL) || defined(GM_PHASE_SPLIT_SETUP)
+#if defined(GM_PHASE_SPLIT_PGS) || defined(GM_PHASE_SPLIT_COLL) || defined(GM_PHASE_SPLIT_SETUP) || defined(GM_PHASE_SPLIT_NARROW)
   PH(0);
 #else
   PH(15);
@@ -328,9 +343,14 @@ __device__ __forceinline__ void kinematics(SharedT<CL>& S, const gm_model* __res
   // B: poses.  The base is the world's child; along each finger / palm chain the
   // local transforms are composed by a segmented inclusive scan (root-side operand on
   // the left: (p_a, q_a) o (p_b, q_b) = (p_a + R(q_a) p_b, q_a (x) q_b)), then the base
-  // pose is applied and the orientation renormalised.
+  // pose is applied and the orientation renormalised.  Every body other than the world has
+  // a scan lane (chain links, palm, base, object), which keeps its pose in registers for C.
+  const int bb = T->body_base;
+  const int grp = T->kl_grp[lane];
+  const bool chain = grp >= 0 && grp <= 3;
+  const bool is_obj = b == T->body_obj;
+  real xp[3], xq[4];
   {
-    const int bb = T->body_base;
     const int lb = T->lane_base;
     real bpos[3], bq[4];
 #pragma unroll
@@ -340,8 +360,6 @@ __device__ __forceinline__ void kinematics(SharedT<CL>& S, const gm_model* __res
     quatnorm(bq);
     real bR[9];
     quat2mat(bR, bq);
-    const int grp = T->kl_grp[lane];
-    const bool chain = grp >= 0 && grp <= 3;
     const int p = T->kl_cpos[lane];
 #pragma unroll
     for (int off = 1; off < CL; off <<= 1) {
@@ -360,46 +378,43 @@ __device__ __forceinline__ void kinematics(SharedT<CL>& S, const gm_model* __res
       }
     }
     if (chain) {
-      real t[3], q[4];
+      real t[3];
       mulmv3(t, bR, lp);
-      quatmul(q, bq, lq);
-      quatnorm(q);
-      S.xpos[b][0] = bpos[0] + t[0]; S.xpos[b][1] = bpos[1] + t[1]; S.xpos[b][2] = bpos[2] + t[2];
-#pragma unroll
-      for (int k = 0; k < 4; k++) S.xquat[b][k] = q[k];
-    } else if (b == bb) {
-      S.xpos[bb][0] = bpos[0]; S.xpos[bb][1] = bpos[1]; S.xpos[bb][2] = bpos[2];
-#pragma unroll
-      for (int k = 0; k < 4; k++) S.xquat[bb][k] = bq[k];
-    } else if (b == T->body_obj) {
+      quatmul(xq, bq, lq);
+      quatnorm(xq);
+      xp[0] = bpos[0] + t[0]; xp[1] = bpos[1] + t[1]; xp[2] = bpos[2] + t[2];
+    } else if (is_obj) {
       // object: free joint, pose straight from qpos
       const int qa = T->qadr_obj;
-      real q[4] = {S.s.qpos[qa + 3], S.s.qpos[qa + 4], S.s.qpos[qa + 5], S.s.qpos[qa + 6]};
-      quatnorm(q);
-      S.xpos[b][0] = S.s.qpos[qa]; S.xpos[b][1] = S.s.qpos[qa + 1]; S.xpos[b][2] = S.s.qpos[qa + 2];
-#pragma unroll
-      for (int k = 0; k < 4; k++) S.xquat[b][k] = q[k];
+      xq[0] = S.s.qpos[qa + 3]; xq[1] = S.s.qpos[qa + 4]; xq[2] = S.s.qpos[qa + 5]; xq[3] = S.s.qpos[qa + 6];
+      quatnorm(xq);
+      xp[0] = S.s.qpos[qa]; xp[1] = S.s.qpos[qa + 1]; xp[2] = S.s.qpos[qa + 2];
+    } else {   // the base lane (the rest hold no body and store nothing)
+      xp[0] = bpos[0]; xp[1] = bpos[1]; xp[2] = bpos[2];
+      xq[0] = bq[0]; xq[1] = bq[1]; xq[2] = bq[2]; xq[3] = bq[3];
     }
   }
-  GM_WAVE_SYNC();
-#if defined(GM_PHASE_SPLIT_PGS) || defined(GM_PHASE_SPLIT_COLL) || defined(GM_PHASE_SPLIT_SETUP)
+#if defined(GM_PHASE_SPLIT_PGS) || defined(GM_PHASE_SPLIT_COLL) || defined(GM_PHASE_SPLIT_SETUP) || defined(GM_PHASE_SPLIT_NARROW)
   PH(0);
 #else
   PH(16);
 #endif
-  // C1: world-origin spatial inertia per body
-  if (lane < T->nbody && lane > 0) {
-    const int b = lane;
-    real R[9], xp[3];
-    body_R(S, b, R);
-    xp[0] = S.xpos[b][0]; xp[1] = S.xpos[b][1]; xp[2] = S.xpos[b][2];
+  // C, on the body's scan lane from the pose in registers: the pose itself, the
+  // world-origin spatial inertia and the motion subspace of the body's dof(s) (the
+  // object's six)
+  if (b > 0) {
+    real R[9];
+    quat2mat(R, xq);
+    S.xpos[b][0] = xp[0]; S.xpos[b][1] = xp[1]; S.xpos[b][2] = xp[2];
+#pragma unroll
+    for (int k = 0; k < 4; k++) S.xquat[b][k] = xq[k];
     real ip[3], c[3];
     ld3(ip, m->body_ipos[b]);
     mulmv3(c, R, ip);
     c[0] += xp[0]; c[1] += xp[1]; c[2] += xp[2];
     real I[3] = {(real)m->body_inertia[b][0], (real)m->body_inertia[b][1], (real)m->body_inertia[b][2]};
     real mass = (real)m->body_mass[b];
-    if (b == m->body_obj) {
+    if (is_obj) {
       mass = S.s.obj_mass;
       I[0] = S.s.obj_inertia[0]; I[1] = S.s.obj_inertia[1]; I[2] = S.s.obj_inertia[2];
     }
@@ -419,29 +434,27 @@ __device__ __forceinline__ void kinematics(SharedT<CL>& S, const gm_model* __res
     ci[5] = Iw[5] - mass * c[1] * c[2];
     ci[6] = mass * c[0]; ci[7] = mass * c[1]; ci[8] = mass * c[2];
     ci[9] = mass;
-  }
-  // C2: motion subspaces, one lane per dof
-  if (lane < T->nv) {
-    const int d = lane;
-    const int b = T->dof_body[d];
-    const int type = T->dof_jtype[d];
-    real* cd = S.cdof[d];
-    const real xp[3] = {S.xpos[b][0], S.xpos[b][1], S.xpos[b][2]};
-    if (type == GM_JNT_FREE) {
-      const int k = T->dof_k[d];
-      if (k < 3) {
+    if (is_obj) {
+      // free joint: translations along the world axes, rotations about the body axes
+      // through the body origin
+      const int d0 = T->dof_obj;
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        real* cd = S.cdof[d0 + k];
         cd[0] = cd[1] = cd[2] = 0; cd[3] = cd[4] = cd[5] = 0; cd[3 + k] = 1;
-      } else {
-        real Rb[9];
-        body_R(S, b, Rb);
-        const real w[3] = {Rb[k - 3], Rb[3 + k - 3], Rb[6 + k - 3]};
+      }
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        real* cd = S.cdof[d0 + 3 + k];
+        const real w[3] = {R[k], R[3 + k], R[6 + k]};
         cd[0] = w[0]; cd[1] = w[1]; cd[2] = w[2];
         cross3(cd + 3, xp, w);
       }
     } else {
-      real ax[3], wa[3], R[9];
-      body_R(S, b, R);
-      ld3(ax, T->dof_axis[d]);
+      // the body's one joint (slide / hinge; kl_axis = the joint's dof axis)
+      const int d = chain ? (grp < 3 ? T->dof_f0[grp] + T->kl_cpos[lane] - 1 : T->dof_palm) : T->dof_base;
+      real* cd = S.cdof[d];
+      real wa[3];
       mulmv3(wa, R, ax);
       if (type == GM_JNT_SLIDE) {
         cd[0] = cd[1] = cd[2] = 0; cd[3] = wa[0]; cd[4] = wa[1]; cd[5] = wa[2];
@@ -629,7 +642,11 @@ __device__ __forceinline__ void crb_rne(SharedT<CL>& S, const gm_model* __restri
     body_force(S, b, cvel, cacc);
   }
   GM_WAVE_SYNC();
+#ifdef GM_PHASE_SPLIT_NARROW
+  PH(1);
+#else
   PH(17);
+#endif
   // base body: its own inertia / force plus the four chain roots
   if (lane == 0) {
     const int bb = T->body_base;
@@ -1176,6 +1193,7 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
       }
       if (pass) {
         if (A.type == GM_GEOM_PLANE) {
+          NB_BEGIN();
           if (B.type == GM_GEOM_SPHERE) { kind = 1; cnt = plane_sphere(A, B, single); }
           else if (B.type == GM_GEOM_BOX) {
             kind = 2;
@@ -1195,9 +1213,13 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
               cnt += ok;
             }
           }
+          NB_END(15);
         } else if (A.type == GM_GEOM_SPHERE && B.type == GM_GEOM_BOX) {
+          NB_BEGIN();
           kind = 1; cnt = sphere_box(A, B, single);
+          NB_END(16);
         } else if (A.type == GM_GEOM_BOX && B.type == GM_GEOM_BOX) {
+          NB_BEGIN();
           // mjc_BoxBox: separating axes, then the face-clipped manifold or one edge contact
           bb_setup(A, B, bbs, ea, eb, da, db);
           if (bbs.kind == 1) {
@@ -1214,10 +1236,13 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
           } else if (bbs.kind == 2) {
             kind = 1; cnt = bb_edge_hit(bbs, ea, eb, da, db, single);
           }
+          NB_END(17);
         } else {
+          NB_BEGIN();
           ran_mpr = true;
           kind = 1; cnt = mpr(A, B, (real)m->mpr_tolerance, m->mpr_iterations, single);
           if (cnt && !(single.dist < 0)) cnt = 0;
+          NB_END(12);
         }
       }
     }
@@ -1235,6 +1260,7 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
     }
     if (pr < T->npair) { S.pair_off[pr] = (int16_t)off; S.pair_cnt[pr] = (int16_t)cnt; }
     if (cnt > 0) {
+      NB_BEGIN();
       real mu = fmax(A.friction, B.friction);
       if (kind == 1) {
         if (off < GM_MAX_CON) write_contact(S, off, g1, g2, b1, b2, single, mu);
@@ -1263,6 +1289,7 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
           w++;
         }
       }
+      NB_END(24);
     }
     written += total;
   }
@@ -1306,7 +1333,7 @@ __device__ __forceinline__ void integrate(SharedT<CL>& S, const gm_model* __rest
   // mj_Euler: under MuJoCo's actuator order the joint damping is implicit here
   // (euler_damping: qacc_e = (M + h D)^-1 (qfrc_smooth + qfrc_constraint) into S.xs)
   const bool mj = m->mujoco_actuators != 0;
-  if (mj) euler_damping<CL>(S, T, h, lane);
+  if (mj) euler_damping<CL>(S, T, h, fresh_lane());
   if (lane < T->nv) S.s.qvel[lane] += h * (mj ? S.xs[lane] : S.qacc[lane]);
   GM_WAVE_SYNC();
   if (lane < T->nv && lane < T->dof_obj) {
@@ -1772,17 +1799,17 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
                                                      int lane, bool prof) {
   unsigned long long t0 = prof ? clock64() : 0;
   if (lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
-  kinematics<CL>(S, m, T, lane, prof);
+  kinematics<CL>(S, m, T, fresh_lane(), prof);
   PH(0);
-  crb_rne<CL>(S, m, T, lane, prof);
+  crb_rne<CL>(S, m, T, fresh_lane(), prof);
   PH(1);
-  mass_and_forces<CL, CAL>(S, m, T, lane);
+  mass_and_forces<CL, CAL>(S, m, T, fresh_lane());
   PH(2);
-  collision(S, m, T, lane, prof);
+  collision(S, m, T, fresh_lane(), prof);
   PH(5);
-  newton_solve<CL, CAL>(S, m, T, lane, prof);
+  newton_solve<CL, CAL>(S, m, T, fresh_lane(), prof);
   PH(6);
-  integrate<CL, CAL>(S, m, T, lane);
+  integrate<CL, CAL>(S, m, T, fresh_lane());
   PH(8);
 }
 

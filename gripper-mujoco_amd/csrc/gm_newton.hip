@@ -1056,7 +1056,11 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     S.xs[bi == 0 ? T->dof_base : T->dof_obj + bi - 1] = y;
   }
   GM_WAVE_SYNC();
+#ifdef GM_PHASE_SPLIT_NARROW
+  PH(14);
+#else
   PH(24);
+#endif
 }
 
 // mj_solNewton restated (oracle newton_solve): warm start, Newton point on the active
@@ -1078,7 +1082,11 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
   const bool clane = lane < ncon;
   if (lane < nv) S.qacc[lane] = S.s.qacc_warm[lane];
   GM_WAVE_SYNC();
+#ifdef GM_PHASE_SPLIT_NARROW
+  PH(11);
+#else
   PH(12);
+#endif
   int it = 0, nls = 0;
   bool capped = true;   // no Newton point accepted within GM_NEWTON_MAXIT iterations
   bool ls_cap = false;  // a line search ran GM_NEWTON_MAXLS evaluations without settling
@@ -1087,7 +1095,7 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
 #pragma unroll
     for (int e = 0; e < 4; e++) act[e] = clane && jq[e] < 0;
     PH(13);
-    newton_point<CL>(S, m, T, lane, R, act, prof);
+    newton_point<CL>(S, m, T, fresh_lane(), R, act, prof);
     if (prof) t0 = clock64();
     real jx[4], jxl;
     rows_jar<CL>(S, m, T, obj_only, S.xs, lane, R, jx, jxl);

@@ -1,7 +1,7 @@
 """Developer probe: per-phase cycle breakdown of the fused env-step kernel on the bench's
 own workload (C3 set6_synthetic, scene spawn, steady state after the staggered pre-roll,
 scripted grasp mix), as opposed to tools/phase_profile.py's random actions from reset.
-usage: python tools/phase_profile_grasp.py [envs]"""
+usage: python tools/phase_profile_grasp.py [envs] [object_set]  (C2: 256 cylinder)"""
 import ctypes as C
 import os
 import sys
@@ -12,8 +12,9 @@ import gmx
 import bench
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+oset = sys.argv[2] if len(sys.argv) > 2 else "set6_synthetic"
 seed, MAX_EP = 1234, 250
-env = gmx.BatchedGripperEnv(n, object_set="set6_synthetic", settings=gmx.canonical_settings(seed=seed), seed=seed)
+env = gmx.BatchedGripperEnv(n, object_set=oset, settings=gmx.canonical_settings(seed=seed), seed=seed)
 env.set_scene_spawn(bench.mjenv_spawn_params(gmx), max_tries=3)
 env.reset()
 d_act = env.lib.gm_device_actions(env.ctx)
@@ -40,7 +41,7 @@ tot /= 3
 S = 63
 TOP = [0, 1, 2, 5, 6, 8, 9, 10]
 allc = tot[TOP].sum()
-print(f"n={n} grasp workload: mean cycles per env-step (lane 0) total {allc:.3e}  per substep {allc / S:.3e}")
+print(f"n={n} {oset} grasp workload: mean cycles per env-step (lane 0) total {allc:.3e}  per substep {allc / S:.3e}")
 for k, name in enumerate(env.PHASES):
     if k in (22, 23, 25, 26, 27) or name == "-":
         continue

@@ -130,7 +130,14 @@ struct __align__(16) SharedT {
 };
 
 // per-phase shader-clock accounting (gm_step_profiled); needs `prof`, `lane`, `t0` in scope
-#define PH(k) do { if (__builtin_expect(prof, 0)) { unsigned long long t_ = clock64(); if (lane == 0) S.tph[k] += t_ - t0; t0 = t_; } } while (0)
+#define PH(k) do { MARK(k); if (__builtin_expect(prof, 0)) { unsigned long long t_ = clock64(); if (lane == 0) S.tph[k] += t_ - t0; t0 = t_; } } while (0)
+// developer marker for static per-phase instruction counts (GM_ISA_MARKERS builds: an
+// s_nop 15 / s_nop k pair at every PH(k) in the disassembly)
+#ifdef GM_ISA_MARKERS
+#define MARK(k) asm volatile("s_nop 15\n\ts_nop " #k)
+#else
+#define MARK(k) do { } while (0)
+#endif
 // developer split of the narrowphase (GM_PHASE_SPLIT_NARROW builds): each collider branch
 // charges its own clocks to slot k from its first active lane (the branches are divergent)
 #ifdef GM_PHASE_SPLIT_NARROW
@@ -714,11 +721,11 @@ __device__ __forceinline__ void mass_and_forces(SharedT<CL>& S, const gm_model* 
       real* Hrow = objd ? &S.Ho[TRI(p, 0)] : (c < 3) ? &S.Hf[c][TRI(p, 0)] : &S.Hp[TRI(p, 0)];
 #pragma unroll
       for (int q = 0; q <= CL; q++) {
-        if (q > p) continue;
-        const int dq = objd ? d0 + q : (q == 0) ? T->dof_base : d0 + q - 1;
+        int dq = objd ? d0 + q : (q == 0) ? T->dof_base : d0 + q - 1;
+        dq = dq < SharedT<CL>::NV ? dq : SharedT<CL>::NV - 1;
         real v = dot6(S.cdof[dq], F);
         if (q == p) v += add;
-        Hrow[q] = v;
+        if (q <= p) Hrow[q] = v;
       }
     }
     // forces: passive springs/damping, PD control (target_.next, base target), RNE bias
@@ -1937,8 +1944,7 @@ __device__ __noinline__ int substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS_
     physics_substep_body<CL, CAL>(S, m, T, lane, prof);
     unsigned long long t0 = prof ? clock64() : 0;
     if (prof && lane == 0) S.tph[22] += t0 - tc;
-    update_all_call<CL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)(uintptr_t)m,
-                        (const GM_AS_GLOBAL GmTopo*)(uintptr_t)T, __lane_id());
+    update_all<CL>(S, m, T, fresh_lane());
     PH(9);
     if (!settle && !CAL && S.s.time > S.next_read) {
       monitor_call<CL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)(uintptr_t)m,

@@ -417,7 +417,7 @@ __device__ void smooth_matvec(SharedT<CL>& S, const GmTopo* __restrict__ T, cons
       acc = H[TRI(p, 0)] * v[T->dof_base];
 #pragma unroll
       for (int j = 1; j <= CL; j++) {
-        const real hv = (j <= p) ? H[TRI(p, j)] : H[TRI(j, p)];
+        const real hv = H[(j <= p) ? TRI(p, j) : TRI(j, p)];
         acc = acc + hv * v[f0 + j - 1];
       }
     } else if (c == GM_GRP_BASE) {
@@ -433,7 +433,7 @@ __device__ void smooth_matvec(SharedT<CL>& S, const GmTopo* __restrict__ T, cons
       acc = 0;
 #pragma unroll
       for (int l = 0; l < 6; l++) {
-        const real hv = (l <= p) ? S.Ho[TRI(p, l)] : S.Ho[TRI(l, p)];
+        const real hv = S.Ho[(l <= p) ? TRI(p, l) : TRI(l, p)];
         acc = acc + hv * v[T->dof_obj + l];
       }
     }
@@ -637,18 +637,27 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
   for (int k = 0; k < 21; k++) Ko[k] = 0;
 #pragma unroll
   for (int k = 0; k < 6; k++) Fo[k] = 0;
-  bool have_g = false, have_o = false;
+  bool have_g = false;
+  // the lane's (up to two) object pairs' contacts, in pair order, as one loop (one set of
+  // accumulator phis instead of one per pair)
+  int cs[2] = {0, 0}, ns[2] = {0, 0};
 #pragma unroll
   for (int s = 0; s < 2; s++) {
     const int pr = T->lane_opair[lane][s];
     const int pg = T->lane_gpair[lane][s];
     if (pg >= 0 && S.pair_cnt[pg] > 0 && S.pair_off[pg] < ncon) have_g = true;
-    if (pr < 0) continue;
-    const int c0 = S.pair_off[pr];
-    int c1 = c0 + S.pair_cnt[pr];
-    if (c1 > ncon) c1 = ncon;
-    have_o = have_o || c1 > c0;
-    for (int c = c0; c < c1; c++) {
+    if (pr >= 0) {
+      const int c0 = S.pair_off[pr];
+      int c1 = c0 + S.pair_cnt[pr];
+      if (c1 > ncon) c1 = ncon;
+      cs[s] = c0;
+      ns[s] = c1 > c0 ? c1 - c0 : 0;
+    }
+  }
+  const bool have_o = ns[0] + ns[1] > 0;
+  {
+    for (int t = 0; t < ns[0] + ns[1]; t++) {
+      const int c = t < ns[0] ? cs[0] + t : cs[1] + (t - ns[0]);
       const real* qf = S.nw.QF[c];
       const real pos[3] = {S.con[c][1], S.con[c][2], S.con[c][3]};
       const real sg = (S.cbody[c][1] == b) ? 1.0 : -1.0;
@@ -752,17 +761,27 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
 #pragma unroll
       for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
       symK_mul(Ko, cd, y);
+      // (all CL entries computed, in range for every p, and kept for j <= p; the motion
+      // subspace of chain position j is lane j's cd, taken by row_newbcast instead of an
+      // LDS round trip per entry)
 #pragma unroll
-      for (int j = 1; j <= CL; j++)
-        if (j <= p) h[j] = H[TRI(p, j)] + dot6(S.cdof[T->dof_f0[rowf] + j - 1], y);
+      for (int j = 1; j <= CL; j++) {
+        real cj[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) cj[k] = row_bcast(cd[k], j);
+        const real v = H[TRI(p, j)] + dot6(cj, y);
+        h[j] = (j <= p) ? v : h[j];
+      }
       hb[0] = H[TRI(p, 0)] + dot6(cdb, y);
 #pragma unroll
       for (int k = 0; k < 6; k++) hb[1 + k] = -dot6(S.cdof[T->dof_obj + k], y);
       rhs = S.frc[d] + dot6(cd, Fo);
     } else {
 #pragma unroll
-      for (int j = 1; j <= CL; j++)
-        if (j <= p) h[j] = H[TRI(p, j)];
+      for (int j = 1; j <= CL; j++) {
+        const real v = H[TRI(p, j)];
+        h[j] = (j <= p) ? v : h[j];
+      }
       hb[0] = H[TRI(p, 0)];
       rhs = S.frc[d];
     }
@@ -806,8 +825,10 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
       symK_mul(Koo, cok, yk);
       hb[0] = -dot6(cok, yob);
 #pragma unroll
-      for (int l2 = 0; l2 < 6; l2++)
-        if (l2 <= k) hb[1 + l2] = S.Ho[TRI(k, l2)] + dot6(S.cdof[T->dof_obj + l2], yk);
+      for (int l2 = 0; l2 < 6; l2++) {
+        const real v = S.Ho[TRI(k, l2)] + dot6(S.cdof[T->dof_obj + l2], yk);
+        hb[1 + l2] = (l2 <= k) ? v : hb[1 + l2];
+      }
       rhs = S.frc[T->dof_obj + k] + dot6(cok, S.st.oo + 21);
     }
   }
@@ -921,19 +942,24 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
       for (int j = 1; j < k; j++) Hpk = (p == j) ? hk[j] : Hpk;
       const real a = Hpk * ihk;
       const real aa = upd ? a : 0.0;
-      const real sc = piv ? ihk : 1.0;
       if (piv && rowf < 3) {
         real* ub = S.fs.lbub[rowf][k - 1] + 7;
 #pragma unroll
         for (int t = 0; t < 7; t++) ub[t] = hb[t];
       }
+      // (the pivot row's scaling by 1 / d_k is applied once after the loop: no later step
+      // changes the row, whose updates from here on subtract exact zeros)
 #pragma unroll
-      for (int j = 1; j < k; j++) h[j] = (h[j] - hk[j] * aa) * sc;
+      for (int j = 1; j < k; j++) h[j] = h[j] - hk[j] * aa;
 #pragma unroll
-      for (int t = 0; t < 7; t++) hb[t] = (hb[t] - hkb[t] * aa) * sc;
+      for (int t = 0; t < 7; t++) hb[t] = hb[t] - hkb[t] * aa;
       h[k] = upd ? a : h[k];
       invd = piv ? ihk : invd;
     }
+#pragma unroll
+    for (int j = 1; j < CL; j++) h[j] = (j < p) ? h[j] * invd : h[j];
+#pragma unroll
+    for (int t = 0; t < 7; t++) hb[t] = hb[t] * invd;
     if (rowf < 3 && p >= 1 && p <= CL) {
       real* lb = S.fs.lbub[rowf][p - 1];
 #pragma unroll
@@ -989,12 +1015,13 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
       for (int j = 0; j < k; j++) Bik = (bi == j) ? bk[j] : Bik;
       const real a = Bik * ihk;
       const real aa = upd ? a : 0.0;
-      const real sc = piv ? ihk : 1.0;
 #pragma unroll
-      for (int j = 0; j < k; j++) hb[j] = (hb[j] - bk[j] * aa) * sc;
+      for (int j = 0; j < k; j++) hb[j] = hb[j] - bk[j] * aa;   // (pivot row scaled after the loop)
       hb[k] = upd ? a : hb[k];
       invd = piv ? ihk : invd;
     }
+#pragma unroll
+    for (int j = 0; j < 6; j++) hb[j] = (j < bi) ? hb[j] * invd : hb[j];
   }
   PH(14);
   // ---- solve: forward (chains leaf first, border sums, border), D, backward
@@ -1216,7 +1243,10 @@ __device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __re
     const int d = T->dof_f0[rowf] + p - 1;
     const real hd = h * T->dof_damp[d];
 #pragma unroll
-    for (int j = 1; j <= CL; j++) L[j] = (j <= p) ? H[TRI(p, j)] : 0.0;
+    for (int j = 1; j <= CL; j++) {
+      const real v = H[TRI(p, j)];
+      L[j] = (j <= p) ? v : 0.0;
+    }
 #pragma unroll
     for (int j = 1; j <= CL; j++) L[j] = (j == p) ? L[j] + hd : L[j];
     lb = H[TRI(p, 0)];
@@ -1248,14 +1278,16 @@ __device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __re
       for (int j = 1; j < k; j++) Hpk = (p == j) ? hk[j] : Hpk;
       const real a = Hpk * ihk;
       const real aa = upd ? a : 0.0;
-      const real sc = piv ? ihk : 1.0;
       ub = piv ? lb : ub;
 #pragma unroll
-      for (int j = 1; j < k; j++) L[j] = (L[j] - hk[j] * aa) * sc;
-      lb = (lb - hkb * aa) * sc;
+      for (int j = 1; j < k; j++) L[j] = L[j] - hk[j] * aa;   // (pivot row scaled after the loop)
+      lb = lb - hkb * aa;
       L[k] = upd ? a : L[k];
       invd = piv ? ihk : invd;
     }
+#pragma unroll
+    for (int j = 1; j < CL; j++) L[j] = (j < p) ? L[j] * invd : L[j];
+    lb = lb * invd;
     // forward over the chains, leaf first
 #pragma unroll
     for (int k = CL; k >= 1; k--) {

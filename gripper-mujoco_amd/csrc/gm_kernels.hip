@@ -83,6 +83,8 @@ struct __align__(16) SharedT {
   static constexpr int TRIC = (CL + 1) * (CL + 2) / 2;
   GmEnvHot s;                     // the env's state minus its sensor windows
   real lock_pre[GM_MAX_LOCK];     // pre-integration qpos of the lock dofs (weld re-anchoring)
+  real lrow_D[GM_MAX_LOCK + 1], lrow_aref[GM_MAX_LOCK + 1];   // lock rows (lock_rows; + a spare slot)
+  int32_t lrow_dof[GM_MAX_LOCK + 2];
   real qacc[NV];                  // the Newton iterate; the substep's qacc at the end
   real xs[NV];                    // the Newton point x (line search: the step d = x - q)
   real Ma[NV], Mv[NV];            // H~ q and H~ d
@@ -517,10 +519,14 @@ __device__ __forceinline__ void chain_sums(SharedT<CL>& S, int b0, real* fs, rea
   }
 }
 
-template <int CL>
+template <int CL, bool CAL>
+__device__ __forceinline__ void lock_rows(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane);
+template <int CL, bool CAL>
 __device__ __forceinline__ void crb_rne(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                         bool prof = false) {
   unsigned long long t0 = prof ? clock64() : 0;
+  // the constraint problem's lock rows ride in this phase's first block (see lock_rows)
+  lock_rows<CL, CAL>(S, m, T, lane);
   // Lanes = bodies.  Along each finger / palm chain the velocities and bias accelerations
   // are segmented prefix sums and the composite forces / inertias segmented suffix sums
   // (Hillis-Steele over the chain position, shuffles within the wave); the base body is
@@ -538,9 +544,12 @@ __device__ __forceinline__ void crb_rne(SharedT<CL>& S, const gm_model* __restri
   const int p = T->kl_cpos[lane];
   const int d = chain ? (grp < 3 ? T->dof_f0[grp] + p - 1 : T->dof_palm) : db;
   real cd[6], v[6];
-  const real qd = chain ? S.s.qvel[d] : 0.0;
+  // (operands loaded on every lane -- d is the base dof off the chains -- and selected: a
+  // select instead of a divergent branch around each load)
+  const real qvd = S.s.qvel[d];
+  const real qd = chain ? qvd : 0.0;
 #pragma unroll
-  for (int k = 0; k < 6; k++) { cd[k] = chain ? S.cdof[d][k] : 0.0; v[k] = cd[k] * qd; }
+  for (int k = 0; k < 6; k++) { const real c = S.cdof[d][k]; cd[k] = chain ? c : 0.0; v[k] = cd[k] * qd; }
   // The scans add their shifted operand unconditionally: every source outside a lane's
   // chain segment holds an exact zero (the empty position 0 of each finger row, the base
   // lane before the palm, the no-body lanes past the chain end, the zero-inertia object
@@ -584,7 +593,7 @@ __device__ __forceinline__ void crb_rne(SharedT<CL>& S, const gm_model* __restri
   // body forces I a + v x* (I v), then suffix sums of forces and inertias
   real ci[10], f[6];
 #pragma unroll
-  for (int k = 0; k < 10; k++) ci[k] = chain ? S.cinert[b][k] : 0.0;
+  for (int k = 0; k < 10; k++) { const real c = S.cinert[b < 0 ? 0 : b][k]; ci[k] = chain ? c : 0.0; }
   {
     real t1[6], t2[6];
     inert_mul(f, ci, ca);
@@ -654,26 +663,36 @@ __device__ __forceinline__ void crb_rne(SharedT<CL>& S, const gm_model* __restri
 #else
   PH(17);
 #endif
-  // base body: its own inertia / force plus the four chain roots
-  if (lane == 0) {
+  // base body: its own inertia / force plus the four chain roots, one lane per value
+  // (lanes 0..9 the composite inertia, 10..15 the force; the base's own body force is
+  // formed on every lane from its uniform operands, the same operations as body_force)
+  {
     const int bb = T->body_base;
-    body_force(S, bb, cvb, cab);
-    real ic[10], fb[6];
+    real ci[10], t1[6], t2[6], fo[6];
 #pragma unroll
-    for (int k = 0; k < 10; k++) ic[k] = S.cinert[bb][k];
+    for (int k = 0; k < 10; k++) ci[k] = S.cinert[bb][k];
+    inert_mul(fo, ci, cab);
+    inert_mul(t1, ci, cvb);
+    cross_force(t2, cvb, t1);
 #pragma unroll
-    for (int k = 0; k < 6; k++) fb[k] = S.cfrc[bb][k];
+    for (int k = 0; k < 6; k++) fo[k] = fo[k] + t2[k];
+    const bool isI = lane < 10;
+    const int k = isI ? lane : (lane < 16 ? lane - 10 : 0);
+    real own = ci[0];
+#pragma unroll
+    for (int t = 1; t < 10; t++) own = (lane == t) ? ci[t] : own;
+#pragma unroll
+    for (int t = 0; t < 6; t++) own = (lane == 10 + t) ? fo[t] : own;
+    real acc = own;
 #pragma unroll
     for (int c = 0; c < 4; c++) {
-#pragma unroll
-      for (int k = 0; k < 10; k++) ic[k] += S.chain_I[c][k];
-#pragma unroll
-      for (int k = 0; k < 6; k++) fb[k] += S.chain_f[c][k];
+      const real vI = S.chain_I[c][k], vf = S.chain_f[c][k];
+      acc += isI ? vI : vf;
     }
-#pragma unroll
-    for (int k = 0; k < 10; k++) S.Ic[bb][k] = ic[k];
-#pragma unroll
-    for (int k = 0; k < 6; k++) S.cfrc[bb][k] = fb[k];
+    if (lane < 16) {
+      real* dst = isI ? &S.Ic[bb][k] : &S.cfrc[bb][k];
+      *dst = acc;
+    }
   }
   GM_WAVE_SYNC();
 }
@@ -1808,7 +1827,7 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
   if (lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
   kinematics<CL>(S, m, T, fresh_lane(), prof);
   PH(0);
-  crb_rne<CL>(S, m, T, fresh_lane(), prof);
+  crb_rne<CL, CAL>(S, m, T, fresh_lane(), prof);
   PH(1);
   mass_and_forces<CL, CAL>(S, m, T, fresh_lane());
   PH(2);
@@ -1878,8 +1897,10 @@ struct GmPreempt {
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// returns the substeps run (nsub unless the preemption test yielded)
-template <int CL, bool CAL>
+// returns the substeps run (nsub unless the preemption test yielded).  PROF = false
+// compiles the per-phase clock reads (PH) out: no uniform branch at every phase boundary,
+// so the scheduler's regions span them (the env-step kernel's chunked path runs this one)
+template <int CL, bool CAL, bool PROF>
 __device__ __noinline__ int substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS_GLOBAL gm_model* m_,
                                          const GM_AS_GLOBAL GmTopo* T_, const GM_AS_GLOBAL gm_config* C_, int lane_in,
                                          bool prof_in, int nsub_in, bool settle_in, GmPreempt pre) {
@@ -1890,7 +1911,7 @@ __device__ __noinline__ int substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS_
   const GM_AS_CONST GmTopo* T_s = uniform_const_ptr(T_);
   const gm_config* C = (const gm_config*)uniform_const_ptr(C_);
   const int nsub = __builtin_amdgcn_readfirstlane(nsub_in);
-  const bool prof = __builtin_amdgcn_readfirstlane((int)prof_in) != 0;
+  const bool prof = PROF && __builtin_amdgcn_readfirstlane((int)prof_in) != 0;
   const bool settle = __builtin_amdgcn_readfirstlane((int)settle_in) != 0;
   (void)lane_in;
   const int every = CAL ? 0 : __builtin_amdgcn_readfirstlane(pre.every);
@@ -2512,7 +2533,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
     const uint32_t own = cost[env];
     const GmPreempt pre{fresh_head, order, cost, n, own, left, cr.nsub,
                         cr.yielded < q.max_yields ? q.chunk : 0, q.margin, bq, cmax, q.cmargin};
-    const int k = substep_loop<CL, false>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
+    const int k = substep_loop<CL, false, false>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
                                           (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
                                           false, left, false, pre);
     cr.sub_done += k;
@@ -2603,9 +2624,12 @@ __global__ __launch_bounds__(NT, GM_WPS) void gm_step_kernel(
   const int nsub = settle ? 400 : calib ? S.s.cal_steps : (mode == 2) ? 1 : C->sim_steps_per_action + S.s.extra_substeps;
   // a calibration run starts from a reset's mj_forward pose
   if (calib && lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
-  const int ran = substep_loop<CL, CAL>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
-                                        (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane, prof,
-                                        nsub, settle, GmPreempt{});
+  const int ran = prof ? substep_loop<CL, CAL, true>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
+                                                     (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
+                                                     prof, nsub, settle, GmPreempt{})
+                       : substep_loop<CL, CAL, false>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
+                                                      (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
+                                                      false, nsub, settle, GmPreempt{});
   // a calibration run reports the substeps it made (the unstable one included: the loop
   // stops right after it, as the reference's retry resumes after it)
   if (calib && lane == 0) S.s.cal_steps = S.s.badqacc ? ran + 1 : ran;

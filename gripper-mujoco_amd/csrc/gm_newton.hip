@@ -294,7 +294,8 @@ __device__ void body_vel(SharedT<CL>& S, const real* const* v, real (*const* V)[
 #pragma unroll
     for (int k = 0; k < 6; k++) {
       cvb[n][k] = S.cdof[db][k] * vb;
-      s[n][k] = (chain ? S.cdof[d][k] : 0.0) * vd;
+      const real c = S.cdof[d][k];   // (d: the base dof off the chains; loaded, then selected)
+      s[n][k] = (chain ? c : 0.0) * vd;
     }
   }
   if (!obj_only) {
@@ -451,14 +452,13 @@ struct RowsT {
   int ldof;
 };
 
-// constraint setup (mj_makeConstraint / mj_makeImpedance): impedance, the regulariser
-// R = (1 - d) / d diagApprox (lock rows: dof_invweight0; pyramid edges:
-// tran + mu^2 tran, tran = the two bodies' invweight0), reference accelerations
+// The motor-lock rows (1-dof joint equalities) of the constraint problem: impedance, the
+// regulariser R = (1 - d) / d dof_invweight0 and the reference acceleration of each active
+// lock, row r on lane r, into S.lrow_* and S.nl.  They need only qpos, qvel and the motion
+// subspaces, so crb_rne issues them in its first basic block: their division chains fill
+// the scans' latency instead of running as a phase of their own.
 template <int CL, bool CAL>
-__device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
-                                 int lane, RowsT& R, real* jq, real& jql, bool& obj_only, bool prof = false) {
-  unsigned long long t0 = prof ? clock64() : 0;
-  (void)t0;
+__device__ __forceinline__ void lock_rows(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
   const real h = CAL ? S.s.dt : m->timestep;
   real tc = m->solref[0];
   if (tc < 2 * h) tc = 2 * h;
@@ -480,8 +480,7 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
     tran = mine ? T->lock_tran[kk] : tran;
     nl += act ? 1 : 0;
   }
-  R.lD = 0; R.laref = 0; R.ldof = 0;
-  if (lane < nl) {
+  {
     const real pos = S.s.qpos[d] - S.s.lock_q[k];
     const real vel = S.s.qvel[d];
     // the reference's weld on a slide as one row on the dof (oracle constraint_setup):
@@ -507,11 +506,36 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
       De = on[r] ? De + Da[r] * av[r] : De;
       Dar = on[r] ? Dar + Da[r] * ar[r] : Dar;
     }
-    R.lD = De;
-    R.laref = div_n(Dar, De);
-    R.ldof = d;
+    // every lane stores (lanes past the active rows into the spare slot GM_MAX_LOCK): no
+    // branch, so the whole computation stays in one basic block with the caller's
+    const int slot = lane < nl ? lane : GM_MAX_LOCK;
+    S.lrow_D[slot] = De;
+    S.lrow_aref[slot] = div_n(Dar, De);
+    S.lrow_dof[slot] = d;
   }
-  if (lane == 0) { S.nl = nl; S.nefc = nl + 4 * S.ncon; }
+  S.nl = nl;   // (wave-uniform: every lane stores the same value)
+}
+
+// constraint setup (mj_makeConstraint / mj_makeImpedance): impedance, the regulariser
+// R = (1 - d) / d diagApprox (lock rows: dof_invweight0; pyramid edges:
+// tran + mu^2 tran, tran = the two bodies' invweight0), reference accelerations
+template <int CL, bool CAL>
+__device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
+                                 int lane, RowsT& R, real* jq, real& jql, bool& obj_only, bool prof = false) {
+  unsigned long long t0 = prof ? clock64() : 0;
+  (void)t0;
+  const real h = CAL ? S.s.dt : m->timestep;
+  real tc = m->solref[0];
+  if (tc < 2 * h) tc = 2 * h;
+  const real dr = m->solref[1], dmax = m->solimp[1];
+  const real K = rcp_n(dmax * dmax * tc * tc * dr * dr);
+  const real Bd = div_n(2.0, dmax * tc);
+  // lock rows: formed in crb_rne's first block (lock_rows below) and read back here
+  const int nl = S.nl;
+  R.lD = 0; R.laref = 0; R.ldof = 0;
+  if (lane < GM_MAX_LOCK) { R.lD = S.lrow_D[lane]; R.laref = S.lrow_aref[lane]; R.ldof = S.lrow_dof[lane]; }
+  if (lane >= nl) { R.lD = 0; R.laref = 0; R.ldof = 0; }
+  if (lane == 0) S.nefc = nl + 4 * S.ncon;
 #ifdef GM_PHASE_SPLIT_SETUP
   PH(15);   // developer split: lock rows
 #endif
@@ -531,7 +555,10 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
 #ifdef GM_PHASE_SPLIT_SETUP
   PH(16);   // developer split: the two velocity scans
 #endif
-  jql = (lane < nl) ? S.s.qacc_warm[R.ldof] - R.laref : 0.0;
+  {
+    const real qw = S.s.qacc_warm[R.ldof];   // (ldof = 0 off the lock lanes)
+    jql = (lane < nl) ? qw - R.laref : 0.0;
+  }
 #pragma unroll
   for (int e = 0; e < 4; e++) jq[e] = 0.0;
   R.cD = 0;
@@ -540,8 +567,9 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
   if (lane < S.ncon) {
     const real* C = S.con[lane];
     const int b1 = S.cbody[lane][0], b2 = S.cbody[lane][1];
-    const real iw1 = (b1 == T->body_obj) ? S.s.obj_invw[0] : m->body_invweight0[b1][0];
-    const real iw2 = (b2 == T->body_obj) ? S.s.obj_invw[0] : m->body_invweight0[b2][0];
+    const real oiw = S.s.obj_invw[0], biw1 = m->body_invweight0[b1][0], biw2 = m->body_invweight0[b2][0];
+    const real iw1 = (b1 == T->body_obj) ? oiw : biw1;
+    const real iw2 = (b2 == T->body_obj) ? oiw : biw2;
     const real tran = iw1 + iw2;
     const real mu = C[10];
     const real diag = tran + (mu * mu) * tran;
@@ -1144,7 +1172,8 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
     if (lane < nv) S.xs[lane] = S.xs[lane] - S.qacc[lane];
     GM_WAVE_SYNC();
     smooth_matvec<CL>(S, T, S.xs, S.Mv, lane);
-    const real dd = lane < nv ? S.xs[lane] : 0.0;
+    const real xl = S.xs[lane];   // (lanes past nv read the next LDS vector; selected away)
+    const real dd = lane < nv ? xl : 0.0;
     const real g0 = wave_sum(lane < nv ? dd * (S.Ma[lane] - S.frc[lane]) : 0.0);
     const real h0 = wave_sum(lane < nv ? dd * S.Mv[lane] : 0.0);
     real dj[4];

@@ -42,6 +42,26 @@ __device__ __forceinline__ int fresh_lane() {
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
   return lane;
 }
+// Pins a value's computation to the current block: the optimizer otherwise sinks the
+// operands of a select or a conditional store (LDS loads, dot products) into a divergent
+// branch per entry, each with its own load -> wait -> use chain.
+__device__ __forceinline__ void keep(double x) { asm volatile("" ::"v"(x)); }
+// ... and a batch of up to 13 values at once: their loads are all issued before the one
+// wait (the scheduler otherwise issues each just before its use, one latency per entry)
+template <int N>
+__device__ __forceinline__ void keep_n(const double* a) {
+  static_assert(N >= 1 && N <= 28, "keep_n: 1..28 values");
+#define GM_K(i) "v"(a[(i) < N ? (i) : 0])
+  if constexpr (N <= 13) {
+    asm volatile("" ::GM_K(0), GM_K(1), GM_K(2), GM_K(3), GM_K(4), GM_K(5), GM_K(6), GM_K(7), GM_K(8), GM_K(9),
+                 GM_K(10), GM_K(11), GM_K(12));
+  } else {
+    asm volatile("" ::GM_K(0), GM_K(1), GM_K(2), GM_K(3), GM_K(4), GM_K(5), GM_K(6), GM_K(7), GM_K(8), GM_K(9),
+                 GM_K(10), GM_K(11), GM_K(12), GM_K(13), GM_K(14), GM_K(15), GM_K(16), GM_K(17), GM_K(18),
+                 GM_K(19), GM_K(20), GM_K(21), GM_K(22), GM_K(23), GM_K(24), GM_K(25), GM_K(26), GM_K(27));
+  }
+#undef GM_K
+}
 #define GM_CQ_NB 16  // priority buckets per XCD of the chunked env-step (gm_step_kernel)
 // gm_step_kernel is instantiated per finger chain length (CL = n_seg + 2) so every chain
 // recursion is unrolled into registers; GM_NSEG_LIST is the set compiled in.
@@ -744,6 +764,7 @@ __device__ __forceinline__ void mass_and_forces(SharedT<CL>& S, const gm_model* 
         dq = dq < SharedT<CL>::NV ? dq : SharedT<CL>::NV - 1;
         real v = dot6(S.cdof[dq], F);
         if (q == p) v += add;
+        keep(v);
         if (q <= p) Hrow[q] = v;
       }
     }
@@ -1185,7 +1206,9 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
   constexpr int NBATCH = gm_pair_batches(CL);
   int written = 0;
   bool ran_mpr = false;   // profiling: a lane of this env ran the convex (MPR) collider
-#pragma unroll
+  // (not unrolled: with two batches (N = 9, 10) the unrolled copies held each other's
+  // collider state live and the pair loop spilled ~1 K scratch operations per substep)
+#pragma nounroll
   for (int bi = 0; bi < NBATCH; bi++) {
     const int pr = bi * NT + lane;
     int cnt = 0, kind = 0, g1 = 0, g2 = 0, b1 = 0, b2 = 0;

@@ -319,16 +319,33 @@ __device__ void body_vel(SharedT<CL>& S, const real* const* v, real (*const* V)[
       for (int k = 0; k < 6; k++) V[n][T->body_base][k] = cvb[n][k];
   } else if (b == T->body_obj) {
     const int d0 = T->dof_obj;
+    real acc[NVEC][6];
 #pragma unroll
-    for (int n = 0; n < NVEC; n++) {
-      real acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int n = 0; n < NVEC; n++)
 #pragma unroll
-      for (int k = 0; k < 6; k++)
+      for (int t = 0; t < 6; t++) acc[n][t] = 0;
 #pragma unroll
-        for (int t = 0; t < 6; t++) acc[t] += S.cdof[d0 + k][t] * v[n][d0 + k];
+    for (int k0 = 0; k0 < 6; k0 += 3) {
+      real co[18], vk[NVEC][3];   // three object dofs' subspaces and velocities, one batch
 #pragma unroll
-      for (int t = 0; t < 6; t++) V[n][b][t] = acc[t];
+      for (int k = 0; k < 3; k++) {
+#pragma unroll
+        for (int t = 0; t < 6; t++) co[6 * k + t] = S.cdof[d0 + k0 + k][t];
+#pragma unroll
+        for (int n = 0; n < NVEC; n++) vk[n][k] = v[n][d0 + k0 + k];
+      }
+      keep_n<18>(co);
+#pragma unroll
+      for (int k = 0; k < 3; k++)
+#pragma unroll
+        for (int n = 0; n < NVEC; n++)
+#pragma unroll
+          for (int t = 0; t < 6; t++) acc[n][t] += co[6 * k + t] * vk[n][k];
     }
+#pragma unroll
+    for (int n = 0; n < NVEC; n++)
+#pragma unroll
+      for (int t = 0; t < 6; t++) V[n][b][t] = acc[n][t];
   } else if (lane == 0) {
 #pragma unroll
     for (int n = 0; n < NVEC; n++)
@@ -785,32 +802,46 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     const int d = T->dof_f0[rowf] + p - 1;
     const real* H = S.Hf[rowf];
     if (any_o) {
-      real cd[6], y[6];
+      real cd[6], y[6], Hr[CL + 1];
 #pragma unroll
       for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
+#pragma unroll
+      for (int j = 0; j <= CL; j++) Hr[j] = H[TRI(p, j)];   // (the row, in range for every p)
+      keep_n<CL + 1>(Hr);
       symK_mul(Ko, cd, y);
-      // (all CL entries computed, in range for every p, and kept for j <= p; the motion
-      // subspace of chain position j is lane j's cd, taken by row_newbcast instead of an
-      // LDS round trip per entry)
+      // (all CL entries computed and kept for j <= p; the motion subspace of chain position
+      // j is lane j's cd, taken by row_newbcast instead of an LDS round trip per entry)
 #pragma unroll
       for (int j = 1; j <= CL; j++) {
         real cj[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) cj[k] = row_bcast(cd[k], j);
-        const real v = H[TRI(p, j)] + dot6(cj, y);
+        const real v = Hr[j] + dot6(cj, y);
+        keep(v);
         h[j] = (j <= p) ? v : h[j];
       }
-      hb[0] = H[TRI(p, 0)] + dot6(cdb, y);
+      hb[0] = Hr[0] + dot6(cdb, y);
+      // the object's six motion subspaces (wave-uniform reads), in two batches of three
 #pragma unroll
-      for (int k = 0; k < 6; k++) hb[1 + k] = -dot6(S.cdof[T->dof_obj + k], y);
+      for (int k0 = 0; k0 < 6; k0 += 3) {
+        real co[18];
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+#pragma unroll
+          for (int t = 0; t < 6; t++) co[6 * k + t] = S.cdof[T->dof_obj + k0 + k][t];
+        keep_n<18>(co);
+#pragma unroll
+        for (int k = 0; k < 3; k++) hb[1 + k0 + k] = -dot6(co + 6 * k, y);
+      }
       rhs = S.frc[d] + dot6(cd, Fo);
     } else {
+      real Hr[CL + 1];
 #pragma unroll
-      for (int j = 1; j <= CL; j++) {
-        const real v = H[TRI(p, j)];
-        h[j] = (j <= p) ? v : h[j];
-      }
-      hb[0] = H[TRI(p, 0)];
+      for (int j = 0; j <= CL; j++) Hr[j] = H[TRI(p, j)];
+      keep_n<CL + 1>(Hr);
+#pragma unroll
+      for (int j = 1; j <= CL; j++) h[j] = (j <= p) ? Hr[j] : h[j];
+      hb[0] = Hr[0];
       rhs = S.frc[d];
     }
   } else if (lane == GM_LANE_PALM_F && !any_o) {
@@ -820,16 +851,27 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
   } else if (lane == GM_LANE_PALM_F) {
     const int d = T->dof_palm;
     const real* st = S.st.root[3];
-    real K0[21], cd[6], y[6];
+    real K0[27], y[6];   // the palm root's composite (21) then its cdof (6), one batch
 #pragma unroll
     for (int k = 0; k < 21; k++) K0[k] = st[k];
 #pragma unroll
-    for (int k = 0; k < 6; k++) cd[k] = S.cdof[d][k];
+    for (int k = 0; k < 6; k++) K0[21 + k] = S.cdof[d][k];
+    keep_n<27>(K0);
+    const real* cd = K0 + 21;
     symK_mul(K0, cd, y);
     h[1] = S.Hp[TRI(1, 1)] + dot6(cd, y);
     hb[0] = S.Hp[TRI(1, 0)] + dot6(cdb, y);
 #pragma unroll
-    for (int k = 0; k < 6; k++) hb[1 + k] = -dot6(S.cdof[T->dof_obj + k], y);
+    for (int k0 = 0; k0 < 6; k0 += 3) {
+      real co[18];   // (the object's subspaces, wave-uniform, in two batches)
+#pragma unroll
+      for (int k = 0; k < 3; k++)
+#pragma unroll
+        for (int t = 0; t < 6; t++) co[6 * k + t] = S.cdof[T->dof_obj + k0 + k][t];
+      keep_n<18>(co);
+#pragma unroll
+      for (int k = 0; k < 3; k++) hb[1 + k0 + k] = -dot6(co + 6 * k, y);
+    }
     rhs = S.frc[d] + dot6(cd, st + 42);
   } else if (lane >= 48 && lane < 55) {
     const int i = lane - 48;
@@ -839,6 +881,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
       real KBo[21];
 #pragma unroll
       for (int k = 0; k < 21; k++) KBo[k] = cp[k];
+      keep_n<21>(KBo);
       symK_mul(KBo, cdb, yob);
     }
     if (i == 0) {
@@ -846,16 +889,30 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
       rhs = any_o ? S.frc[T->dof_base] + dot6(cdb, cp + 42) : S.frc[T->dof_base];
     } else {
       const int k = i - 1;
-      const real* cok = S.cdof[T->dof_obj + k];
-      real Koo[21], yk[6];
+      real KC[27], yk[6];   // Koo (21) then the row's cdof (6), loaded in one batch
 #pragma unroll
-      for (int t = 0; t < 21; t++) Koo[t] = S.st.oo[t];
-      symK_mul(Koo, cok, yk);
+      for (int t = 0; t < 21; t++) KC[t] = S.st.oo[t];
+#pragma unroll
+      for (int t = 0; t < 6; t++) KC[21 + t] = S.cdof[T->dof_obj + k][t];
+      keep_n<27>(KC);
+      const real* cok = KC + 21;
+      symK_mul(KC, cok, yk);
       hb[0] = -dot6(cok, yob);
 #pragma unroll
-      for (int l2 = 0; l2 < 6; l2++) {
-        const real v = S.Ho[TRI(k, l2)] + dot6(S.cdof[T->dof_obj + l2], yk);
-        hb[1 + l2] = (l2 <= k) ? v : hb[1 + l2];
+      for (int l0 = 0; l0 < 6; l0 += 3) {
+        real co[18];   // three of the object's motion subspaces (wave-uniform), one batch
+#pragma unroll
+        for (int l = 0; l < 3; l++)
+#pragma unroll
+          for (int t = 0; t < 6; t++) co[6 * l + t] = S.cdof[T->dof_obj + l0 + l][t];
+        keep_n<18>(co);
+#pragma unroll
+        for (int l = 0; l < 3; l++) {
+          const int l2 = l0 + l;
+          const real v = S.Ho[TRI(k, l2)] + dot6(co + 6 * l, yk);
+          keep(v);
+          hb[1 + l2] = (l2 <= k) ? v : hb[1 + l2];
+        }
       }
       rhs = S.frc[T->dof_obj + k] + dot6(cok, S.st.oo + 21);
     }
@@ -1271,10 +1328,14 @@ __device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __re
     const real* H = S.Hf[rowf];
     const int d = T->dof_f0[rowf] + p - 1;
     const real hd = h * T->dof_damp[d];
+    {
+      real Hr[CL + 1];
 #pragma unroll
-    for (int j = 1; j <= CL; j++) {
-      const real v = H[TRI(p, j)];
-      L[j] = (j <= p) ? v : 0.0;
+      for (int j = 1; j <= CL; j++) Hr[j] = H[TRI(p, j)];
+      Hr[0] = Hr[1];
+      keep_n<CL + 1>(Hr);
+#pragma unroll
+      for (int j = 1; j <= CL; j++) L[j] = (j <= p) ? Hr[j] : 0.0;
     }
 #pragma unroll
     for (int j = 1; j <= CL; j++) L[j] = (j == p) ? L[j] + hd : L[j];

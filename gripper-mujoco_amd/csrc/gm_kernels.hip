@@ -62,7 +62,8 @@ __device__ __forceinline__ void keep_n(const double* a) {
   }
 #undef GM_K
 }
-#define GM_CQ_NB 16  // priority buckets per XCD of the chunked env-step (gm_step_kernel)
+#define GM_CQ_NB 16
+#define GM_BB_SLOTS 18   // box-box hit slots in the LDS union (18 x 256 B <= the union's smallest size)  // priority buckets per XCD of the chunked env-step (gm_step_kernel)
 // gm_step_kernel is instantiated per finger chain length (CL = n_seg + 2) so every chain
 // recursion is unrolled into registers; GM_NSEG_LIST is the set compiled in.
 #ifndef GM_NSEG_LIST
@@ -138,6 +139,9 @@ struct __align__(16) SharedT {
     struct { real qf_[GM_MAX_CON][9]; real root[4][54]; real comp[54]; real oo[27]; } st;
     struct { real lbub[3][CL][14]; real plb[14]; real bbx[28]; real ych[3][CL]; real ypalm; } fs;
     struct { real efc[GM_MAX_EFC]; } dbg;
+    // collision: the face-clipped box-box hits of pass 1 (point, depth), one slot of 8 per
+    // face-case lane in lane order, for pass 2 to write without re-deriving the manifold
+    struct { real hit[GM_BB_SLOTS][8][4]; } cl;
   };
   int32_t ncon, nefc, nl, overflow;
   int32_t work_nefc, work_mpr, work_newton;   // this env-step's rows / MPR substeps / Newton iterations
@@ -1217,6 +1221,8 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
     GeomV A, B;
     CylFrame cf;
     BBox bbs;
+    int bslot = -1;          // box-box face case: this lane's hit slot (S.cl), -1 = none
+    real bn[3] = {0, 0, 0}, bsg = 0;   // and its manifold normal / sign
     real ea[3], eb[3], da[3], db[3];
     if (pr < T->npair) {
       const int a = T->pr_g[pr][0], b = T->pr_g[pr][1];
@@ -1273,15 +1279,24 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
           bb_setup(A, B, bbs, ea, eb, da, db);
           if (bbs.kind == 1) {
             kind = 4;
+            // this lane's hit slot: its rank among the face-case lanes (the active lanes here)
+            const unsigned long long fb = __ballot(1);
+            const int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(fb >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)fb, 0u));
+            bslot = rank < GM_BB_SLOTS ? rank : -1;
 #pragma unroll
             for (int i = 0; i < BB_NCAND; i++) {
               if (cnt < 8) {
                 real P[3], dep;
                 const int ok = bb_face_cand(bbs, i, P, dep);
+                if (ok && bslot >= 0) {
+                  real* hs = S.cl.hit[bslot][cnt];
+                  hs[0] = P[0]; hs[1] = P[1]; hs[2] = P[2]; hs[3] = dep;
+                }
                 hm |= (unsigned)ok << i;
                 cnt += ok;
               }
             }
+            bn[0] = bbs.n[0]; bn[1] = bbs.n[1]; bn[2] = bbs.n[2]; bsg = bbs.sgn;
           } else if (bbs.kind == 2) {
             kind = 1; cnt = bb_edge_hit(bbs, ea, eb, da, db, single);
           }
@@ -1313,7 +1328,19 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
       real mu = fmax(A.friction, B.friction);
       if (kind == 1) {
         if (off < GM_MAX_CON) write_contact(S, off, g1, g2, b1, b2, single, mu);
+      } else if (kind == 4 && bslot >= 0) {
+        // the stored hits, in candidate order as pass 1 found them (bb_face_hit's operations)
+        for (int w = 0; w < cnt; w++) {
+          const real* hs = S.cl.hit[bslot][w];
+          const real dep = hs[3];
+          Hit t;
+          t.dist = -dep;
+#pragma unroll
+          for (int k = 0; k < 3; k++) { t.pos[k] = hs[k] + (0.5 * dep) * bn[k]; t.n[k] = bsg * bn[k]; }
+          if (off + w < GM_MAX_CON) write_contact(S, off + w, g1, g2, b1, b2, t, mu);
+        }
       } else if (kind == 4) {
+        // (more face-case lanes than slots: the counted candidates again)
         int w = 0;
 #pragma unroll
         for (int i = 0; i < BB_NCAND; i++) {

@@ -1072,10 +1072,25 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     const int j = lane - i * (i + 1) / 2;
     // one partial sum per finger chain: three independent dependent-chains of CL terms
     real acc[3] = {0.0, 0.0, 0.0};
+    // (the transfers read four pivots at a time, one batch of loads per group)
 #pragma unroll
-    for (int k = CL; k >= 1; k--)
+    for (int k0 = CL; k0 >= 1; k0 -= 4) {
+      real lv[24];
 #pragma unroll
-      for (int f = 0; f < 3; f++) acc[f] = acc[f] + S.fs.lbub[f][k - 1][i] * S.fs.lbub[f][k - 1][7 + j];
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int f = 0; f < 3; f++) {
+          const int k = (k0 - q >= 1) ? k0 - q : 1;
+          lv[6 * q + 2 * f] = S.fs.lbub[f][k - 1][i];
+          lv[6 * q + 2 * f + 1] = S.fs.lbub[f][k - 1][7 + j];
+        }
+      keep_n<24>(lv);
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int f = 0; f < 3; f++)
+          if (k0 - q >= 1) acc[f] = acc[f] + lv[6 * q + 2 * f] * lv[6 * q + 2 * f + 1];
+    }
     real v = S.fs.bbx[lane];
     v = (((v - acc[0]) - acc[1]) - acc[2]) - S.fs.plb[i] * S.fs.plb[7 + j];
     S.fs.bbx[lane] = v;
@@ -1126,9 +1141,23 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
   if (border) {
     real acc[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-    for (int k = CL; k >= 1; k--)
+    for (int k0 = CL; k0 >= 1; k0 -= 4) {   // (four pivots' transfers per batch of loads)
+      real lv[24];
 #pragma unroll
-      for (int f = 0; f < 3; f++) acc[f] = acc[f] + S.fs.lbub[f][k - 1][bi] * S.fs.ych[f][k - 1];
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int f = 0; f < 3; f++) {
+          const int k = (k0 - q >= 1) ? k0 - q : 1;
+          lv[6 * q + 2 * f] = S.fs.lbub[f][k - 1][bi];
+          lv[6 * q + 2 * f + 1] = S.fs.ych[f][k - 1];
+        }
+      keep_n<24>(lv);
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int f = 0; f < 3; f++)
+          if (k0 - q >= 1) acc[f] = acc[f] + lv[6 * q + 2 * f] * lv[6 * q + 2 * f + 1];
+    }
     y = (((y - acc[0]) - acc[1]) - acc[2]) - S.fs.plb[bi] * S.fs.ypalm;
 #pragma unroll
     for (int k = 6; k >= 0; k--) {

@@ -983,28 +983,32 @@ __device__ __forceinline__ int sphere_box(const GeomV& Sp, const GeomV& B, Hit& 
 
 // ---- MPR ----
 struct SV { real v[3], p1[3], p2[3]; };
+// TYPE: the geom type when known at compile time (mpr's cylinder-box instance), -1 = read it
+template <int TYPE = -1>
 __device__ __forceinline__ void support_geom(const GeomV& G, const real* d, real* out) {
   real dl[3];
   mulmtv3(dl, G.R, d);
   real pl[3] = {0, 0, 0};
+  const int type = TYPE >= 0 ? TYPE : G.type;
   // face / rim-line ties take the centre (oracle.c support_geom, GM_SUPPORT_TIE)
-  if (G.type == GM_GEOM_BOX) {
+  if (type == GM_GEOM_BOX) {
     for (int k = 0; k < 3; k++) pl[k] = fabs(dl[k]) < GM_SUPPORT_TIE ? 0.0 : (dl[k] >= 0 ? G.size[k] : -G.size[k]);
-  } else if (G.type == GM_GEOM_CYLINDER) {
+  } else if (type == GM_GEOM_CYLINDER) {
     real rr = sqrt_n(dl[0] * dl[0] + dl[1] * dl[1]);
     if (rr > 1e-12) { pl[0] = div_n(G.size[0] * dl[0], rr); pl[1] = div_n(G.size[0] * dl[1], rr); }
     pl[2] = fabs(dl[2]) < GM_SUPPORT_TIE ? 0.0 : (dl[2] >= 0 ? G.size[1] : -G.size[1]);
-  } else if (G.type == GM_GEOM_SPHERE) {
+  } else if (type == GM_GEOM_SPHERE) {
     real l = sqrt_n(dot3(dl, dl));
     if (l > 1e-12) { pl[0] = div_n(dl[0] * G.size[0], l); pl[1] = div_n(dl[1] * G.size[0], l); pl[2] = div_n(dl[2] * G.size[0], l); }
   }
   mulmv3(out, G.R, pl);
   out[0] += G.c[0]; out[1] += G.c[1]; out[2] += G.c[2];
 }
+template <int TA, int TB>
 __device__ __forceinline__ void mpr_support(const GeomV& A, const GeomV& B, const real* d, SV& sv) {
   real nd[3] = {-d[0], -d[1], -d[2]};
-  support_geom(A, d, sv.p1);
-  support_geom(B, nd, sv.p2);
+  support_geom<TA>(A, d, sv.p1);
+  support_geom<TB>(B, nd, sv.p2);
   sv.v[0] = sv.p1[0] - sv.p2[0]; sv.v[1] = sv.p1[1] - sv.p2[1]; sv.v[2] = sv.p1[2] - sv.p2[2];
 }
 __device__ __forceinline__ int fzero(real x) { return fabs(x) < 1e-12; }
@@ -1099,13 +1103,15 @@ __device__ __forceinline__ void mpr_pos(const SV& P0, const SV& P1, const SV& P2
   }
   for (int k = 0; k < 3; k++) pos[k] = 0.5 * (p1[k] + p2[k]) * inv;
 }
+// TA, TB: the two geoms' types when known at compile time (-1: read per lane)
+template <int TA = -1, int TB = -1>
 __device__ __forceinline__ int mpr(const GeomV& A, const GeomV& B, real tol, int maxit, Hit& h) {
   SV P0, P1, P2, P3;
   for (int k = 0; k < 3; k++) { P0.v[k] = A.c[k] - B.c[k]; P0.p1[k] = A.c[k]; P0.p2[k] = B.c[k]; }
   if (fzero(P0.v[0]) && fzero(P0.v[1]) && fzero(P0.v[2])) P0.v[0] += 1e-5;
   real d[3] = {-P0.v[0], -P0.v[1], -P0.v[2]};
   normalize3(d);
-  mpr_support(A, B, d, P1);
+  mpr_support<TA, TB>(A, B, d, P1);
   if (dot3(P1.v, d) <= 0) return 0;
   cross3(d, P0.v, P1.v);
   if (fzero(sqrt_n(dot3(d, d)))) {
@@ -1117,7 +1123,7 @@ __device__ __forceinline__ int mpr(const GeomV& A, const GeomV& B, real tol, int
     return 1;
   }
   normalize3(d);
-  mpr_support(A, B, d, P2);
+  mpr_support<TA, TB>(A, B, d, P2);
   if (dot3(P2.v, d) <= 0) return 0;
   real va[3], vb[3];
   for (int k = 0; k < 3; k++) { va[k] = P1.v[k] - P0.v[k]; vb[k] = P2.v[k] - P0.v[k]; }
@@ -1130,7 +1136,7 @@ __device__ __forceinline__ int mpr(const GeomV& A, const GeomV& B, real tol, int
   }
   int it = 0;
   for (;;) {
-    mpr_support(A, B, d, P3);
+    mpr_support<TA, TB>(A, B, d, P3);
     if (dot3(P3.v, d) <= 0) return 0;
     cross3(va, P1.v, P3.v);
     const bool c2 = dot3(va, P0.v) < -1e-12;
@@ -1149,7 +1155,7 @@ __device__ __forceinline__ int mpr(const GeomV& A, const GeomV& B, real tol, int
     portal_dir(P1, P2, P3, d);
     if (dot3(d, P1.v) >= -1e-12) break;
     SV v4;
-    mpr_support(A, B, d, v4);
+    mpr_support<TA, TB>(A, B, d, v4);
     real dv4 = dot3(v4.v, d);
     if (!(fzero(dv4) || dv4 > 0)) return 0;
     if (reach_tol(P1, P2, P3, v4, d, tol)) return 0;
@@ -1160,7 +1166,7 @@ __device__ __forceinline__ int mpr(const GeomV& A, const GeomV& B, real tol, int
   for (;;) {
     portal_dir(P1, P2, P3, d);
     SV v4;
-    mpr_support(A, B, d, v4);
+    mpr_support<TA, TB>(A, B, d, v4);
     if (reach_tol(P1, P2, P3, v4, d, tol) || it > maxit) {
       real cp[3];
       tri_closest_origin(P1.v, P2.v, P3.v, cp);
@@ -1304,7 +1310,14 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
         } else {
           NB_BEGIN();
           ran_mpr = true;
-          kind = 1; cnt = mpr(A, B, (real)m->mpr_tolerance, m->mpr_iterations, single);
+          // a cylinder against a box (the gripper's links against a cylinder object) on every
+          // MPR lane: the instance with the support types fixed, no type test per support call
+          const bool cb = A.type == GM_GEOM_CYLINDER && B.type == GM_GEOM_BOX;
+          if (__ballot(!cb) == 0ull)
+            cnt = mpr<GM_GEOM_CYLINDER, GM_GEOM_BOX>(A, B, (real)m->mpr_tolerance, m->mpr_iterations, single);
+          else
+            cnt = mpr(A, B, (real)m->mpr_tolerance, m->mpr_iterations, single);
+          kind = 1;
           if (cnt && !(single.dist < 0)) cnt = 0;
           NB_END(12);
         }

@@ -1,5 +1,6 @@
 """Developer A/B probe: the bench's steady-state C3 workload for a given segment count N,
-mean kernel time over `steps` env-steps (10) and a digest of the final fp64 env states.  usage: python tools/quick_bench_n.py N [envs] [steps]"""
+mean kernel time over `steps` env-steps (10) and a digest of the final fp64 env states.  usage: python tools/quick_bench_n.py N [envs] [steps] [object_set]
+(object_set "cylinder" with 256 envs is the C2 workload)."""
 import ctypes as C
 import os
 import sys
@@ -12,6 +13,7 @@ import bench
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+oset = sys.argv[4] if len(sys.argv) > 4 else "set6_synthetic"
 seed, MAX_EP = 1234, 250
 p = gmx.ModelParams()
 gmx.load_library().gm_default_model_params(C.byref(p))
@@ -22,7 +24,7 @@ if os.environ.get("GM_MJ") is not None:       # 0: the folded actuator scheme (r
     if p.mujoco_actuators == 0:
         p.actuator_armature[1] = 0.0
         p.segment_damping, p.segment_damping_power = 0.24, 1.0
-env = gmx.BatchedGripperEnv(n, object_set="set6_synthetic", settings=gmx.canonical_settings(seed=seed), seed=seed,
+env = gmx.BatchedGripperEnv(n, object_set=oset, settings=gmx.canonical_settings(seed=seed), seed=seed,
                             model_params=p)
 env.set_scene_spawn(bench.mjenv_spawn_params(gmx), max_tries=3)
 env.reset()
@@ -50,7 +52,7 @@ import hashlib  # noqa: E402
 st = env.env_states()
 digest = hashlib.sha1(np.ascontiguousarray(st).tobytes()).hexdigest()[:12]   # bit-identity across builds
 cs = env.chunk_stats() if hasattr(env, "chunk_stats") else {}
-print(f"N={N} n={n} lib={os.environ.get('GM_LIB', 'default')} kernel ms mean {np.mean(ms):.3f} min {np.min(ms):.3f}"
+print(f"N={N} n={n} {oset} lib={os.environ.get('GM_LIB', 'default')} kernel ms mean {np.mean(ms):.3f} min {np.min(ms):.3f}"
       f" state sha1 {digest} yields {cs.get('yields', '-')} resumes {cs.get('resumes', '-')}"
       f" span {cs.get('span_ms', 0):.3f} fresh-empty {cs.get('fresh_empty_ms', 0):.3f} busy {cs.get('busy', 0):.3f}"
       f" poll {cs.get('poll', 0):.3f}", flush=True)

@@ -9,7 +9,8 @@ tests pin the oracle independently:
   at 1e-12 of their scale, on reset states and on grasp states with random velocities;
 - the narrowphase against closed-form answers: box-box face (aligned, rotated, clipped)
   and edge-edge, sphere-box (outside and inside), plane-cylinder rim points, plane-box
-  corners, plane-sphere, and MPR on sphere-sphere and sphere-cylinder;
+  corners, plane-sphere, and MPR on sphere-sphere, sphere-cylinder and cylinder-box
+  (the cylinder object against the finger links: the MPR pair of the benched scenes);
 - the oracle rebuilt with glibc sin / cos instead of gm_math.h's shared kernel: one
   substep from the same state agrees to rounding.
 MuJoCo conventions: the contact normal points from geom1 to geom2 (geom1 = the lower
@@ -261,6 +262,27 @@ def test_mpr_sphere_sphere_and_sphere_cylinder(direction):
     assert len(dist) == 1
     assert dist[0] == pytest.approx(-0.001, abs=1e-6)
     np.testing.assert_allclose(n[0], [0, 0, -1.0], atol=2e-3)
+
+
+@pytest.mark.parametrize("yaw", [0.0, 0.4])
+def test_mpr_cylinder_box(yaw):
+    """MPR on a cylinder (r 2 cm, half-height 3 cm) against a box (5 x 4 x 1 cm half
+    sizes, top face at z = 1 cm, turned `yaw` about z): upright on its bottom cap 1 mm into
+    the top face, then lying on its side (axis along x) 0.8 mm into it.  Depth to MPR's
+    tolerance (1e-6); the normal points from geom1 (the cylinder, above) into the box, -z."""
+    L = ol.lib()
+    r, hh = 0.02, 0.03
+    hs, Rb = [0.05, 0.04, 0.01], ip.rotz(yaw)
+    for Rc, zc, pen in ((I3, 0.01 + hh - 1e-3, 1e-3), (ip.roty(np.pi / 2), 0.01 + r - 0.8e-3, 0.8e-3)):
+        c = np.array([0.004, -0.006, zc])
+        dist, pos, n = collide(L, CYL, [r, hh], c, Rc, BOX, hs, [0, 0, 0], Rb)
+        assert len(dist) == 1
+        assert dist[0] == pytest.approx(-pen, abs=1e-6)
+        np.testing.assert_allclose(n[0], [0, 0, -1.0], atol=2e-3)
+        # the point lies inside the overlap slab, under the cylinder's footprint
+        assert 0.01 - pen - 1e-6 <= pos[0][2] <= 0.01 + 1e-6
+        assert abs(pos[0][0] - c[0]) <= (hh if Rc is not I3 else r) + 1e-9
+        assert abs(pos[0][1] - c[1]) <= r + 1e-9
 
 
 def test_oracle_with_libm_trig_agrees(world):

@@ -16,7 +16,8 @@ spawn_into_scene grid search), at STEADY STATE: before the timed 
 uniformly over episode steps 1..250, driven by the scripted grasp mix (close, squeeze,
 palm press, lift, with jitter), so grasp contacts, done flags and resets all fall inside
 the timed window.  N GPUs run N x 4096 envs sharded by env id (weak scaling); the only
-collective is an RCCL all-gather of the per-env episode returns each step.
+collective is an RCCL all-gather of the per-env episode-end records (return, length,
+success) each step.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -357,27 +358,32 @@ def policy_rollout(gmx, torch, dev, stream, n: int, steps: int, seed: int, env_o
     return out
 
 
-def measure(drive, returns, K: int, W: int, world: int, dev, sync):
+def measure(drive, episodes, K: int, W: int, world: int, dev, sync):
     """The contract's timed region, independent of what steps the envs (the device here,
     the oracle in tests/test_distributed.py): W untimed warmup drives, then EXACTLY K
     drives bracketed by sync + barrier + sync on both sides; the wall time is the MAX over
-    ranks.  Every drive's episode returns are all-gathered (the one collective, SURVEY.md
-    8e) and the finished episodes counted over the whole job.  drive(k) takes the timed
-    index k (None when untimed); `returns` holds NaN where an env's episode did not end."""
+    ranks.  Every drive's episode-end records (return, length, success per env:
+    gm_episode_end) are all-gathered -- the one collective, SURVEY.md 8e -- and the finished
+    episodes, their successes and their lengths summed over the whole job.  drive(k) takes
+    the timed index k (None when untimed); `episodes` is the [n, 3] int32 record buffer the
+    drive's auto-reset writes (length 0 where an env's episode did not end)."""
     import torch
     import torch.distributed as dist
-    from gmx.shard import gather_returns, max_over_ranks
-    episodes = torch.zeros((), device=dev, dtype=torch.int64)
+    from gmx.shard import gather_episodes, max_over_ranks, unpack_episodes
+    tally = torch.zeros(3, device=dev, dtype=torch.int64)   # episodes, successes, length sum
 
     def step(k=None):
         drive(k)
-        episodes.add_(torch.isfinite(gather_returns(returns, world)).sum())
+        _, length, success = unpack_episodes(gather_episodes(episodes, world))
+        tally[0] += (length > 0).sum()
+        tally[1] += success.sum()
+        tally[2] += length.sum()
 
     # warmup counts episodes too, so every kernel the timed loop launches (incl. torch's
-    # isfinite / sum / add for the episode counter) is loaded before the clock starts
+    # reductions for the tally) is loaded before the clock starts
     for _ in range(max(W, 1)):
         step()
-    episodes.zero_()
+    tally.zero_()
     sync()
     if world > 1:
         dist.barrier()
@@ -390,10 +396,11 @@ def measure(drive, returns, K: int, W: int, world: int, dev, sync):
         dist.barrier()
     sync()
     elapsed = time.perf_counter() - t0
-    return max_over_ranks(elapsed, dev), int(episodes.item())
+    t = [int(x) for x in tally.tolist()]
+    return max_over_ranks(elapsed, dev), {"episodes": t[0], "successes": t[1], "length_sum": t[2]}
 
 
-def headline(world: int, n: int, K: int, W: int, elapsed: float, episodes: int) -> dict:
+def headline(world: int, n: int, K: int, W: int, elapsed: float, ep: dict) -> dict:
     """The contract fields of rank 0's JSON line: value = env-steps of ALL ranks / the
     slowest rank's wall time (weak scaling: n envs per rank)."""
     return {"metric": METRIC, "value": round(world * n * K / elapsed, 1), "unit": "env-steps/s", "n_gpus": world,
@@ -401,7 +408,10 @@ def headline(world: int, n: int, K: int, W: int, elapsed: float, episodes: int) 
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic",
             "config": {"envs_per_gpu": n, "global_envs": world * n, "parallelism": f"env-shard x{world}"},
-            "episodes_finished": episodes}
+            "episodes_finished": ep["episodes"],
+            # from the all-gathered episode-end records (gm_episode_end: return, length, success)
+            "episode_successes": ep["successes"],
+            "mean_episode_length": round(ep["length_sum"] / ep["episodes"], 2) if ep["episodes"] else None}
 
 
 def main():
@@ -453,7 +463,8 @@ def main():
     S = env.cfg.sim_steps_per_action
     env.set_scene_spawn(mjenv_spawn_params(gmx), max_tries=3)
     env.reset()
-    returns = torch.full((n,), float("nan"), device=dev)
+    from gmx.shard import new_episode_records
+    episodes = new_episode_records(n, device=dev)
     d_act = env.lib.gm_device_actions(env.ctx)
 
     def drive(timed=None):
@@ -465,7 +476,7 @@ def main():
         env.lib.gm_step(env.ctx)
         if timed is not None:
             ev[timed][1].record(stream)
-        env.autoreset_device(0, returns.data_ptr(), max_episode_steps=MAX_EP)
+        env.autoreset_device(0, None, max_episode_steps=MAX_EP, episodes_dev_ptr=episodes.data_ptr())
 
     # steady state: env e (global id) starts its episode at pre-roll step t_e, so after
     # MAX_EP untimed steps the batch covers episode steps 1..MAX_EP uniformly
@@ -479,7 +490,7 @@ def main():
                 __import__("ctypes").POINTER(__import__("ctypes").c_uint8)), None)
         drive()
     K, W = args.steps, args.warmup
-    elapsed, episodes = measure(drive, returns, K, W, world, dev, torch.cuda.synchronize)
+    elapsed, ep_stats = measure(drive, episodes, K, W, world, dev, torch.cuda.synchronize)
     steps_view = gmx.env_state_view(env.env_states())["num_action_steps"]
 
     kern_ms = [a.elapsed_time(b) for a, b in ev]
@@ -529,7 +540,7 @@ def main():
         c1 = None if (args.no_c1 or world > 1) else c1_line(gmx, args.seed)
         c5 = None if (args.no_policy or world > 1) else policy_rollout(gmx, torch, dev, stream, n, max(3, K // 2), args.seed,
                                                         first_env)
-        out = headline(world, n, K, W, elapsed, episodes)
+        out = headline(world, n, K, W, elapsed, ep_stats)
         out["config"].update({"workload": "C3: set6_synthetic 20 mixed objects, randomised spawn (object drawn per "
                                    "episode, spawn_into_scene grid search on the device), steady state: envs "
                                    "staggered over episode steps 1..250 by an untimed pre-roll, scripted grasp "

@@ -397,7 +397,9 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   // one-time calibrate_reset settle (myfunctions.cpp:1470-1505) on env 0 -- per context, or,
   // with gm_set_settle_cache(1), once per process as the reference's function-static
   // first_call does (myfunctions.cpp:1447): later contexts with the same joint count reuse
-  // the first settle's equilibrium whatever else changed
+  // the cached settle's equilibrium whatever else changed; a context whose joint count
+  // differs settles again and replaces the cache (the reference's changed-joint-count
+  // check sets first_call = true and keeps the new settle, myfunctions.cpp:1453-1468)
   bool from_cache = false;
   {
     std::lock_guard<std::mutex> lk(g_settle_mu);
@@ -413,7 +415,7 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
     HIPCHK(c, launch_step(c, 1, 1, 1, dbg));
     HIPCHK(c, hipMemcpyAsync(c->d_eq, reinterpret_cast<char*>(c->d_state) + offsetof(GmEnvHot, qpos), sizeof(double) * GM_MAX_QPOS, hipMemcpyDeviceToDevice, c->stream));
     std::lock_guard<std::mutex> lk(g_settle_mu);
-    if (g_settle_cache_on && !g_settle_valid) {
+    if (g_settle_cache_on && (!g_settle_valid || g_settle_nseg != c->model.n_seg)) {
       HIPCHK(c, hipMemcpyAsync(g_settle_eq, c->d_eq, sizeof(double) * GM_MAX_QPOS, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));
       g_settle_valid = true;
@@ -997,6 +999,12 @@ int gm_set_stream(gm_ctx* c, void* stream) {
 }
 
 int gm_autoreset(gm_ctx* c, int max_episode_steps, const gm_spawn* spawn, int spawn_on_device, float* returns) {
+  return gm_autoreset_episodes(c, max_episode_steps, spawn, spawn_on_device, returns, nullptr);
+}
+
+int gm_autoreset_episodes(gm_ctx* c, int max_episode_steps, const gm_spawn* spawn, int spawn_on_device,
+                          float* returns, gm_episode_end* episodes) {
+  static_assert(sizeof(gm_episode_end) == 12, "episode-end record is 3 x 4 bytes");
   if (!c) return GM_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   const gm_spawn* ds = nullptr;
@@ -1008,7 +1016,7 @@ int gm_autoreset(gm_ctx* c, int max_episode_steps, const gm_spawn* spawn, int sp
   }
   int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
   hipLaunchKernelGGL(gm_autoreset_mask_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_done,
-                     max_episode_steps, c->d_mask, returns, c->n_envs);
+                     max_episode_steps, c->d_mask, returns, episodes, c->n_envs);
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(gm_reset_kernel, dim3(c->n_envs), dim3(64), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
                      c->d_topo, c->d_eq, c->d_mask, ds, c->d_objs, c->n_objects, c->n_envs, c->d_scene,

@@ -62,8 +62,9 @@ __device__ __forceinline__ void keep_n(const double* a) {
   }
 #undef GM_K
 }
-#define GM_CQ_NB 16
-#define GM_BB_SLOTS 18   // box-box hit slots in the LDS union (18 x 256 B <= the union's smallest size)  // priority buckets per XCD of the chunked env-step (gm_step_kernel)
+#define GM_CQ_NB 16      // priority buckets per XCD of the chunked env-step (gm_step_kernel)
+#define GM_BB_SLOTS 18   // box-box hit slots in the LDS union (18 x 256 B; SharedT asserts it fits
+                         // inside the union's CL-independent chain-root stage, so it never grows LDS)
 // gm_step_kernel is instantiated per finger chain length (CL = n_seg + 2) so every chain
 // recursion is unrolled into registers; GM_NSEG_LIST is the set compiled in.
 #ifndef GM_NSEG_LIST
@@ -143,6 +144,8 @@ struct __align__(16) SharedT {
     // face-case lane in lane order, for pass 2 to write without re-deriving the manifold
     struct { real hit[GM_BB_SLOTS][8][4]; } cl;
   };
+  static_assert(sizeof(real[GM_BB_SLOTS][8][4]) <= sizeof(real) * (GM_MAX_CON * 9 + 4 * 54 + 54 + 27),
+                "box-box hit slots must fit inside the chain-root stage (st): they may not grow the union");
   int32_t ncon, nefc, nl, overflow;
   int32_t work_nefc, work_mpr, work_newton;   // this env-step's rows / MPR substeps / Newton iterations
   int32_t stp_fixed;              // update_all: `next` is a fixed point of the stepper this env-step (see there)
@@ -3187,13 +3190,24 @@ extern "C" __global__ void gm_spawn_into_scene_kernel(GmEnvState* __restrict__ s
 extern "C" __global__ void gm_autoreset_mask_kernel(const GmEnvState* __restrict__ states,
                                                     const uint8_t* __restrict__ done, int max_steps,
                                                     uint8_t* __restrict__ mask, float* __restrict__ returns,
-                                                    int n_envs) {
+                                                    gm_episode_end* __restrict__ episodes, int n_envs) {
   int env = blockIdx.x * blockDim.x + threadIdx.x;
   if (env >= n_envs) return;
   const GmEnvState& s = states[env];
   uint8_t r = (done[env] || (max_steps > 0 && s.num_action_steps >= max_steps)) ? 1 : 0;
   mask[env] = r;
-  if (returns) returns[env] = r ? s.cumulative_reward : __builtin_nanf("");
+  const float ret = r ? s.cumulative_reward : __builtin_nanf("");
+  if (returns) returns[env] = ret;
+  if (episodes) {
+    // successful_grasp (mjclass.cpp:1295-1322): this env-step's event value, which
+    // update_events leaves in bev_last
+    gm_episode_end e;
+    e.ret = ret;
+    e.length = r ? s.num_action_steps : 0;
+    e.success = (r && s.bev_last[GM_EV_successful_grasp]) ? 1 : 0;
+    e.pad[0] = e.pad[1] = e.pad[2] = 0;
+    episodes[env] = e;
+  }
 }
 #endif
 

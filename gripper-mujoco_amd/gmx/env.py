@@ -228,12 +228,14 @@ class BatchedGripperEnv:
         return self._spawn_dev.data_ptr()
 
     def autoreset_device(self, spawn_dev_ptr: int, returns_dev_ptr: int | None = None,
-                         max_episode_steps: int | None = None):
-        """Episode boundary on the device: done/truncated envs report their return and are
-        reset + respawned (MjEnv.py:616-637, 2222-2263)."""
+                         max_episode_steps: int | None = None, episodes_dev_ptr: int | None = None):
+        """Episode boundary on the device: done/truncated envs report their return (and, with
+        episodes_dev_ptr, the gm_episode_end record: return, length, success) and are reset
+        + respawned (MjEnv.py:616-637, 2222-2263)."""
         mx = self.max_episode_steps if max_episode_steps is None else max_episode_steps
-        self._check(self.lib.gm_autoreset(self._ctx, int(mx), C.c_void_p(spawn_dev_ptr), 1,
-                                          C.c_void_p(returns_dev_ptr or 0)))
+        self._check(self.lib.gm_autoreset_episodes(self._ctx, int(mx), C.c_void_p(spawn_dev_ptr), 1,
+                                                   C.c_void_p(returns_dev_ptr or 0),
+                                                   C.c_void_p(episodes_dev_ptr or 0)))
 
     def device_buffers(self):
         return (self.lib.gm_device_obs(self._ctx), self.lib.gm_device_reward(self._ctx),

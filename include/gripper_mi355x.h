@@ -527,6 +527,22 @@ int  gm_set_stream(gm_ctx* ctx, void* stream);
 int  gm_autoreset(gm_ctx* ctx, int max_episode_steps, const gm_spawn* spawn, int spawn_on_device,
                   float* returns);
 void* gm_device_reset_mask(gm_ctx* ctx);   /* uint8 [n_envs], written by gm_autoreset */
+/* The episode-end record north_star's RCCL all-gather carries: per env, the
+ * episode return (MjEnv's cumulative reward, MjEnv.py:616-637), its length in env-steps
+ * (MjClass::env_.num_action_steps) and success -- the reference's successful_grasp metric
+ * (mjclass.cpp:1295-1322: a +1-reward, done-setting binary event triggered this step).  Envs
+ * whose episode continues hold {NaN, 0, 0}.  12 bytes, so a [n_envs] array is a plain
+ * [n_envs x 3] 4-byte tensor for the collective. */
+typedef struct gm_episode_end {
+  float   ret;
+  int32_t length;
+  uint8_t success;
+  uint8_t pad[3];
+} gm_episode_end;
+/* gm_autoreset that also writes the episode-end record of every env (device array
+ * [n_envs], may be NULL) -- returns may be NULL too. */
+int  gm_autoreset_episodes(gm_ctx* ctx, int max_episode_steps, const gm_spawn* spawn, int spawn_on_device,
+                           float* returns, gm_episode_end* episodes);
 
 /* Timing of the fused env-step kernel (HIP events on the context's stream). */
 int  gm_last_step_ms(gm_ctx* ctx, float* ms);

@@ -1148,7 +1148,8 @@ static void settle(or_env* e) {
   pthread_mutex_unlock(&g_settle_mu);
   settle_uncached(e);
   pthread_mutex_lock(&g_settle_mu);
-  if (g_settle_cache_on && !g_settle_valid) {
+  /* a changed joint count re-settles and keeps the new settle (myfunctions.cpp:1453-1468) */
+  if (g_settle_cache_on && (!g_settle_valid || g_settle_nseg != e->m.n_seg)) {
     for (int i = 0; i < NQ; i++) g_settle_eq[i] = e->eq_q[i];
     g_settle_valid = 1;
     g_settle_nseg = e->m.n_seg;

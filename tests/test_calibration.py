@@ -225,6 +225,22 @@ def test_timestep_search_all_72_points_within_stated_bands(world):
             assert got[(n + 1, t, w, s)] < ms, (n, t, w, s)
 
 
+
+@pytest.mark.xfail(strict=True, reason="open fidelity gap (DESIGN.md section 2): the reference's stable "
+                   "timestep grows 2.9x from inertia x1 to x100; this engine's stays damping-limited, "
+                   "so x1 and x10 sit 2.0-3.5x / 1.45-2.25x above the CSV and x100 0.70-0.87x below")
+def test_timestep_search_keeps_the_references_inertia_ordering(world):
+    """mujoco_timesteps.csv orders every (t, w, N) column by the segment inertia scaling:
+    x1 < x10 < x50 < x100 (more rotational inertia per segment, larger stable step).  Kept
+    as a strict xfail so the regression the r04 actuator order introduced stays visible
+    (it passes -- and so fails this marker -- once a model change restores the ordering)."""
+    gm = world[0]
+    ms = [search_ms(gm, 8, 0.9, 28.0, s)[0] for s in (1.0, 10.0, 50.0, 100.0)]
+    ref = json.load(open(GOLDEN))["columns"]
+    col = [ref[f"t=0.9, w=28.0, inertia={s}"]["8"] for s in (1, 10, 50, 100)]
+    assert col == sorted(col)
+    assert ms == sorted(ms) and ms[3] / ms[0] > 2.0, ms
+
 # validate_curve_under_force's retry branch (mjclass.cpp:4073-4090), forced: at a 4.8 ms
 # model step with a 50x saturation load the loaded 50 s settle reaches mjWARN_BADQACC, the
 # run is repeated at 0.8x the step and settles.
@@ -371,6 +387,44 @@ def test_settle_cache_first_call_quirk_on_the_oracle(world):
     c = oracle_lib.OracleEnv(m2, cfg2, objs, 0)
     assert np.abs(c.eq() - ea).max() > 1e-6
 
+
+
+def seg_model(gm, n_seg, thickness=None):
+    import ctypes as C
+    p = gm.ModelParams()
+    gm.load_library().gm_default_model_params(C.byref(p))
+    p.n_seg = n_seg
+    if thickness is not None:
+        p.finger_thickness = thickness
+    return gm.ModelBlob(p)
+
+
+def test_settle_cache_recalibrates_on_changed_joint_count(world):
+    """calibrate_reset's changed-joint-count branch (myfunctions.cpp:1453-1468): a model with
+    a different number of gripper joints sets first_call = true, settles, and its settle is
+    the one kept.  Sequence N=8, N=6 (stiff), N=6 (default), N=8 (stiff): the second N=6 env
+    takes the stiff N=6 settle, and the last N=8 env settles its own model rather than
+    reusing the first N=8 settle."""
+    gm = world[0]
+    objs = gm.make_object_set("set1_synthetic", 1)
+    cfg_of = lambda m: gm.ConfigBlob(gm.canonical_settings(noise=False, seed=1), m)
+    m8, m6s, m6, m8s = seg_model(gm, 8), seg_model(gm, 6, 1.0e-3), seg_model(gm, 6), seg_model(gm, 8, 1.0e-3)
+    own = {}
+    for name, m in (("m6", m6), ("m8s", m8s)):
+        own[name] = oracle_lib.OracleEnv(m, cfg_of(m), objs, 0).eq()     # cache off: own settle
+    L = oracle_lib.lib()
+    try:
+        L.or_set_settle_cache(1)
+        a = oracle_lib.OracleEnv(m8, cfg_of(m8), objs, 0).eq()
+        b = oracle_lib.OracleEnv(m6s, cfg_of(m6s), objs, 0).eq()
+        c = oracle_lib.OracleEnv(m6, cfg_of(m6), objs, 0).eq()
+        d = oracle_lib.OracleEnv(m8s, cfg_of(m8s), objs, 0).eq()
+    finally:
+        L.or_set_settle_cache(0)
+    np.testing.assert_array_equal(c, b)                  # same joint count: the cached N=6 settle
+    assert np.abs(c - own["m6"]).max() > 1e-6           # ... not its own
+    np.testing.assert_array_equal(d, own["m8s"])         # changed count: settles its own model
+    assert np.abs(d - a).max() > 1e-6                    # ... not the stale first N=8 settle
 
 @pytest.mark.gpu
 def test_gpu_settle_cache_first_call_quirk_matches_oracle(world):

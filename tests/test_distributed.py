@@ -24,27 +24,41 @@ def free_port():
     return p
 
 
-def run_envs(env_ids, steps):
-    """Cumulative reward per env after `steps` random-action env-steps (oracle)."""
+def run_envs(env_ids, steps, records=False):
+    """Cumulative reward per env after `steps` random-action env-steps (oracle); with
+    records=True the episode-end record of each env's first episode instead (return,
+    length, successful_grasp), packed as gm_episode_end ([n, 3] int32)."""
     import gmx
     import oracle_lib
     s = gmx.canonical_settings(noise=True, seed=11)
     model = gmx.ModelBlob()
     cfg = gmx.ConfigBlob(s, model)
     objs = gmx.make_object_set("set1_synthetic", 11)
-    out = []
+    out, recs = [], []
+    i_succ = list(gmx.BINARY_EVENTS).index("successful_grasp")
     for g in env_ids:
         e = oracle_lib.OracleEnv(model, cfg, objs, int(g))
         sp = gmx.Spawn()
         sp.object_index = int(g) % len(objs)
-        sp.x, sp.y, sp.zrot = 0.0, 0.0, 0.0
+        # env 1 spawns its object out of bounds: its episode ends (done) at the first step
+        sp.x, sp.y, sp.zrot = (0.09 if int(g) == 1 else 0.0), 0.0, 0.0
         e.reset(sp)
         rng = np.random.default_rng(1000 + int(g))
         tot = 0.0
-        for _ in range(steps):
-            _, r, _ = e.step(rng.uniform(-1, 1, size=cfg.n_actions).astype(np.float32))
-            tot += r
+        rec = None
+        for k in range(steps):
+            _, r, d = e.step(rng.uniform(-1, 1, size=cfg.n_actions).astype(np.float32))
+            tot = np.float32(tot + np.float32(r))
+            if rec is None and (d or k + 1 == steps):
+                rec = (tot, k + 1, int(e.event_rows()[2][i_succ] > 0))
         out.append(tot)
+        recs.append(rec)
+    if records:
+        import torch
+        from gmx.shard import pack_episodes
+        r = np.array(recs, dtype=np.float64)
+        return pack_episodes(torch.tensor(r[:, 0], dtype=torch.float32), torch.tensor(r[:, 1]),
+                             torch.tensor(r[:, 2])).numpy()
     return np.array(out, dtype=np.float32)
 
 
@@ -53,13 +67,15 @@ def worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from gmx.shard import shard_range, gather_returns, max_over_ranks
+        from gmx.shard import shard_range, gather_episodes, gather_returns, max_over_ranks
         lo, hi = shard_range(rank, world, N_PER_RANK)
         ret = torch.from_numpy(run_envs(range(lo, hi), STEPS))
         allr = gather_returns(ret, world)
+        rec = torch.from_numpy(run_envs(range(lo, hi), STEPS, records=True))
+        allrec = gather_episodes(rec, world)
         t = max_over_ranks(0.5 + rank)
         if rank == 0:
-            q.put((allr.numpy().tolist(), t))
+            q.put((allr.numpy().tolist(), allrec.numpy().tolist(), t))
     finally:
         dist.destroy_process_group()
 
@@ -80,12 +96,19 @@ def test_two_rank_gather_matches_single_process(gm):
     procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got, tmax = q.get(timeout=240)
+    got, got_rec, tmax = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     ref = run_envs(range(world * N_PER_RANK), STEPS)
     np.testing.assert_array_equal(np.array(got, dtype=np.float32), ref)
+    # the episode-end records (return, length, success), bit for bit in global env order
+    ref_rec = run_envs(range(world * N_PER_RANK), STEPS, records=True)
+    np.testing.assert_array_equal(np.array(got_rec, dtype=np.int32), ref_rec)
+    from gmx.shard import unpack_episodes
+    r, length, _ = unpack_episodes(torch.from_numpy(ref_rec))
+    assert length[1] == 1 and length[0] == STEPS      # env 1's episode ended at once (oob)
+    assert r.isfinite().all()
     assert tmax == 1.5
 
 
@@ -110,8 +133,12 @@ class OracleRollout:
         self.rng = [np.random.default_rng(2000 + g) for g in self.ids]
         self.steps = [0] * len(self.ids)
         self.ret = [np.float32(0)] * len(self.ids)
-        self.returns = torch.full((len(self.ids),), float("nan"))
+        from gmx.shard import new_episode_records
+        self.episodes = new_episode_records(len(self.ids))
         self.ended = 0          # episodes ended inside the timed drives
+        self.succeeded = 0
+        self.length_sum = 0
+        self.i_succ = list(gmx.BINARY_EVENTS).index("successful_grasp")
         self.sleep_s = sleep_s
         for i in range(len(self.ids)):
             self._reset(i)
@@ -127,15 +154,25 @@ class OracleRollout:
 
     def drive(self, k=None):
         import time
-        self.returns.fill_(float("nan"))
+        from gmx.shard import pack_episodes
+        n = len(self.envs)
+        ret = torch.full((n,), float("nan"))
+        length = torch.zeros(n, dtype=torch.int32)
+        succ = torch.zeros(n, dtype=torch.int32)
         for i, e in enumerate(self.envs):
             _, r, d = e.step(self.rng[i].uniform(-1, 1, size=self.cfg.n_actions).astype(np.float32))
             self.ret[i] = np.float32(self.ret[i] + np.float32(r))
             self.steps[i] += 1
             if d or self.steps[i] >= BENCH_EP:
-                self.returns[i] = float(self.ret[i])
-                self.ended += k is not None
+                ret[i] = float(self.ret[i])
+                length[i] = self.steps[i]
+                succ[i] = int(e.event_rows()[2][self.i_succ] > 0)
+                if k is not None:
+                    self.ended += 1
+                    self.succeeded += int(succ[i])
+                    self.length_sum += int(length[i])
                 self._reset(i)
+        self.episodes.copy_(pack_episodes(ret, length, succ))
         if self.sleep_s:
             time.sleep(self.sleep_s)
 
@@ -149,10 +186,10 @@ def bench_worker(rank, world, port, q):
         from gmx.shard import shard_range
         lo, hi = shard_range(rank, world, BENCH_N)
         ro = OracleRollout(range(lo, hi), sleep_s=0.25 if rank == 1 else 0.0)   # rank 1 is the slow one
-        elapsed, episodes = bench.measure(ro.drive, ro.returns, BENCH_K, BENCH_W, world, torch.device("cpu"),
-                                          lambda: None)
-        line = bench.headline(world, BENCH_N, BENCH_K, BENCH_W, elapsed, episodes)
-        q.put((rank, line, episodes, elapsed, ro.ended))
+        elapsed, ep = bench.measure(ro.drive, ro.episodes, BENCH_K, BENCH_W, world, torch.device("cpu"),
+                                    lambda: None)
+        line = bench.headline(world, BENCH_N, BENCH_K, BENCH_W, elapsed, ep)
+        q.put((rank, line, ep, elapsed, (ro.ended, ro.succeeded, ro.length_sum)))
     finally:
         dist.destroy_process_group()
 
@@ -175,9 +212,12 @@ def test_bench_timed_loop_two_ranks(gm):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    line, episodes, elapsed, _ = res[0]
-    ended = res[0][3] + res[1][3]
-    assert episodes == res[1][1] == ended > 0          # every rank counts the whole job's episodes
+    line, ep, elapsed, _ = res[0]
+    ended = res[0][3][0] + res[1][3][0]
+    assert ep == res[1][1]                             # every rank tallies the whole job's records
+    assert ep["episodes"] == ended > 0
+    assert ep["successes"] == res[0][3][1] + res[1][3][1]
+    assert ep["length_sum"] == res[0][3][2] + res[1][3][2]
     assert elapsed == res[1][2] >= BENCH_K * 0.25     # the max over ranks: rank 1 slept 0.25 s per drive
     for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
                 "scaling", "vs_baseline", "dtype", "data"):
@@ -188,3 +228,5 @@ def test_bench_timed_loop_two_ranks(gm):
     assert line["ms_per_step"] == round(elapsed / BENCH_K * 1e3, 3)
     assert line["config"]["global_envs"] == world * BENCH_N and line["config"]["envs_per_gpu"] == BENCH_N
     assert line["episodes_finished"] == ended
+    assert line["episode_successes"] == ep["successes"]
+    assert line["mean_episode_length"] == round(ep["length_sum"] / ended, 2)

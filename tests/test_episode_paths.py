@@ -84,6 +84,9 @@ def test_autoreset_matches_oracle(gm, ol):
     episode = np.ones(n, dtype=np.int64)
     steps = np.zeros(n, dtype=np.int64)
     returns = torch.full((n,), float("nan"), device="cuda")
+    from gmx.shard import new_episode_records, unpack_episodes
+    recs_ep = new_episode_records(n, device="cuda")
+    i_succ = list(gm.BINARY_EVENTS).index("successful_grasp")
     rng = np.random.default_rng(5)
     n_reset = 0
     for t in range(7):
@@ -92,9 +95,12 @@ def test_autoreset_matches_oracle(gm, ol):
         env.action_step()
         obs = env.observation()
         rew, done = env.reward_done()
-        env.autoreset_device(0, returns.data_ptr(), max_episode_steps=max_steps)
+        env.autoreset_device(0, returns.data_ptr(), max_episode_steps=max_steps,
+                             episodes_dev_ptr=recs_ep.data_ptr())
         torch.cuda.synchronize()
         ret = returns.cpu().numpy()
+        ep_ret, ep_len, ep_succ = (x.cpu().numpy() for x in unpack_episodes(recs_ep))
+        np.testing.assert_array_equal(ep_ret.view(np.int32), ret.view(np.int32))   # same bits, NaNs included
         recs = env.env_states()
         view = gm.env_state_view(recs)
         obs_after = env.observation()
@@ -109,6 +115,9 @@ def test_autoreset_matches_oracle(gm, ol):
                 # of tests/test_grasp_parity.py (the gauge fit's rounding differs at ~1e-7)
                 assert ret[e] == pytest.approx(o.export_state().view(gm.env_state_dtype())[0]["cumulative_reward"],
                                                rel=1e-5, abs=1e-6), (t, e)
+                # the episode-end record: length in env-steps, successful_grasp bit for bit
+                assert ep_len[e] == steps[e], (t, e)
+                assert bool(ep_succ[e]) == (o.event_rows()[2][i_succ] > 0), (t, e)
                 episode[e] += 1
                 steps[e] = 0
                 oracle_mjenv_reset(gm, o, seed, e, int(episode[e]), len(env.objects), params)
@@ -122,7 +131,7 @@ def test_autoreset_matches_oracle(gm, ol):
                 np.testing.assert_allclose(view["qpos"][e][:qa], ov["qpos"][:qa], rtol=0, atol=2e-6)
                 np.testing.assert_array_equal(obs_after[e], o.observation())
             else:
-                assert math.isnan(ret[e]), (t, e)
+                assert math.isnan(ret[e]) and ep_len[e] == 0 and not ep_succ[e], (t, e)
     assert n_reset >= n + n // 4
 
 

@@ -110,6 +110,39 @@ def test_kinematics_mass_matrix_and_bias_match_natural_order_newton_euler(world)
         assert berr.max() <= 1e-12, (berr.max(), int(np.argmax(berr)))
 
 
+
+def test_euler_implicit_damping_matches_dense_solve(world):
+    """mj_Euler's implicit joint damping (MuJoCo 2.1.5, the default actuator order):
+    qvel' = qvel + h (M + h D)^-1 (qfrc_smooth + qfrc_constraint).  The oracle's (and the
+    device's, lane for lane) tree LDL^T of M + h D with the base as the border column is
+    checked against a dense numpy solve built from the independent joint-space inertia
+    (sum of J^T M_b J, tests/indep_physics.py) and the model's joint damping, on grasp
+    states with contacts and random velocities.  At the solve's optimum qfrc_smooth +
+    qfrc_constraint = M qacc (M with armature, the solve's matrix), so the right-hand side
+    is formed from the solver's qacc; a capped solve carries the residual, see
+    test_euler_damping_uses_the_constraint_forces_on_a_capped_solve."""
+    gm, model, cfg, objs = world
+    M = ip.Model(model)
+    ip.set_object(M, objs[1])
+    damp = np.asarray(ip.arr(M.raw.jnt_damping), dtype=np.float64)[M.jnt[M.dof_body]]
+    arm = M.armature[M.jnt[M.dof_body]]
+    h = model.params.timestep
+    o, states = dynamic_states(gm, model, cfg, objs)
+    checked = 0
+    for q, v in states:
+        o.L.or_set_state(o.h, q.ctypes.data_as(f64p), v.ctypes.data_as(f64p))
+        ncon, _, _, qacc = o.debug_substep()
+        _, v1, _ = o.state()
+        Mi = ip.mass_matrix(M, q) + np.diag(arm)
+        qe = np.linalg.solve(Mi + h * np.diag(damp), Mi @ qacc)
+        dv = (v1 - v) / h
+        scale = np.abs(qe).max()
+        assert np.abs(dv - qe).max() <= 1e-12 * scale, (np.abs(dv - qe).max(), scale)
+        # the damping matters: the explicit update would be off by far more
+        assert np.abs(qacc - qe).max() > 1e3 * np.abs(dv - qe).max()
+        checked += ncon > 0
+    assert checked >= 3
+
 # ---------------------------------------------------------------- narrowphase
 def collide(L, t1, s1, c1, R1, t2, s2, c2, R2, tol=1e-6, it=50):
     out = np.zeros(8 * 7)

@@ -493,6 +493,46 @@ int gm_spawn_object(gm_ctx* c, const uint8_t* mask, const gm_spawn* spawn) {
   return GM_OK;
 }
 
+int gm_set_motor_target(gm_ctx* c, const uint8_t* mask, const double* xyz, int n_xyz, uint8_t* in_limits) {
+  if (!c || !xyz || (n_xyz != 1 && n_xyz != c->n_envs)) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t n = (size_t)c->n_envs;
+  const uint8_t* dm = nullptr;
+  if (mask) { HIPCHK(c, hipMemcpyAsync(c->d_mask, mask, n, hipMemcpyHostToDevice, c->stream)); dm = c->d_mask; }
+  double* d_xyz = nullptr;
+  uint8_t* d_ok = nullptr;
+  HIPCHK(c, hipMalloc(&d_xyz, sizeof(double) * 3 * (size_t)n_xyz));
+  HIPCHK(c, hipMalloc(&d_ok, n));
+  HIPCHK(c, hipMemcpyAsync(d_xyz, xyz, sizeof(double) * 3 * (size_t)n_xyz, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(d_ok, 1, n, c->stream));
+  int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
+  hipLaunchKernelGGL(gm_motor_target_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, dm, d_xyz,
+                     n_xyz == c->n_envs ? 1 : 0, d_ok, c->n_envs);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && in_limits) e = hipMemcpyAsync(in_limits, d_ok, n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d_xyz);
+  (void)hipFree(d_ok);
+  HIPCHK(c, e);
+  return GM_OK;
+}
+
+int gm_get_sensor_si(gm_ctx* c, float* out) {
+  if (!c || !out) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t n = (size_t)c->n_envs;
+  float* d_out = nullptr;
+  HIPCHK(c, hipMalloc(&d_out, sizeof(float) * 5 * n));
+  int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
+  hipLaunchKernelGGL(gm_sensor_si_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, d_out, c->n_envs);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, sizeof(float) * 5 * n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d_out);
+  HIPCHK(c, e);
+  return GM_OK;
+}
+
 int gm_set_action(gm_ctx* c, const float* actions, int on_device) {
   if (!c || !actions) return GM_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));

@@ -464,10 +464,16 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
     for (int i = 0; i < 3; i++) in_seg[i] *= p->segment_inertia_scaling;
     double ipos_seg[3] = {0.5 * Ls, 0, 0};
     // finger_f body (carries fixed segment link 1): revolute "finger_f_revolute_joint",
-    // +q tilts the tip inward (tilt_fing_x = x - L sin th, myfunctions.cpp:3653)
+    // about +z: +q tilts the tip outward, so th = asin((y - x) / 35 mm) < 0 (the y motor
+    // inside the x motor) tilts it inward -- luke::Gripper's own fingertip geometry
+    // (calc_fingertip_radius = x - hyp sin(rest - th), gripper.h:88-93) and the reference's
+    // MuJoCo "measure tilt" run (mysimulate.cpp:2762-2811: y stepped below x = 100 mm presses
+    // the fingertips into the sphere, rl/juypter/thesis_plots/sim_vs_real_forces_tilt.csv;
+    // tests/test_force_curves.py).  (The analytic get_fingerend_and_palm_xyz,
+    // myfunctions.cpp:3653, uses the opposite sign; it stays as the reference wrote it.)
     int bf = B.add_body(bint, GM_GRP_FINGER0 + f, zero3, qf, mseg, ipos_seg, in_seg);
     m->body_finger[f] = bf;
-    double axr[3] = {0, 0, -1};
+    double axr[3] = {0, 0, 1};
     m->dof_rev[f] = B.add_joint(bf, GM_JNT_HINGE, axr, 0, 0.0, p->actuator_armature[1], m->dof_pris[f]);
     double gpos[3] = {0.5 * Ls, 0, 0};
     double gsz[3] = {0.5 * Ls, ht, hw};
@@ -654,7 +660,7 @@ static int n_samples(int fcn, const gm_sensor& s) {
 // 4023-4105: every fingertip pulled outward for 50 s, then read_armadillo_gauge of finger
 // 0).  That settled state is the static equilibrium of finger 0's joint chain, solved
 // here directly in the finger's plane (x down the finger, y outward): revolute motor
-// (PD spring kp about -z at the finger root), the fixed first segment, N segment hinges
+// (PD spring kp about the joint's axis at the finger root), the fixed first segment, N segment hinges
 // (stiffness c_k about +z); loads = the tip pull at the last link's centre of mass and
 // gravity on every link.  The gauge then fits the settled joint points as
 // read_armadillo_gauge does.  gm_calibrate runs the actual simulation (device) and the
@@ -695,14 +701,15 @@ static double static_gauge_reading(const gm_model* m, double P) {
   const double Ls = m->segment_length;
   const int b0 = m->body_finger[0];            // fixed first segment; segments b0+1 .. b0+N
   const double g = -m->gravity[2];              // finger x axis points down: gravity is +x
-  double q[GM_MAX_SEG + 1] = {0};               // q[0]: revolute (about -z), q[1..N]: segments
+  double q[GM_MAX_SEG + 1] = {0};               // q[0]: revolute (about az z), q[1..N]: segments
+  const double az = m->jnt_axis[m->body_jnt[b0]][2];   // the revolute's axis (+-1 along z)
   double stiff[GM_MAX_SEG + 1];
   stiff[0] = m->kp_gripper[1];
   for (int k = 1; k <= N; k++) stiff[k] = m->jnt_stiffness[m->body_jnt[b0 + k]];
   for (int it = 0; it < 2000; it++) {
     double px[GM_MAX_SEG + 2], py[GM_MAX_SEG + 2], phi[GM_MAX_SEG + 2];
     double cx[GM_MAX_SEG + 2], cy[GM_MAX_SEG + 2], mass[GM_MAX_SEG + 2];
-    px[0] = 0; py[0] = 0; phi[0] = -q[0];
+    px[0] = 0; py[0] = 0; phi[0] = az * q[0];
     for (int k = 0; k <= N; k++) {
       if (k > 0) {
         px[k] = px[k - 1] + Ls * std::cos(phi[k - 1]);
@@ -719,7 +726,7 @@ static double static_gauge_reading(const gm_model* m, double P) {
       // torque about +z at joint j from the loads on links j .. N (the revolute carries all)
       double tau = (cx[N] - px[j]) * P;                      // tip pull (0, P)
       for (int k = j; k <= N; k++) tau += -(cy[k] - py[j]) * mass[k] * g;   // gravity (m g, 0)
-      const double qn = (j == 0) ? -tau / stiff[0] : tau / stiff[j];
+      const double qn = (j == 0) ? az * tau / stiff[0] : tau / stiff[j];
       change = std::max(change, std::fabs(qn - q[j]));
       q[j] = qn;
     }

@@ -3378,6 +3378,25 @@ extern "C" __global__ void gm_init_envs_kernel(GmEnvState* __restrict__ states, 
 
 // spawn only (MjClass::spawn_object after MjClass::reset, MjEnv.py:1212-1267)
 #ifndef GM_CAL_TU   // env-step translation unit only
+// MjClass::set_motor_target -> Gripper::set_xyz_m on the env's target (thread per env)
+extern "C" __global__ void gm_motor_target_kernel(GmEnvState* __restrict__ states, const uint8_t* __restrict__ mask,
+                                                  const double* __restrict__ xyz, int per_env,
+                                                  uint8_t* __restrict__ in_limits, int n_envs) {
+  int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n_envs) return;
+  if (mask && !mask[env]) return;
+  const double* t = xyz + (per_env ? 3 * env : 0);
+  in_limits[env] = (uint8_t)g_set_xyz_m(states[env].end, t[0], t[1], t[2]);
+}
+// the latest sim_sensors_SI_ readings (finger 1..3 gauges, palm, wrist Z), thread per env
+extern "C" __global__ void gm_sensor_si_kernel(const GmEnvState* __restrict__ states, float* __restrict__ out, int n_envs) {
+  int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n_envs) return;
+  const GmEnvState& s = states[env];
+  RingRef R = const_cast<RingRef>(s.ring);
+  const int st[5] = {ST_SI_GAUGE, ST_SI_GAUGE + 1, ST_SI_GAUGE + 2, ST_SI_PALM, ST_SI_WZ};
+  for (int k = 0; k < 5; k++) out[5 * env + k] = ring_latest(s, R, st[k]);
+}
 extern "C" __global__ void gm_spawn_kernel(GmEnvState* __restrict__ states, const GmTopo* __restrict__ T,
                                            const uint8_t* __restrict__ mask, const gm_spawn* __restrict__ spawn,
                                            const gm_object* __restrict__ objs, int n_objects, int n_envs) {

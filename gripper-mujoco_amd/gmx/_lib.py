@@ -257,6 +257,8 @@ def _declare(lib):
         "gm_set_settle_cache": (None, [i32]),
         "gm_autoreset": (i32, [vp, i32, vp, i32, vp]),
         "gm_autoreset_episodes": (i32, [vp, i32, vp, i32, vp, vp]),
+        "gm_set_motor_target": (i32, [vp, vp, vp, i32, vp]),
+        "gm_get_sensor_si": (i32, [vp, vp]),
         "gm_set_random_spawn": (i32, [vp, i32, C.c_uint64, i32, i32]),
         "gm_scripted_actions": (i32, [vp, C.c_uint64, C.c_float, vp, i32]),
         "gm_device_reset_mask": (vp, [vp]),

@@ -59,13 +59,14 @@ class BatchedGripperEnv:
     def __init__(self, n_envs: int, object_set: str = "set6_synthetic", settings=None,
                  model_params: ModelParams | None = None, device: int = 0, seed: int = 1234,
                  env_offset: int = 0, max_episode_steps: int = MAX_EPISODE_STEPS, lib=None,
-                 model_blob: ModelBlob | None = None):
+                 model_blob: ModelBlob | None = None, objects=None):
         self.lib = lib if lib is not None else load_library()
         self.n_envs = int(n_envs)
         self.model = model_blob if model_blob is not None else ModelBlob(model_params)
         self.settings = settings if settings is not None else canonical_settings(seed=seed)
         self.cfg = ConfigBlob(self.settings, self.model)
-        self.objects = make_object_set(object_set, seed)
+        # an explicit gm_object array (e.g. the force-measurement spheres) or a named set
+        self.objects = objects if objects is not None else make_object_set(object_set, seed)
         self.max_episode_steps = max_episode_steps
         self.device = device
         self.seed = int(seed)
@@ -186,6 +187,24 @@ class BatchedGripperEnv:
 
     def action_step(self):
         self._check(self.lib.gm_step(self._ctx))
+
+    def set_motor_target(self, xyz, mask=None):
+        """MjClass::set_motor_target(x, y, z) (bind.cpp:82) for every env (xyz: 3 values, or
+        [n_envs, 3]); returns the reference's in-limits flags per env."""
+        t = np.ascontiguousarray(np.asarray(xyz, dtype=np.float64).reshape(-1, 3))
+        if t.shape[0] not in (1, self.n_envs):
+            raise ValueError(f"xyz must be 3 values or [{self.n_envs}, 3]")
+        ok = np.ones(self.n_envs, dtype=np.uint8)
+        m = None if mask is None else np.ascontiguousarray(np.asarray(mask, dtype=np.uint8).reshape(self.n_envs))
+        self._check(self.lib.gm_set_motor_target(self._ctx, None if m is None else m.ctypes.data, t.ctypes.data,
+                                                 t.shape[0], ok.ctypes.data))
+        return ok.astype(bool)
+
+    def sensor_si(self):
+        """Latest sim_sensors_SI_ readings [n_envs, 5]: finger 1..3 gauges, palm, wrist Z (N)."""
+        out = np.zeros((self.n_envs, 5), dtype=np.float32)
+        self._check(self.lib.gm_get_sensor_si(self._ctx, out.ctypes.data))
+        return out
 
     def observation(self):
         self._check(self.lib.gm_get_obs(self._ctx, self._obs.ctypes.data, 0))

@@ -217,6 +217,10 @@ class MjClass:
         raise NotImplementedError("single physics substeps are inside action_step() on the device")
 
     # ------------------------------------------------------------ actions
+    def set_motor_target(self, x: float, y: float, z: float) -> bool:
+        """MjClass::set_motor_target (bind.cpp:82, mjclass.cpp:1359-1364)."""
+        return bool(self._ensure().set_motor_target([x, y, z])[0])
+
     def set_continous_action(self, action: int, fraction: float):
         """MjClass::set_continous_action (mjclass.cpp:1517-1526). MjEnv calls it for every
         index in order then action_step(); the vector is applied in that order on the

@@ -464,6 +464,20 @@ int  gm_set_scene_spawn(gm_ctx* ctx, const gm_spawn_params* params, int max_trie
  * goes to spawn_into_scene first, as MjEnv does. */
 int  gm_set_random_spawn(gm_ctx* ctx, int enable, uint64_t seed, int position_noise_mm, int rotation_noise_deg);
 
+/* MjClass::set_motor_target(x, y, z) (bind.cpp:82; mjclass.cpp:1359-1364 ->
+ * luke::set_gripper_target_m, myfunctions.cpp:2347-2355 -> Gripper::set_xyz_m, gripper.h:152):
+ * the gripper's motor-position target in metres for envs with mask[e] != 0 (NULL = all);
+ * the stepper walks toward it over the following action_step()s.  xyz: 3 doubles shared
+ * (n_xyz == 1) or 3 per env (n_xyz == n_envs), host array.  in_limits[e] (may be NULL) is
+ * the reference's return value: 0 when a motor limit clamped the target.  Used by the
+ * reference's force-measurement programs (mysimulate.cpp:2720-2811). */
+int  gm_set_motor_target(gm_ctx* ctx, const uint8_t* mask, const double* xyz, int n_xyz, uint8_t* in_limits);
+/* MjClass::sim_sensors_SI_ (mjclass.cpp:741-898, read through SensorData::read_finger1_gauge
+ * etc., bind.cpp:1149-1151): the latest SI reading of every env, out[e * 5 + k] for k =
+ * finger 1..3 bending gauge (N, the raw gauge times sim_gauge_raw_to_N_factor), palm (N),
+ * wrist Z (N).  Host array [n_envs x 5]. */
+int  gm_get_sensor_si(gm_ctx* ctx, float* out);
+
 /* Synthetic driver for benchmarks and parity tests (not a reference interface): the
  * scripted grasp mix -- per env and episode, phase lengths from splitmix64(seed, global
  * env id, episode); close the fingers, squeeze, press the palm, lift the base, indexed by

@@ -1593,6 +1593,18 @@ void or_get_event_rows(const or_env* e, int32_t* rows, int32_t* absc, float* las
     if (lastv) lastv[GM_N_BINARY + k] = e->lev[k].last_value;
   }
 }
+/* MjClass::set_motor_target (mjclass.cpp:1359-1364) -> luke::set_gripper_target_m
+ * (myfunctions.cpp:2347-2355) -> Gripper::set_xyz_m (gripper.h:152-154) */
+int or_set_motor_target(or_env* e, double x, double y, double z) {
+  e->end.x = x; e->end.y = y; e->end.z = z;
+  return g_update(&e->end);
+}
+/* sim_sensors_SI_.read_finger1_gauge() ... read_wrist_Z_sensor() (mjclass.h SensorData) */
+void or_get_sensor_si(const or_env* e, float* out) {
+  for (int f = 0; f < 3; f++) out[f] = ring_latest(&e->si_gauge[f]);
+  out[3] = ring_latest(&e->si_palm);
+  out[4] = ring_latest(&e->si_wz);
+}
 int or_overflow(const or_env* e) { return e->overflow; }
 void or_get_eq(const or_env* e, double* eq) { for (int i = 0; i < e->m.nq; i++) eq[i] = e->eq_q[i]; }
 

@@ -102,6 +102,8 @@ def load(path):
             "or_set_solver": (None, [vp, i32]),
             "or_dynamics": (None, [vp, f64p, f64p, f64p, f64p, f64p]),
             "or_set_settle_cache": (None, [i32]),
+            "or_set_motor_target": (i32, [vp, C.c_double, C.c_double, C.c_double]),
+            "or_get_sensor_si": (None, [vp, f32p]),
             "or_collide": (i32, [i32, f64p, f64p, f64p, i32, f64p, f64p, f64p, C.c_double, i32, f64p]),
         }
         for n, (r, a) in sig.items():
@@ -201,6 +203,16 @@ class OracleEnv:
         q = np.zeros(self.model.nq)
         self.L.or_get_eq(self.h, q.ctypes.data_as(C.POINTER(C.c_double)))
         return q
+
+    def set_motor_target(self, x, y, z) -> bool:
+        """MjClass::set_motor_target (bind.cpp:82): Gripper::set_xyz_m on the target."""
+        return bool(self.L.or_set_motor_target(self.h, float(x), float(y), float(z)))
+
+    def sensor_si(self):
+        """[finger1, finger2, finger3 gauge, palm, wrist Z] latest sim_sensors_SI_ readings (N)."""
+        out = np.zeros(5, dtype=np.float32)
+        self.L.or_get_sensor_si(self.h, out.ctypes.data_as(C.POINTER(C.c_float)))
+        return out
 
     def overflow(self):
         return int(self.L.or_overflow(self.h))

@@ -10,8 +10,12 @@
  * reference checkout).  Parity status is recorded in DESIGN.md section "Oracle":
  * pinned by the reference's own compilable code (src/gripper.cpp,
  * src/slidingwindow.h via oracle/_ref), the test.cpp:293-311 known answer and
- * numpy.polyfit; the MuJoCo physics restatement is "parity unpinned" against
- * MuJoCo 2.1.5 itself (not present), and pinned only to this oracle.
+ * numpy.polyfit; MuJoCo 2.1.5 itself is absent, so the physics restatement is pinned
+ * by the MuJoCo outputs the reference kept as data (the force curves of its
+ * measure-constrict / measure-tilt programs, rl/juypter/thesis_plots/sim_vs_real_forces*.csv,
+ * tests/test_force_curves.py; the stable timesteps of mujoco_timesteps.csv at inertia x50)
+ * and by independent restatements of MuJoCo's published algorithms
+ * (tests/test_physics_independent.py).
  */
 #ifndef GM_ORACLE_H_
 #define GM_ORACLE_H_

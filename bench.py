@@ -7,7 +7,10 @@ substeps + sense_gripper_state + update_env, then observation, done and reward
 (mjclass.cpp:1483-1508, 1632-1959, 3000-3049), followed by the episode-boundary
 bookkeeping (return hand-off, reset + respawn of done/truncated envs, MjEnv.py:616-637).
 Everything runs on the device: the actions come from a device driver reading each env's
-episode step (gm_scripted_actions), resets draw their object and pose on the device.
+episode step (gm_scripted_actions), resets draw their object and pose on the device.  The
+headline drives R = --rollout env-steps per launch with gm_rollout (the same sequence fused
+per env in one persistent launch, bit-identical to the per-step calls); `per_step_api`
+reports the same workload through the per-step launches.
 
 Workload = BASELINE.json configs[2] ("C3"): 4096 envs per GPU, 20-object synthetic
 set6-like mixed set, randomised spawn (MjEnv._spawn_object: object drawn per episode,
@@ -131,88 +134,88 @@ def obs_parity(gmx, env, seed: int):
             "oracle_s": round(time.time() - t, 2)}
 
 
-def c2_line(gmx, torch, dev, stream, steps: int, seed: int, env_offset: int):
-    """C2 (BASELINE.json configs[1]): 256 envs, one cylinder (r 20 mm, h 60 mm), the same
-    steady-state scripted workload as the headline."""
+def steady_env(gmx, torch, dev, stream, n: int, object_set: str, seed: int, env_offset: int, mode: int = 0):
+    """A batch at steady state: env e (global id) starts its episode at pre-roll step t_e, so
+    after MAX_EP untimed per-step drives the batch covers episode steps 1..MAX_EP uniformly.
+    Returns (env, per-step drive)."""
+    import ctypes
     s = gmx.canonical_settings(seed=seed)
-    n = 256
-    env = gmx.BatchedGripperEnv(n, object_set="cylinder", settings=s, seed=seed, env_offset=env_offset,
+    env = gmx.BatchedGripperEnv(n, object_set=object_set, settings=s, seed=seed, env_offset=env_offset,
                                 device=dev.index)
     env.set_stream(stream.cuda_stream)
     env.set_scene_spawn(mjenv_spawn_params(gmx), max_tries=3)
     env.reset()
-    returns = torch.full((n,), float("nan"), device=dev)
     d_act = env.lib.gm_device_actions(env.ctx)
 
     def drive():
-        env.lib.gm_scripted_actions(env.ctx, seed, 0.2, d_act, 1)
+        if mode == 0:
+            env.lib.gm_scripted_actions(env.ctx, seed, 0.2, d_act, 1)
+        else:
+            env.lib.gm_random_actions(env.ctx, seed, d_act, 1)
         env.lib.gm_set_action(env.ctx, d_act, 1)
         env.lib.gm_step(env.ctx)
-        env.autoreset_device(0, returns.data_ptr(), max_episode_steps=MAX_EP)
+        env.autoreset_device(0, None, max_episode_steps=MAX_EP)
 
     t_start = gmx.spawn_int(seed, env_offset + np.arange(n), 0, 99, 0, MAX_EP - 1)
-    import ctypes
     for t in range(MAX_EP):
         m = (t_start == t)
         if m.any():
             env.lib.gm_reset(env.ctx, np.ascontiguousarray(m.astype(np.uint8)).ctypes.data_as(
                 ctypes.POINTER(ctypes.c_uint8)), None)
         drive()
+    return env, drive
+
+
+def time_both(env, drive, torch, steps: int, R: int, seed: int, mode: int):
+    """Wall ms per env-step of the same workload driven per step (5 launches per env-step)
+    and as gm_rollout launches of R env-steps."""
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         drive()
     torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+    per_step = (time.perf_counter() - t0) / steps
+    out = {"per_step_api_ms": round(per_step * 1e3, 3)}
+    if R > 0:
+        n_l = max(1, steps // R)
+        env.rollout(R, mode, seed, 0.2, MAX_EP)          # untimed: the dispatch costs in the job's scale
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n_l):
+            env.rollout(R, mode, seed, 0.2, MAX_EP)
+        torch.cuda.synchronize()
+        out["rollout_ms"] = round((time.perf_counter() - t0) / (n_l * R) * 1e3, 3)
+        out["rollout_steps_per_launch"] = R
+    return out
+
+
+def c2_line(gmx, torch, dev, stream, steps: int, seed: int, env_offset: int, R: int):
+    """C2 (BASELINE.json configs[1]): 256 envs, one cylinder (r 20 mm, h 60 mm), the same
+    steady-state scripted workload as the headline, per-step API and rollout launches."""
+    n = 256
+    env, drive = steady_env(gmx, torch, dev, stream, n, "cylinder", seed, env_offset)
+    t = time_both(env, drive, torch, steps, R, seed, 0)
     env.close()
-    return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "envs": n, "steps": steps,
-            "ms_per_step": round(el / steps * 1e3, 3), "workload": "C2: 256 envs, one cylinder, steady-state "
-                                                                   "scripted grasp mix"}
+    ms = t.get("rollout_ms", t["per_step_api_ms"])
+    return {"value": round(n / ms * 1e3, 1), "unit": "env-steps/s", "envs": n, "steps": steps, "ms_per_step": ms,
+            **t, "workload": "C2: 256 envs, one cylinder, steady-state scripted grasp mix"}
 
 
-def c3_random_line(gmx, torch, dev, stream, steps: int, seed: int, env_offset: int, n: int):
+def c3_random_line(gmx, torch, dev, stream, steps: int, seed: int, env_offset: int, n: int, R: int):
     """C3 with synthetic random actions (BASELINE.json north_star: "throughput on synthetic
-    random-action rollouts"): every env draws U[-1,1]^4 each step from one device generator
-    seeded 1234 (TrainDQN.profile's seed, TrainDQN.py:2520), written straight into the
-    context's action buffer; same set6 objects, scene spawn, auto-reset and steady-state
-    pre-roll as the scripted headline."""
-    import ctypes
-    s = gmx.canonical_settings(seed=seed)
-    env = gmx.BatchedGripperEnv(n, object_set="set6_synthetic", settings=s, seed=seed, env_offset=env_offset,
-                                device=dev.index)
-    env.set_stream(stream.cuda_stream)
-    env.set_scene_spawn(mjenv_spawn_params(gmx), max_tries=3)
-    env.reset()
-    returns = torch.full((n,), float("nan"), device=dev)
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed)
-    act = torch.empty((n, env.n_actions), device=dev, dtype=torch.float32)
-
-    def drive():
-        act.uniform_(-1.0, 1.0, generator=g)
-        env.lib.gm_set_action(env.ctx, ctypes.c_void_p(act.data_ptr()), 1)
-        env.lib.gm_step(env.ctx)
-        env.autoreset_device(0, returns.data_ptr(), max_episode_steps=MAX_EP)
-
-    t_start = gmx.spawn_int(seed, env_offset + np.arange(n), 0, 99, 0, MAX_EP - 1)
-    for t in range(MAX_EP):
-        m = (t_start == t)
-        if m.any():
-            env.lib.gm_reset(env.ctx, np.ascontiguousarray(m.astype(np.uint8)).ctypes.data_as(
-                ctypes.POINTER(ctypes.c_uint8)), None)
-        drive()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        drive()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+    random-action rollouts"): every env draws U[-1,1)^4 each env-step on the device
+    (gm_random_actions: a counter-based hash of seed 1234 -- TrainDQN.profile's seed,
+    TrainDQN.py:2520 -- env id, episode and step); same set6 objects, scene spawn, auto-reset
+    and steady-state pre-roll as the scripted headline."""
+    env, drive = steady_env(gmx, torch, dev, stream, n, "set6_synthetic", seed, env_offset, mode=1)
+    t = time_both(env, drive, torch, steps, R, seed, 1)
     caps = int(gmx.env_state_view(env.env_states())["newton_caps"].sum())
     env.close()
-    return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "envs": n, "steps": steps,
-            "ms_per_step": round(el / steps * 1e3, 3), "newton_cap_hits": caps,
-            "workload": "C3 with random actions U[-1,1]^4 (device generator, seed 1234), set6_synthetic, scene "
-                        "spawn, auto-reset, steady state after a staggered pre-roll"}
+    ms = t.get("rollout_ms", t["per_step_api_ms"])
+    return {"value": round(n / ms * 1e3, 1), "unit": "env-steps/s", "envs": n, "steps": steps, "ms_per_step": ms,
+            **t, "newton_cap_hits": caps,
+            "workload": "C3 with random actions U[-1,1)^4 (device counter-based draws, seed 1234), set6_synthetic, "
+                        "scene spawn, auto-reset, steady state after a staggered pre-roll"}
 
 
 def c1_line(gmx, seed: int, n_steps: int = 200):
@@ -433,6 +436,8 @@ def main():
     ap.add_argument("--no-c1", action="store_true", help="skip the C1 (1 env, 200 random steps) line item")
     ap.add_argument("--no-preroll", dest="preroll", action="store_false",
                     help="skip the steady-state pre-roll (profiling runs only; the headline needs it)")
+    ap.add_argument("--rollout", type=int, default=10,
+                    help="env-steps per gm_rollout launch for the headline (0: the per-step API's launches)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -463,12 +468,19 @@ def main():
     S = env.cfg.sim_steps_per_action
     env.set_scene_spawn(mjenv_spawn_params(gmx), max_tries=3)
     env.reset()
-    from gmx.shard import new_episode_records
-    episodes = new_episode_records(n, device=dev)
+    import math
+    K, W = args.steps, args.warmup
+    # the headline drives R env-steps per launch (gm_rollout: driver actions, env-step and
+    # auto-reset fused per env in one persistent launch); R divides K so exactly K are timed
+    R = math.gcd(K, args.rollout) if args.rollout > 0 else 1
+    rollout = args.rollout > 0
+    n_drives, w_drives = K // R, -(-W // R)
+    episodes = torch.zeros((R, n, 3), dtype=torch.int32, device=dev)   # gm_episode_end [R][n]
     d_act = env.lib.gm_device_actions(env.ctx)
 
-    def drive(timed=None):
-        """one MjEnv.step-equivalent for the whole batch, all on the device"""
+    def drive_ps(timed=None, rec=None):
+        """one MjEnv.step-equivalent for the whole batch through the per-step API, all on the
+        device (driver actions, set_action, step, auto-reset: five launches)"""
         env.lib.gm_scripted_actions(env.ctx, args.seed, 0.2, d_act, 1)
         env.lib.gm_set_action(env.ctx, d_act, 1)
         if timed is not None:
@@ -476,11 +488,22 @@ def main():
         env.lib.gm_step(env.ctx)
         if timed is not None:
             ev[timed][1].record(stream)
-        env.autoreset_device(0, None, max_episode_steps=MAX_EP, episodes_dev_ptr=episodes.data_ptr())
+        env.autoreset_device(0, None, max_episode_steps=MAX_EP, episodes_dev_ptr=rec)
+
+    def drive(timed=None):
+        """R env-steps of the whole batch: one gm_rollout launch (or one per-step round)"""
+        if not rollout:
+            drive_ps(timed, episodes.data_ptr())
+            return
+        if timed is not None:
+            ev[timed][0].record(stream)
+        env.rollout(R, 0, args.seed, 0.2, MAX_EP, episodes.data_ptr())
+        if timed is not None:
+            ev[timed][1].record(stream)
 
     # steady state: env e (global id) starts its episode at pre-roll step t_e, so after
     # MAX_EP untimed steps the batch covers episode steps 1..MAX_EP uniformly
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(max(K, 1))]
     gids = first_env + np.arange(n)
     t_start = gmx.spawn_int(args.seed, gids, 0, 99, 0, MAX_EP - 1)
     for t in range(MAX_EP if args.preroll else 0):
@@ -488,13 +511,26 @@ def main():
         if m.any():
             env.lib.gm_reset(env.ctx, np.ascontiguousarray(m.astype(np.uint8)).ctypes.data_as(
                 __import__("ctypes").POINTER(__import__("ctypes").c_uint8)), None)
-        drive()
-    K, W = args.steps, args.warmup
-    elapsed, ep_stats = measure(drive, episodes, K, W, world, dev, torch.cuda.synchronize)
+        drive_ps()
+    elapsed, ep_stats = measure(drive, episodes.view(-1, 3), n_drives, w_drives, world, dev, torch.cuda.synchronize)
     steps_view = gmx.env_state_view(env.env_states())["num_action_steps"]
 
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
+    kern_ms = [a.elapsed_time(b) for a, b in ev[:n_drives]]
+    kern_launch_s = sum(kern_ms) / len(kern_ms) / 1e3
+    kern_avg_s = kern_launch_s / R                      # the kernel's time per env-step
+    # the same workload through the per-step API (five launches per env-step), for reference
+    per_step_api = None
+    if rollout and rank == 0 and world == 1:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(K):
+            drive_ps(k)
+        torch.cuda.synchronize()
+        ps_s = (time.perf_counter() - t0) / K
+        ps_k = sum(a.elapsed_time(b) for a, b in ev[:K]) / K
+        per_step_api = {"ms_per_step": round(ps_s * 1e3, 3), "value": round(n / ps_s, 1), "unit": "env-steps/s",
+                        "step_kernel_ms": round(ps_k, 4),
+                        "path": "gm_scripted_actions + gm_set_action + gm_step + gm_autoreset_episodes per env-step"}
     finite = bool(torch.isfinite(torch.as_tensor(env.observation())).all())
     overflow = int(env.overflow().sum())
     parity = None if (args.no_parity or rank != 0) else obs_parity(gmx, env, args.seed)
@@ -523,6 +559,8 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "kernel": "gm_step_kernel", "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
+                # one launch runs R env-steps of every env (gm_rollout); per-step = launch / R
+                "kernel_launch_ms": round(kern_launch_s * 1e3, 4), "env_steps_per_launch": R,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "traffic_source": traffic_src,
                 "traffic_measured_in_this_run": False,   # PMC counters need their own rocprofv3 pass
@@ -535,17 +573,22 @@ def main():
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(gmx, args.cpu_envs * args.cpu_threads // 4, args.cpu_steps, args.cpu_threads)
             cpu["single_thread"] = cpu_baseline(gmx, args.cpu_envs, args.cpu_steps, 1)["value"]
-        c2 = None if (args.no_c2 or world > 1) else c2_line(gmx, torch, dev, stream, K, args.seed, first_env)
-        c3r = None if (args.no_random or world > 1) else c3_random_line(gmx, torch, dev, stream, K, args.seed, first_env, n)
+        c2 = None if (args.no_c2 or world > 1) else c2_line(gmx, torch, dev, stream, K, args.seed, first_env, R if rollout else 0)
+        c3r = None if (args.no_random or world > 1) else c3_random_line(gmx, torch, dev, stream, K, args.seed, first_env, n,
+                                                                        R if rollout else 0)
         c1 = None if (args.no_c1 or world > 1) else c1_line(gmx, args.seed)
         c5 = None if (args.no_policy or world > 1) else policy_rollout(gmx, torch, dev, stream, n, max(3, K // 2), args.seed,
                                                         first_env)
         out = headline(world, n, K, W, elapsed, ep_stats)
+        out["warmup_steps_run"] = max(w_drives, 1) * R
         out["config"].update({"workload": "C3: set6_synthetic 20 mixed objects, randomised spawn (object drawn per "
                                    "episode, spawn_into_scene grid search on the device), steady state: envs "
                                    "staggered over episode steps 1..250 by an untimed pre-roll, scripted grasp "
                                    "mix (close / squeeze / palm / lift + jitter), canonical sensor/reward "
-                                   "config, device auto-reset at done / 250 steps",
+                                   "config, device auto-reset at done / 250 steps; driven as gm_rollout launches "
+                                   f"of {R} env-steps (driver actions, env-step, episode-end record and reset "
+                                   "fused per env; bit-identical to the per-step API, tests/test_rollout.py)"
+                                   if rollout else "the per-step API",
                        "substeps_per_env_step": S,
                        "B_substep_bytes": B["bytes"], "B_substep_ncon": B["ncon"], "B_substep_nefc": B["nefc"],
                        "measured_contacts": {"mean_ncon": round(float(ncon_m.mean()), 3),
@@ -562,6 +605,7 @@ def main():
             "constraint_solver": solver,
             "cpu_baseline": cpu,
             "obs_max_rel_err": parity,
+            "per_step_api": per_step_api,
             "c2_single_cylinder_256": c2,
             "c3_random_actions": c3r,
             "c1_single_env_200_steps": c1,

@@ -93,15 +93,39 @@ bool nseg_supported(int n) {
     default: return false;
   }
 }
-hipError_t launch_step(gm_ctx* c, int grid, int n_envs, int mode, DebugOut dbg) {
+struct RolloutArgs {
+  int steps, act_mode;
+  uint64_t act_seed;
+  float jitter;
+  int max_ep;
+  gm_episode_end* rec;
+};
+hipError_t launch_step(gm_ctx* c, int grid, int n_envs, int mode, DebugOut dbg, const RolloutArgs* roll = nullptr) {
   // the full env-step (mode 0) runs in cost-sorted order and records each env's cost
   const int32_t* order = (mode == 0 && grid == c->n_envs) ? c->d_order : nullptr;
   uint32_t* cost = (mode == 0 && grid == c->n_envs) ? c->d_cost : nullptr;
   // the chunked work queue (gm_kernels.hip chunked_env_steps): one workgroup per resident
   // wave slot, each pulling env chunks until every env has finished
   const bool chunked = order && c->chunk > 0 && c->chunk_grid > 0 && dbg.phase == nullptr;
-  const GmChunkQ q{c->d_chunk_ctr, c->d_chunk_ring, c->d_chunk_carry, c->chunk_cap, chunked ? c->chunk : 0,
-                   c->chunk_margin, c->chunk_yields, c->chunk_cmargin, c->d_chunk_st};
+  GmChunkQ q{c->d_chunk_ctr, c->d_chunk_ring, c->d_chunk_carry, c->chunk_cap, chunked ? c->chunk : 0,
+             c->chunk_margin, c->chunk_yields, c->chunk_cmargin, c->d_chunk_st};
+  q.steps = 1;
+  q.act_mode = -1;   // gm_step: one plain env-step per env (gm_rollout sets the rollout fields)
+  if (roll && chunked) {
+    q.steps = roll->steps;
+    q.act_mode = roll->act_mode;
+    q.act_seed = roll->act_seed;
+    q.jitter = roll->jitter;
+    q.max_ep = roll->max_ep;
+    q.rec = roll->rec;
+    q.eq = c->d_eq;
+    q.objs = c->d_objs;
+    q.n_objects = c->n_objects;
+    q.scene = c->d_scene;
+    q.scene_tries = c->scene_tries;
+    q.sr = c->spawn_rand;
+    q.sr.env_offset = c->env_offset;   // (the driver's global env ids even without random spawns)
+  }
   if (chunked) grid = c->chunk_grid;
   switch (c->model.n_seg) {
 #define X(N)                                                                                               \
@@ -356,9 +380,12 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   HIPCHK(c, hipMemsetAsync(c->d_cost, 0, sizeof(uint32_t) * 2 * (size_t)n_envs, c->stream));
   {
     // chunked env-step: as many workgroups as wave slots are resident (occupancy query),
-    // GM_CHUNK_SUBSTEPS substeps per chunk (default 8; 0 selects the one-shot kernel)
+    // GM_CHUNK_SUBSTEPS substeps per preemption test (default 16; 0 selects the one-shot
+    // kernel).  r05 sweep on the C3 workload (tools/rollout_probe.py): 8 / 16 / 24 / 32 give
+    // 5.28 / 5.22 / 5.35 / 5.21 ms per env-step for 10-step rollouts, the per-step API the same
+    // 5.74-5.76 ms at 8 and 16
     const char* ev = std::getenv("GM_CHUNK_SUBSTEPS");
-    c->chunk = ev ? std::atoi(ev) : 8;
+    c->chunk = ev ? std::atoi(ev) : 16;
     if (const char* e2 = std::getenv("GM_CHUNK_MARGIN")) c->chunk_margin = std::atoi(e2);
     if (const char* e3 = std::getenv("GM_CHUNK_YIELDS")) c->chunk_yields = std::atoi(e3);
     if (const char* e4 = std::getenv("GM_CHUNK_CMARGIN")) c->chunk_cmargin = std::atoi(e4);
@@ -621,6 +648,51 @@ int gm_scripted_actions(gm_ctx* c, uint64_t seed, float jitter, float* out, int 
     HIPCHK(c, hipMemcpyAsync(out, d, sizeof(float) * (size_t)c->n_envs * c->cfg.n_actions, hipMemcpyDeviceToHost,
                              c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return GM_OK;
+}
+
+int gm_random_actions(gm_ctx* c, uint64_t seed, float* out, int on_device) {
+  if (!c || !out) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  float* d = on_device ? out : c->d_act;
+  int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
+  hipLaunchKernelGGL(gm_random_action_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_cfg, d,
+                     c->n_envs, seed, (long long)c->env_offset);
+  HIPCHK(c, hipGetLastError());
+  if (!on_device) {
+    HIPCHK(c, hipMemcpyAsync(out, d, sizeof(float) * (size_t)c->n_envs * c->cfg.n_actions, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return GM_OK;
+}
+
+int gm_rollout(gm_ctx* c, int n_steps, const gm_rollout_params* p, gm_episode_end* records) {
+  if (!c || !p || n_steps < 1 || (p->action_mode != 0 && p->action_mode != 1)) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  DebugOut dbg{nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (c->chunk > 0 && c->chunk_grid > 0) {
+    // one persistent launch: every env runs its n_steps env-steps back to back
+    const RolloutArgs ra{n_steps, p->action_mode, p->seed, p->jitter, p->max_episode_steps, records};
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, launch_step(c, c->n_envs, c->n_envs, 0, dbg, &ra));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    hipLaunchKernelGGL(gm_dispatch_order_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_cost, c->d_order, c->n_envs,
+                       c->d_chunk_ctr, c->d_chunk_st);
+    HIPCHK(c, hipGetLastError());
+    c->timed = true;
+    return GM_OK;
+  }
+  // the one-shot kernel (GM_CHUNK_SUBSTEPS=0): the same sequence as per-step launches
+  for (int k = 0; k < n_steps; k++) {
+    int rc = p->action_mode == 0 ? gm_scripted_actions(c, p->seed, p->jitter, c->d_act, 1)
+                                 : gm_random_actions(c, p->seed, c->d_act, 1);
+    if (rc == GM_OK) rc = gm_set_action(c, c->d_act, 1);
+    if (rc == GM_OK) rc = gm_step(c);
+    if (rc == GM_OK) rc = gm_autoreset_episodes(c, p->max_episode_steps, nullptr, 1, nullptr,
+                                                records ? records + (size_t)k * c->n_envs : nullptr);
+    if (rc != GM_OK) return rc;
   }
   return GM_OK;
 }

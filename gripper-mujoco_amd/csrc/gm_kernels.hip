@@ -2449,6 +2449,8 @@ struct GmChunkCarry {        // what a chunk hands the next besides the hot stat
   int32_t work_nefc, work_mpr, work_newton, stp_fixed;
   uint32_t clk;              // s_memtime / 64 summed over this env-step's chunks
   int32_t yielded;           // yields so far this env-step (at most GmChunkQ::max_yields)
+  int32_t steps_left;        // env-steps of this launch's job still to run, the current one included
+  int32_t step_idx;          // index of the current env-step in the launch (rollout records)
 };
 // counters (zeroed by gm_dispatch_order_kernel before every launch), one 128-B line each:
 // ring r = x * GM_CQ_NB + bucket: [r * 32] its head, [r * 32 + 1] its tail; GM_CQ_FRESH the
@@ -2472,6 +2474,22 @@ struct GmChunkQ {
   unsigned long long* st;    // [0] first pick, [1] first pick that found no unstarted env,
                              // [2] last env finished (100 MHz clock), [3] wave-busy, [4] wave
                              // polling (sums, 100 MHz ticks); [8 ..] the previous launch's
+  // rollout (gm_rollout; act_mode < 0: one plain env-step per env, gm_step): each env runs
+  // `steps` env-steps in a row, every one of them the per-step API's sequence -- driver actions
+  // (gm_scripted_actions / gm_random_actions) -> set_continous_action -> action_step + obs /
+  // done / reward -> gm_autoreset_episodes' episode-end record and reset
+  int steps;
+  int act_mode;              // 0 scripted grasp mix, 1 uniform random, -1 none
+  uint64_t act_seed;
+  float jitter;
+  int max_ep;                // truncation (num_action_steps >= max_ep), <= 0 off
+  gm_episode_end* rec;       // [steps][n_envs] episode-end records (may be NULL)
+  const double* eq;          // the settled equilibrium (calibrate_reset) for the resets
+  const gm_object* objs;
+  int n_objects;
+  int scene_tries;
+  const gm_spawn_params* scene;
+  GmSpawnRand sr;
 };
 __device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2481,6 +2499,34 @@ __device__ __forceinline__ uint64_t ld_agent64(const uint64_t* p) {
 }
 __device__ __forceinline__ uint32_t add_agent(uint32_t* p, uint32_t v) {
   return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// what survives a reset (see reset_env)
+struct GmResetKeep {
+  uint32_t rng;
+  int32_t ox, oy, oz, episode, newton_caps;
+};
+__device__ __noinline__ void reset_env(GmEnvHot& s, GmEnvState& rec, GmResetKeep keep, const gm_model* __restrict__ m,
+                                       const gm_config* __restrict__ C, const GmTopo* __restrict__ T,
+                                       const double* __restrict__ eq_qpos, const gm_spawn* __restrict__ spawn,
+                                       const gm_object* __restrict__ objs, int n_objects, int env,
+                                       const gm_spawn_params* __restrict__ scene, int scene_tries, GmSpawnRand sr,
+                                       uint16_t* sh_pxy, uint16_t* sh_prot, int lane);
+__device__ void set_action_one(GmEnvHot& s, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
+                               int action, float frac);
+// the rollout driver's actions for the env's next env-step (lane 0): the same fractions
+// gm_scripted_actions / gm_random_actions produce, applied as gm_set_action applies them
+__device__ __noinline__ void driver_actions(GmEnvHot& s, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
+                                            int mode, uint64_t seed, float jitter, int64_t gid) {
+  const int na = C->n_actions;
+  for (int i = 0; i < na; i++) {
+    const int code = C->action_options[i];
+    const int kind = (code >= 0 && code < GM_ACTION_TERMINATION) ? code / 3 : -1;
+    float f = mode == 0 ? gm_script_fraction(seed, gid, s.episode, s.num_action_steps, i, kind, jitter)
+                        : gm_random_fraction(seed, gid, s.episode, s.num_action_steps, i);
+    if (f < -1.0f) f = -1.0f; else if (f > 1.0f) f = 1.0f;
+    set_action_one(s, m, C, i, f);
+  }
 }
 
 // the persistent loop of gm_step_kernel's chunked mode (a mode of the one kernel, not a
@@ -2582,6 +2628,8 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       cr.work_nefc = 0; cr.work_mpr = 0; cr.work_newton = 0; cr.stp_fixed = 0;
       cr.clk = 0;
       cr.yielded = 0;
+      cr.steps_left = q.steps;
+      cr.step_idx = 0;
     } else {
       // agent-scope loads: never served by a scalar cache that the acquire does not reach
       const uint32_t* src = reinterpret_cast<const uint32_t*>(q.carry + env);
@@ -2594,23 +2642,71 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       S.stp_fixed = cr.stp_fixed;
     }
     __syncthreads();
-    // run to the end of the env-step unless an unstarted env has become the longer job
-    const int left = cr.nsub - cr.sub_done;
     const uint32_t own = cost[env];
-    const GmPreempt pre{fresh_head, order, cost, n, own, left, cr.nsub,
-                        cr.yielded < q.max_yields ? q.chunk : 0, q.margin, bq, cmax, q.cmargin};
-    const int k = substep_loop<CL, false, false>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
-                                          (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
-                                          false, left, false, pre);
-    cr.sub_done += k;
-    if (cr.sub_done >= cr.nsub) {
+    const int s_nom = C->sim_steps_per_action;
+    bool finished = false;
+    for (;;) {   // the env-steps of this pick
+      if (cr.sub_done == 0 && q.act_mode >= 0) {
+        // a new env-step of a rollout: the driver's actions first (they may add the
+        // termination lift's substeps), as gm_set_action before gm_step
+        if (lane == 0) {
+          driver_actions(S.s, m, C, q.act_mode, q.act_seed, q.jitter, q.sr.env_offset + env);
+          S.stp_fixed = 0;
+        }
+        __syncthreads();
+        cr.nsub = C->sim_steps_per_action + S.s.extra_substeps;
+      }
+      // run to the end of the env-step unless an unstarted env has become the longer job
+      // (work left counted over the launch's whole job of env-steps)
+      const int left = cr.nsub - cr.sub_done;
+      const int job_left = (cr.steps_left - 1) * s_nom + left;
+      const int job_total = q.steps > 1 ? q.steps * s_nom : cr.nsub;
+      const GmPreempt pre{fresh_head, order, cost, n, own, job_left, job_total,
+                          cr.yielded < q.max_yields ? q.chunk : 0, q.margin, bq, cmax, q.cmargin};
+      const int k = substep_loop<CL, false, false>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
+                                            (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
+                                            false, left, false, pre);
+      cr.sub_done += k;
+      if (cr.sub_done < cr.nsub) break;   // yielded
       unsigned long long t0 = 0;
       env_step_epilogue(S, m, C, T, obs, rew, done, env, lane, false, t0);
+      if (q.act_mode >= 0) {
+        // gm_autoreset_episodes on this env: the episode-end record, then MjEnv.reset
+        const int r = __builtin_amdgcn_readfirstlane(
+            (S.s.done || (q.max_ep > 0 && S.s.num_action_steps >= q.max_ep)) ? 1 : 0);
+        if (lane == 0 && q.rec) {
+          gm_episode_end e;
+          e.ret = r ? S.s.cumulative_reward : __builtin_nanf("");
+          e.length = r ? S.s.num_action_steps : 0;
+          e.success = (r && S.s.bev_last[GM_EV_successful_grasp]) ? 1 : 0;
+          e.pad[0] = e.pad[1] = e.pad[2] = 0;
+          q.rec[(size_t)cr.step_idx * n + env] = e;
+        }
+        if (r) {
+          __syncthreads();   // lane 0's epilogue writes (RNG, counters) before every lane reads them
+          const GmResetKeep keep{S.s.rng, S.s.old_x, S.s.old_y, S.s.old_z, S.s.episode + 1, S.s.newton_caps};
+          __syncthreads();   // every lane has read what survives before the image is cleared
+          static_assert(sizeof(S.st) >= sizeof(uint16_t) * (GM_SPAWN_MAX_XY + GM_SPAWN_MAX_ROT),
+                        "spawn search buffers alias the (dead between env-steps) dynamics union");
+          uint16_t* sh_pxy = reinterpret_cast<uint16_t*>(&S.st);
+          reset_env(S.s, *g, keep, m, C, T, q.eq, nullptr, q.objs, q.n_objects, env, q.scene, q.scene_tries, q.sr,
+                    sh_pxy, sh_pxy + GM_SPAWN_MAX_XY, lane);
+          get_obs_lanes(S.s, g->ring, C, obs + (size_t)env * C->n_obs, lane);
+        }
+      }
+      cr.steps_left -= 1;
+      cr.step_idx += 1;
+      if (cr.steps_left <= 0) { finished = true; break; }
+      cr.sub_done = 0;
+      cr.yielded = 0;
+      __syncthreads();
+    }
+    if (finished) {
       if (cost && lane == 0) {
-        // the dispatch cost (see gm_step_kernel): clocks of this env-step's chunks, blended
-        // with the work model
+        // the dispatch cost (see gm_step_kernel): clocks of this job's chunks, blended with
+        // the work model
         const uint32_t now = cr.clk + (uint32_t)((__builtin_amdgcn_s_memtime() - t_start) >> 6);
-        const uint32_t model = 14000u + 19u * (uint32_t)S.work_nefc + 188u * (uint32_t)S.work_mpr +
+        const uint32_t model = 14000u * (uint32_t)q.steps + 19u * (uint32_t)S.work_nefc + 188u * (uint32_t)S.work_mpr +
                                940u * (uint32_t)S.work_newton;
         cost[n + env] = (now >> 1) + (model >> 1);   // recorded for the next launch's order
       }
@@ -2634,7 +2730,9 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       // acquire pairs with it)
       __syncthreads();
       if (lane == 0) {
-        const uint64_t rem = (uint64_t)own * (uint64_t)(cr.nsub - cr.sub_done) / (uint64_t)cr.nsub;
+        const int job_total = q.steps > 1 ? q.steps * s_nom : cr.nsub;
+        const int job_left = (cr.steps_left - 1) * s_nom + (cr.nsub - cr.sub_done);
+        const uint64_t rem = (uint64_t)own * (uint64_t)job_left / (uint64_t)job_total;
         add_agent(q.ctr + GM_CQ_DONE + 1, 1u);
         const uint32_t b = rem * GM_CQ_NB / cmax < GM_CQ_NB - 1 ? (uint32_t)(rem * GM_CQ_NB / cmax) : GM_CQ_NB - 1;
         const uint32_t t = add_agent(bq + b * 32 + 1, 1u) % (uint32_t)q.cap;
@@ -2821,7 +2919,7 @@ extern "C" __global__ __launch_bounds__(1024) void gm_dispatch_order_kernel(uint
 
 // ---------------------------------------------------------------- actions
 // MjClass::set_action for every action index (mjclass.cpp:1528-1630); one thread per env.
-__device__ int move_base_target_m(GmEnvState& s, const gm_config* __restrict__ C, double x, double y, double z) {
+__device__ int move_base_target_m(GmEnvHot& s, const gm_config* __restrict__ C, double x, double y, double z) {
   double* b = s.base;
   b[0] += x; b[1] += y; b[2] += z;
   int wl = 1;
@@ -2831,7 +2929,7 @@ __device__ int move_base_target_m(GmEnvState& s, const gm_config* __restrict__ C
   }
   return wl;
 }
-__device__ int call_action(GmEnvState& s, const gm_config* __restrict__ C, int kind, double v) {
+__device__ int call_action(GmEnvHot& s, const gm_config* __restrict__ C, int kind, double v) {
   const gm_action* acts[GM_N_ACTION_KINDS] = {
 #define GM_AA(n, u, vv, sg) &C->s.n,
 #include "gm_settings.def"
@@ -2857,7 +2955,7 @@ __device__ int call_action(GmEnvState& s, const gm_config* __restrict__ C, int k
     }
   }
 }
-__device__ void set_action_one(GmEnvState& s, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
+__device__ void set_action_one(GmEnvHot& s, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
                                int action, float frac) {
   const gm_settings& st = C->s;
   int wl = 1;
@@ -2938,6 +3036,21 @@ extern "C" __global__ void gm_scripted_action_kernel(const GmEnvState* __restric
     const int kind = (code >= 0 && code < GM_ACTION_TERMINATION) ? code / 3 : -1;
     out[(size_t)env * na + i] = gm_script_fraction(seed, env_offset + env, s.episode, s.num_action_steps, i, kind, jitter);
   }
+}
+#endif
+
+// uniform random action fractions (gm_random_actions; the rollout's random mode): U[-1, 1)
+// per (env, episode, episode step, action) from the counter-based hash (gm_state.h)
+#ifndef GM_CAL_TU   // env-step translation unit only
+extern "C" __global__ void gm_random_action_kernel(const GmEnvState* __restrict__ states, const gm_config* __restrict__ C,
+                                                   float* __restrict__ out, int n_envs, uint64_t seed,
+                                                   long long env_offset) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n_envs) return;
+  const GmEnvState& s = states[env];
+  const int na = C->n_actions;
+  for (int i = 0; i < na; i++)
+    out[(size_t)env * na + i] = gm_random_fraction(seed, env_offset + env, s.episode, s.num_action_steps, i);
 }
 #endif
 
@@ -3214,40 +3327,32 @@ extern "C" __global__ void gm_autoreset_mask_kernel(const GmEnvState* __restrict
 // MjClass::reset (mjclass.cpp:434-486) -> luke::reset / calibrate_reset (non-first call),
 // configure_settings RNG draws, random_base_Z_movement, then spawn_object.
 #ifndef GM_CAL_TU   // env-step translation unit only
-// One wave per env (grid = n_envs workgroups of 64; unmasked envs exit at once): the
-// wave clears the 11.6 KB record with coalesced 16-byte stores, lane 0 then runs the
-// reference's serial reset (RNG draws, spawn search) on it.
-extern "C" __global__ __launch_bounds__(64) void gm_reset_kernel(
-    GmEnvState* __restrict__ states, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
-    const GmTopo* __restrict__ T, const double* __restrict__ eq_qpos, const uint8_t* __restrict__ mask,
-    const gm_spawn* __restrict__ spawn, const gm_object* __restrict__ objs, int n_objects, int n_envs,
-    const gm_spawn_params* __restrict__ scene, int scene_tries, float* __restrict__ obs, GmSpawnRand sr) {
-  __shared__ uint16_t sh_pxy[GM_SPAWN_MAX_XY], sh_prot[GM_SPAWN_MAX_ROT];   // spawn grid shuffles
-  const int env = blockIdx.x;
-  if (env >= n_envs) return;
-  if (mask && !mask[env]) return;
-  // the new record's hot part is built in LDS (lane 0's serial reset reads back what it
-  // wrote many times over) and stored to HBM in one coalesced sweep; the sensor windows
-  // are cleared in place
-  __shared__ uint4 hot_words[GM_HOT_WORDS / 4];
-  GmEnvHot& s = *reinterpret_cast<GmEnvHot*>(hot_words);
-  GmEnvState& rec = states[env];
-  // keep the per-env RNG stream and the function-static stepper flags (quirk)
-  const uint32_t rng = rec.rng;
-  const int ox = rec.old_x, oy = rec.old_y, oz = rec.old_z;
-  const int32_t episode = rec.episode + 1;
-  const int32_t newton_caps = rec.newton_caps;   // solver diagnostics survive resets
+// The whole reset of one env by one wave on an LDS image `s` of its hot state (rec: its HBM
+// record, whose sensor windows are cleared in place): the image is cleared with coalesced
+// 16-byte stores, then lane 0 runs the reference's serial reset (RNG draws, spawn search --
+// pxy / prot: LDS work buffers of GM_SPAWN_MAX_XY / GM_SPAWN_MAX_ROT entries).  What survives
+// a reset (the per-env RNG stream, the function-static stepper flags -- a reference quirk --,
+// the episode counter, the solver diagnostics) comes in as arguments, read by the caller
+// before the clear.  Used by gm_reset_kernel and by the rollout's in-kernel auto-reset.
+__device__ __noinline__ void reset_env(GmEnvHot& s, GmEnvState& rec, GmResetKeep keep, const gm_model* __restrict__ m,
+                                       const gm_config* __restrict__ C, const GmTopo* __restrict__ T,
+                                       const double* __restrict__ eq_qpos, const gm_spawn* __restrict__ spawn,
+                                       const gm_object* __restrict__ objs, int n_objects, int env,
+                                       const gm_spawn_params* __restrict__ scene, int scene_tries, GmSpawnRand sr,
+                                       uint16_t* sh_pxy, uint16_t* sh_prot, int lane) {
   {
     static_assert(sizeof(GmEnvState) % 16 == 0 && sizeof(GmEnvHot) % 16 == 0, "records move in 16-byte words");
-    for (int i = threadIdx.x; i < GM_HOT_WORDS / 4; i += 64) hot_words[i] = make_uint4(0u, 0u, 0u, 0u);
+    uint4* hw = reinterpret_cast<uint4*>(&s);
+    for (int i = lane; i < GM_HOT_WORDS / 4; i += 64) hw[i] = make_uint4(0u, 0u, 0u, 0u);
     uint4* w = reinterpret_cast<uint4*>(&rec);
-    for (int i = GM_HOT_WORDS / 4 + threadIdx.x; i < GM_STATE_WORDS / 4; i += 64) w[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = GM_HOT_WORDS / 4 + lane; i < GM_STATE_WORDS / 4; i += 64) w[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {   // the reference's serial reset on lane 0
-    s.rng = rng; s.old_x = ox; s.old_y = oy; s.old_z = oz;
+  if (lane == 0) {   // the reference's serial reset on lane 0
+    const int32_t episode = keep.episode;
+    s.rng = keep.rng; s.old_x = keep.ox; s.old_y = keep.oy; s.old_z = keep.oz;
     s.episode = episode;
-    s.newton_caps = newton_caps;
+    s.newton_caps = keep.newton_caps;
     g_reset(s.end); g_reset(s.next);
     for (int k = 0; k < GM_MAX_QPOS; k++) s.qpos[k] = m->qpos0[k];
     s.time = 0; s.last_step_time = 0;
@@ -3312,10 +3417,32 @@ extern "C" __global__ __launch_bounds__(64) void gm_reset_kernel(
     s.done = 0;
     s.reward = 0;
   }
+  __syncthreads();
+}
+
+// One wave per env (grid = n_envs workgroups of 64; unmasked envs exit at once): the new
+// record's hot part is built in LDS (lane 0's serial reset reads back what it wrote many
+// times over) and stored to HBM in one coalesced sweep; the sensor windows are cleared in
+// place.
+extern "C" __global__ __launch_bounds__(64) void gm_reset_kernel(
+    GmEnvState* __restrict__ states, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
+    const GmTopo* __restrict__ T, const double* __restrict__ eq_qpos, const uint8_t* __restrict__ mask,
+    const gm_spawn* __restrict__ spawn, const gm_object* __restrict__ objs, int n_objects, int n_envs,
+    const gm_spawn_params* __restrict__ scene, int scene_tries, float* __restrict__ obs, GmSpawnRand sr) {
+  __shared__ uint16_t sh_pxy[GM_SPAWN_MAX_XY], sh_prot[GM_SPAWN_MAX_ROT];   // spawn grid shuffles
+  const int env = blockIdx.x;
+  if (env >= n_envs) return;
+  if (mask && !mask[env]) return;
+  __shared__ uint4 hot_words[GM_HOT_WORDS / 4];
+  GmEnvHot& s = *reinterpret_cast<GmEnvHot*>(hot_words);
+  GmEnvState& rec = states[env];
+  // keep the per-env RNG stream and the function-static stepper flags (quirk)
+  const GmResetKeep keep{rec.rng, rec.old_x, rec.old_y, rec.old_z, rec.episode + 1, rec.newton_caps};
+  reset_env(s, rec, keep, m, C, T, eq_qpos, spawn, objs, n_objects, env, scene, scene_tries, sr, sh_pxy, sh_prot,
+            (int)threadIdx.x);
   // MjEnv.reset returns _next_observation() of the fresh episode (MjEnv.py:2222-2263):
   // the observation buffer holds the reset env's sensor windows, not the last episode's;
   // sampled one stream per lane as in the env-step epilogue
-  __syncthreads();
   {
     uint4* w = reinterpret_cast<uint4*>(&rec);
     for (int i = threadIdx.x; i < GM_HOT_WORDS / 4; i += 64) w[i] = hot_words[i];

@@ -191,6 +191,21 @@ float gm_script_fraction(uint64_t seed, int64_t gid, int32_t ep, int32_t k, int 
   return a > 1.0f ? 1.0f : (a < -1.0f ? -1.0f : a);
 }
 
+// uniform random action fraction in [-1, 1) for action index i of env-step k (the rollout
+// driver's random mode, gm_random_actions; host mirror gmx.random_fractions): 24 bits of a
+// counter-based hash of (seed, global env id, episode, k, i), so draws do not depend on
+// sharding or launch boundaries
+static inline
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+float gm_random_fraction(uint64_t seed, int64_t gid, int32_t ep, int32_t k, int i) {
+  const uint64_t h = gm_splitmix64(seed * 0xA24BAED4963EE407ull + (uint64_t)gid * 0xD1B54A32D192ED03ull +
+                                   (uint64_t)(uint32_t)ep * 0x8CB92BA72F3D8DD7ull +
+                                   (uint64_t)(uint32_t)k * 0x9E3779B97F4A7C15ull + (uint64_t)i * 0xF1357AEA2E62A9C5ull);
+  return (float)(h >> 40) * (2.0f / 16777216.0f) - 1.0f;
+}
+
 // Topology derived from gm_model on the host (the canonical gripper tree):
 // dof/body of chain position p in finger chain f is first + p - 1 (p >= 1),
 // position 0 of every finger / palm chain is the base dof.

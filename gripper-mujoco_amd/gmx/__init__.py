@@ -10,7 +10,7 @@ from ._lib import (load_library, Settings, ModelParams, Object, Spawn, SpawnPara
                    default_settings, make_object_set, BINARY_EVENTS, LINEAR_EVENTS, ACTION_KINDS,
                    SENSORS, LIB_PATH, env_state_dtype, env_state_view)
 from .settings import canonical_settings, disable_noise, MAX_EPISODE_STEPS
-from .env import BatchedGripperEnv, spawn_draws, spawn_int
+from .env import BatchedGripperEnv, spawn_draws, spawn_int, random_fractions
 from .policy import DevicePolicy, eps_threshold
 from .scripted import GraspScript, in_use_actions
 
@@ -18,6 +18,6 @@ __all__ = ["load_library", "Settings", "ModelParams", "Object", "Spawn", "SpawnP
            "Calibration", "calibrate", "CAL_TIMESTEP", "CAL_GAUGES", "CAL_REFERENCE_RETRY",
            "ModelBlob", "ConfigBlob",
            "default_settings", "make_object_set", "canonical_settings", "disable_noise",
-           "BatchedGripperEnv", "spawn_draws", "spawn_int", "MAX_EPISODE_STEPS", "BINARY_EVENTS",
+           "BatchedGripperEnv", "spawn_draws", "spawn_int", "random_fractions", "MAX_EPISODE_STEPS", "BINARY_EVENTS",
            "LINEAR_EVENTS", "ACTION_KINDS", "SENSORS", "LIB_PATH", "DevicePolicy", "eps_threshold",
            "GraspScript", "in_use_actions", "env_state_dtype", "env_state_view"]

@@ -127,6 +127,12 @@ class SpawnParams(C.Structure):
                 ("xy_increment", C.c_double), ("rot_increment", C.c_double)]
 
 
+class RolloutParams(C.Structure):
+    """gm_rollout_params (include/gripper_mi355x.h)."""
+    _fields_ = [("action_mode", C.c_int32), ("max_episode_steps", C.c_int32), ("seed", C.c_uint64),
+                ("jitter", C.c_float), ("pad", C.c_int32)]
+
+
 class Calibration(C.Structure):
     """gm_calibration: the automatic settings of MjClass::configure_settings
     (mjclass.cpp:241-308) found by simulation."""
@@ -258,6 +264,8 @@ def _declare(lib):
         "gm_autoreset": (i32, [vp, i32, vp, i32, vp]),
         "gm_autoreset_episodes": (i32, [vp, i32, vp, i32, vp, vp]),
         "gm_set_motor_target": (i32, [vp, vp, vp, i32, vp]),
+        "gm_random_actions": (i32, [vp, C.c_uint64, vp, i32]),
+        "gm_rollout": (i32, [vp, i32, vp, vp]),
         "gm_get_sensor_si": (i32, [vp, vp]),
         "gm_set_random_spawn": (i32, [vp, i32, C.c_uint64, i32, i32]),
         "gm_scripted_actions": (i32, [vp, C.c_uint64, C.c_float, vp, i32]),

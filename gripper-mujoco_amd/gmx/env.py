@@ -12,7 +12,7 @@ import ctypes as C
 import numpy as np
 
 from ._lib import (GM_MAX_CON, GM_MAX_DOF, GM_MAX_EFC, load_library, ModelBlob, ConfigBlob, ModelParams, Spawn, SpawnParams, make_object_set,
-                   BINARY_EVENTS, LINEAR_EVENTS)
+                   BINARY_EVENTS, LINEAR_EVENTS, RolloutParams)
 from .settings import canonical_settings, MAX_EPISODE_STEPS
 
 
@@ -38,6 +38,21 @@ def spawn_int(seed, gid, episode, k, lo, hi):
         h = _splitmix64(x)
         span = np.uint64(hi - lo + 1)
         return lo + (((h >> np.uint64(32)) * span) >> np.uint64(32)).astype(np.int64)
+
+
+def random_fractions(seed, gid, episode, step, n_actions):
+    """gm_random_fraction (csrc/gm_state.h) vectorised over envs: [n, n_actions] uniform
+    fractions in [-1, 1) for episode step `step` -- bit-identical to gm_random_actions."""
+    with np.errstate(over="ignore"):
+        gid = np.asarray(gid, dtype=np.int64).astype(np.uint64).reshape(-1, 1)
+        ep = np.asarray(episode, dtype=np.int64).astype(np.uint32).astype(np.uint64).reshape(-1, 1)
+        kk = np.asarray(step, dtype=np.int64).astype(np.uint32).astype(np.uint64).reshape(-1, 1)
+        ii = np.arange(n_actions, dtype=np.uint64).reshape(1, -1)
+        x = (np.uint64(seed) * np.uint64(0xA24BAED4963EE407) + gid * np.uint64(0xD1B54A32D192ED03)
+             + ep * np.uint64(0x8CB92BA72F3D8DD7) + kk * np.uint64(0x9E3779B97F4A7C15)
+             + ii * np.uint64(0xF1357AEA2E62A9C5)) & _M64
+        h = _splitmix64(x)
+        return ((h >> np.uint64(40)).astype(np.float32) * np.float32(2.0 / 16777216.0) - np.float32(1.0)).astype(np.float32)
 
 
 def spawn_draws(seed, gids, episodes, n_objects, position_noise_mm: int = 10, rotation_noise_deg: int = 5):
@@ -187,6 +202,17 @@ class BatchedGripperEnv:
 
     def action_step(self):
         self._check(self.lib.gm_step(self._ctx))
+
+    def rollout(self, n_steps: int, action_mode: int = 0, seed: int = 1234, jitter: float = 0.2,
+                max_episode_steps: int | None = None, records_dev_ptr: int | None = None):
+        """gm_rollout: n_steps env-steps of every env in one launch with the device driver
+        (0: scripted grasp mix, 1: uniform random actions) and the device auto-reset; equal bit
+        for bit to n_steps rounds of driver actions -> set_action -> step -> autoreset.
+        records_dev_ptr: device [n_steps x n_envs] gm_episode_end records (or None)."""
+        mx = self.max_episode_steps if max_episode_steps is None else max_episode_steps
+        p = RolloutParams()
+        p.action_mode, p.max_episode_steps, p.seed, p.jitter = int(action_mode), int(mx), int(seed), float(jitter)
+        self._check(self.lib.gm_rollout(self._ctx, int(n_steps), C.byref(p), C.c_void_p(records_dev_ptr or 0)))
 
     def set_motor_target(self, xyz, mask=None):
         """MjClass::set_motor_target(x, y, z) (bind.cpp:82) for every env (xyz: 3 values, or

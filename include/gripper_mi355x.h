@@ -485,6 +485,11 @@ int  gm_get_sensor_si(gm_ctx* ctx, float* out);
  * [n_envs x n_actions] to `out` (a device pointer when on_device; feed it to
  * gm_set_action).  Runs on the context's stream after whatever reset came before it. */
 int  gm_scripted_actions(gm_ctx* ctx, uint64_t seed, float jitter, float* out, int on_device);
+/* Synthetic driver (not a reference interface): uniform random action fractions U[-1, 1)
+ * per env and action from a counter-based hash of (seed, global env id, episode, episode
+ * step, action index) -- the north star's "synthetic random-action rollouts" -- written like
+ * gm_scripted_actions. */
+int  gm_random_actions(gm_ctx* ctx, uint64_t seed, float* out, int on_device);
 
 /* MjClass::set_continous_action for every action index i in order
  * (mjclass.cpp:1517-1630; called per index by MjEnv._set_action, MjEnv.py:591-594).
@@ -557,6 +562,27 @@ typedef struct gm_episode_end {
  * [n_envs], may be NULL) -- returns may be NULL too. */
 int  gm_autoreset_episodes(gm_ctx* ctx, int max_episode_steps, const gm_spawn* spawn, int spawn_on_device,
                            float* returns, gm_episode_end* episodes);
+
+/* A fused batched rollout (the env-step hot path with its synthetic driver on the device):
+ * n_steps repetitions, for every env, of exactly the per-step API's sequence
+ *   gm_scripted_actions (action_mode 0, seed, jitter) or gm_random_actions (1, seed)
+ *   -> gm_set_action -> gm_step -> gm_autoreset_episodes(max_episode_steps, spawn = NULL,
+ *      records + k * n_envs)
+ * -- the same code on the same state, so the results are bit for bit those of the n_steps
+ * per-step calls -- but as ONE persistent launch: an env that finishes env-step k starts k + 1
+ * at once on its wave (actions, the termination lift's extra substeps, the episode-end record
+ * and MjEnv.reset's reset + spawn included) while the work queue balances envs at substep
+ * granularity, so the launch's tail is paid once per n_steps env-steps instead of every step.
+ * records: device array [n_steps x n_envs] (or NULL); obs / reward / done buffers hold the last
+ * env-step's (the reset observation for envs reset at its end), as after the per-step calls. */
+typedef struct gm_rollout_params {
+  int32_t  action_mode;        /* 0: scripted grasp mix, 1: uniform random */
+  int32_t  max_episode_steps;  /* MjEnv truncation; <= 0 disables it */
+  uint64_t seed;
+  float    jitter;             /* scripted mode only */
+  int32_t  pad;
+} gm_rollout_params;
+int  gm_rollout(gm_ctx* ctx, int n_steps, const gm_rollout_params* params, gm_episode_end* records);
 
 /* Timing of the fused env-step kernel (HIP events on the context's stream). */
 int  gm_last_step_ms(gm_ctx* ctx, float* ms);

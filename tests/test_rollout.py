@@ -1,0 +1,114 @@
+"""gm_rollout: n env-steps of every env in ONE persistent launch with the synthetic driver and
+the auto-reset on the device must equal, bit for bit, n rounds of the per-step API
+(driver actions -> gm_set_action -> gm_step -> gm_autoreset_episodes): the same code on the
+same state in the same order per env (include/gripper_mi355x.h gm_rollout).  Checked on the
+whole fp64 state record, observations, rewards, done flags and every episode-end record, in
+both driver modes, with episodes short enough that resets (and their spawn searches) happen
+inside the launch.  The random driver's host mirror (gmx.random_fractions) equals the device
+draws."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+N, K, MAX_EP, SEED = 96, 14, 6, 77
+
+
+# the hand-off heavy dispatch: a preemption test every substep, no margins, many yields, so
+# envs change waves inside and across the env-steps of the launch (the carry's step index,
+# steps left and per-step counters)
+HANDOFF = {"GM_CHUNK_SUBSTEPS": "1", "GM_CHUNK_MARGIN": "0", "GM_CHUNK_YIELDS": "60", "GM_CHUNK_CMARGIN": "0"}
+
+
+def make_env(gm, env_vars=None):
+    import bench
+    s = gm.canonical_settings(noise=True, seed=SEED)          # noise on: the RNG streams matter
+    old = {k: os.environ.get(k) for k in (env_vars or {})}
+    os.environ.update(env_vars or {})
+    try:
+        env = gm.BatchedGripperEnv(N, object_set="set6_synthetic", settings=s, seed=SEED)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    env.set_scene_spawn(bench.mjenv_spawn_params(gm), max_tries=3)
+    env.reset()
+    return env
+
+
+def per_step(gm, env, mode, records):
+    import torch
+    d_act = env.lib.gm_device_actions(env.ctx)
+    for k in range(K):
+        if mode == 0:
+            env.lib.gm_scripted_actions(env.ctx, SEED, 0.2, d_act, 1)
+        else:
+            env.lib.gm_random_actions(env.ctx, SEED, d_act, 1)
+        env.lib.gm_set_action(env.ctx, d_act, 1)
+        env.lib.gm_step(env.ctx)
+        env.autoreset_device(0, None, max_episode_steps=MAX_EP, episodes_dev_ptr=records[k].data_ptr())
+    torch.cuda.synchronize()
+
+
+def snapshot(env, records):
+    import torch
+    torch.cuda.synchronize()
+    st = env.env_states()
+    rew, done = env.reward_done()
+    return (hashlib.sha1(np.ascontiguousarray(st).tobytes()).hexdigest(), st, env.observation(), rew, done,
+            records.cpu().numpy())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,dispatch", [(0, "default"), (1, "default"), (0, "handoff-heavy")])
+def test_rollout_equals_per_step_api(gm, mode, dispatch):
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import torch
+    from gmx.shard import unpack_episodes
+    ra = torch.zeros((K, N, 3), dtype=torch.int32, device="cuda")
+    rb = torch.zeros((K, N, 3), dtype=torch.int32, device="cuda")
+    a = make_env(gm)
+    b = make_env(gm, HANDOFF if dispatch == "handoff-heavy" else None)
+    try:
+        per_step(gm, a, mode, ra)
+        b.rollout(K, action_mode=mode, seed=SEED, jitter=0.2, max_episode_steps=MAX_EP, records_dev_ptr=rb.data_ptr())
+        sa, sb = snapshot(a, ra), snapshot(b, rb)
+        va, vb = gm.env_state_view(sa[1]), gm.env_state_view(sb[1])
+        for f in va.dtype.names:
+            np.testing.assert_array_equal(va[f], vb[f], err_msg=f)
+        assert sa[0] == sb[0]
+        np.testing.assert_array_equal(sa[2], sb[2])
+        np.testing.assert_array_equal(sa[3], sb[3])
+        np.testing.assert_array_equal(sa[4], sb[4])
+        np.testing.assert_array_equal(sa[5], sb[5])
+        # the launch really crossed episode boundaries: resets with their spawn searches
+        _, length, _ = unpack_episodes(torch.from_numpy(sa[5].reshape(-1, 3)))
+        assert int((length > 0).sum()) >= N, int((length > 0).sum())
+        assert int(va["episode"].min()) >= 2
+        if dispatch == "handoff-heavy":
+            assert b.chunk_stats()["yields"] > N, b.chunk_stats()
+    finally:
+        a.close()
+        b.close()
+
+
+@pytest.mark.gpu
+def test_random_actions_match_host_mirror(gm):
+    if not gpu_available():
+        pytest.skip("no GPU")
+    env = make_env(gm)
+    try:
+        out = np.zeros((N, env.n_actions), dtype=np.float32)
+        env.lib.gm_random_actions(env.ctx, SEED, out.ctypes.data, 0)
+        v = gm.env_state_view(env.env_states())
+        ref = gm.random_fractions(SEED, np.arange(N), v["episode"], v["num_action_steps"], env.n_actions)
+        np.testing.assert_array_equal(out, ref)
+        assert out.min() >= -1.0 and out.max() < 1.0 and out.std() > 0.4
+    finally:
+        env.close()

@@ -147,6 +147,7 @@ struct __align__(16) SharedT {
   static_assert(sizeof(real[GM_BB_SLOTS][8][4]) <= sizeof(real) * (GM_MAX_CON * 9 + 4 * 54 + 54 + 27),
                 "box-box hit slots must fit inside the chain-root stage (st): they may not grow the union");
   int32_t ncon, nefc, nl, overflow;
+  int32_t res_valid;              // newton_solve: a capped solve's residual sits in Mv (euler_damping)
   int32_t work_nefc, work_mpr, work_newton;   // this env-step's rows / MPR substeps / Newton iterations
   int32_t stp_fixed;              // update_all: `next` is a fixed point of the stepper this env-step (see there)
   float forces[32];            // extract_forces_faster results (see extract_forces)

@@ -645,7 +645,10 @@ __device__ __forceinline__ real row_sum(int lane, int ncon, int nl, const real* 
 // finger chain rows on 16 f + p (p = 1..CL), border rows [base, obj0..5] on 48..54, the
 // palm on 56 -- assemble H and rhs, factor, solve; x goes to S.xs.
 #define GM_LANE_PALM_F 56
-template <int CL>
+// RHS_ONLY: stop after the assembly and leave the right-hand side f + J_a^T (D aref)_a in S.xs
+// (the capped-solve residual of newton_solve calls it with D aref replaced by the row forces,
+// so S.xs = qfrc_smooth + J^T efc)
+template <int CL, bool RHS_ONLY = false>
 __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                              const RowsT& R, const bool* act, bool prof) {
   unsigned long long t0 = prof ? clock64() : 0;
@@ -1007,6 +1010,13 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
       rhs += lR;
     }
   }
+  if constexpr (RHS_ONLY) {
+    if (rowf < 3 && p >= 1 && p <= CL) S.xs[T->dof_f0[rowf] + p - 1] = rhs;
+    else if (lane == GM_LANE_PALM_F) S.xs[T->dof_palm] = rhs;
+    else if (lane >= 48 && lane < 55) S.xs[lane == 48 ? T->dof_base : T->dof_obj + lane - 49] = rhs;
+    GM_WAVE_SYNC();
+    return;
+  }
   GM_WAVE_SYNC();   // the stage is read; the factor's transfers reuse the union
   PH(7);
   // ---- factor: finger chains (rows 0..2), pivots CL .. 1
@@ -1231,7 +1241,8 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
   int it = 0, nls = 0;
   bool capped = true;   // no Newton point accepted within GM_NEWTON_MAXIT iterations
   bool ls_cap = false;  // a line search ran GM_NEWTON_MAXLS evaluations without settling
-  for (it = 0; it < GM_NEWTON_MAXIT; it++) {
+  const int maxit = (m->newton_maxit > 0 && m->newton_maxit < GM_NEWTON_MAXIT) ? m->newton_maxit : GM_NEWTON_MAXIT;
+  for (it = 0; it < maxit; it++) {
     bool act[4];
 #pragma unroll
     for (int e = 0; e < 4; e++) act[e] = clane && jq[e] < 0;
@@ -1309,6 +1320,47 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
     GM_WAVE_SYNC();
   }
   PH(13);
+  // A capped solve (wave-uniform, rare: none in the benchmarks): qacc is no optimum, so what
+  // mj_Euler integrates, qfrc_smooth + J^T efc, differs from H~ qacc by the residual
+  // r = H~ qacc - qfrc_smooth - J^T efc.  J^T efc is the Newton right-hand side with the row
+  // forces in place of D aref (efc = -D jar on the active rows: caref := -jq); H~ qacc is Ma,
+  // which the line search of every capped iteration kept up to date.  r goes to S.Mv for
+  // euler_damping; the object rows (decoupled from the gripper in M, undamped) take their
+  // correction Moo^-1 r right here on lane 0 (oracle/physics.c ldl6_solve, same order).
+  if (lane == 0) S.res_valid = capped ? 1 : 0;
+  if (capped) {
+    RowsT Rc = R;
+    bool ac[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) { Rc.caref[e] = -jq[e]; ac[e] = clane && jq[e] < 0; }
+    Rc.laref = -jql;
+    newton_point<CL, true>(S, m, T, fresh_lane(), Rc, ac, false);
+    if (lane < nv) S.Mv[lane] = S.Ma[lane] - S.xs[lane];
+    GM_WAVE_SYNC();
+    if (lane == 0) {
+      real A[6][6], x[6];
+      for (int k = 0; k < 6; k++)
+        for (int l = 0; l <= k; l++) A[k][l] = S.Ho[TRI(k, l)];
+      for (int k = 0; k < 6; k++) x[k] = S.Mv[T->dof_obj + k];
+      for (int k = 5; k >= 0; k--) {
+        const real ik = 1.0 / A[k][k];
+        real col[6];
+        for (int i = 0; i < k; i++) col[i] = A[k][i];
+        for (int i = 0; i < k; i++) {
+          const real a = col[i] * ik;
+          for (int j = 0; j <= i; j++) A[i][j] = A[i][j] - a * col[j];
+          A[k][i] = a;
+        }
+      }
+      for (int k = 5; k >= 0; k--)
+        for (int i = 0; i < k; i++) x[i] = x[i] - A[k][i] * x[k];
+      for (int k = 0; k < 6; k++) x[k] = x[k] / A[k][k];
+      for (int k = 0; k < 6; k++)
+        for (int i = 0; i < k; i++) x[k] = x[k] - A[k][i] * x[i];
+      for (int k = 0; k < 6; k++) S.Mv[T->dof_obj + k] = x[k];
+    }
+    GM_WAVE_SYNC();
+  }
   // constraint forces at the solution and the contact-frame forces (mj_contactForce)
   real fe[4];
 #pragma unroll
@@ -1350,6 +1402,7 @@ __device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __re
   const int rowf = lane >> 4, p = lane & 15;
   const bool chainrow = rowf < 3 && p >= 1 && p <= CL;
   const bool palm = lane == GM_LANE_PALM_F;
+  const bool res = S.res_valid != 0;   // a capped solve's residual in S.Mv (newton_solve)
   real L[CL + 1], lb = 0.0, y = 0.0;
 #pragma unroll
   for (int j = 0; j <= CL; j++) L[j] = 0.0;
@@ -1370,18 +1423,20 @@ __device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __re
     for (int j = 1; j <= CL; j++) L[j] = (j == p) ? L[j] + hd : L[j];
     lb = H[TRI(p, 0)];
     y = hd * S.qacc[d];
+    if (res) y = y + S.Mv[d];
   } else if (palm) {
     const int d = T->dof_palm;
     const real hd = h * T->dof_damp[d];
     L[1] = S.Hp[TRI(1, 1)] + hd;
     lb = S.Hp[TRI(1, 0)];
     y = hd * S.qacc[d];
+    if (res) y = y + S.Mv[d];
   }
   // the base row (wave-uniform: one scalar dof)
   const int db = T->dof_base;
   const real hdb = h * T->dof_damp[db];
   const real bb = S.Hbb + hdb;
-  const real yb0 = hdb * S.qacc[db];
+  const real yb0 = res ? hdb * S.qacc[db] + S.Mv[db] : hdb * S.qacc[db];
   real invd = 1.0, ub = 0.0;
   if (lane < 48) {
 #pragma unroll
@@ -1452,7 +1507,8 @@ __device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __re
   } else if (lane == 48) {
     S.xs[db] = S.qacc[db] - xb;
   } else if (lane >= 57 && lane < 63) {
-    S.xs[T->dof_obj + lane - 57] = S.qacc[T->dof_obj + lane - 57];
+    const int d = T->dof_obj + lane - 57;
+    S.xs[d] = res ? S.qacc[d] - S.Mv[d] : S.qacc[d];
   }
   GM_WAVE_SYNC();
 }

@@ -290,7 +290,10 @@ typedef struct gm_model {
   double  tip_dir[3][3];
   /* gm_model_params.mujoco_actuators */
   int32_t mujoco_actuators;
-  int32_t pad_model;
+  /* Newton iterations per constraint solve (0: GM_NEWTON_MAXIT): a test knob that makes
+   * capped solves happen (their qacc is no optimum; mj_Euler then integrates qfrc_smooth +
+   * J^T efc, not M qacc, see euler_damping) */
+  int32_t newton_maxit;
 } gm_model;
 
 /* one graspable object (a synthetic object-set entry) */

@@ -289,6 +289,12 @@ struct or_env {
   double cinert[NB][10], cdof[NV][6], Ic[NB][10], cfrc[NB][6];
   double Hf[3][GM_TRIF], Hp[3], Ho[21], Hbb;   /* H~ tree blocks (TRI: finger p = 0 base .. CL) */
   double frc[NV], qacc[NV];
+  /* a capped Newton solve's residual H~ qacc - (qfrc_smooth + J^T efc) (mj_Euler integrates
+   * qfrc_smooth + qfrc_constraint, which only equals H~ qacc at the optimum) */
+  double res[NV];
+  int res_valid;
+  double last_smooth[NV], last_constraint[NV];   /* the last substep's forces (want_forces) */
+  int want_forces;
   int ncon, ncon_total, overflow;
   con_t con[NC];
   int pair_off[GM_MAX_PAIR], pair_cnt[GM_MAX_PAIR];
@@ -1633,6 +1639,12 @@ void or_object_net_wrench(const or_env* e, double* out) {
   }
 }
 
+/* the last substep's qfrc_smooth and qfrc_constraint = J^T efc (dense, test hook); only
+ * recorded while or_want_forces(e, 1) is on */
+void or_want_forces(or_env* e, int on) { e->want_forces = on != 0; }
+void or_last_forces(const or_env* e, double* smooth, double* constraint) {
+  for (int d = 0; d < e->m.nv; d++) { smooth[d] = e->last_smooth[d]; constraint[d] = e->last_constraint[d]; }
+}
 void or_debug_substep(or_env* e, int32_t* ncon, double* contact, double* efc_force, double* qacc,
                       double* obj_wrench) {
   full_substep(e);

@@ -55,6 +55,8 @@ int   or_overflow(const or_env* e);
 void  or_get_eq(const or_env* e, double* eq_qpos);                 /* settled equilibrium */
 void  or_set_settle_cache(int on);            /* calibrate_reset's process-wide first_call settle */
 int   or_set_motor_target(or_env* e, double x, double y, double z);   /* MjClass::set_motor_target */
+void  or_want_forces(or_env* e, int on);    /* record each substep's qfrc_smooth / J^T efc (dense) */
+void  or_last_forces(const or_env* e, double* qfrc_smooth, double* qfrc_constraint);
 void  or_get_sensor_si(const or_env* e, float* out5);   /* sim_sensors_SI_: gauges 1..3, palm, wrist Z */
 
 /* one physics substep, with diagnostics (same layout as gm_debug_substep, fp64);

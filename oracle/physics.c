@@ -1643,6 +1643,27 @@ static void rows_jar(or_env* e, const double* v, double* jar) {
     for (int ed = 0; ed < 4; ed++) jar[e->nl + 4 * c + ed] = jv[ed] - e->efc_aref[e->nl + 4 * c + ed];
   }
 }
+/* J^T f over every constraint row, dense (body_vel per unit vector); test paths and the
+ * capped-solve residual only */
+static void jt_force(or_env* e, const double* f, double* out) {
+  const gm_model* m = &e->m;
+  const int nv = m->nv;
+  for (int i = 0; i < nv; i++) {
+    double ev[NV];
+    for (int k = 0; k < NV; k++) ev[k] = (k == i) ? 1.0 : 0.0;
+    double V[NB][6];
+    body_vel(e, ev, V);
+    double acc = 0.0;
+    for (int r = 0; r < e->nl; r++)
+      if (e->lock_row_dof[r] == i) acc += e->lock_row_a[r] * f[r];
+    for (int c = 0; c < e->ncon; c++) {
+      double jv[4];
+      contact_jv(e, c, V, jv);
+      for (int ed = 0; ed < 4; ed++) acc += jv[ed] * f[e->nl + 4 * c + ed];
+    }
+    out[i] = acc;
+  }
+}
 /* per-lane partial of a row sum (contact c's 4 edges on lane c, lock row r on lane r),
  * then the 64-lane butterfly: the device's row reduction */
 static double row_reduce(const or_env* e, const double* t) {
@@ -1681,7 +1702,8 @@ static void newton_solve(or_env* e) {
   rows_jar(e, q, jq);
   int it = 0, capped = 1, ls_cap = 0;
   e->stat_ls = 0;
-  for (it = 0; it < GM_NEWTON_MAXIT; it++) {
+  const int maxit = (m->newton_maxit > 0 && m->newton_maxit < GM_NEWTON_MAXIT) ? m->newton_maxit : GM_NEWTON_MAXIT;
+  for (it = 0; it < maxit; it++) {
     for (int r = 0; r < nefc; r++) act[r] = row_active(e, r, jq[r]);
     nsys_t S;
     newton_assemble(e, act, &S);
@@ -1756,6 +1778,20 @@ static void newton_solve(or_env* e) {
     C->force[2] = C->mu * (fe[2] - fe[3]);
   }
   for (int i = 0; i < nv; i++) e->qacc_warm[i] = q[i];
+  /* a capped solve: qacc is no optimum, so qfrc_smooth + J^T efc (what mj_Euler integrates)
+   * differs from H~ qacc by the residual; euler_damping takes it into account (H~ q = Ma,
+   * kept up to date by the line searches every capped iteration ran) */
+  e->res_valid = 0;
+  if (capped || e->want_forces) {
+    double jtf[NV];
+    jt_force(e, e->efc_f, jtf);
+    if (capped) {
+      for (int i = 0; i < nv; i++) e->res[i] = Ma[i] - (e->frc[i] + jtf[i]);
+      e->res_valid = 1;
+    }
+    if (e->want_forces)
+      for (int i = 0; i < nv; i++) { e->last_smooth[i] = e->frc[i]; e->last_constraint[i] = jtf[i]; }
+  }
 }
 
 /* ---- independent cross-check: the same soft-constraint problem in its dual form,
@@ -1859,6 +1895,26 @@ static void ref_pgs_solve(or_env* e, int sweeps) {
  * one physics substep: before_step + step + after_step (physics part),
  * myfunctions.cpp:1864-1908 -> mj_step1 / control / mj_step2 (the engine spec)
  * ===================================================================== */
+/* A x = b for a symmetric positive definite 6 x 6 block, LDL^T with pivots 5 .. 0 (rows
+ * eliminated last-first, as the device's serial version on lane 0), x overwrites b */
+static void ldl6_solve(double A[6][6], double* b) {
+  /* lower triangle only: A = U D U^T with U unit upper, U[i][k] kept at A[k][i] (i < k) */
+  for (int k = 5; k >= 0; k--) {
+    const double ik = 1.0 / A[k][k];
+    double col[6];
+    for (int i = 0; i < k; i++) col[i] = A[k][i];
+    for (int i = 0; i < k; i++) {
+      const double a = col[i] * ik;
+      for (int j = 0; j <= i; j++) A[i][j] = A[i][j] - a * col[j];
+      A[k][i] = a;
+    }
+  }
+  for (int k = 5; k >= 0; k--)          /* U z = b */
+    for (int i = 0; i < k; i++) b[i] = b[i] - A[k][i] * b[k];
+  for (int k = 0; k < 6; k++) b[k] = b[k] / A[k][k];
+  for (int k = 0; k < 6; k++)           /* U^T x = D^-1 z */
+    for (int i = 0; i < k; i++) b[k] = b[k] - A[k][i] * b[i];
+}
 /* MuJoCo 2.1.5 mj_Euler's implicit joint damping (mujoco_actuators): qacc_e =
  * (M + h D)^-1 (qfrc_smooth + qfrc_constraint) = qacc - (M + h D)^-1 (h D qacc), qacc the
  * solve's (M qacc = qfrc_smooth + qfrc_constraint at its optimum).  The system on the
@@ -1884,6 +1940,7 @@ static void euler_damping(const or_env* e, double* qe) {
       L[l][p] = L[l][p] + hd;
       lb[l] = e->Hf[f][TRI(p, 0)];
       y[l] = hd * e->qacc[d];
+      if (e->res_valid) y[l] = y[l] + e->res[d];
     }
   const int lp = 56, lbase = 48;
   {
@@ -1891,10 +1948,12 @@ static void euler_damping(const or_env* e, double* qe) {
     L[lp][1] = e->Hp[TRI(1, 1)] + hd;
     lb[lp] = e->Hp[TRI(1, 0)];
     y[lp] = hd * e->qacc[m->dof_palm];
+    if (e->res_valid) y[lp] = y[lp] + e->res[m->dof_palm];
   }
   const double hdb = h * T->dof_damp[m->dof_base];
   const double bb = e->Hbb + hdb;
   y[lbase] = hdb * e->qacc[m->dof_base];
+  if (e->res_valid) y[lbase] = y[lbase] + e->res[m->dof_base];
   /* chain factor, pivots CL .. 1, every lane of rows 0..2 in lock step */
   for (int k = CL; k >= 1; k--) {
     double hk[3][GM_CHAIN + 1], hkb[3], ihk[3];
@@ -1972,6 +2031,17 @@ static void euler_damping(const or_env* e, double* qe) {
   }
   y[lp] = y[lp] * invd[lp] - lb[lp] * xb;
   for (int d = 0; d < m->nv; d++) qe[d] = e->qacc[d];
+  if (e->res_valid) {
+    /* the object block of M (no damping, no coupling to the gripper): qacc_e = qacc - Moo^-1 r,
+     * the 6 x 6 block (H~'s Ho, lower triangle) by LDL^T from the last row as the device's
+     * lane 0 does it */
+    double A[6][6], x[6];
+    for (int k = 0; k < 6; k++)
+      for (int l = 0; l <= k; l++) { A[k][l] = e->Ho[TRI(k, l)]; A[l][k] = A[k][l]; }
+    for (int k = 0; k < 6; k++) x[k] = e->res[m->dof_obj + k];
+    ldl6_solve(A, x);
+    for (int k = 0; k < 6; k++) qe[m->dof_obj + k] = e->qacc[m->dof_obj + k] - x[k];
+  }
   for (int f = 0; f < 3; f++)
     for (int p = 1; p <= CL; p++) qe[T->dof_f0[f] + p - 1] = e->qacc[T->dof_f0[f] + p - 1] - y[16 * f + p];
   qe[m->dof_palm] = e->qacc[m->dof_palm] - y[lp];

@@ -70,7 +70,7 @@ class GmModel(C.Structure):
         ("time_per_step", _d), ("stepper_num_steps", _i),
         ("gauge_xpos", _d), ("gauge_order", _i),
         ("body_tip", _i * 3), ("tip_dir", _d * 3 * 3),
-        ("mujoco_actuators", _i), ("pad_model", _i),
+        ("mujoco_actuators", _i), ("newton_maxit", _i),
     ]
 
 

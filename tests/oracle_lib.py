@@ -104,6 +104,8 @@ def load(path):
             "or_set_settle_cache": (None, [i32]),
             "or_set_motor_target": (i32, [vp, C.c_double, C.c_double, C.c_double]),
             "or_get_sensor_si": (None, [vp, f32p]),
+            "or_want_forces": (None, [vp, i32]),
+            "or_last_forces": (None, [vp, f64p, f64p]),
             "or_collide": (i32, [i32, f64p, f64p, f64p, i32, f64p, f64p, f64p, C.c_double, i32, f64p]),
         }
         for n, (r, a) in sig.items():

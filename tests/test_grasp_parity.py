@@ -244,3 +244,34 @@ def test_other_segment_counts_256(gm, ol, n_seg):
     sub = [compare_substep(gm, ol, env, sn) for sn in snaps]
     print(f"N={n_seg}", rep, sub)
     env.close()
+
+
+def test_capped_newton_substep_matches_oracle_256(gm, ol):
+    """A Newton solve that runs out of iterations (gm_model.newton_maxit = 1) on grasp
+    states: mj_Euler integrates qfrc_smooth + J^T efc of the unconverged forces, not M qacc
+    (the residual path of gm_newton.hip newton_solve / euler_damping).  Device and oracle
+    take one substep from the same states: qpos and qvel after it to ~1e-9 (scaled), the
+    capped-solve counters bit-exact, and most contact envs really capped."""
+    import indep_physics as ip
+    env, snaps = rollout(gm, 256, "set6_synthetic", 5, steps=53, snaps=(40, 52))
+    capped = gm.ModelBlob(env.model.params)
+    ip.GmModel.from_buffer(capped.buf).newton_maxit = 1
+    cenv = gm.BatchedGripperEnv(256, settings=env.settings, seed=5, model_blob=capped, objects=env.objects)
+    try:
+        n_capped = 0
+        for sn in snaps:
+            cenv.set_env_states(sn["rec"])
+            cenv.debug_substep(full=True)
+            after_d = cenv.env_states()
+            *_, after_o = ol.batch_substep(cenv.model, cenv.cfg, cenv.objects, sn["rec"])
+            dv, ov, v0 = gm.env_state_view(after_d), gm.env_state_view(after_o), gm.env_state_view(sn["rec"])
+            np.testing.assert_array_equal(dv["newton_caps"], ov["newton_caps"], err_msg="newton_caps")
+            n_capped += int((ov["newton_caps"] > v0["newton_caps"]).sum())
+            np.testing.assert_allclose(dv["qpos"], ov["qpos"], rtol=0, atol=1e-9, err_msg="qpos after a capped substep")
+            vs = np.maximum(1.0, np.abs(ov["qvel"]).max(axis=1, keepdims=True))
+            np.testing.assert_allclose(dv["qvel"] / vs, ov["qvel"] / vs, rtol=0, atol=1e-9,
+                                       err_msg="qvel after a capped substep")
+        assert n_capped > 100, n_capped
+    finally:
+        cenv.close()
+        env.close()

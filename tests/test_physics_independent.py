@@ -120,7 +120,7 @@ def test_euler_implicit_damping_matches_dense_solve(world):
     states with contacts and random velocities.  At the solve's optimum qfrc_smooth +
     qfrc_constraint = M qacc (M with armature, the solve's matrix), so the right-hand side
     is formed from the solver's qacc; a capped solve carries the residual, see
-    test_euler_damping_uses_the_constraint_forces_on_a_capped_solve."""
+    test_euler_damping_integrates_the_constraint_forces_on_capped_solves."""
     gm, model, cfg, objs = world
     M = ip.Model(model)
     ip.set_object(M, objs[1])
@@ -142,6 +142,53 @@ def test_euler_implicit_damping_matches_dense_solve(world):
         assert np.abs(qacc - qe).max() > 1e3 * np.abs(dv - qe).max()
         checked += ncon > 0
     assert checked >= 3
+
+
+def test_euler_damping_integrates_the_constraint_forces_on_capped_solves(world):
+    """MuJoCo's mj_Euler integrates qfrc_smooth + qfrc_constraint, qfrc_constraint = J^T efc of
+    the solve's final forces.  At an optimum that is M qacc; a Newton solve capped before
+    convergence (gm_model.newton_maxit = 1 forces it) leaves a residual, and the update must
+    still be qvel' = qvel + h (M + h D)^-1 (qfrc_smooth + J^T efc).  Checked against a dense
+    numpy solve with the independent joint-space inertia on grasp states, for the capped
+    substeps (the correction is large there) and the converged ones."""
+    gm, model, cfg, objs = world
+    import ctypes as C
+    capped_model = gm.ModelBlob(model.params)
+    ip.GmModel.from_buffer(capped_model.buf).newton_maxit = 1
+    ccfg = gm.ConfigBlob(gm.canonical_settings(noise=False, seed=3), capped_model)
+    M = ip.Model(capped_model)
+    ip.set_object(M, objs[1])
+    damp = np.asarray(ip.arr(M.raw.jnt_damping), dtype=np.float64)[M.jnt[M.dof_body]]
+    arm = M.armature[M.jnt[M.dof_body]]
+    h = model.params.timestep
+    _, states = dynamic_states(gm, model, cfg, objs)
+    o = ol.OracleEnv(capped_model, ccfg, objs, env_id=2)
+    sp = gm.Spawn()
+    sp.object_index, sp.x, sp.y, sp.zrot = 1, 0.004, -0.003, 0.3
+    o.reset(sp)
+    o.L.or_want_forces(o.h, 1)
+    seen = {True: 0, False: 0}
+    fs, fc = np.zeros(model.nv), np.zeros(model.nv)
+    for q, v in states:
+        for _ in range(3):
+            caps0 = int(gm.env_state_view(o.export_state())["newton_caps"])
+            o.L.or_set_state(o.h, q.ctypes.data_as(f64p), v.ctypes.data_as(f64p))
+            _, _, _, qacc = o.debug_substep()
+            capped = int(gm.env_state_view(o.export_state())["newton_caps"]) > caps0
+            _, v1, _ = o.state()
+            o.L.or_last_forces(o.h, fs.ctypes.data_as(f64p), fc.ctypes.data_as(f64p))
+            Mi = ip.mass_matrix(M, q) + np.diag(arm)
+            qe = np.linalg.solve(Mi + h * np.diag(damp), fs + fc)
+            dv = (v1 - v) / h
+            scale = np.abs(qe).max()
+            assert np.abs(dv - qe).max() <= 1e-9 * scale, (capped, np.abs(dv - qe).max(), scale)
+            if capped:
+                # the residual-free formula (M + h D)^-1 M qacc would be wrong here
+                qe_opt = np.linalg.solve(Mi + h * np.diag(damp), Mi @ qacc)
+                assert np.abs(qe_opt - qe).max() > 1e3 * np.abs(dv - qe).max()
+            seen[capped] += 1
+            q, v, _ = o.state()
+    assert seen[True] >= 3 and seen[False] >= 1, seen
 
 # ---------------------------------------------------------------- narrowphase
 def collide(L, t1, s1, c1, R1, t2, s2, c2, R2, tol=1e-6, it=50):

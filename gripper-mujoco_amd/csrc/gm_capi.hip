@@ -65,6 +65,9 @@ struct gm_ctx {
   GmChunkCarry* d_chunk_carry = nullptr;
   unsigned long long* d_chunk_st = nullptr;
   int chunk = 0, chunk_grid = 0, chunk_cap = 0, chunk_margin = 50, chunk_yields = 20, chunk_cmargin = 50;
+  // DUO workgroups (gm_step_kernel<CL, false, true>): two waves per env, the second running
+  // the collider concurrently -- for batches small enough that wave slots are spare
+  bool duo = false;
   gm_spawn_params* d_scene = nullptr;  // gm_set_scene_spawn parameters (NULL: plain spawn_object)
   int scene_tries = 0;
   GmSpawnRand spawn_rand{};            // gm_set_random_spawn (enable = 0: spawn tables)
@@ -127,12 +130,20 @@ hipError_t launch_step(gm_ctx* c, int grid, int n_envs, int mode, DebugOut dbg, 
     q.sr.env_offset = c->env_offset;   // (the driver's global env ids even without random spawns)
   }
   if (chunked) grid = c->chunk_grid;
+  // the env-step proper (not the settle, a diagnostic substep or a profiled step) on DUO
+  // workgroups when the context chose them; the chunked grid was sized for that kernel
+  const bool duo = c->duo && mode == 0 && dbg.phase == nullptr;
   switch (c->model.n_seg) {
-#define X(N)                                                                                               \
-  case N:                                                                                                  \
-    hipLaunchKernelGGL((gm_step_kernel<N + 2, false>), dim3(grid), dim3(NT), 0, c->stream, c->d_state,      \
-                       c->d_model, c->d_cfg, c->d_topo, c->d_obs, c->d_rew, c->d_done, n_envs, mode, dbg,    \
-                       order, cost, q);                                                                      \
+#define X(N)                                                                                                 \
+  case N:                                                                                                    \
+    if (duo)                                                                                                 \
+      hipLaunchKernelGGL((gm_step_kernel<N + 2, false, true>), dim3(grid), dim3(2 * NT), 0, c->stream,        \
+                         c->d_state, c->d_model, c->d_cfg, c->d_topo, c->d_obs, c->d_rew, c->d_done, n_envs,   \
+                         mode, dbg, order, cost, q);                                                           \
+    else                                                                                                     \
+      hipLaunchKernelGGL((gm_step_kernel<N + 2, false>), dim3(grid), dim3(NT), 0, c->stream, c->d_state,      \
+                         c->d_model, c->d_cfg, c->d_topo, c->d_obs, c->d_rew, c->d_done, n_envs, mode, dbg,    \
+                         order, cost, q);                                                                      \
     return hipGetLastError();
     GM_NSEG_LIST
 #undef X
@@ -389,18 +400,27 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
     if (const char* e2 = std::getenv("GM_CHUNK_MARGIN")) c->chunk_margin = std::atoi(e2);
     if (const char* e3 = std::getenv("GM_CHUNK_YIELDS")) c->chunk_yields = std::atoi(e3);
     if (const char* e4 = std::getenv("GM_CHUNK_CMARGIN")) c->chunk_cmargin = std::atoi(e4);
-    int per_cu = 0, n_cu = 0;
+    int per_cu = 0, per_cu_duo = 0, n_cu = 0;
     switch (c->model.n_seg) {
 #define X(N)                                                                                              \
   case N:                                                                                                 \
     HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gm_step_kernel<N + 2, false>, NT, 0)); \
+    HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_duo, (gm_step_kernel<N + 2, false, true>), \
+                                                           2 * NT, 0));                                   \
     break;
       GM_NSEG_LIST
 #undef X
       default: break;
     }
     HIPCHK(c, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
-    c->chunk_grid = std::min(n_envs, per_cu * n_cu);
+    // DUO when every env gets its two waves resident at once (GM_DUO = 0 / 1 forces it off
+    // / on): the helper wave then costs no env a slot
+    const char* ed = std::getenv("GM_DUO");
+    c->duo = ed ? std::atoi(ed) != 0 : (per_cu_duo > 0 && n_envs <= per_cu_duo * n_cu);
+    c->chunk_grid = std::min(n_envs, (c->duo ? per_cu_duo : per_cu) * n_cu);
+    // GM_CHUNK_GRID caps the persistent grid (tests: a small batch on fewer workgroups than
+    // envs, so the work queue hands envs off between waves)
+    if (const char* e5 = std::getenv("GM_CHUNK_GRID")) c->chunk_grid = std::max(1, std::min(c->chunk_grid, std::atoi(e5)));
     c->chunk_cap = n_envs + c->chunk_grid;
     HIPCHK(c, hipMalloc(&c->d_chunk_ctr, sizeof(uint32_t) * GM_CQ_ALLOC));
     HIPCHK(c, hipMemsetAsync(c->d_chunk_ctr, 0, sizeof(uint32_t) * GM_CQ_ALLOC, c->stream));
@@ -932,6 +952,12 @@ int gm_chunk_stats(gm_ctx* c, uint32_t* out, uint64_t* times) {
   out[0] = std::min<uint32_t>(w[0], (uint32_t)c->n_envs);
   out[1] = w[32]; out[2] = w[33]; out[3] = w[34];
   out[4] = (uint32_t)c->chunk; out[5] = (uint32_t)c->chunk_grid;
+  return GM_OK;
+}
+
+int gm_dispatch_info(const gm_ctx* c, int32_t* out) {
+  if (!c || !out) return GM_E_ARG;
+  out[0] = c->chunk; out[1] = c->chunk_grid; out[2] = c->duo ? 2 : 1; out[3] = 0;
   return GM_OK;
 }
 

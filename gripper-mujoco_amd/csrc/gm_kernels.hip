@@ -34,6 +34,14 @@
 // on loads whose results it does not yet need.
 #define GM_WAVE_SYNC() do { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); \
                             __builtin_amdgcn_wave_barrier(); } while (0)
+// Synchronisation of the env's own work, which one wave does: __syncthreads' fences around
+// a wave barrier instead of s_barrier.  For the 64-thread workgroups this is what
+// __syncthreads lowers to anyway; in a DUO workgroup (gm_step_kernel<.., true>: a second,
+// helper wave runs the collider concurrently, duo_helper) the helper is parked at its own
+// s_barrier handshake and must not be counted by the owner wave's bookkeeping syncs.
+#define GM_ENV_SYNC() do { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); \
+                           __builtin_amdgcn_wave_barrier(); \
+                           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); } while (0)
 // The lane id, opaque to the compiler: each phase derives its lane predicates (chain row,
 // border, contact lane, ...) from its own copy, so they are recomputed per phase instead of
 // being computed once per substep and held live (in spilled SGPR pairs) across all of them.
@@ -148,6 +156,7 @@ struct __align__(16) SharedT {
                 "box-box hit slots must fit inside the chain-root stage (st): they may not grow the union");
   int32_t ncon, nefc, nl, overflow;
   int32_t res_valid;              // newton_solve: a capped solve's residual sits in Mv (euler_damping)
+  int32_t duo_cmd;                // DUO workgroups: 1 = the helper wave runs this substep's collider, 0 = exit
   int32_t work_nefc, work_mpr, work_newton;   // this env-step's rows / MPR substeps / Newton iterations
   int32_t stp_fixed;              // update_all: `next` is a fixed point of the stepper this env-step (see there)
   float forces[32];            // extract_forces_faster results (see extract_forces)
@@ -1209,9 +1218,11 @@ __device__ __forceinline__ void write_contact(SharedT<CL>& S, int slot, int g1, 
 
 #include "gm_newton.hip"
 
+// hit: the box-box hit slots (S.cl.hit, in the union; a DUO workgroup's helper wave passes
+// its own array, the union being live with crb_rne's composites while it runs)
 template <int CL>
 __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
-                          bool prof = false) {
+                          bool prof, real (*hit)[8][4]) {
   unsigned long long t0 = prof ? clock64() : 0;
   (void)t0;
   // one lane per candidate pair, in batches of 64 pairs: the 6 N + 15 pairs fit one batch
@@ -1299,7 +1310,7 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
                 real P[3], dep;
                 const int ok = bb_face_cand(bbs, i, P, dep);
                 if (ok && bslot >= 0) {
-                  real* hs = S.cl.hit[bslot][cnt];
+                  real* hs = hit[bslot][cnt];
                   hs[0] = P[0]; hs[1] = P[1]; hs[2] = P[2]; hs[3] = dep;
                 }
                 hm |= (unsigned)ok << i;
@@ -1348,7 +1359,7 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
       } else if (kind == 4 && bslot >= 0) {
         // the stored hits, in candidate order as pass 1 found them (bb_face_hit's operations)
         for (int w = 0; w < cnt; w++) {
-          const real* hs = S.cl.hit[bslot][w];
+          const real* hs = hit[bslot][w];
           const real dep = hs[3];
           Hit t;
           t.dist = -dep;
@@ -1887,18 +1898,30 @@ GM_EPI_ATTR void monitor_sensors(SharedT<CL>& S, const gm_model* __restrict__ m,
 }
 
 // ============================================================ one full substep
-template <int CL, bool CAL>
+template <int CL, bool CAL, bool DUO>
 __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
                                                      int lane, bool prof) {
   unsigned long long t0 = prof ? clock64() : 0;
   if (lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
   kinematics<CL>(S, m, T, fresh_lane(), prof);
   PH(0);
-  crb_rne<CL, CAL>(S, m, T, fresh_lane(), prof);
-  PH(1);
-  mass_and_forces<CL, CAL>(S, m, T, fresh_lane());
-  PH(2);
-  collision(S, m, T, fresh_lane(), prof);
+  if constexpr (DUO) {
+    // the collider needs only the poses: the helper wave runs it (duo_helper) while this
+    // wave forms the inertia and forces; the two barriers are the handshake
+    if (lane == 0) S.duo_cmd = 1;
+    __syncthreads();
+    crb_rne<CL, CAL>(S, m, T, fresh_lane(), prof);
+    PH(1);
+    mass_and_forces<CL, CAL>(S, m, T, fresh_lane());
+    PH(2);
+    __syncthreads();
+  } else {
+    crb_rne<CL, CAL>(S, m, T, fresh_lane(), prof);
+    PH(1);
+    mass_and_forces<CL, CAL>(S, m, T, fresh_lane());
+    PH(2);
+    collision(S, m, T, fresh_lane(), prof, S.cl.hit);
+  }
   PH(5);
   newton_solve<CL, CAL>(S, m, T, fresh_lane(), prof);
   PH(6);
@@ -1967,7 +1990,7 @@ __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
 // returns the substeps run (nsub unless the preemption test yielded).  PROF = false
 // compiles the per-phase clock reads (PH) out: no uniform branch at every phase boundary,
 // so the scheduler's regions span them (the env-step kernel's chunked path runs this one)
-template <int CL, bool CAL, bool PROF>
+template <int CL, bool CAL, bool PROF, bool DUO = false>
 __device__ __noinline__ int substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS_GLOBAL gm_model* m_,
                                          const GM_AS_GLOBAL GmTopo* T_, const GM_AS_GLOBAL gm_config* C_, int lane_in,
                                          bool prof_in, int nsub_in, bool settle_in, GmPreempt pre) {
@@ -2029,7 +2052,7 @@ __device__ __noinline__ int substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS_
       S.s.lock_q[lane] = S.lock_pre[lane];
     }
     const unsigned long long tc = prof ? clock64() : 0;
-    physics_substep_body<CL, CAL>(S, m, T, lane, prof);
+    physics_substep_body<CL, CAL, DUO>(S, m, T, lane, prof);
     unsigned long long t0 = prof ? clock64() : 0;
     if (prof && lane == 0) S.tph[22] += t0 - tc;
     update_all<CL>(S, m, T, fresh_lane());
@@ -2414,11 +2437,11 @@ __device__ __forceinline__ void load_state(SharedT<CL>& S, GmEnvState* __restric
   uint32_t* dst = reinterpret_cast<uint32_t*>(&S.s);
   for (int i = lane; i < GM_HOT_WORDS; i += NT) dst[i] = src[i];
   S.gs = g;
-  __syncthreads();
+  GM_ENV_SYNC();
 }
 template <int CL>
 __device__ __forceinline__ void store_state(const SharedT<CL>& S, GmEnvState* __restrict__ g, int lane) {
-  __syncthreads();
+  GM_ENV_SYNC();
   const uint32_t* src = reinterpret_cast<const uint32_t*>(&S.s);
   uint32_t* dst = reinterpret_cast<uint32_t*>(g);
   for (int i = lane; i < GM_HOT_WORDS; i += NT) dst[i] = src[i];
@@ -2532,7 +2555,7 @@ __device__ __noinline__ void driver_actions(GmEnvHot& s, const gm_model* __restr
 
 // the persistent loop of gm_step_kernel's chunked mode (a mode of the one kernel, not a
 // kernel of its own: substep_loop keeps its single caller and so its constant LDS base)
-template <int CL>
+template <int CL, bool DUO>
 __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __restrict__ states,
                                                   const gm_model* __restrict__ m, const gm_config* __restrict__ C,
                                                   const GmTopo* __restrict__ T, float* __restrict__ obs,
@@ -2642,7 +2665,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       S.work_nefc = cr.work_nefc; S.work_mpr = cr.work_mpr; S.work_newton = cr.work_newton;
       S.stp_fixed = cr.stp_fixed;
     }
-    __syncthreads();
+    GM_ENV_SYNC();
     const uint32_t own = cost[env];
     const int s_nom = C->sim_steps_per_action;
     bool finished = false;
@@ -2654,7 +2677,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
           driver_actions(S.s, m, C, q.act_mode, q.act_seed, q.jitter, q.sr.env_offset + env);
           S.stp_fixed = 0;
         }
-        __syncthreads();
+        GM_ENV_SYNC();
         cr.nsub = C->sim_steps_per_action + S.s.extra_substeps;
       }
       // run to the end of the env-step unless an unstarted env has become the longer job
@@ -2664,7 +2687,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       const int job_total = q.steps > 1 ? q.steps * s_nom : cr.nsub;
       const GmPreempt pre{fresh_head, order, cost, n, own, job_left, job_total,
                           cr.yielded < q.max_yields ? q.chunk : 0, q.margin, bq, cmax, q.cmargin};
-      const int k = substep_loop<CL, false, false>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
+      const int k = substep_loop<CL, false, false, DUO>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
                                             (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
                                             false, left, false, pre);
       cr.sub_done += k;
@@ -2684,9 +2707,9 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
           q.rec[(size_t)cr.step_idx * n + env] = e;
         }
         if (r) {
-          __syncthreads();   // lane 0's epilogue writes (RNG, counters) before every lane reads them
+          GM_ENV_SYNC();   // lane 0's epilogue writes (RNG, counters) before every lane reads them
           const GmResetKeep keep{S.s.rng, S.s.old_x, S.s.old_y, S.s.old_z, S.s.episode + 1, S.s.newton_caps};
-          __syncthreads();   // every lane has read what survives before the image is cleared
+          GM_ENV_SYNC();   // every lane has read what survives before the image is cleared
           static_assert(sizeof(S.st) >= sizeof(uint16_t) * (GM_SPAWN_MAX_XY + GM_SPAWN_MAX_ROT),
                         "spawn search buffers alias the (dead between env-steps) dynamics union");
           uint16_t* sh_pxy = reinterpret_cast<uint16_t*>(&S.st);
@@ -2700,7 +2723,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       if (cr.steps_left <= 0) { finished = true; break; }
       cr.sub_done = 0;
       cr.yielded = 0;
-      __syncthreads();
+      GM_ENV_SYNC();
     }
     if (finished) {
       if (cost && lane == 0) {
@@ -2729,7 +2752,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       // the workgroup barrier orders every lane's state / carry stores before lane 0's
       // release store of the ring entry, which publishes them at agent scope (the consumer's
       // acquire pairs with it)
-      __syncthreads();
+      GM_ENV_SYNC();
       if (lane == 0) {
         const int job_total = q.steps > 1 ? q.steps * s_nom : cr.nsub;
         const int job_left = (cr.steps_left - 1) * s_nom + (cr.nsub - cr.sub_done);
@@ -2742,7 +2765,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
                            __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    __syncthreads();   // LDS image reused by the next pick
+    GM_ENV_SYNC();   // LDS image reused by the next pick
     busy += __builtin_amdgcn_s_memrealtime() - tp;
   }
   if (lane == 0) {
@@ -2755,17 +2778,28 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
 #ifndef GM_WPS
 #define GM_WPS 2   // waves per SIMD the register allocation is held to
 #endif
-template <int CL, bool CAL>
-__global__ __launch_bounds__(NT, GM_WPS) void gm_step_kernel(
+// DUO workgroups (small batches, gm_capi.hip launch_step): the second wave of the
+// workgroup runs each substep's collider for the env the first wave owns, between the two
+// barriers of physics_substep_body, with its own box-box hit slots; duo_cmd = 0 releases it.
+template <int CL>
+__device__ __forceinline__ void duo_helper(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T) {
+  __shared__ real hit[GM_BB_SLOTS][8][4];
+  for (;;) {
+    __syncthreads();
+    if (S.duo_cmd == 0) return;
+    collision<CL>(S, m, T, fresh_lane(), false, hit);
+    __syncthreads();
+  }
+}
+template <int CL, bool CAL, bool DUO>
+__device__ __forceinline__ void step_kernel_body(SharedT<CL>& S,
     GmEnvState* __restrict__ states, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
     const GmTopo* __restrict__ T, float* __restrict__ obs, float* __restrict__ rew,
     uint8_t* __restrict__ done, int n_envs, int mode, DebugOut dbg, const int32_t* __restrict__ order,
-    uint32_t* __restrict__ cost, GmChunkQ q) {
-  __shared__ SharedT<CL> S;
-  const int lane = threadIdx.x;
+    uint32_t* __restrict__ cost, const GmChunkQ& q, int lane) {
   if constexpr (!CAL) {
     if (q.chunk > 0) {   // chunked work queue (gm_step): the grid is the resident wave slots
-      chunked_env_steps<CL>(S, states, m, C, T, obs, rew, done, n_envs, order, cost, q, lane);
+      chunked_env_steps<CL, DUO>(S, states, m, C, T, obs, rew, done, n_envs, order, cost, q, lane);
       return;
     }
   }
@@ -2785,16 +2819,23 @@ __global__ __launch_bounds__(NT, GM_WPS) void gm_step_kernel(
   if (prof && lane == 0) { S.tph[25] = __builtin_amdgcn_s_memrealtime(); S.tph[27] = __smid(); }
   if (lane == 0) { S.work_nefc = 0; S.work_mpr = 0; S.work_newton = 0; S.stp_fixed = 0; }
   const unsigned long long t_kernel = prof ? clock64() : 0;
-  __syncthreads();
+  GM_ENV_SYNC();
   const int nsub = settle ? 400 : calib ? S.s.cal_steps : (mode == 2) ? 1 : C->sim_steps_per_action + S.s.extra_substeps;
   // a calibration run starts from a reset's mj_forward pose
   if (calib && lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
-  const int ran = prof ? substep_loop<CL, CAL, true>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
-                                                     (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
-                                                     prof, nsub, settle, GmPreempt{})
-                       : substep_loop<CL, CAL, false>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
-                                                      (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
-                                                      false, nsub, settle, GmPreempt{});
+  int ran;
+  if constexpr (DUO) {   // (no profiled DUO build: gm_step_profiled launches the one-wave kernel)
+    ran = substep_loop<CL, CAL, false, true>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
+                                             (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
+                                             false, nsub, settle, GmPreempt{});
+  } else {
+    ran = prof ? substep_loop<CL, CAL, true>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
+                                             (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
+                                             prof, nsub, settle, GmPreempt{})
+               : substep_loop<CL, CAL, false>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
+                                              (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
+                                              false, nsub, settle, GmPreempt{});
+  }
   // a calibration run reports the substeps it made (the unstable one included: the loop
   // stops right after it, as the reference's retry resumes after it)
   if (calib && lane == 0) S.s.cal_steps = S.s.badqacc ? ran + 1 : ran;
@@ -2834,7 +2875,7 @@ __global__ __launch_bounds__(NT, GM_WPS) void gm_step_kernel(
       S.tph[23] = clock64() - t_kernel;   // whole env-step on this wave
       S.tph[26] = __builtin_amdgcn_s_memrealtime();
     }
-    __syncthreads();
+    GM_ENV_SYNC();
     if (lane < GM_NPHASE) dbg.phase[(size_t)env * GM_NPHASE + lane] = S.tph[lane];
   }
   if (cost && lane == 0) {
@@ -2850,6 +2891,27 @@ __global__ __launch_bounds__(NT, GM_WPS) void gm_step_kernel(
     cost[n_envs + env] = (now >> 1) + (model >> 1);   // recorded for the next launch's order
   }
   store_state(S, states + env, lane);
+}
+template <int CL, bool CAL, bool DUO = false>
+__global__ __launch_bounds__(DUO ? 2 * NT : NT, GM_WPS) void gm_step_kernel(
+    GmEnvState* __restrict__ states, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
+    const GmTopo* __restrict__ T, float* __restrict__ obs, float* __restrict__ rew,
+    uint8_t* __restrict__ done, int n_envs, int mode, DebugOut dbg, const int32_t* __restrict__ order,
+    uint32_t* __restrict__ cost, GmChunkQ q) {
+  __shared__ SharedT<CL> S;
+  if constexpr (DUO) {
+    static_assert(!CAL, "DUO workgroups run the env-step only");
+    if (threadIdx.x >= NT) {
+      duo_helper<CL>(S, m, T);
+      return;
+    }
+  }
+  step_kernel_body<CL, CAL, DUO>(S, states, m, C, T, obs, rew, done, n_envs, mode, dbg, order, cost, q, (int)threadIdx.x);
+  if constexpr (DUO) {
+    // every path of the owner wave ends here: release the helper
+    if (threadIdx.x == 0) S.duo_cmd = 0;
+    __syncthreads();
+  }
 }
 
 
@@ -3348,7 +3410,7 @@ __device__ __noinline__ void reset_env(GmEnvHot& s, GmEnvState& rec, GmResetKeep
     uint4* w = reinterpret_cast<uint4*>(&rec);
     for (int i = GM_HOT_WORDS / 4 + lane; i < GM_STATE_WORDS / 4; i += 64) w[i] = make_uint4(0u, 0u, 0u, 0u);
   }
-  __syncthreads();
+  GM_ENV_SYNC();
   if (lane == 0) {   // the reference's serial reset on lane 0
     const int32_t episode = keep.episode;
     s.rng = keep.rng; s.old_x = keep.ox; s.old_y = keep.oy; s.old_z = keep.oz;
@@ -3418,7 +3480,7 @@ __device__ __noinline__ void reset_env(GmEnvHot& s, GmEnvState& rec, GmResetKeep
     s.done = 0;
     s.reward = 0;
   }
-  __syncthreads();
+  GM_ENV_SYNC();
 }
 
 // One wave per env (grid = n_envs workgroups of 64; unmasked envs exit at once): the new

@@ -302,6 +302,12 @@ class BatchedGripperEnv:
                     busy=(t[3] / (v[5] * (t[2] - t[0]))) if span and v[5] else 0.0,
                     poll=(t[4] / (v[5] * (t[2] - t[0]))) if span and v[5] else 0.0)
 
+    def dispatch_info(self) -> dict:
+        """How gm_step / gm_rollout dispatch this context (include/gripper_mi355x.h gm_dispatch_info)."""
+        v = (C.c_int32 * 4)()
+        self._check(self.lib.gm_dispatch_info(self._ctx, v))
+        return dict(chunk=v[0], grid=v[1], waves_per_env=v[2])
+
     # ------------------------------------------------------------ inspection
     def state(self):
         """fp64 qpos [n, nq], qvel [n, nv], time [n] (mjData's precision)."""

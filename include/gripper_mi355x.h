@@ -597,6 +597,12 @@ int  gm_last_step_ms(gm_ctx* ctx, float* ms);
  * unstarted env, [2] last env finished, [3] sum of wave-busy time, [4] sum of wave polling.
  * Synchronises the context's stream. */
 int  gm_chunk_stats(gm_ctx* ctx, uint32_t* out6, uint64_t* times5);
+/* How gm_step / gm_rollout dispatch this context (fixed at gm_create): out[0] substeps
+ * between preemption tests (0: the one-shot kernel), out[1] workgroups of the chunked
+ * grid, out[2] waves per env (1; 2 = DUO workgroups, whose second wave runs the collider
+ * concurrently -- chosen when every env's two waves fit resident, GM_DUO=0/1 forces it),
+ * out[3] reserved (0). */
+int  gm_dispatch_info(const gm_ctx* ctx, int32_t* out4);
 
 /* ---- single-substep stage hooks for parity testing (GPU vs oracle) ---- */
 /* Runs exactly one MjClass::step (mj_step1 + control + mj_step2 + mj_rnePostConstraint

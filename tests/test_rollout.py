@@ -20,7 +20,9 @@ N, K, MAX_EP, SEED = 96, 14, 6, 77
 # the hand-off heavy dispatch: a preemption test every substep, no margins, many yields, so
 # envs change waves inside and across the env-steps of the launch (the carry's step index,
 # steps left and per-step counters)
-HANDOFF = {"GM_CHUNK_SUBSTEPS": "1", "GM_CHUNK_MARGIN": "0", "GM_CHUNK_YIELDS": "60", "GM_CHUNK_CMARGIN": "0"}
+# (on 24 workgroups: with a wave slot per env nothing would ever wait in the queue)
+HANDOFF = {"GM_CHUNK_SUBSTEPS": "1", "GM_CHUNK_MARGIN": "0", "GM_CHUNK_YIELDS": "60", "GM_CHUNK_CMARGIN": "0",
+           "GM_CHUNK_GRID": "24"}
 
 
 def make_env(gm, env_vars=None):
@@ -41,10 +43,10 @@ def make_env(gm, env_vars=None):
     return env
 
 
-def per_step(gm, env, mode, records):
+def per_step(gm, env, mode, records, steps=K):
     import torch
     d_act = env.lib.gm_device_actions(env.ctx)
-    for k in range(K):
+    for k in range(steps):
         if mode == 0:
             env.lib.gm_scripted_actions(env.ctx, SEED, 0.2, d_act, 1)
         else:
@@ -77,7 +79,12 @@ def test_rollout_equals_per_step_api(gm, mode, dispatch):
     b = make_env(gm, HANDOFF if dispatch == "handoff-heavy" else None)
     try:
         per_step(gm, a, mode, ra)
-        b.rollout(K, action_mode=mode, seed=SEED, jitter=0.2, max_episode_steps=MAX_EP, records_dev_ptr=rb.data_ptr())
+        # (the hand-off test needs dispatch costs, which a context records from its first
+        # env-step on: b takes that one through the per-step API too)
+        k0 = 1 if dispatch == "handoff-heavy" else 0
+        per_step(gm, b, mode, rb, steps=k0)
+        b.rollout(K - k0, action_mode=mode, seed=SEED, jitter=0.2, max_episode_steps=MAX_EP,
+                  records_dev_ptr=rb[k0:].data_ptr())
         sa, sb = snapshot(a, ra), snapshot(b, rb)
         va, vb = gm.env_state_view(sa[1]), gm.env_state_view(sb[1])
         for f in va.dtype.names:

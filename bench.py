@@ -79,14 +79,15 @@ def mjenv_spawn_params(gmx):
     return p
 
 
-def load_traffic(n_envs: int):
-    """HBM bytes per launch of gm_step_kernel from the committed rocprofv3 PMC pass
-    (profiles/*pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950 guide)."""
+def load_traffic(n_envs: int, steps_per_launch: int):
+    """HBM bytes per launch of gm_step_kernel from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950 guide), for the
+    same batch and the same env-steps per launch as this run's timed launches."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        if int(d.get("n_envs", -1)) == n_envs:
+        if int(d.get("n_envs", -1)) == n_envs and int(d.get("env_steps_per_launch", 1)) == steps_per_launch:
             return float(d["bytes_per_launch"]), d.get("source")
     except (OSError, ValueError, KeyError):
         pass
@@ -555,7 +556,7 @@ def main():
         Bm = algorithmic_bytes_per_substep(env.model, ncon=int(round(float(ncon_m.mean()))))
         bytes_per_launch = n * S * B["bytes"]
         achieved = bytes_per_launch / kern_avg_s / 1e9
-        traffic, traffic_src = load_traffic(n)
+        traffic, traffic_src = load_traffic(n, R)
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "kernel": "gm_step_kernel", "kernel_avg_ms": round(kern_avg_s * 1e3, 4),

@@ -424,8 +424,8 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
     c->chunk_cap = n_envs + c->chunk_grid;
     HIPCHK(c, hipMalloc(&c->d_chunk_ctr, sizeof(uint32_t) * GM_CQ_ALLOC));
     HIPCHK(c, hipMemsetAsync(c->d_chunk_ctr, 0, sizeof(uint32_t) * GM_CQ_ALLOC, c->stream));
-    HIPCHK(c, hipMalloc(&c->d_chunk_st, sizeof(unsigned long long) * 16));
-    HIPCHK(c, hipMemsetAsync(c->d_chunk_st, 0, sizeof(unsigned long long) * 16, c->stream));
+    HIPCHK(c, hipMalloc(&c->d_chunk_st, sizeof(unsigned long long) * (16 + (size_t)c->chunk_grid)));
+    HIPCHK(c, hipMemsetAsync(c->d_chunk_st, 0, sizeof(unsigned long long) * (16 + (size_t)c->chunk_grid), c->stream));
     HIPCHK(c, hipMalloc(&c->d_chunk_ring, sizeof(uint64_t) * 8 * GM_CQ_NB * (size_t)c->chunk_cap));
     HIPCHK(c, hipMalloc(&c->d_chunk_carry, sizeof(GmChunkCarry) * (size_t)n_envs));
     HIPCHK(c, hipMemsetAsync(c->d_chunk_ring, 0, sizeof(uint64_t) * 8 * GM_CQ_NB * (size_t)c->chunk_cap, c->stream));
@@ -953,6 +953,15 @@ int gm_chunk_stats(gm_ctx* c, uint32_t* out, uint64_t* times) {
   out[1] = w[32]; out[2] = w[33]; out[3] = w[34];
   out[4] = (uint32_t)c->chunk; out[5] = (uint32_t)c->chunk_grid;
   return GM_OK;
+}
+
+int gm_chunk_timeline(gm_ctx* c, uint64_t* out, int max_out) {
+  if (!c || !out || max_out < 0) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  const int n = std::min(max_out, c->chunk_grid);
+  HIPCHK(c, hipMemcpyAsync(out, c->d_chunk_st + 16, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return n;
 }
 
 int gm_dispatch_info(const gm_ctx* c, int32_t* out) {

@@ -2497,7 +2497,8 @@ struct GmChunkQ {
   int cmargin;               // yield to a yielded env with cmargin percent more work left (< 0: off)
   unsigned long long* st;    // [0] first pick, [1] first pick that found no unstarted env,
                              // [2] last env finished (100 MHz clock), [3] wave-busy, [4] wave
-                             // polling (sums, 100 MHz ticks); [8 ..] the previous launch's
+                             // polling (sums, 100 MHz ticks); [8 ..] the previous launch's;
+                             // [16 + w] workgroup w's exit time
   // rollout (gm_rollout; act_mode < 0: one plain env-step per env, gm_step): each env runs
   // `steps` env-steps in a row, every one of them the per-step API's sequence -- driver actions
   // (gm_scripted_actions / gm_random_actions) -> set_continous_action -> action_step + obs /
@@ -2771,6 +2772,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
   if (lane == 0) {
     __hip_atomic_fetch_add(q.st + 3, busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(q.st + 4, poll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st_agent(reinterpret_cast<uint64_t*>(q.st) + 16 + blockIdx.x, __builtin_amdgcn_s_memrealtime());   // this workgroup's exit (gm_chunk_timeline)
   }
 }
 // mode 0: action_step + obs/done/reward; mode 1: calibrate_reset settle (400 substeps,

@@ -302,6 +302,19 @@ class BatchedGripperEnv:
                     busy=(t[3] / (v[5] * (t[2] - t[0]))) if span and v[5] else 0.0,
                     poll=(t[4] / (v[5] * (t[2] - t[0]))) if span and v[5] else 0.0)
 
+    def chunk_timeline(self):
+        """The last chunked launch's workgroup exit times, ms after its first pick (gm_chunk_timeline)."""
+        import numpy as np
+        info = self.dispatch_info()
+        buf = (C.c_uint64 * max(1, info["grid"]))()
+        n = self.lib.gm_chunk_timeline(self._ctx, buf, info["grid"])
+        if n < 0:
+            raise RuntimeError(f"gm_chunk_timeline failed ({n})")
+        t = (C.c_uint64 * 5)()
+        v = (C.c_uint32 * 6)()
+        self._check(self.lib.gm_chunk_stats(self._ctx, v, t))
+        return (np.frombuffer(buf, dtype=np.uint64, count=n).astype(np.float64) - float(t[0])) * 1e-5
+
     def dispatch_info(self) -> dict:
         """How gm_step / gm_rollout dispatch this context (include/gripper_mi355x.h gm_dispatch_info)."""
         v = (C.c_int32 * 4)()

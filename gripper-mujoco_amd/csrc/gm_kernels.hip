@@ -1424,8 +1424,16 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
   GM_WAVE_SYNC();
 }
 
+// DUO workgroups: the helper wave's euler_factor results, lane-major ([j][64]: L[1..CL], lb,
+// 1 / d), then the base pivot's Schur sum
+template <int CL>
+__device__ __forceinline__ real* duo_ef() {
+  __shared__ real ef[64 * (CL + 2) + 1];
+  return ef;
+}
+
 // ============================================================ integrate
-template <int CL, bool CAL>
+template <int CL, bool CAL, bool DUO = false>
 __device__ __forceinline__ void integrate(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane) {
   const real h = CAL ? S.s.dt : m->timestep;
   if constexpr (CAL) {
@@ -1437,7 +1445,21 @@ __device__ __forceinline__ void integrate(SharedT<CL>& S, const gm_model* __rest
   // mj_Euler: under MuJoCo's actuator order the joint damping is implicit here
   // (euler_damping: qacc_e = (M + h D)^-1 (qfrc_smooth + qfrc_constraint) into S.xs)
   const bool mj = m->mujoco_actuators != 0;
-  if (mj) euler_damping<CL>(S, T, h, fresh_lane());
+  if constexpr (DUO) {
+    // the helper factored M + h D during the constraint solve (duo_helper); third barrier
+    __syncthreads();
+    if (mj) {
+      const int ln = fresh_lane();
+      const real* ef = duo_ef<CL>();
+      real L[CL + 1];
+      L[0] = 0.0;
+#pragma unroll
+      for (int j = 1; j <= CL; j++) L[j] = ef[(j - 1) * 64 + ln];
+      euler_solve<CL>(S, T, h, ln, L, ef[CL * 64 + ln], ef[(CL + 1) * 64 + ln], ef[64 * (CL + 2)]);
+    }
+  } else {
+    if (mj) euler_damping<CL>(S, T, h, fresh_lane());
+  }
   if (lane < T->nv) S.s.qvel[lane] += h * (mj ? S.xs[lane] : S.qacc[lane]);
   GM_WAVE_SYNC();
   if (lane < T->nv && lane < T->dof_obj) {
@@ -1471,6 +1493,8 @@ using gmf::mass_and_forces;
 using gmf::collision;
 using gmf::newton_solve;
 using gmf::integrate;
+using gmf::euler_factor;
+using gmf::duo_ef;
 
 // ============================================================ reference scalar logic (lane 0)
 // luke::Gripper in fp64 (gripper.cpp), bit-for-bit the same operations as the reference
@@ -1925,7 +1949,7 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
   PH(5);
   newton_solve<CL, CAL>(S, m, T, fresh_lane(), prof);
   PH(6);
-  integrate<CL, CAL>(S, m, T, fresh_lane());
+  integrate<CL, CAL, DUO>(S, m, T, fresh_lane());
   PH(8);
 }
 
@@ -2781,8 +2805,10 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
 #define GM_WPS 2   // waves per SIMD the register allocation is held to
 #endif
 // DUO workgroups (small batches, gm_capi.hip launch_step): the second wave of the
-// workgroup runs each substep's collider for the env the first wave owns, between the two
-// barriers of physics_substep_body, with its own box-box hit slots; duo_cmd = 0 releases it.
+// workgroup runs each substep's collider for the env the first wave owns, between the
+// first two barriers of physics_substep_body, with its own box-box hit slots, then the
+// factor of integrate's Euler damping solve while the owner runs the constraint solve
+// (third barrier, in integrate); duo_cmd = 0 releases it.
 template <int CL>
 __device__ __forceinline__ void duo_helper(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T) {
   __shared__ real hit[GM_BB_SLOTS][8][4];
@@ -2790,6 +2816,20 @@ __device__ __forceinline__ void duo_helper(SharedT<CL>& S, const gm_model* __res
     __syncthreads();
     if (S.duo_cmd == 0) return;
     collision<CL>(S, m, T, fresh_lane(), false, hit);
+    __syncthreads();
+    // M is formed (the owner wave's mass_and_forces ran before the barrier): the Euler
+    // damping factor for integrate, while the owner runs the constraint solve
+    if (m->mujoco_actuators != 0) {
+      const int ln = fresh_lane();
+      real L[CL + 1], lb, invd;
+      const real sch = euler_factor<CL>(S, T, m->timestep, ln, L, lb, invd);
+      real* ef = duo_ef<CL>();
+#pragma unroll
+      for (int j = 1; j <= CL; j++) ef[(j - 1) * 64 + ln] = L[j];
+      ef[CL * 64 + ln] = lb;
+      ef[(CL + 1) * 64 + ln] = invd;
+      if (ln == 0) ef[64 * (CL + 2)] = sch;
+    }
     __syncthreads();
   }
 }

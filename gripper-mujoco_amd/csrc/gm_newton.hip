@@ -1397,13 +1397,18 @@ __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __r
 // back as scalars, so the base solve is computed wave-uniformly.  The object has no damping
 // and no coupling to the gripper in M: its rows take no correction.  qacc_e goes to S.xs
 // (free after the solve); oracle/physics.c euler_damping restates it lane for lane.
+// The factor half: L (chain rows, scaled), lb (the base column, scaled), 1 / d on the pivot
+// lanes, and the base pivot's Schur sum (returned, wave-uniform).  It reads only M's blocks
+// (mass_and_forces) and the damping, so a DUO workgroup's helper wave runs it during the
+// constraint solve (duo_helper) and hands it over in LDS; the one-wave kernel keeps it in
+// registers.  The same operations either way.
 template <int CL>
-__device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __restrict__ T, real h, int lane) {
+__device__ __forceinline__ real euler_factor(const SharedT<CL>& S, const GmTopo* __restrict__ T, real h, int lane,
+                                             real (&L)[CL + 1], real& lb, real& invd) {
   const int rowf = lane >> 4, p = lane & 15;
   const bool chainrow = rowf < 3 && p >= 1 && p <= CL;
   const bool palm = lane == GM_LANE_PALM_F;
-  const bool res = S.res_valid != 0;   // a capped solve's residual in S.Mv (newton_solve)
-  real L[CL + 1], lb = 0.0, y = 0.0;
+  lb = 0.0;
 #pragma unroll
   for (int j = 0; j <= CL; j++) L[j] = 0.0;
   if (chainrow) {
@@ -1422,22 +1427,14 @@ __device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __re
 #pragma unroll
     for (int j = 1; j <= CL; j++) L[j] = (j == p) ? L[j] + hd : L[j];
     lb = H[TRI(p, 0)];
-    y = hd * S.qacc[d];
-    if (res) y = y + S.Mv[d];
   } else if (palm) {
     const int d = T->dof_palm;
     const real hd = h * T->dof_damp[d];
     L[1] = S.Hp[TRI(1, 1)] + hd;
     lb = S.Hp[TRI(1, 0)];
-    y = hd * S.qacc[d];
-    if (res) y = y + S.Mv[d];
   }
-  // the base row (wave-uniform: one scalar dof)
-  const int db = T->dof_base;
-  const real hdb = h * T->dof_damp[db];
-  const real bb = S.Hbb + hdb;
-  const real yb0 = res ? hdb * S.qacc[db] + S.Mv[db] : hdb * S.qacc[db];
-  real invd = 1.0, ub = 0.0;
+  invd = 1.0;
+  real ub = 0.0;
   if (lane < 48) {
 #pragma unroll
     for (int k = CL; k >= 1; k--) {
@@ -1462,6 +1459,50 @@ __device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __re
 #pragma unroll
     for (int j = 1; j < CL; j++) L[j] = (j < p) ? L[j] * invd : L[j];
     lb = lb * invd;
+  } else if (palm) {
+    const real ih = rcp_n(L[1]);
+    ub = lb;
+    lb = lb * ih;
+    invd = ih;
+  }
+  // the base pivot's Schur sum: per DPP row an inclusive scan of lb ub (lane 15 of the row
+  // holds the row total; lanes outside the chain hold zeros), then rows 0, 1, 2 and the palm
+  const bool part = chainrow || palm;
+  real s1 = part ? lb * ub : 0.0;
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) {
+    const real t1 = row_shr(s1, off);
+    s1 += t1;
+  }
+  return ((readlane_real(s1, 15) + readlane_real(s1, 31)) + readlane_real(s1, 47)) + readlane_real(s1, 56);
+}
+
+// The solve half: qacc_e = qacc - (M + h D)^-1 (h D qacc [- r on a capped solve]) into S.xs.
+template <int CL>
+__device__ __forceinline__ void euler_solve(SharedT<CL>& S, const GmTopo* __restrict__ T, real h, int lane,
+                                            const real (&L)[CL + 1], real lb, real invd, real sch) {
+  const int rowf = lane >> 4, p = lane & 15;
+  const bool chainrow = rowf < 3 && p >= 1 && p <= CL;
+  const bool palm = lane == GM_LANE_PALM_F;
+  const bool res = S.res_valid != 0;   // a capped solve's residual in S.Mv (newton_solve)
+  real y = 0.0;
+  if (chainrow) {
+    const int d = T->dof_f0[rowf] + p - 1;
+    const real hd = h * T->dof_damp[d];
+    y = hd * S.qacc[d];
+    if (res) y = y + S.Mv[d];
+  } else if (palm) {
+    const int d = T->dof_palm;
+    const real hd = h * T->dof_damp[d];
+    y = hd * S.qacc[d];
+    if (res) y = y + S.Mv[d];
+  }
+  // the base row (wave-uniform: one scalar dof)
+  const int db = T->dof_base;
+  const real hdb = h * T->dof_damp[db];
+  const real bb = S.Hbb + hdb;
+  const real yb0 = res ? hdb * S.qacc[db] + S.Mv[db] : hdb * S.qacc[db];
+  if (lane < 48) {
     // forward over the chains, leaf first
 #pragma unroll
     for (int k = CL; k >= 1; k--) {
@@ -1469,23 +1510,15 @@ __device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __re
       const real Lc = (p >= 1 && p < k) ? L[k] : 0.0;
       y = y - Lc * yk;
     }
-  } else if (palm) {
-    const real ih = rcp_n(L[1]);
-    ub = lb;
-    lb = lb * ih;
-    invd = ih;
   }
-  // base sums: per DPP row an inclusive scan of (lb ub, lb y) (lane 15 of the row holds the
-  // row total; lanes outside the chain hold zeros), then rows 0, 1, 2 and the palm in order
+  // the base pivot's forward sum, as the Schur sum (euler_factor)
   const bool part = chainrow || palm;
-  real s1 = part ? lb * ub : 0.0, s2 = part ? lb * y : 0.0;
+  real s2 = part ? lb * y : 0.0;
 #pragma unroll
   for (int off = 1; off < 16; off <<= 1) {
-    const real t1 = row_shr(s1, off), t2 = row_shr(s2, off);
-    s1 += t1;
+    const real t2 = row_shr(s2, off);
     s2 += t2;
   }
-  const real sch = ((readlane_real(s1, 15) + readlane_real(s1, 31)) + readlane_real(s1, 47)) + readlane_real(s1, 56);
   const real fs = ((readlane_real(s2, 15) + readlane_real(s2, 31)) + readlane_real(s2, 47)) + readlane_real(s2, 56);
   const real xb = (yb0 - fs) * rcp_n(bb - sch);
   // back substitution: D^-1, the border column, then the chains root -> leaf
@@ -1511,4 +1544,11 @@ __device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __re
     S.xs[d] = res ? S.qacc[d] - S.Mv[d] : S.qacc[d];
   }
   GM_WAVE_SYNC();
+}
+
+template <int CL>
+__device__ __forceinline__ void euler_damping(SharedT<CL>& S, const GmTopo* __restrict__ T, real h, int lane) {
+  real L[CL + 1], lb, invd;
+  const real sch = euler_factor<CL>(S, T, h, lane, L, lb, invd);
+  euler_solve<CL>(S, T, h, lane, L, lb, invd, sch);
 }

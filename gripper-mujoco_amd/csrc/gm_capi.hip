@@ -53,6 +53,11 @@ struct gm_ctx {
   float* d_rew = nullptr;
   uint8_t* d_done = nullptr;
   float* d_act = nullptr;
+  // host actions are staged through a pinned buffer so gm_set_action / gm_set_discrete_action
+  // return without a stream synchronisation (stage_ev: the previous staging copy is done)
+  void* h_stage = nullptr;
+  size_t stage_bytes = 0;
+  hipEvent_t stage_ev = nullptr;
   int32_t* d_dact = nullptr;
   uint8_t* d_mask = nullptr;
   gm_spawn* d_spawn = nullptr;
@@ -371,6 +376,9 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   c->stream = c->own_stream;
   HIPCHK(c, hipEventCreate(&c->ev0));
   HIPCHK(c, hipEventCreate(&c->ev1));
+  HIPCHK(c, hipEventCreateWithFlags(&c->stage_ev, hipEventDisableTiming));
+  c->stage_bytes = std::max(sizeof(float) * (size_t)n_envs * GM_ACTION_CODE_COUNT, sizeof(int32_t) * (size_t)n_envs);
+  HIPCHK(c, hipHostMalloc(&c->h_stage, c->stage_bytes, hipHostMallocDefault));
   HIPCHK(c, hipMalloc(&c->d_state, sizeof(GmEnvState) * (size_t)n_envs));
   HIPCHK(c, hipMalloc(&c->d_model, sizeof(gm_model)));
   HIPCHK(c, hipMalloc(&c->d_cfg, sizeof(gm_config)));
@@ -482,6 +490,8 @@ void gm_destroy(gm_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   (void)hipFree(c->d_state); (void)hipFree(c->d_model); (void)hipFree(c->d_cfg); (void)hipFree(c->d_topo); (void)hipFree(c->d_objs);
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
+  if (c->stage_ev) (void)hipEventDestroy(c->stage_ev);
   (void)hipFree(c->d_eq); (void)hipFree(c->d_obs); (void)hipFree(c->d_rew); (void)hipFree(c->d_done); (void)hipFree(c->d_act);
   (void)hipFree(c->d_dact); (void)hipFree(c->d_mask); (void)hipFree(c->d_spawn);
   (void)hipFree(c->d_order); (void)hipFree(c->d_cost); (void)hipFree(c->d_scene);
@@ -585,15 +595,17 @@ int gm_set_action(gm_ctx* c, const float* actions, int on_device) {
   HIPCHK(c, hipSetDevice(c->device));
   const float* da = actions;
   if (!on_device) {
-    HIPCHK(c, hipMemcpyAsync(c->d_act, actions, sizeof(float) * (size_t)c->n_envs * c->cfg.n_actions,
-                             hipMemcpyHostToDevice, c->stream));
+    const size_t bytes = sizeof(float) * (size_t)c->n_envs * c->cfg.n_actions;
+    HIPCHK(c, hipEventSynchronize(c->stage_ev));   // the last staging copy has left the buffer
+    std::memcpy(c->h_stage, actions, bytes);
+    HIPCHK(c, hipMemcpyAsync(c->d_act, c->h_stage, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipEventRecord(c->stage_ev, c->stream));
     da = c->d_act;
   }
   int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
   hipLaunchKernelGGL(gm_action_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
                      da, (const int32_t*)nullptr, c->n_envs);
   HIPCHK(c, hipGetLastError());
-  if (!on_device) HIPCHK(c, hipStreamSynchronize(c->stream));
   return GM_OK;
 }
 
@@ -602,14 +614,17 @@ int gm_set_discrete_action(gm_ctx* c, const int32_t* actions, int on_device) {
   HIPCHK(c, hipSetDevice(c->device));
   const int32_t* da = actions;
   if (!on_device) {
-    HIPCHK(c, hipMemcpyAsync(c->d_dact, actions, sizeof(int32_t) * (size_t)c->n_envs, hipMemcpyHostToDevice, c->stream));
+    const size_t bytes = sizeof(int32_t) * (size_t)c->n_envs;
+    HIPCHK(c, hipEventSynchronize(c->stage_ev));
+    std::memcpy(c->h_stage, actions, bytes);
+    HIPCHK(c, hipMemcpyAsync(c->d_dact, c->h_stage, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipEventRecord(c->stage_ev, c->stream));
     da = c->d_dact;
   }
   int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
   hipLaunchKernelGGL(gm_action_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model, c->d_cfg,
                      (const float*)nullptr, da, c->n_envs);
   HIPCHK(c, hipGetLastError());
-  if (!on_device) HIPCHK(c, hipStreamSynchronize(c->stream));
   return GM_OK;
 }
 

@@ -156,6 +156,7 @@ class MjClass:
             self._env = None
 
     def _ensure(self):
+        self._rd = None              # any call that may change the env drops the cached reward / done
         if self._env is None:
             model_params = self._params
             self._env = gmx.BatchedGripperEnv(1, object_set=self.object_set_name, settings=self.set,
@@ -256,17 +257,25 @@ class MjClass:
     def get_observation(self):
         return self.get_observation_numpy().tolist()
 
+    def _reward_done(self):
+        """(reward, done) of the current transition, one device read per transition:
+        MjEnv.step asks is_done() then reward() (MjEnv.py:616-637) with nothing in between."""
+        rd = getattr(self, "_rd", None)
+        if rd is None:
+            env = self._ensure()
+            r, d = env.reward_done()
+            rd = self._rd = (float(r[0]), bool(d[0]))
+        return rd
+
     def is_done(self) -> bool:
-        _, d = self._ensure().reward_done()
-        return bool(d[0])
+        return self._reward_done()[1]
 
     def reward(self, event: "EventTrack | None" = None) -> float:
         """MjClass::reward (mjclass.cpp:3000-3049): the current transition's reward; with
         an EventTrack, calc_rewards over that track (mjclass.cpp:5471-5528: binary
         reward if row >= trigger, linear reward x linear_reward(last_value) likewise)."""
         if event is None:
-            r, _ = self._ensure().reward_done()
-            return float(r[0])
+            return self._reward_done()[0]
         st = self.set
         r = np.float32(0.0)
         for n in BINARY_EVENTS:

@@ -496,7 +496,9 @@ int  gm_random_actions(gm_ctx* ctx, uint64_t seed, float* out, int on_device);
 
 /* MjClass::set_continous_action for every action index i in order
  * (mjclass.cpp:1517-1630; called per index by MjEnv._set_action, MjEnv.py:591-594).
- * actions: [n_envs x n_actions] float32. */
+ * actions: [n_envs x n_actions] float32.  Host actions are copied into a pinned staging
+ * buffer before the call returns (the caller may reuse its array at once); the upload and
+ * the action kernel run asynchronously on the context's stream. */
 int  gm_set_action(gm_ctx* ctx, const float* actions, int on_device);
 /* MjClass::set_discrete_action (mjclass.cpp:1510-1515). actions: [n_envs] int32. */
 int  gm_set_discrete_action(gm_ctx* ctx, const int32_t* actions, int on_device);

@@ -4,7 +4,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${1:-duo}; mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest $R/tests/test_duo.py $R/tests/test_rollout.py $R/tests/test_grasp_parity.py -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|assert" $OUT/tests.log | head -30; tail -5 $OUT/tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest $R/tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|assert" $OUT/tests.log | head -30; tail -5 $OUT/tests.log; exit 1; }
 tail -2 $OUT/tests.log
 timeout -k 10 300 env GM_DUO=0 python -u $R/bench.py --no-cpu --no-parity --no-policy --no-random > $OUT/bench_one.json 2> $OUT/bench_one.err || { echo "bench one failed"; tail -20 $OUT/bench_one.err; exit 1; }
 timeout -k 10 300 python -u $R/bench.py --no-cpu --no-parity --no-policy --no-random > $OUT/bench_duo.json 2> $OUT/bench_duo.err || { echo "bench duo failed"; tail -20 $OUT/bench_duo.err; exit 1; }

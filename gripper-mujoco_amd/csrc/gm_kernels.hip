@@ -157,7 +157,6 @@ struct __align__(16) SharedT {
   int32_t ncon, nefc, nl, overflow;
   int32_t res_valid;              // newton_solve: a capped solve's residual sits in Mv (euler_damping)
   int32_t duo_cmd;                // DUO workgroups: 1 = the helper wave runs this substep's collider, 0 = exit
-  int32_t duo_coll_done;          // DUO: the helper has finished this substep's collider (a hint, see there)
   int32_t work_nefc, work_mpr, work_newton;   // this env-step's rows / MPR substeps / Newton iterations
   int32_t stp_fixed;              // update_all: `next` is a fixed point of the stepper this env-step (see there)
   float forces[32];            // extract_forces_faster results (see extract_forces)
@@ -1496,7 +1495,6 @@ using gmf::newton_solve;
 using gmf::integrate;
 using gmf::euler_factor;
 using gmf::duo_ef;
-using gmf::body_vel_qv_qw;
 
 // ============================================================ reference scalar logic (lane 0)
 // luke::Gripper in fp64 (gripper.cpp), bit-for-bit the same operations as the reference
@@ -1931,22 +1929,15 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
   if (lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
   kinematics<CL>(S, m, T, fresh_lane(), prof);
   PH(0);
-  bool vel_done = false;
   if constexpr (DUO) {
     // the collider needs only the poses: the helper wave runs it (duo_helper) while this
     // wave forms the inertia and forces; the two barriers are the handshake
-    if (lane == 0) { S.duo_cmd = 1; S.duo_coll_done = 0; }
+    if (lane == 0) S.duo_cmd = 1;
     __syncthreads();
     crb_rne<CL, CAL>(S, m, T, fresh_lane(), prof);
     PH(1);
     mass_and_forces<CL, CAL>(S, m, T, fresh_lane());
     PH(2);
-    // still waiting for the collider: form the constraint setup's body velocities now (all
-    // of them; with the collider done first, the setup forms them itself and may skip the
-    // chains when only the object touches the ground).  Either way the same values: the
-    // flag only picks who computes them.
-    vel_done = __builtin_amdgcn_readfirstlane(__atomic_load_n(&S.duo_coll_done, __ATOMIC_RELAXED)) == 0;
-    if (vel_done) body_vel_qv_qw<CL>(S, m, T, fresh_lane(), false);
     __syncthreads();
   } else {
     crb_rne<CL, CAL>(S, m, T, fresh_lane(), prof);
@@ -1956,7 +1947,7 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
     collision(S, m, T, fresh_lane(), prof, S.cl.hit);
   }
   PH(5);
-  newton_solve<CL, CAL>(S, m, T, fresh_lane(), prof, vel_done);
+  newton_solve<CL, CAL>(S, m, T, fresh_lane(), prof);
   PH(6);
   integrate<CL, CAL, DUO>(S, m, T, fresh_lane());
   PH(8);
@@ -2825,7 +2816,6 @@ __device__ __forceinline__ void duo_helper(SharedT<CL>& S, const gm_model* __res
     __syncthreads();
     if (S.duo_cmd == 0) return;
     collision<CL>(S, m, T, fresh_lane(), false, hit);
-    if (fresh_lane() == 0) __atomic_store_n(&S.duo_coll_done, 1, __ATOMIC_RELAXED);
     __syncthreads();
     // M is formed (the owner wave's mass_and_forces ran before the barrier): the Euler
     // damping factor for integrate, while the owner runs the constraint solve

@@ -355,15 +355,6 @@ __device__ void body_vel(SharedT<CL>& S, const real* const* v, real (*const* V)[
   GM_WAVE_SYNC();
 }
 
-// the constraint setup's two: qvel -> nw2.V, the warm start -> nw2.V2
-template <int CL>
-__device__ __forceinline__ void body_vel_qv_qw(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
-                                               int lane, bool obj_only) {
-  const real* vv[2] = {S.s.qvel, S.s.qacc_warm};
-  real (*VV[2])[6] = {S.nw2.V, S.nw2.V2};
-  body_vel<CL, 2>(S, vv, VV, m, T, lane, obj_only);
-}
-
 // J v of contact c's 4 pyramid edges from the body velocities V (n + mu t1, n - mu t1,
 // n + mu t2, n - mu t2)
 template <int CL>
@@ -547,8 +538,7 @@ __device__ __forceinline__ void lock_rows(SharedT<CL>& S, const gm_model* __rest
 // tran + mu^2 tran, tran = the two bodies' invweight0), reference accelerations
 template <int CL, bool CAL>
 __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
-                                 int lane, RowsT& R, real* jq, real& jql, bool& obj_only, bool prof = false,
-                                 bool vel_done = false) {
+                                 int lane, RowsT& R, real* jq, real& jql, bool& obj_only, bool prof = false) {
   unsigned long long t0 = prof ? clock64() : 0;
   (void)t0;
   const real h = CAL ? S.s.dt : m->timestep;
@@ -567,16 +557,17 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
   PH(15);   // developer split: lock rows
 #endif
   // body velocities at qvel (reference accelerations) and at the warm start (the first
-  // iterate's J q - aref), one fused pass (vel_done: a DUO owner wave formed them, all of
-  // them, while its helper was still in the collider -- the same values)
+  // iterate's J q - aref), one fused pass
   {
+    const real* vv[2] = {S.s.qvel, S.s.qacc_warm};
+    real (*VV[2])[6] = {S.nw2.V, S.nw2.V2};
     bool og = true;
     if (lane < S.ncon) {
       const int b1 = S.cbody[lane][0], b2 = S.cbody[lane][1];
       og = (b1 == 0 && b2 == T->body_obj) || (b2 == 0 && b1 == T->body_obj);
     }
     obj_only = __ballot(!og) == 0ull;
-    if (!vel_done) body_vel_qv_qw<CL>(S, m, T, lane, obj_only);
+    body_vel<CL, 2>(S, vv, VV, m, T, lane, obj_only);
   }
 #ifdef GM_PHASE_SPLIT_SETUP
   PH(16);   // developer split: the two velocity scans
@@ -1228,12 +1219,12 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
 // an exact line search along x - q; contact forces and the warm start at the end.
 template <int CL, bool CAL>
 __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
-                             bool prof, bool vel_done = false) {
+                             bool prof) {
   unsigned long long t0 = prof ? clock64() : 0;
   RowsT R;
   real jq[4], jql;
   bool obj_only;
-  constraint_setup<CL, CAL>(S, m, T, lane, R, jq, jql, obj_only, prof, vel_done);
+  constraint_setup<CL, CAL>(S, m, T, lane, R, jq, jql, obj_only, prof);
 #ifdef GM_PHASE_SPLIT_SETUP
   if (prof) t0 = clock64();   // the split phases above were charged inside; the rest: contact rows
 #endif

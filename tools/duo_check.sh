@@ -8,7 +8,6 @@ timeout -k 10 600 python -u -m pytest $R/tests -m gpu -x -v --timeout 300 --time
 tail -2 $OUT/tests.log
 timeout -k 10 300 env GM_DUO=0 python -u $R/bench.py --no-cpu --no-parity --no-policy --no-random > $OUT/bench_one.json 2> $OUT/bench_one.err || { echo "bench one failed"; tail -20 $OUT/bench_one.err; exit 1; }
 timeout -k 10 300 python -u $R/bench.py --no-cpu --no-parity --no-policy --no-random > $OUT/bench_duo.json 2> $OUT/bench_duo.err || { echo "bench duo failed"; tail -20 $OUT/bench_duo.err; exit 1; }
-timeout -k 10 300 env GM_DUO=1 python -u $R/bench.py --no-cpu --no-parity --no-policy --no-random --no-c2 --no-c1 > $OUT/bench_duo4096.json 2> $OUT/bench_duo4096.err || { echo "bench duo 4096 failed"; tail -20 $OUT/bench_duo4096.err; exit 1; }
 timeout -k 10 200 python -u $R/tools/tail_timeline.py 4096 10 > $OUT/t4096.txt 2>&1 || { tail -5 $OUT/t4096.txt; exit 1; }
 timeout -k 10 200 python -u $R/tools/tail_timeline.py 8192 10 > $OUT/t8192.txt 2>&1 || { tail -5 $OUT/t8192.txt; exit 1; }
 grep "n=" $OUT/t*.txt

@@ -2522,7 +2522,7 @@ struct GmChunkQ {
   unsigned long long* st;    // [0] first pick, [1] first pick that found no unstarted env,
                              // [2] last env finished (100 MHz clock), [3] wave-busy, [4] wave
                              // polling (sums, 100 MHz ticks); [8 ..] the previous launch's;
-                             // [16 + w] workgroup w's exit time
+                             // [16 + w] when workgroup w finished its last piece of work
   // rollout (gm_rollout; act_mode < 0: one plain env-step per env, gm_step): each env runs
   // `steps` env-steps in a row, every one of them the per-step API's sequence -- driver actions
   // (gm_scripted_actions / gm_random_actions) -> set_continous_action -> action_step + obs /
@@ -2598,7 +2598,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
   // bucket scale: the heaviest env's last cost + 1, snapshot by gm_dispatch_order_kernel, so
   // every wave of the launch buckets alike (costs of this launch go to the second half)
   const uint32_t cmax = q.ctr[GM_CQ_CMAX];
-  unsigned long long busy = 0, poll = 0;
+  unsigned long long busy = 0, poll = 0, last_end = 0;
   bool first = true, saw_empty = false;
   for (;;) {
     const unsigned long long tw = __builtin_amdgcn_s_memrealtime();
@@ -2791,12 +2791,13 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       }
     }
     GM_ENV_SYNC();   // LDS image reused by the next pick
-    busy += __builtin_amdgcn_s_memrealtime() - tp;
+    last_end = __builtin_amdgcn_s_memrealtime();
+    busy += last_end - tp;
   }
   if (lane == 0) {
     __hip_atomic_fetch_add(q.st + 3, busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(q.st + 4, poll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    st_agent(reinterpret_cast<uint64_t*>(q.st) + 16 + blockIdx.x, __builtin_amdgcn_s_memrealtime());   // this workgroup's exit (gm_chunk_timeline)
+    st_agent(reinterpret_cast<uint64_t*>(q.st) + 16 + blockIdx.x, last_end);   // this workgroup's last work (gm_chunk_timeline)
   }
 }
 // mode 0: action_step + obs/done/reward; mode 1: calibrate_reset settle (400 substeps,

@@ -303,7 +303,8 @@ class BatchedGripperEnv:
                     poll=(t[4] / (v[5] * (t[2] - t[0]))) if span and v[5] else 0.0)
 
     def chunk_timeline(self):
-        """The last chunked launch's workgroup exit times, ms after its first pick (gm_chunk_timeline)."""
+        """When each workgroup of the last chunked launch finished its last work, ms after the
+        launch's first pick (gm_chunk_timeline)."""
         import numpy as np
         info = self.dispatch_info()
         buf = (C.c_uint64 * max(1, info["grid"]))()

@@ -605,8 +605,9 @@ int  gm_chunk_stats(gm_ctx* ctx, uint32_t* out6, uint64_t* times5);
  * concurrently -- chosen when every env's two waves fit resident, GM_DUO=0/1 forces it),
  * out[3] reserved (0). */
 int  gm_dispatch_info(const gm_ctx* ctx, int32_t* out4);
-/* The last chunked launch's per-workgroup exit times (100 MHz constant clock, the clock of
- * gm_chunk_stats' times): out[w] for workgroup w < min(max_out, out[1] of
+/* The last chunked launch's per-workgroup end of work: when workgroup w finished the last
+ * env (or env chunk) it ran, before it polled out the rest of the launch (100 MHz constant
+ * clock, the clock of gm_chunk_stats' times): out[w] for w < min(max_out, out[1] of
  * gm_dispatch_info).  Returns the count written (>= 0) or a negative error.  Synchronises
  * the context's stream.  Diagnostics: the shape of the launch's tail. */
 int  gm_chunk_timeline(gm_ctx* ctx, uint64_t* out, int max_out);

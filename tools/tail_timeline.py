@@ -1,6 +1,6 @@
 """Developer probe: the tail of a gm_rollout launch on the bench's steady-state C3 workload.
-Per-workgroup exit times (gm_chunk_timeline) of the timed launch: when the waves ran out of
-work, against the launch span and the queue's busy fraction.
+Per-workgroup end of work (gm_chunk_timeline) of the timed launch: when each wave ran out of
+work for good, against the launch span and the queue's busy fraction.
 usage: python tools/tail_timeline.py [envs] [R]"""
 import ctypes as C
 import os
@@ -39,5 +39,5 @@ for it in range(3):
     # wave-time lost to the tail: each workgroup idle from its exit to the last exit
     idle = float((ex[-1] - ex).sum() / (len(ex) * ex[-1]))
     print(f"n={n} R={R} launch {env.last_step_ms():.2f} ms span {span:.2f} busy {cs['busy']:.3f} poll {cs['poll']:.3f} "
-          f"yields {cs['yields']} fresh-empty {cs['fresh_empty_ms']:.2f} ms | exits (ms) p1/10/25/50/75/90/99/100 "
+          f"yields {cs['yields']} fresh-empty {cs['fresh_empty_ms']:.2f} ms | work ends (ms) p1/10/25/50/75/90/99/100 "
           + " ".join(f"{x:.2f}" for x in q) + f" | tail idle {idle:.3f}", flush=True)

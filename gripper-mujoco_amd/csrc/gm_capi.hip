@@ -70,6 +70,7 @@ struct gm_ctx {
   GmChunkCarry* d_chunk_carry = nullptr;
   unsigned long long* d_chunk_st = nullptr;
   int chunk = 0, chunk_grid = 0, chunk_cap = 0, chunk_margin = 50, chunk_yields = 20, chunk_cmargin = 50;
+  int chunk_steal = 1;                 // idle waves resume yielded envs of other XCDs (GM_CHUNK_STEAL=0: off)
   // DUO workgroups (gm_step_kernel<CL, false, true>): two waves per env, the second running
   // the collider concurrently -- for batches small enough that wave slots are spare
   bool duo = false;
@@ -117,6 +118,7 @@ hipError_t launch_step(gm_ctx* c, int grid, int n_envs, int mode, DebugOut dbg, 
   const bool chunked = order && c->chunk > 0 && c->chunk_grid > 0 && dbg.phase == nullptr;
   GmChunkQ q{c->d_chunk_ctr, c->d_chunk_ring, c->d_chunk_carry, c->chunk_cap, chunked ? c->chunk : 0,
              c->chunk_margin, c->chunk_yields, c->chunk_cmargin, c->d_chunk_st};
+  q.steal = c->chunk_steal;
   q.steps = 1;
   q.act_mode = -1;   // gm_step: one plain env-step per env (gm_rollout sets the rollout fields)
   if (roll && chunked) {
@@ -408,6 +410,7 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
     if (const char* e2 = std::getenv("GM_CHUNK_MARGIN")) c->chunk_margin = std::atoi(e2);
     if (const char* e3 = std::getenv("GM_CHUNK_YIELDS")) c->chunk_yields = std::atoi(e3);
     if (const char* e4 = std::getenv("GM_CHUNK_CMARGIN")) c->chunk_cmargin = std::atoi(e4);
+    if (const char* e6 = std::getenv("GM_CHUNK_STEAL")) c->chunk_steal = std::atoi(e6) != 0;
     int per_cu = 0, per_cu_duo = 0, n_cu = 0;
     switch (c->model.n_seg) {
 #define X(N)                                                                                              \
@@ -432,8 +435,10 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
     c->chunk_cap = n_envs + c->chunk_grid;
     HIPCHK(c, hipMalloc(&c->d_chunk_ctr, sizeof(uint32_t) * GM_CQ_ALLOC));
     HIPCHK(c, hipMemsetAsync(c->d_chunk_ctr, 0, sizeof(uint32_t) * GM_CQ_ALLOC, c->stream));
-    HIPCHK(c, hipMalloc(&c->d_chunk_st, sizeof(unsigned long long) * (16 + (size_t)c->chunk_grid)));
-    HIPCHK(c, hipMemsetAsync(c->d_chunk_st, 0, sizeof(unsigned long long) * (16 + (size_t)c->chunk_grid), c->stream));
+    // [0, 16) launch stats, then per workgroup its end of work, then per env its start and finish
+    const size_t st_words = 16 + (size_t)c->chunk_grid + 2 * (size_t)n_envs;
+    HIPCHK(c, hipMalloc(&c->d_chunk_st, sizeof(unsigned long long) * st_words));
+    HIPCHK(c, hipMemsetAsync(c->d_chunk_st, 0, sizeof(unsigned long long) * st_words, c->stream));
     HIPCHK(c, hipMalloc(&c->d_chunk_ring, sizeof(uint64_t) * 8 * GM_CQ_NB * (size_t)c->chunk_cap));
     HIPCHK(c, hipMalloc(&c->d_chunk_carry, sizeof(GmChunkCarry) * (size_t)n_envs));
     HIPCHK(c, hipMemsetAsync(c->d_chunk_ring, 0, sizeof(uint64_t) * 8 * GM_CQ_NB * (size_t)c->chunk_cap, c->stream));
@@ -960,20 +965,21 @@ int gm_step(gm_ctx* c) {
 int gm_chunk_stats(gm_ctx* c, uint32_t* out, uint64_t* times) {
   if (!c || !out) return GM_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
-  uint32_t w[36];
+  uint32_t w[37];
   HIPCHK(c, hipMemcpyAsync(w, c->d_chunk_ctr + GM_CQ_LAST, sizeof(w), hipMemcpyDeviceToHost, c->stream));
   if (times) HIPCHK(c, hipMemcpyAsync(times, c->d_chunk_st + 8, sizeof(uint64_t) * 5, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   out[0] = std::min<uint32_t>(w[0], (uint32_t)c->n_envs);
   out[1] = w[32]; out[2] = w[33]; out[3] = w[34];
   out[4] = (uint32_t)c->chunk; out[5] = (uint32_t)c->chunk_grid;
+  out[6] = w[36];
   return GM_OK;
 }
 
 int gm_chunk_timeline(gm_ctx* c, uint64_t* out, int max_out) {
   if (!c || !out || max_out < 0) return GM_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
-  const int n = std::min(max_out, c->chunk_grid);
+  const int n = std::min(max_out, c->chunk_grid + 2 * c->n_envs);
   HIPCHK(c, hipMemcpyAsync(out, c->d_chunk_st + 16, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return n;

@@ -2502,8 +2502,8 @@ struct GmChunkCarry {        // what a chunk hands the next besides the hot stat
 };
 // counters (zeroed by gm_dispatch_order_kernel before every launch), one 128-B line each:
 // ring r = x * GM_CQ_NB + bucket: [r * 32] its head, [r * 32 + 1] its tail; GM_CQ_FRESH the
-// next unstarted env, GM_CQ_DONE envs finished, + 1 yields, + 2 resumes; GM_CQ_LAST the
-// previous launch's [GM_CQ_FRESH ..] (36 words, diagnostics)
+// next unstarted env, GM_CQ_DONE envs finished, + 1 yields, + 2 resumes, + 4 resumes on another
+// XCD; GM_CQ_LAST the previous launch's [GM_CQ_FRESH ..] (37 words, diagnostics)
 #define GM_CQ_FRESH (8 * GM_CQ_NB * 32)
 #define GM_CQ_DONE (GM_CQ_FRESH + 32)
 #define GM_CQ_CMAX (GM_CQ_DONE + 3)   // this launch's bucket scale (written by the order kernel)
@@ -2539,6 +2539,7 @@ struct GmChunkQ {
   int scene_tries;
   const gm_spawn_params* scene;
   GmSpawnRand sr;
+  int steal;                 // an idle wave may resume a yielded env of another XCD
 };
 __device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2649,6 +2650,46 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
           if (i < n) { pick = order[i]; fresh = 1; }
         }
         if (__builtin_amdgcn_readfirstlane(pick) >= 0) break;
+      } else if (q.steal) {
+        // nothing unstarted and nothing yielded on this XCD: the best yielded env of another
+        // XCD (its hot state was published with an agent-scope release, the acquire below
+        // makes it visible here; same-XCD resumption is only the faster case).  Lane l looks
+        // at XCD l / 8, buckets 15 - l % 8 and 7 - l % 8.
+        const int x2 = lane >> 3;
+        const uint32_t* bq2 = q.ctr + x2 * GM_CQ_NB * 32;
+        const int bh = 15 - (lane & 7), bl = 7 - (lane & 7);
+        const bool other = x2 != xcc;
+        const bool nh = other && ld_agent(bq2 + bh * 32) < ld_agent(bq2 + bh * 32 + 1);
+        const bool nl = other && ld_agent(bq2 + bl * 32) < ld_agent(bq2 + bl * 32 + 1);
+        const unsigned long long mh = __ballot(nh), ml = __ballot(nl);
+        if (mh | ml) {
+          // the highest non-empty bucket over the other XCDs (lowest lane among equals)
+          int src = -1, sb = -1;
+          for (int r = 0; r < 8 && src < 0; r++) {   // bucket 15 - r in the high half, lanes with lane % 8 == r
+            const unsigned long long m8 = mh & (0x0101010101010101ull << r);
+            if (m8) { src = (int)__builtin_ctzll(m8) >> 3; sb = 15 - r; }
+          }
+          for (int r = 0; r < 8 && src < 0; r++) {
+            const unsigned long long m8 = ml & (0x0101010101010101ull << r);
+            if (m8) { src = (int)__builtin_ctzll(m8) >> 3; sb = 7 - r; }
+          }
+          if (lane == 0) {
+            uint32_t* sbq = q.ctr + src * GM_CQ_NB * 32;
+            uint64_t* rb = q.ring + (size_t)src * GM_CQ_NB * q.cap + (size_t)sb * q.cap;
+            const uint32_t i = add_agent(sbq + sb * 32, 1u) % (uint32_t)q.cap;
+            uint64_t v;
+            while ((v = __hip_atomic_load(rb + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0ull &&
+                   ld_agent(n_done) < n)
+              __builtin_amdgcn_s_sleep(2);
+            if (v != 0ull) {
+              st_agent(rb + i, 0ull);
+              add_agent(q.ctr + GM_CQ_DONE + 2, 1u);
+              add_agent(q.ctr + GM_CQ_DONE + 4, 1u);   // steals
+              pick = (int)(uint32_t)v - 1;
+            }
+          }
+          break;                           // pick < 0: everything finished while waiting
+        }
       }
       if (__builtin_amdgcn_readfirstlane(ld_agent(n_done)) >= n) break;
       __builtin_amdgcn_s_sleep(2);
@@ -2662,6 +2703,8 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       __hip_atomic_fetch_min(q.st, tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     first = false;
     const int env = pick;
+    uint64_t* env_t = reinterpret_cast<uint64_t*>(q.st) + 16 + gridDim.x + 2 * (size_t)env;   // gm_chunk_timeline
+    if (fresh && lane == 0) st_agent(env_t, tp);
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     if (!fresh) {
       // lane 0's acquire load saw the entry; the fence extends that acquire to the whole
@@ -2762,6 +2805,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       store_state(S, g, lane);
       if (lane == 0) {
         add_agent(n_done, 1u);
+        st_agent(env_t + 1, __builtin_amdgcn_s_memrealtime());
         __hip_atomic_fetch_max(q.st + 2, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -2774,11 +2818,15 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
         cr.clk += (uint32_t)((__builtin_amdgcn_s_memtime() - t_start) >> 6);
         q.carry[env] = cr;
       }
-      // the workgroup barrier orders every lane's state / carry stores before lane 0's
-      // release store of the ring entry, which publishes them at agent scope (the consumer's
-      // acquire pairs with it)
+      // publish (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms): the wave's
+      // state / carry stores drained, then lane 0's agent-scope release (the XCD L2 written
+      // back, so a consumer on ANY XCD sees the bytes after its acquire), drained again
+      // before the ring entry's relaxed agent store
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       GM_ENV_SYNC();
       if (lane == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int job_total = q.steps > 1 ? q.steps * s_nom : cr.nsub;
         const int job_left = (cr.steps_left - 1) * s_nom + (cr.nsub - cr.sub_done);
         const uint64_t rem = (uint64_t)own * (uint64_t)job_left / (uint64_t)job_total;
@@ -2786,7 +2834,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
         const uint32_t b = rem * GM_CQ_NB / cmax < GM_CQ_NB - 1 ? (uint32_t)(rem * GM_CQ_NB / cmax) : GM_CQ_NB - 1;
         const uint32_t t = add_agent(bq + b * 32 + 1, 1u) % (uint32_t)q.cap;
         __hip_atomic_store(ring + (size_t)b * q.cap + t,
-                           ((rem > 0xFFFFFFFFull ? 0xFFFFFFFFull : rem) << 32) | ((uint64_t)env + 1u), __ATOMIC_RELEASE,
+                           ((rem > 0xFFFFFFFFull ? 0xFFFFFFFFull : rem) << 32) | ((uint64_t)env + 1u), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -2797,7 +2845,8 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
   if (lane == 0) {
     __hip_atomic_fetch_add(q.st + 3, busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(q.st + 4, poll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    st_agent(reinterpret_cast<uint64_t*>(q.st) + 16 + blockIdx.x, last_end);   // this workgroup's last work (gm_chunk_timeline)
+    // this workgroup's last work (gm_chunk_timeline), its XCD in the top four bits
+    st_agent(reinterpret_cast<uint64_t*>(q.st) + 16 + blockIdx.x, last_end | ((uint64_t)xcc << 60));
   }
 }
 // mode 0: action_step + obs/done/reward; mode 1: calibrate_reset settle (400 substeps,
@@ -2970,7 +3019,7 @@ extern "C" __global__ __launch_bounds__(1024) void gm_dispatch_order_kernel(uint
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t cmax;
   const int t = threadIdx.x;
-  if (chunk_ctr && t < 36) chunk_ctr[GM_CQ_LAST + t] = chunk_ctr[GM_CQ_FRESH + t];   // last launch's, for diagnostics
+  if (chunk_ctr && t < 37) chunk_ctr[GM_CQ_LAST + t] = chunk_ctr[GM_CQ_FRESH + t];   // last launch's, for diagnostics
   __syncthreads();
   if (chunk_ctr)
     for (int w = t; w < GM_CQ_WORDS; w += 1024) chunk_ctr[w] = 0;   // the chunked launch's queue counters

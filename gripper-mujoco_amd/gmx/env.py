@@ -293,28 +293,33 @@ class BatchedGripperEnv:
 
     def chunk_stats(self) -> dict:
         """The last gm_step's chunked-dispatch counters (include/gripper_mi355x.h gm_chunk_stats)."""
-        v = (C.c_uint32 * 6)()
+        v = (C.c_uint32 * 7)()
         t = (C.c_uint64 * 5)()
         self._check(self.lib.gm_chunk_stats(self._ctx, v, t))
         span = (t[2] - t[0]) * 1e-5 if t[2] > t[0] else 0.0   # ms
-        return dict(started=v[0], finished=v[1], yields=v[2], resumes=v[3], every=v[4], workgroups=v[5],
+        return dict(started=v[0], finished=v[1], yields=v[2], resumes=v[3], every=v[4], workgroups=v[5], steals=v[6],
                     span_ms=span, fresh_empty_ms=(t[1] - t[0]) * 1e-5 if t[1] >= t[0] and span else 0.0,
                     busy=(t[3] / (v[5] * (t[2] - t[0]))) if span and v[5] else 0.0,
                     poll=(t[4] / (v[5] * (t[2] - t[0]))) if span and v[5] else 0.0)
 
     def chunk_timeline(self):
         """When each workgroup of the last chunked launch finished its last work, ms after the
-        launch's first pick (gm_chunk_timeline)."""
+        launch's first pick, its XCD, and per env [start, finish] ms (gm_chunk_timeline)."""
         import numpy as np
         info = self.dispatch_info()
-        buf = (C.c_uint64 * max(1, info["grid"]))()
-        n = self.lib.gm_chunk_timeline(self._ctx, buf, info["grid"])
+        G = info["grid"]
+        buf = (C.c_uint64 * max(1, G + 2 * self.n_envs))()
+        n = self.lib.gm_chunk_timeline(self._ctx, buf, G + 2 * self.n_envs)
         if n < 0:
             raise RuntimeError(f"gm_chunk_timeline failed ({n})")
         t = (C.c_uint64 * 5)()
-        v = (C.c_uint32 * 6)()
+        v = (C.c_uint32 * 7)()
         self._check(self.lib.gm_chunk_stats(self._ctx, v, t))
-        return (np.frombuffer(buf, dtype=np.uint64, count=n).astype(np.float64) - float(t[0])) * 1e-5
+        raw = np.frombuffer(buf, dtype=np.uint64, count=n)
+        wg = raw[:G]
+        ends = ((wg & np.uint64((1 << 60) - 1)).astype(np.float64) - float(t[0])) * 1e-5
+        ev = (raw[G:].astype(np.float64).reshape(-1, 2) - float(t[0])) * 1e-5
+        return ends, (wg >> np.uint64(60)).astype(np.int32), ev
 
     def dispatch_info(self) -> dict:
         """How gm_step / gm_rollout dispatch this context (include/gripper_mi355x.h gm_dispatch_info)."""

@@ -594,11 +594,12 @@ int  gm_last_step_ms(gm_ctx* ctx, float* ms);
 /* The last gm_step's work queue (chunked dispatch): out[0] envs started,
  * out[1] envs finished, out[2] yields (an env handed back to its XCD's queue because an
  * unstarted env had more work left), out[3] resumptions; out[4] substeps between
- * preemption tests (0: the one-shot kernel ran), out[5] resident workgroups.  times (may
+ * preemption tests (0: the one-shot kernel ran), out[5] resident workgroups, out[6] the
+ * resumptions by a wave of another XCD than the yielding one's.  times (may
  * be NULL; 100 MHz constant-clock ticks): [0] first pick, [1] first pick that found no
  * unstarted env, [2] last env finished, [3] sum of wave-busy time, [4] sum of wave polling.
  * Synchronises the context's stream. */
-int  gm_chunk_stats(gm_ctx* ctx, uint32_t* out6, uint64_t* times5);
+int  gm_chunk_stats(gm_ctx* ctx, uint32_t* out7, uint64_t* times5);
 /* How gm_step / gm_rollout dispatch this context (fixed at gm_create): out[0] substeps
  * between preemption tests (0: the one-shot kernel), out[1] workgroups of the chunked
  * grid, out[2] waves per env (1; 2 = DUO workgroups, whose second wave runs the collider
@@ -607,8 +608,9 @@ int  gm_chunk_stats(gm_ctx* ctx, uint32_t* out6, uint64_t* times5);
 int  gm_dispatch_info(const gm_ctx* ctx, int32_t* out4);
 /* The last chunked launch's per-workgroup end of work: when workgroup w finished the last
  * env (or env chunk) it ran, before it polled out the rest of the launch (100 MHz constant
- * clock, the clock of gm_chunk_stats' times): out[w] for w < min(max_out, out[1] of
- * gm_dispatch_info).  Returns the count written (>= 0) or a negative error.  Synchronises
+ * clock, the clock of gm_chunk_stats' times, in the low 60 bits; the workgroup's XCD in
+ * the top 4): out[w] for w < G = out[1] of gm_dispatch_info; then, per env e, when it was first
+ * picked and when its job finished: out[G + 2 e], out[G + 2 e + 1] (up to max_out words).  Returns the count written (>= 0) or a negative error.  Synchronises
  * the context's stream.  Diagnostics: the shape of the launch's tail. */
 int  gm_chunk_timeline(gm_ctx* ctx, uint64_t* out, int max_out);
 

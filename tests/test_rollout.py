@@ -99,7 +99,10 @@ def test_rollout_equals_per_step_api(gm, mode, dispatch):
         assert int((length > 0).sum()) >= N, int((length > 0).sum())
         assert int(va["episode"].min()) >= 2
         if dispatch == "handoff-heavy":
-            assert b.chunk_stats()["yields"] > N, b.chunk_stats()
+            st = b.chunk_stats()
+            assert st["yields"] > N, st
+            # idle waves resumed yielded envs of other XCDs (cross-XCD hand-offs)
+            assert st["steals"] > 0, st
     finally:
         a.close()
         b.close()

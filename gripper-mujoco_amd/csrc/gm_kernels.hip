@@ -1470,12 +1470,14 @@ __device__ __forceinline__ void integrate(SharedT<CL>& S, const gm_model* __rest
     for (int k = 0; k < 3; k++) S.s.qpos[qa + k] += h * S.s.qvel[da + k];
     real* q = &S.s.qpos[qa + 3];
     real w[3] = {S.s.qvel[da + 3], S.s.qvel[da + 4], S.s.qvel[da + 5]};
-    real wn = sqrt(dot3(w, w));
+    // (sqrt_n / div_n: the library operations' results wherever their range scaling is
+    // inactive -- a |w| below 2^-383 takes the branch either way)
+    real wn = sqrt_n(dot3(w, w));
     if (wn > 1e-15) {
       real ang = wn * h;
       real sn, cs;
       gm_sincos(0.5 * ang, &sn, &cs);
-      sn = sn / wn;
+      sn = div_n(sn, wn);
       real dq[4] = {cs, w[0] * sn, w[1] * sn, w[2] * sn};
       quatmul(q, q, dq);
     }
@@ -1619,7 +1621,7 @@ GM_EPI_ATTR void update_all(SharedT<CL>& S, const gm_model* __restrict__ m, cons
                     a.sy == before.sy && a.sz == before.sz;
     }
     const real* v = &s.qvel[T->dof_obj];
-    real mag = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    real mag = sqrt_n(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);   // (= sqrt wherever it decides anything)
     if (mag < 1e-6) for (int k = 0; k < 6; k++) s.qvel[T->dof_obj + k] = 0;
   }
   GM_WAVE_SYNC();

@@ -1,7 +1,7 @@
 """Developer probe: the bench's C3 steady-state workload (set6_synthetic, scene spawn,
 staggered pre-roll over the episode, scripted grasp mix) for PMC counter passes; the
 analysis takes the last `steps` gm_step_kernel dispatches.
-usage: python tools/pmc_grasp.py [envs] [steps]"""
+usage: python tools/pmc_grasp.py [envs] [steps] [object_set]"""
 import ctypes as C
 import os
 import sys
@@ -13,8 +13,9 @@ import bench
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+oset = sys.argv[3] if len(sys.argv) > 3 else "set6_synthetic"
 seed, MAX_EP = 1234, 250
-env = gmx.BatchedGripperEnv(n, object_set="set6_synthetic", settings=gmx.canonical_settings(seed=seed), seed=seed)
+env = gmx.BatchedGripperEnv(n, object_set=oset, settings=gmx.canonical_settings(seed=seed), seed=seed)
 env.set_scene_spawn(bench.mjenv_spawn_params(gmx), max_tries=3)
 env.reset()
 d_act = env.lib.gm_device_actions(env.ctx)

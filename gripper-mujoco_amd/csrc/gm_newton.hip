@@ -1416,13 +1416,15 @@ __device__ __forceinline__ real euler_factor(const SharedT<CL>& S, const GmTopo*
     const int d = T->dof_f0[rowf] + p - 1;
     const real hd = h * T->dof_damp[d];
     {
+      // the full symmetric row (M's upper part read from its lower triangle): the factor
+      // then takes each pivot's column entry from the lane's own row
       real Hr[CL + 1];
 #pragma unroll
-      for (int j = 1; j <= CL; j++) Hr[j] = H[TRI(p, j)];
+      for (int j = 1; j <= CL; j++) Hr[j] = H[j <= p ? TRI(p, j) : TRI(j, p)];
       Hr[0] = Hr[1];
       keep_n<CL + 1>(Hr);
 #pragma unroll
-      for (int j = 1; j <= CL; j++) L[j] = (j <= p) ? Hr[j] : 0.0;
+      for (int j = 1; j <= CL; j++) L[j] = Hr[j];
     }
 #pragma unroll
     for (int j = 1; j <= CL; j++) L[j] = (j == p) ? L[j] + hd : L[j];
@@ -1444,10 +1446,7 @@ __device__ __forceinline__ real euler_factor(const SharedT<CL>& S, const GmTopo*
       for (int j = 1; j < k; j++) hk[j] = row_bcast(L[j], k);
       const real hkb = row_bcast(lb, k);
       const bool upd = p >= 1 && p < k, piv = p == k;
-      real Hpk = 0.0;
-#pragma unroll
-      for (int j = 1; j < k; j++) Hpk = (p == j) ? hk[j] : Hpk;
-      const real a = Hpk * ihk;
+      const real a = L[k] * ihk;   // (the lane's own row holds the pivot column: full symmetric rows)
       const real aa = upd ? a : 0.0;
       ub = piv ? lb : ub;
 #pragma unroll

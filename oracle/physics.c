@@ -1936,7 +1936,7 @@ static void euler_damping(const or_env* e, double* qe) {
     for (int p = 1; p <= CL; p++) {
       const int l = 16 * f + p, d = T->dof_f0[f] + p - 1;
       const double hd = h * T->dof_damp[d];
-      for (int j = 1; j <= p; j++) L[l][j] = e->Hf[f][TRI(p, j)];
+      for (int j = 1; j <= CL; j++) L[l][j] = e->Hf[f][j <= p ? TRI(p, j) : TRI(j, p)];   /* full symmetric row */
       L[l][p] = L[l][p] + hd;
       lb[l] = e->Hf[f][TRI(p, 0)];
       y[l] = hd * e->qacc[d];
@@ -1966,9 +1966,7 @@ static void euler_damping(const or_env* e, double* qe) {
     for (int l = 0; l < 48; l++) {
       const int f = l >> 4, p = l & 15;
       const int upd = p >= 1 && p < k, piv = p == k;
-      double Hpk = 0.0;
-      for (int j = 1; j < k; j++) Hpk = (p == j) ? hk[f][j] : Hpk;
-      const double a = Hpk * ihk[f];
+      const double a = L[l][k] * ihk[f];   /* the row's own pivot-column entry */
       const double aa = upd ? a : 0.0;
       const double sc = piv ? ihk[f] : 1.0;
       if (piv) ub[l] = lb[l];

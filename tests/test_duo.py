@@ -101,3 +101,42 @@ def test_dispatch_defaults(gm):
     finally:
         small.close()
         big.close()
+
+
+@pytest.mark.parametrize("n_seg,dt", [(5, 6.76e-3), (10, 2.1e-3)])
+def test_duo_other_segment_counts(gm, n_seg, dt):
+    """The DUO instances for other chain lengths (CL = 7, 12: N = 10 takes the collider's
+    second 64-pair batch on the helper wave) equal the one-wave kernel bit for bit."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import ctypes as C
+    p = gm.ModelParams()
+    gm.load_library().gm_default_model_params(C.byref(p))
+    p.n_seg, p.timestep = n_seg, dt
+    n, steps, seed = 128, 25, 9
+    envs = []
+    for v in ("1", "0"):
+        old = os.environ.get("GM_DUO")
+        os.environ["GM_DUO"] = v
+        try:
+            e = gm.BatchedGripperEnv(n, object_set="set6_synthetic", settings=gm.canonical_settings(noise=True, seed=seed),
+                                     seed=seed, model_params=p)
+        finally:
+            if old is None:
+                os.environ.pop("GM_DUO", None)
+            else:
+                os.environ["GM_DUO"] = old
+        e.set_scene_spawn(gm.default_spawn_params(), max_tries=3)
+        e.reset()
+        envs.append(e)
+    a, b = envs
+    try:
+        assert a.dispatch_info()["waves_per_env"] == 2 and b.dispatch_info()["waves_per_env"] == 1
+        ra, rb = grasp(gm, a, steps, seed), grasp(gm, b, steps, seed)
+        for k, ((oa, wa, da), (ob, wb, db)) in enumerate(zip(ra, rb)):
+            np.testing.assert_array_equal(oa, ob, err_msg=f"obs, step {k}")
+            np.testing.assert_array_equal(wa, wb, err_msg=f"reward, step {k}")
+        np.testing.assert_array_equal(a.env_states(), b.env_states())
+    finally:
+        a.close()
+        b.close()

@@ -211,6 +211,15 @@ __device__ __forceinline__ double sqrt_n(double x) {
   g = fma(d, h, g);
   return x == 0.0 ? x : g;
 }
+// 1 / sqrt(x) for normal x > 0: v_rsq_f64 and two Newton steps (MPR's direction normalising)
+__device__ __forceinline__ double rsq_n(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double hx = 0.5 * x;
+  double e = fma(-hx * y, y, 0.5);
+  y = fma(y, e, y);
+  e = fma(-hx * y, y, 0.5);
+  return fma(y, e, y);
+}
 __device__ __forceinline__ double rcp_refined(double b) {
   double r = __builtin_amdgcn_rcp(b);
   double e = fma(-b, r, 1.0);
@@ -229,6 +238,7 @@ __device__ __forceinline__ double div_n(double a, double b) {
 }
 #else
 __device__ __forceinline__ double sqrt_n(double x) { return sqrt(x); }
+__device__ __forceinline__ double rsq_n(double x) { return 1.0 / sqrt(x); }
 __device__ __forceinline__ double rcp_n(double b) { return 1.0 / b; }
 __device__ __forceinline__ double div_n(double a, double b) { return a / b; }
 #endif
@@ -1007,8 +1017,8 @@ __device__ __forceinline__ void support_geom(const GeomV& G, const real* d, real
   if (type == GM_GEOM_BOX) {
     for (int k = 0; k < 3; k++) pl[k] = fabs(dl[k]) < GM_SUPPORT_TIE ? 0.0 : (dl[k] >= 0 ? G.size[k] : -G.size[k]);
   } else if (type == GM_GEOM_CYLINDER) {
-    real rr = sqrt_n(dl[0] * dl[0] + dl[1] * dl[1]);
-    if (rr > 1e-12) { pl[0] = div_n(G.size[0] * dl[0], rr); pl[1] = div_n(G.size[0] * dl[1], rr); }
+    const real rr2 = dl[0] * dl[0] + dl[1] * dl[1];
+    if (rr2 > 1e-24) { const real irr = rsq_n(rr2); pl[0] = (G.size[0] * dl[0]) * irr; pl[1] = (G.size[0] * dl[1]) * irr; }
     pl[2] = fabs(dl[2]) < GM_SUPPORT_TIE ? 0.0 : (dl[2] >= 0 ? G.size[1] : -G.size[1]);
   } else if (type == GM_GEOM_SPHERE) {
     real l = sqrt_n(dot3(dl, dl));
@@ -1025,9 +1035,12 @@ __device__ __forceinline__ void mpr_support(const GeomV& A, const GeomV& B, cons
   sv.v[0] = sv.p1[0] - sv.p2[0]; sv.v[1] = sv.p1[1] - sv.p2[1]; sv.v[2] = sv.p1[2] - sv.p2[2];
 }
 __device__ __forceinline__ int fzero(real x) { return fabs(x) < 1e-12; }
+// (1 / |d| as one refined reciprocal square root: half the dependent chain of sqrt then
+// reciprocal; the oracle's 1 / sqrt(x) rounds twice, this once -- the MPR iterates agree to
+// the last bits, the collider's contacts to ~1e-15 relative)
 __device__ __forceinline__ void normalize3(real* d) {
-  real l = sqrt_n(dot3(d, d));
-  if (l > 0) { real il = rcp_n(l); d[0] *= il; d[1] *= il; d[2] *= il; }
+  const real l2 = dot3(d, d);
+  if (l2 > 0) { const real il = rsq_n(l2); d[0] *= il; d[1] *= il; d[2] *= il; }
 }
 // The simplex vertices are four named values (not an array), conditional vertex copies
 // are per-component selects and every helper is inlined, so the whole MPR state stays in

@@ -211,7 +211,11 @@ __device__ __forceinline__ double sqrt_n(double x) {
   g = fma(d, h, g);
   return x == 0.0 ? x : g;
 }
-// 1 / sqrt(x) for normal x > 0: v_rsq_f64 and two Newton steps (MPR's direction normalising)
+// 1 / sqrt(x) for normal x > 0: v_rsq_f64 and two Newton steps (normalising directions in
+// the physics substep); rcp_piv: a factor pivot's reciprocal, two Newton steps without the
+// final correction.  The calibration build (GM_CAL_TU: stability verdicts compared with the
+// oracle candidate for candidate) takes the correctly rounded forms instead.
+#ifndef GM_CAL_TU
 __device__ __forceinline__ double rsq_n(double x) {
   double y = __builtin_amdgcn_rsq(x);
   const double hx = 0.5 * x;
@@ -220,6 +224,7 @@ __device__ __forceinline__ double rsq_n(double x) {
   e = fma(-hx * y, y, 0.5);
   return fma(y, e, y);
 }
+#endif
 __device__ __forceinline__ double rcp_refined(double b) {
   double r = __builtin_amdgcn_rcp(b);
   double e = fma(-b, r, 1.0);
@@ -236,9 +241,16 @@ __device__ __forceinline__ double div_n(double a, double b) {
   const double q = a * r;
   return fma(fma(-b, q, a), r, q);
 }
+#ifdef GM_CAL_TU
+__device__ __forceinline__ double rsq_n(double x) { return rcp_n(sqrt_n(x)); }
+__device__ __forceinline__ double rcp_piv(double b) { return rcp_n(b); }
+#else
+__device__ __forceinline__ double rcp_piv(double b) { return rcp_refined(b); }
+#endif
 #else
 __device__ __forceinline__ double sqrt_n(double x) { return sqrt(x); }
 __device__ __forceinline__ double rsq_n(double x) { return 1.0 / sqrt(x); }
+__device__ __forceinline__ double rcp_piv(double b) { return 1.0 / b; }
 __device__ __forceinline__ double rcp_n(double b) { return 1.0 / b; }
 __device__ __forceinline__ double div_n(double a, double b) { return a / b; }
 #endif
@@ -360,7 +372,9 @@ __host__ __device__ constexpr int gm_pair_batches(int CL) { return CL <= 10 ? 1 
 #pragma clang fp contract(fast)
 #endif
 namespace gmf {
+#define GM_FP_PHYSICS
 #include "gm_fphelpers.inc"
+#undef GM_FP_PHYSICS
 
 template <int CL>
 __device__ __forceinline__ void kinematics(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
@@ -841,7 +855,7 @@ __device__ void make_frame(real* F, const real* n) {
   if (fabs(n[0]) < 0.5) a[0] = 1; else a[1] = 1;
   real d = dot3(a, n);
   real t1[3] = {a[0] - d * n[0], a[1] - d * n[1], a[2] - d * n[2]};
-  const real il = rcp_n(sqrt_n(dot3(t1, t1)));
+  const real il = rsq_n(dot3(t1, t1));
   t1[0] *= il; t1[1] *= il; t1[2] *= il;
   real t2[3];
   cross3(t2, n, t1);
@@ -918,9 +932,10 @@ __device__ __forceinline__ void cyl_frame(const GeomV& P, const GeomV& Cy, CylFr
   F.a[0] = Cy.R[2]; F.a[1] = Cy.R[5]; F.a[2] = Cy.R[8];
   real na = dot3(F.nz, F.a);
   real w[3] = {-F.nz[0] + na * F.a[0], -F.nz[1] + na * F.a[1], -F.nz[2] + na * F.a[2]};
-  real lw = sqrt_n(dot3(w, w));
+  const real lw2 = dot3(w, w);
+  const real lw = sqrt_n(lw2), ilw = rsq_n(lw2);   // (independent: the test and the scale)
   if (lw < 1e-6) { w[0] = Cy.R[0]; w[1] = Cy.R[3]; w[2] = Cy.R[6]; }
-  else { w[0] = div_n(w[0], lw); w[1] = div_n(w[1], lw); w[2] = div_n(w[2], lw); }
+  else { w[0] = w[0] * ilw; w[1] = w[1] * ilw; w[2] = w[2] * ilw; }
   F.w[0] = w[0]; F.w[1] = w[1]; F.w[2] = w[2];
   cross3(F.axw, F.a, F.w);
 }
@@ -971,11 +986,13 @@ __device__ __forceinline__ int sphere_box(const GeomV& Sp, const GeomV& B, Hit& 
   real nl[3], dist, ql[3];
   if (!inside) {
     real df[3] = {cl[0] - q[0], cl[1] - q[1], cl[2] - q[2]};
-    real l = sqrt_n(dot3(df, df));
+    const real l2 = dot3(df, df);
+    real l = sqrt_n(l2);
     if (l < 1e-12) return 0;
     dist = l - r;
     if (!(dist < 0)) return 0;
-    nl[0] = div_n(-df[0], l); nl[1] = div_n(-df[1], l); nl[2] = div_n(-df[2], l);
+    const real il = rsq_n(l2);
+    nl[0] = -df[0] * il; nl[1] = -df[1] * il; nl[2] = -df[2] * il;
     ql[0] = q[0]; ql[1] = q[1]; ql[2] = q[2];
   } else {
     int kmin = 0;
@@ -1021,8 +1038,9 @@ __device__ __forceinline__ void support_geom(const GeomV& G, const real* d, real
     if (rr2 > 1e-24) { const real irr = rsq_n(rr2); pl[0] = (G.size[0] * dl[0]) * irr; pl[1] = (G.size[0] * dl[1]) * irr; }
     pl[2] = fabs(dl[2]) < GM_SUPPORT_TIE ? 0.0 : (dl[2] >= 0 ? G.size[1] : -G.size[1]);
   } else if (type == GM_GEOM_SPHERE) {
-    real l = sqrt_n(dot3(dl, dl));
-    if (l > 1e-12) { pl[0] = div_n(dl[0] * G.size[0], l); pl[1] = div_n(dl[1] * G.size[0], l); pl[2] = div_n(dl[2] * G.size[0], l); }
+    const real l2 = dot3(dl, dl);
+    real l = sqrt_n(l2);
+    if (l > 1e-12) { const real il = rsq_n(l2); pl[0] = (dl[0] * G.size[0]) * il; pl[1] = (dl[1] * G.size[0]) * il; pl[2] = (dl[2] * G.size[0]) * il; }
   }
   mulmv3(out, G.R, pl);
   out[0] += G.c[0]; out[1] += G.c[1]; out[2] += G.c[2];
@@ -1196,10 +1214,11 @@ __device__ __forceinline__ int mpr(const GeomV& A, const GeomV& B, real tol, int
     if (reach_tol(P1, P2, P3, v4, d, tol) || it > maxit) {
       real cp[3];
       tri_closest_origin(P1.v, P2.v, P3.v, cp);
-      real depth = sqrt_n(dot3(cp, cp));
+      const real dp2 = dot3(cp, cp);
+      real depth = sqrt_n(dp2);
       if (fzero(depth)) return 0;
       h.dist = -depth;
-      real id = rcp_n(depth);
+      real id = rsq_n(dp2);
       h.n[0] = cp[0] * id; h.n[1] = cp[1] * id; h.n[2] = cp[2] * id;
       mpr_pos(P0, P1, P2, P3, h.pos);
       return depth > 0;

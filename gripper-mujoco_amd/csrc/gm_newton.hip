@@ -65,9 +65,10 @@ __device__ __forceinline__ void bb_setup(const GeomV& A, const GeomV& B, BBox& S
     for (int j = 0; j < 3; j++) {
       real L[3];
       cross3(L, a[i], b[j]);
-      const real len = sqrt_n(dot3(L, L));
+      const real len2 = dot3(L, L);
+      const real len = sqrt_n(len2);
       if (len < 1e-6) continue;
-      const real il = rcp_n(len);
+      const real il = rsq_n(len2);
       L[0] *= il; L[1] *= il; L[2] *= il;
       const real ra = A.size[0] * fabs(dot3(a[0], L)) + A.size[1] * fabs(dot3(a[1], L)) + A.size[2] * fabs(dot3(a[2], L));
       const real rb = B.size[0] * fabs(dot3(b[0], L)) + B.size[1] * fabs(dot3(b[1], L)) + B.size[2] * fabs(dot3(b[2], L));
@@ -1025,7 +1026,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
 #pragma unroll
     for (int k = CL; k >= 1; k--) {
       const real hkk = row_bcast(h[k], k);
-      const real ihk = rcp_n(hkk);
+      const real ihk = rcp_piv(hkk);
       real hk[CL + 1], hkb[7];
 #pragma unroll
       for (int j = 1; j < k; j++) hk[j] = row_bcast(h[j], k);
@@ -1061,7 +1062,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
       for (int t = 0; t < 7; t++) lb[t] = hb[t];
     }
   } else if (lane == GM_LANE_PALM_F) {
-    const real ih = rcp_n(h[1]);
+    const real ih = rcp_piv(h[1]);
     real* pl = S.fs.plb;
 #pragma unroll
     for (int t = 0; t < 7; t++) { pl[7 + t] = hb[t]; hb[t] = hb[t] * ih; pl[t] = hb[t]; }
@@ -1115,7 +1116,7 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
     // border LDL^T: pivots 6 .. 0 (row 3 lanes 48 + k)
 #pragma unroll
     for (int k = 6; k >= 0; k--) {
-      const real ihk = rcp_n(row_bcast(hb[k], k));
+      const real ihk = rcp_piv(row_bcast(hb[k], k));
       real bk[7];
 #pragma unroll
       for (int j = 0; j < k; j++) bk[j] = row_bcast(hb[j], k);
@@ -1440,7 +1441,7 @@ __device__ __forceinline__ real euler_factor(const SharedT<CL>& S, const GmTopo*
   if (lane < 48) {
 #pragma unroll
     for (int k = CL; k >= 1; k--) {
-      const real ihk = rcp_n(row_bcast(L[k], k));
+      const real ihk = rcp_piv(row_bcast(L[k], k));
       real hk[CL + 1];
 #pragma unroll
       for (int j = 1; j < k; j++) hk[j] = row_bcast(L[j], k);
@@ -1459,7 +1460,7 @@ __device__ __forceinline__ real euler_factor(const SharedT<CL>& S, const GmTopo*
     for (int j = 1; j < CL; j++) L[j] = (j < p) ? L[j] * invd : L[j];
     lb = lb * invd;
   } else if (palm) {
-    const real ih = rcp_n(L[1]);
+    const real ih = rcp_piv(L[1]);
     ub = lb;
     lb = lb * ih;
     invd = ih;
@@ -1519,7 +1520,7 @@ __device__ __forceinline__ void euler_solve(SharedT<CL>& S, const GmTopo* __rest
     s2 += t2;
   }
   const real fs = ((readlane_real(s2, 15) + readlane_real(s2, 31)) + readlane_real(s2, 47)) + readlane_real(s2, 56);
-  const real xb = (yb0 - fs) * rcp_n(bb - sch);
+  const real xb = (yb0 - fs) * rcp_piv(bb - sch);
   // back substitution: D^-1, the border column, then the chains root -> leaf
   y = y * invd;
   y = y - lb * xb;

@@ -1007,6 +1007,16 @@ int gm_get_obs(gm_ctx* c, float* out, int on_device) {
   return GM_OK;
 }
 
+int gm_get_outputs(gm_ctx* c, float* obs, float* reward, uint8_t* done) {
+  if (!c || !obs || !reward || !done) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpyAsync(obs, c->d_obs, sizeof(float) * (size_t)c->n_envs * c->cfg.n_obs, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(reward, c->d_rew, sizeof(float) * (size_t)c->n_envs, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(done, c->d_done, (size_t)c->n_envs, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+
 int gm_get_reward_done(gm_ctx* c, float* reward, uint8_t* done, int on_device) {
   if (!c) return GM_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));

@@ -253,6 +253,7 @@ def _declare(lib):
         "gm_last_step_ms": (i32, [vp, f32p]),
         "gm_chunk_stats": (i32, [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
         "gm_dispatch_info": (i32, [vp, C.POINTER(C.c_int32)]),
+        "gm_get_outputs": (i32, [vp, vp, vp, vp]),
         "gm_chunk_timeline": (i32, [vp, C.POINTER(C.c_uint64), i32]),
         "gm_debug_substep": (i32, [vp, i32p, f64p, f64p, f64p, i32p, f64p]),
         "gm_step_profiled": (i32, [vp, C.POINTER(C.c_uint64)]),

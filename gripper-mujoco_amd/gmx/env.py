@@ -236,6 +236,12 @@ class BatchedGripperEnv:
         self._check(self.lib.gm_get_obs(self._ctx, self._obs.ctypes.data, 0))
         return self._obs.copy()
 
+    def outputs(self):
+        """(obs, reward, done) of the last env-step, one device read (gm_get_outputs)."""
+        self._check(self.lib.gm_get_outputs(self._ctx, self._obs.ctypes.data, self._rew.ctypes.data,
+                                            self._done.ctypes.data))
+        return self._obs.copy(), self._rew.copy(), self._done.astype(bool)
+
     def reward_done(self):
         self._check(self.lib.gm_get_reward_done(self._ctx, self._rew.ctypes.data, self._done.ctypes.data, 0))
         return self._rew.copy(), self._done.astype(bool)
@@ -248,8 +254,7 @@ class BatchedGripperEnv:
         else:
             self.set_action(actions)
         self.action_step()
-        obs = self.observation()
-        rew, term = self.reward_done()
+        obs, rew, term = self.outputs()
         trunc = self.current_step >= self.max_episode_steps
         term = np.where(trunc, False, term)
         return obs, rew, term, trunc

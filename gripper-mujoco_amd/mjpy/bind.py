@@ -252,7 +252,11 @@ class MjClass:
 
     # ------------------------------------------------------------ outputs
     def get_observation_numpy(self):
-        return self._ensure().observation()[0]
+        # one device read for the transition: the reward and done flag ride along for the
+        # is_done() / reward() calls MjEnv.step makes next (dropped by any other call)
+        obs, r, d = self._ensure().outputs()
+        self._rd = (float(r[0]), bool(d[0]))
+        return obs[0]
 
     def get_observation(self):
         return self.get_observation_numpy().tolist()

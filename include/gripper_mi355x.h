@@ -510,6 +510,9 @@ int  gm_step(gm_ctx* ctx);
 
 int  gm_get_obs(gm_ctx* ctx, float* out, int on_device);                 /* [n_envs x n_obs] */
 int  gm_get_reward_done(gm_ctx* ctx, float* reward, uint8_t* done, int on_device);
+/* The three at once into host buffers, one stream synchronisation (the facade's
+ * get_observation_numpy / is_done / reward of one transition). */
+int  gm_get_outputs(gm_ctx* ctx, float* obs, float* reward, uint8_t* done);
 /* EventTrack rows: [n_envs x (GM_N_BINARY + GM_N_LINEAR)] int32 `row`, and
  * `abs` counters; MjClass::get_event_state / EventTrack (bind.cpp:525-590). */
 int  gm_get_event_rows(gm_ctx* ctx, int32_t* rows, int32_t* abs_counts, float* last_values);

@@ -139,7 +139,7 @@ hipError_t launch_step(gm_ctx* c, int grid, int n_envs, int mode, DebugOut dbg, 
   if (chunked) grid = c->chunk_grid;
   // the env-step proper (not the settle, a diagnostic substep or a profiled step) on DUO
   // workgroups when the context chose them; the chunked grid was sized for that kernel
-  const bool duo = c->duo && mode == 0 && dbg.phase == nullptr;
+  const bool duo = c->duo && mode == 0;   // (a profiled step too: the owner wave's phase clocks)
   switch (c->model.n_seg) {
 #define X(N)                                                                                                 \
   case N:                                                                                                    \

@@ -2950,10 +2950,13 @@ __device__ __forceinline__ void step_kernel_body(SharedT<CL>& S,
   // a calibration run starts from a reset's mj_forward pose
   if (calib && lane < T->nlock) S.lock_pre[lane] = S.s.qpos[m->lock_dof[lane]];
   int ran;
-  if constexpr (DUO) {   // (no profiled DUO build: gm_step_profiled launches the one-wave kernel)
-    ran = substep_loop<CL, CAL, false, true>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
-                                             (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
-                                             false, nsub, settle, GmPreempt{});
+  if constexpr (DUO) {   // (profiled: the owner wave's clocks; its "collision" is the wait for the helper)
+    ran = prof ? substep_loop<CL, CAL, true, true>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
+                                                   (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
+                                                   prof, nsub, settle, GmPreempt{})
+               : substep_loop<CL, CAL, false, true>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
+                                                    (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
+                                                    false, nsub, settle, GmPreempt{});
   } else {
     ran = prof ? substep_loop<CL, CAL, true>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
                                              (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,

@@ -321,11 +321,13 @@ def cpu_baseline(gmx, n_envs: int, n_steps: int, n_threads: int):
                       f"done / 250 steps), {time.time() - t:.1f} s wall"}
 
 
-def policy_rollout(gmx, torch, dev, stream, n: int, steps: int, seed: int, env_offset: int):
+def policy_rollout(gmx, torch, dev, stream, n: int, steps: int, seed: int, env_offset: int, R: int = 10):
     """C5: the C3 workload with discrete actions chosen on the device by the
     DQN policy (VariableNetwork [63,150,100,50,8], eps-greedy) -- policy, env-step and
     auto-reset with no host round trip.  Returns env-steps/s and the policy kernel's
-    share of the step (HIP events on the shared stream)."""
+    share of the step (HIP events on the shared stream), driven per step (gm_policy_act,
+    gm_step, gm_autoreset_episodes) and fused into gm_policy_rollout launches of R env-steps
+    (each env's wave selects its own action; bit for bit the per-step sequence)."""
     s = gmx.canonical_settings(seed=seed)
     s.continous_actions = 0
     env = gmx.BatchedGripperEnv(n, object_set="set6_synthetic", settings=s, seed=seed, env_offset=env_offset,
@@ -357,6 +359,20 @@ def policy_rollout(gmx, torch, dev, stream, n: int, steps: int, seed: int, env_o
     out = {"value": round(n * steps / el, 1), "unit": "env-steps/s", "envs": n, "steps": steps,
            "ms_per_step": round(el / steps * 1e3, 3), "policy_select_ms": round(pol_ms, 4),
            "network": pol.sizes, "dtype": "f32 policy (MFMA) + f64 env"}
+    if R > 0:
+        t = 1 + steps
+        pol.rollout([gmx.eps_threshold(t + i) for i in range(R)], seed=seed, decision0=t)   # untimed: costs
+        t += R
+        n_l = 2
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n_l):
+            pol.rollout([gmx.eps_threshold(t + i) for i in range(R)], seed=seed, decision0=t)
+            t += R
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        out["fused_rollout"] = {"value": round(n * n_l * R / el, 1), "ms_per_step": round(el / (n_l * R) * 1e3, 3),
+                                "steps_per_launch": R, "launches": n_l}
     pol.close()
     env.close()
     return out
@@ -579,7 +595,7 @@ def main():
                                                                         R if rollout else 0)
         c1 = None if (args.no_c1 or world > 1) else c1_line(gmx, args.seed)
         c5 = None if (args.no_policy or world > 1) else policy_rollout(gmx, torch, dev, stream, n, max(3, K // 2), args.seed,
-                                                        first_env)
+                                                        first_env, R if rollout else 0)
         out = headline(world, n, K, W, elapsed, ep_stats)
         out["warmup_steps_run"] = max(w_drives, 1) * R
         out["config"].update({"workload": "C3: set6_synthetic 20 mixed objects, randomised spawn (object drawn per "

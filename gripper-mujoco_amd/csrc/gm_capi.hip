@@ -108,6 +108,11 @@ struct RolloutArgs {
   float jitter;
   int max_ep;
   gm_episode_end* rec;
+  // act_mode 2 (gm_policy_rollout): the packed network, its layout, eps per env-step
+  const float* pparams = nullptr;
+  GpNet pnet{};
+  const float* peps = nullptr;
+  uint64_t pdecision = 0;
 };
 hipError_t launch_step(gm_ctx* c, int grid, int n_envs, int mode, DebugOut dbg, const RolloutArgs* roll = nullptr) {
   // the full env-step (mode 0) runs in cost-sorted order and records each env's cost
@@ -135,6 +140,11 @@ hipError_t launch_step(gm_ctx* c, int grid, int n_envs, int mode, DebugOut dbg, 
     q.scene_tries = c->scene_tries;
     q.sr = c->spawn_rand;
     q.sr.env_offset = c->env_offset;   // (the driver's global env ids even without random spawns)
+    q.pparams = roll->pparams;
+    q.pnet = roll->pnet;
+    q.peps = roll->peps;
+    q.pseed = roll->act_seed;
+    q.pdecision = roll->pdecision;
   }
   if (chunked) grid = c->chunk_grid;
   // the env-step proper (not the settle, a diagnostic substep or a profiled step) on DUO
@@ -708,21 +718,26 @@ int gm_random_actions(gm_ctx* c, uint64_t seed, float* out, int on_device) {
   return GM_OK;
 }
 
+// the persistent rollout launch (gm_rollout, gm_policy_rollout) and the next launch's order
+static int rollout_launch(gm_ctx* c, const RolloutArgs& ra) {
+  DebugOut dbg{nullptr, nullptr, nullptr, nullptr, nullptr};
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  HIPCHK(c, launch_step(c, c->n_envs, c->n_envs, 0, dbg, &ra));
+  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  hipLaunchKernelGGL(gm_dispatch_order_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_cost, c->d_order, c->n_envs,
+                     c->d_chunk_ctr, c->d_chunk_st);
+  HIPCHK(c, hipGetLastError());
+  c->timed = true;
+  return GM_OK;
+}
+
 int gm_rollout(gm_ctx* c, int n_steps, const gm_rollout_params* p, gm_episode_end* records) {
   if (!c || !p || n_steps < 1 || (p->action_mode != 0 && p->action_mode != 1)) return GM_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
-  DebugOut dbg{nullptr, nullptr, nullptr, nullptr, nullptr};
   if (c->chunk > 0 && c->chunk_grid > 0) {
     // one persistent launch: every env runs its n_steps env-steps back to back
     const RolloutArgs ra{n_steps, p->action_mode, p->seed, p->jitter, p->max_episode_steps, records};
-    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    HIPCHK(c, launch_step(c, c->n_envs, c->n_envs, 0, dbg, &ra));
-    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-    hipLaunchKernelGGL(gm_dispatch_order_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_cost, c->d_order, c->n_envs,
-                       c->d_chunk_ctr, c->d_chunk_st);
-    HIPCHK(c, hipGetLastError());
-    c->timed = true;
-    return GM_OK;
+    return rollout_launch(c, ra);
   }
   // the one-shot kernel (GM_CHUNK_SUBSTEPS=0): the same sequence as per-step launches
   for (int k = 0; k < n_steps; k++) {
@@ -1230,6 +1245,8 @@ struct gm_policy {
   float* d_params = nullptr;
   int32_t* d_actions = nullptr;
   float* d_q = nullptr;
+  float* d_eps = nullptr;      // gm_policy_rollout's exploration thresholds, one per env-step
+  int eps_cap = 0;
 };
 
 static int64_t policy_layout(const int32_t* sizes, int n_sizes, GpNet* net) {
@@ -1310,6 +1327,7 @@ void gm_policy_destroy(gm_policy* p) {
   (void)hipFree(p->d_params);
   (void)hipFree(p->d_actions);
   (void)hipFree(p->d_q);
+  (void)hipFree(p->d_eps);
   delete p;
 }
 
@@ -1322,6 +1340,41 @@ int gm_policy_act(gm_policy* p, float eps, uint64_t seed, uint64_t decision) {
                      (long long)c->env_offset, p->d_params, p->net, eps, seed, decision, p->d_actions, p->d_q);
   HIPCHK(c, hipGetLastError());
   return gm_set_discrete_action(c, p->d_actions, 1);
+}
+
+int gm_policy_rollout(gm_policy* p, int n_steps, const float* eps, uint64_t seed, uint64_t decision0,
+                      int max_episode_steps, gm_episode_end* records) {
+  if (!p || !p->ctx || !eps || n_steps < 1) return GM_E_ARG;
+  gm_ctx* c = p->ctx;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (c->chunk > 0 && c->chunk_grid > 0) {
+    if (n_steps > p->eps_cap) {
+      // (the stream may still read the old buffer: wait before freeing it)
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      (void)hipFree(p->d_eps);
+      p->d_eps = nullptr;
+      p->eps_cap = 0;
+      HIPCHK(c, hipMalloc(&p->d_eps, sizeof(float) * (size_t)n_steps));
+      p->eps_cap = n_steps;
+    }
+    // (a pageable source: the copy is staged before the call returns, the caller may reuse eps)
+    HIPCHK(c, hipMemcpyAsync(p->d_eps, eps, sizeof(float) * (size_t)n_steps, hipMemcpyHostToDevice, c->stream));
+    RolloutArgs ra{n_steps, 2, seed, 0.0f, max_episode_steps, records};
+    ra.pparams = p->d_params;
+    ra.pnet = p->net;
+    ra.peps = p->d_eps;
+    ra.pdecision = decision0;
+    return rollout_launch(c, ra);
+  }
+  // the one-shot kernel (GM_CHUNK_SUBSTEPS=0): the per-step sequence it fuses
+  for (int k = 0; k < n_steps; k++) {
+    int rc = gm_policy_act(p, eps[k], seed, decision0 + (uint64_t)k);
+    if (rc == GM_OK) rc = gm_step(c);
+    if (rc == GM_OK) rc = gm_autoreset_episodes(c, max_episode_steps, nullptr, 1, nullptr,
+                                                records ? records + (size_t)k * c->n_envs : nullptr);
+    if (rc != GM_OK) return rc;
+  }
+  return GM_OK;
 }
 
 int gm_policy_read(gm_policy* p, int32_t* actions, float* q) {

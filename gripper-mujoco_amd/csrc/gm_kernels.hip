@@ -24,6 +24,7 @@
 #include <stdint.h>
 #include "gm_state.h"
 #include "gm_math.h"
+#include "gm_policy_net.h"
 
 #define NT 64
 // Phase boundary inside one env's physics.  Every kernel that runs the substep is launched
@@ -2574,6 +2575,12 @@ struct GmChunkQ {
   const gm_spawn_params* scene;
   GmSpawnRand sr;
   int steal;                 // an idle wave may resume a yielded env of another XCD
+  // act_mode 2: the DQN policy picks each env-step's discrete action on the env's own wave
+  // (gm_policy_rollout; gp_select_one = gm_policy_kernel's select_action for one env)
+  const float* pparams;      // packed network (gm_policy_pack layout)
+  GpNet pnet;
+  const float* peps;         // [steps] exploration threshold per env-step of the launch
+  uint64_t pseed, pdecision; // the policy's seed and the first env-step's decision index
 };
 __device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2775,7 +2782,19 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       if (cr.sub_done == 0 && q.act_mode >= 0) {
         // a new env-step of a rollout: the driver's actions first (they may add the
         // termination lift's substeps), as gm_set_action before gm_step
-        if (lane == 0) {
+        if (q.act_mode == 2) {
+          // gm_policy_act on this env alone: select_action from its current observation,
+          // then set_discrete_action (the LDS scratch: the dynamics union, dead between
+          // env-steps)
+          static_assert(sizeof(S.st) >= sizeof(float) * 2 * (GP_MAX_WIDTH + 4), "policy activations fit the union");
+          const int a = gp_select_one(obs + (size_t)env * C->n_obs, q.pparams, q.pnet, q.peps[cr.step_idx], q.pseed,
+                                      q.pdecision + (uint64_t)cr.step_idx, (uint64_t)(q.sr.env_offset + env),
+                                      reinterpret_cast<float*>(&S.st), lane);
+          if (lane == 0) {
+            set_action_one(S.s, m, C, a, 0.0f);
+            S.stp_fixed = 0;
+          }
+        } else if (lane == 0) {
           driver_actions(S.s, m, C, q.act_mode, q.act_seed, q.jitter, q.sr.env_offset + env);
           S.stp_fixed = 0;
         }

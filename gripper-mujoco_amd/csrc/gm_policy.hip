@@ -1,49 +1,7 @@
-// gm_policy.hip -- on-device DQN action selection for the batched env (SURVEY.md 8f,
-// rank 1: "fused on-device DQN inference").
-//
-// Reference: rl/networks.py:7-41 VariableNetwork.forward (Linear + ReLU per hidden
-// layer, a final Linear, Softmax over dim 1) and rl/agents/DQN.py:184-209
-// Agent_DQN.select_action (a uniform random action with probability eps_threshold,
-// otherwise policy_net(state).max(1)[1]).  The canonical network is
-// [n_obs = 63, 150, 100, 50, n_actions = 8] (launch_training.py:850-857).
-//
-// f32 throughout (torch's default dtype).  The layer products run on the f32-input MFMA
-// v_mfma_f32_16x16x4_f32, whose result is bit-for-bit a k-ordered fmaf chain.  One wave
-// handles a tile of 16 envs: activations live in LDS as [16 envs][width] f32 (ping-pong
-// between layers); weights are repacked on the host into B-fragment order -- for each
-// 16-output tile and 4-wide k step, 64 floats in lane order (lane l holds
-// W[16 t + (l & 15)][4 s + (l >> 4)]) -- so every MFMA's B operand is one coalesced
-// 256-byte load from L2 (the canonical network is 119 KB).  Zero padding in k and in
-// the output tiles keeps every lane's arithmetic defined.
+// gm_policy.hip -- the batched select_action kernel; network layout, MFMA forward and the
+// selection are in gm_policy_net.h (shared with gm_rollout's per-env policy driver).
 #pragma once
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-
-#define GP_MAX_LAYERS 8
-#define GP_MAX_WIDTH 256
-#define GP_TILE 16
-
-struct GpNet {
-  int n_layers;                   // Linear layers
-  int width[GP_MAX_LAYERS + 1];   // layer sizes: width[0] = n_obs, width[n_layers] = n_actions
-  int kpad[GP_MAX_LAYERS];        // width[l] rounded up to 4 (MFMA k step)
-  int tiles[GP_MAX_LAYERS];       // ceil(width[l + 1] / 16)
-  long long woff[GP_MAX_LAYERS];  // float offset of layer l's packed weights
-  long long boff[GP_MAX_LAYERS];  // float offset of layer l's bias (padded to tiles * 16)
-};
-
-typedef float gp_f32x4 __attribute__((ext_vector_type(4)));
-
-// counter-based uniform in [0, 1) and integer draws for epsilon-greedy: splitmix64 of
-// (seed, global env id, decision index) -- one independent stream per env, so actions do
-// not depend on how envs are sharded (the reference draws from one numpy Generator per
-// agent, which a batched device policy cannot reproduce draw for draw)
-__device__ __forceinline__ uint64_t gp_mix(uint64_t z) {
-  z += 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
+#include "gm_policy_net.h"
 
 __global__ __launch_bounds__(64) void gm_policy_kernel(const float* __restrict__ obs, int n_envs, long long env_offset,
                                                        const float* __restrict__ params, GpNet P, float eps,
@@ -87,28 +45,11 @@ __global__ __launch_bounds__(64) void gm_policy_kernel(const float* __restrict__
     __syncthreads();
     cur ^= 1;
   }
-  // softmax over the logits (nn.Softmax(dim=1)), then select_action: argmax (first
-  // maximum, like torch's max on CPU) or, with probability eps, a uniform random action
+  // softmax over the logits (nn.Softmax(dim=1)), then select_action (gp_choose)
   if (lane < GP_TILE && e0 + lane < n_envs) {
-    const int n_out = P.width[P.n_layers];
-    const float* x = act[cur][lane];
-    float m = x[0];
-    for (int j = 1; j < n_out; j++) m = fmaxf(m, x[j]);
-    float sum = 0.0f;
-    for (int j = 0; j < n_out; j++) sum += expf(x[j] - m);
-    int best = 0;
-    float qbest = -1.0f;
     const size_t env = (size_t)(e0 + lane);
-    for (int j = 0; j < n_out; j++) {
-      const float q = expf(x[j] - m) / sum;
-      if (qout) qout[env * n_out + j] = q;
-      if (q > qbest) { qbest = q; best = j; }
-    }
-    const uint64_t gid = (uint64_t)(env_offset + (long long)env);
-    const uint64_t h1 = gp_mix(seed ^ gp_mix(gid * 0x100000001B3ull + decision));
-    const uint64_t h2 = gp_mix(h1);
-    const float u = (float)((h1 >> 40) * (1.0 / 16777216.0));   // 24-bit uniform in [0, 1)
-    if (u < eps) best = (int)(h2 % (uint64_t)n_out);
-    actions[env] = best;
+    const int n_out = P.width[P.n_layers];
+    actions[env] = gp_choose(act[cur][lane], n_out, eps, seed, decision, (uint64_t)(env_offset + (long long)env),
+                             qout ? qout + env * n_out : nullptr);
   }
 }

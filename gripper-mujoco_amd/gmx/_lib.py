@@ -278,6 +278,7 @@ def _declare(lib):
         "gm_policy_pack": (C.c_int64, [i32p, i32, f32p, f32p]),
         "gm_policy_act": (i32, [vp, C.c_float, C.c_uint64, C.c_uint64]),
         "gm_policy_read": (i32, [vp, i32p, f32p]),
+        "gm_policy_rollout": (i32, [vp, i32, f32p, C.c_uint64, C.c_uint64, i32, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)

@@ -92,6 +92,18 @@ class DevicePolicy:
         if rc != 0:
             raise RuntimeError(self.lib.gm_last_error(self.env.ctx).decode() or f"gm_policy_act failed ({rc})")
 
+    def rollout(self, eps, seed: int = 0, decision0: int = 0, max_episode_steps: int | None = None,
+                records_dev_ptr: int | None = None):
+        """gm_policy_rollout: len(eps) rounds of act(eps[k], seed, decision0 + k) -> env step ->
+        auto-reset, fused into one persistent launch (bit for bit the per-step sequence).
+        records_dev_ptr: device [len(eps) x n_envs] gm_episode_end records (or None)."""
+        e = np.ascontiguousarray(np.atleast_1d(eps), dtype=np.float32)
+        mx = self.env.max_episode_steps if max_episode_steps is None else max_episode_steps
+        rc = self.lib.gm_policy_rollout(self._p, len(e), e.ctypes.data_as(C.POINTER(C.c_float)), C.c_uint64(seed),
+                                        C.c_uint64(decision0), int(mx), C.c_void_p(records_dev_ptr or 0))
+        if rc != 0:
+            raise RuntimeError(self.lib.gm_last_error(self.env.ctx).decode() or f"gm_policy_rollout failed ({rc})")
+
     def read(self):
         n, a = self.env.n_envs, self.env.n_actions
         acts = np.zeros(n, dtype=np.int32)

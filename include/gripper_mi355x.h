@@ -659,6 +659,18 @@ int  gm_policy_act(gm_policy* p, float eps, uint64_t seed, uint64_t decision);
 /* last selected actions [n_envs] int32 and softmax outputs [n_envs x n_actions] f32
  * (either may be NULL); host copies */
 int  gm_policy_read(gm_policy* p, int32_t* actions, float* q);
+/* A fused on-device DQN rollout: n_steps repetitions, for every env, of
+ *   gm_policy_act(p, eps[k], seed, decision0 + k) -> gm_step
+ *   -> gm_autoreset_episodes(max_episode_steps, spawn = NULL, records + k * n_envs)
+ * as ONE persistent launch of gm_rollout's kind: each env's own wave runs select_action on
+ * its observation (the batched kernel's MFMA tiles with the env in row 0 -- rows are
+ * independent, so the action is bit for bit the batched kernel's) before each env-step.
+ * Results (state, observations, records) equal the per-step sequence's bit for bit.
+ * eps: host array [n_steps] (copied before the call returns); records: device array
+ * [n_steps x n_envs] or NULL.  gm_policy_read's buffers are not written by the fused
+ * launch (they are under GM_CHUNK_SUBSTEPS=0, which runs the per-step sequence). */
+int  gm_policy_rollout(gm_policy* p, int n_steps, const float* eps, uint64_t seed, uint64_t decision0,
+                       int max_episode_steps, gm_episode_end* records);
 
 #ifdef __cplusplus
 }

@@ -21,14 +21,14 @@ HANDOFF = {"GM_CHUNK_SUBSTEPS": "1", "GM_CHUNK_MARGIN": "0", "GM_CHUNK_YIELDS": 
            "GM_CHUNK_GRID": "24"}
 
 
-def make_env(gm, env_vars=None):
+def make_env(gm, env_vars=None, n=N):
     import bench
     s = gm.canonical_settings(noise=True, seed=SEED)
     s.continous_actions = 0                                  # the DQN policy's discrete actions
     old = {k: os.environ.get(k) for k in (env_vars or {})}
     os.environ.update(env_vars or {})
     try:
-        env = gm.BatchedGripperEnv(N, object_set="set6_synthetic", settings=s, seed=SEED)
+        env = gm.BatchedGripperEnv(n, object_set="set6_synthetic", settings=s, seed=SEED)
     finally:
         for k, v in old.items():
             if v is None:
@@ -45,14 +45,14 @@ def eps_schedule(k0, k1):
     return np.array([0.9 if k % 3 == 0 else 0.2 for k in range(k0, k1)], dtype=np.float32)
 
 
-def per_step(env, pol, records, k0, k1):
+def per_step(env, pol, records, k0, k1, max_ep=MAX_EP):
     import torch
     acts = []
     for k in range(k0, k1):
         pol.act(float(eps_schedule(k, k + 1)[0]), seed=PSEED, decision=DEC0 + k)
         acts.append(pol.read()[0])
         env.lib.gm_step(env.ctx)
-        env.autoreset_device(0, None, max_episode_steps=MAX_EP, episodes_dev_ptr=records[k].data_ptr())
+        env.autoreset_device(0, None, max_episode_steps=max_ep, episodes_dev_ptr=records[k].data_ptr())
     torch.cuda.synchronize()
     return acts
 
@@ -129,3 +129,32 @@ def test_policy_rollout_greedy_differs_from_random(gm):
         a.close()
         b.close()
 
+
+
+def test_policy_rollout_equals_per_step_full_size(gm):
+    """The same identity at the headline batch (4096 envs, every XCD's queue busy), with
+    3-step episodes so every env resets inside the launch."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import torch
+    from gmx.policy import DevicePolicy
+    n, k, mx = 4096, 4, 3
+    ra = torch.zeros((k, n, 3), dtype=torch.int32, device="cuda")
+    rb = torch.zeros((k, n, 3), dtype=torch.int32, device="cuda")
+    a, b = make_env(gm, n=n), make_env(gm, n=n)
+    pa, pb = DevicePolicy(a, seed=5), DevicePolicy(b, seed=5)
+    try:
+        per_step(a, pa, ra, 0, k, max_ep=mx)
+        per_step(b, pb, rb, 0, 1, max_ep=mx)         # (b's dispatch costs from one env-step)
+        pb.rollout(eps_schedule(1, k), seed=PSEED, decision0=DEC0 + 1, max_episode_steps=mx,
+                   records_dev_ptr=rb[1:].data_ptr())
+        sa, sb = snapshot(a, ra), snapshot(b, rb)
+        assert sa[0] == sb[0]
+        for i in range(2, 6):
+            np.testing.assert_array_equal(sa[i], sb[i])
+        assert int((sa[5][..., 1] > 0).sum()) >= n      # every env's episode ended inside
+    finally:
+        pa.close()
+        pb.close()
+        a.close()
+        b.close()

@@ -25,13 +25,13 @@ HANDOFF = {"GM_CHUNK_SUBSTEPS": "1", "GM_CHUNK_MARGIN": "0", "GM_CHUNK_YIELDS": 
            "GM_CHUNK_GRID": "24"}
 
 
-def make_env(gm, env_vars=None):
+def make_env(gm, env_vars=None, n=N):
     import bench
     s = gm.canonical_settings(noise=True, seed=SEED)          # noise on: the RNG streams matter
     old = {k: os.environ.get(k) for k in (env_vars or {})}
     os.environ.update(env_vars or {})
     try:
-        env = gm.BatchedGripperEnv(N, object_set="set6_synthetic", settings=s, seed=SEED)
+        env = gm.BatchedGripperEnv(n, object_set="set6_synthetic", settings=s, seed=SEED)
     finally:
         for k, v in old.items():
             if v is None:
@@ -43,7 +43,7 @@ def make_env(gm, env_vars=None):
     return env
 
 
-def per_step(gm, env, mode, records, steps=K):
+def per_step(gm, env, mode, records, steps=K, max_ep=MAX_EP):
     import torch
     d_act = env.lib.gm_device_actions(env.ctx)
     for k in range(steps):
@@ -53,7 +53,7 @@ def per_step(gm, env, mode, records, steps=K):
             env.lib.gm_random_actions(env.ctx, SEED, d_act, 1)
         env.lib.gm_set_action(env.ctx, d_act, 1)
         env.lib.gm_step(env.ctx)
-        env.autoreset_device(0, None, max_episode_steps=MAX_EP, episodes_dev_ptr=records[k].data_ptr())
+        env.autoreset_device(0, None, max_episode_steps=max_ep, episodes_dev_ptr=records[k].data_ptr())
     torch.cuda.synchronize()
 
 
@@ -122,3 +122,31 @@ def test_random_actions_match_host_mirror(gm):
         assert out.min() >= -1.0 and out.max() < 1.0 and out.std() > 0.4
     finally:
         env.close()
+
+
+@pytest.mark.gpu
+def test_rollout_equals_per_step_api_full_size(gm):
+    """The identity at the headline batch (4096 envs on every XCD's queue, yields and
+    cross-XCD resumptions under the default dispatch), 3-step episodes so every env resets
+    inside the launch."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import torch
+    n, k, mx = 4096, 5, 3
+    ra = torch.zeros((k, n, 3), dtype=torch.int32, device="cuda")
+    rb = torch.zeros((k, n, 3), dtype=torch.int32, device="cuda")
+    a, b = make_env(gm, n=n), make_env(gm, n=n)
+    try:
+        per_step(gm, a, 0, ra, steps=k, max_ep=mx)
+        per_step(gm, b, 0, rb, steps=1, max_ep=mx)     # (b's dispatch costs from one env-step)
+        b.rollout(k - 1, action_mode=0, seed=SEED, jitter=0.2, max_episode_steps=mx, records_dev_ptr=rb[1:].data_ptr())
+        sa, sb = snapshot(a, ra), snapshot(b, rb)
+        assert sa[0] == sb[0]
+        for i in range(2, 6):
+            np.testing.assert_array_equal(sa[i], sb[i])
+        assert int((sa[5][..., 1] > 0).sum()) >= n
+        st = b.chunk_stats()
+        assert st["finished"] == n and st["yields"] > 0, st
+    finally:
+        a.close()
+        b.close()

@@ -2046,6 +2046,18 @@ struct GmPreempt {
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Claim the next entry of a yielded-env bucket (head at b[0], tail at b[1]; lane 0): the head
+// advances only while it is below the tail, so every claimed slot was reserved by a producer
+// that is about to store it -- two waves that saw the same last entry cannot both claim, and
+// the loser parks on no slot that a future yield would have to fill.  Returns the slot or -1.
+__device__ __forceinline__ int64_t claim_bucket(uint32_t* b) {
+  uint32_t h = ld_agent(b);
+  for (;;) {
+    if (h >= ld_agent(b + 1)) return -1;
+    if (__hip_atomic_compare_exchange_strong(b, &h, h + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      return (int64_t)h;
+  }
+}
 // returns the substeps run (nsub unless the preemption test yielded).  PROF = false
 // compiles the per-phase clock reads (PH) out: no uniform branch at every phase boundary,
 // so the scheduler's regions span them (the env-step kernel's chunked path runs this one)
@@ -2669,21 +2681,27 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
         take_c = e == 0ull || (uint32_t)(e >> 32) >= cost[order[fh]];
       }
       if (take_c) {
+        int got = 0;
         if (lane == 0) {
           uint64_t* rb = ring + (size_t)bsel * q.cap;
-          const uint32_t i = add_agent(bq + bsel * 32, 1u) % (uint32_t)q.cap;
-          uint64_t v;
-          // acquire: pairs with the producer's release store of this entry
-          while ((v = __hip_atomic_load(rb + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0ull &&
-                 ld_agent(n_done) < n)
-            __builtin_amdgcn_s_sleep(2);
-          if (v != 0ull) {
-            st_agent(rb + i, 0ull);
-            add_agent(q.ctr + GM_CQ_DONE + 2, 1u);
-            pick = (int)(uint32_t)v - 1;
+          const int64_t c = claim_bucket(bq + bsel * 32);
+          if (c >= 0) {
+            got = 1;
+            const uint32_t i = (uint32_t)c % (uint32_t)q.cap;
+            uint64_t v;
+            // acquire: pairs with the producer's release store of this entry
+            while ((v = __hip_atomic_load(rb + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0ull &&
+                   ld_agent(n_done) < n)
+              __builtin_amdgcn_s_sleep(2);
+            if (v != 0ull) {
+              st_agent(rb + i, 0ull);
+              add_agent(q.ctr + GM_CQ_DONE + 2, 1u);
+              pick = (int)(uint32_t)v - 1;
+            }
           }
         }
-        break;                             // pick < 0: everything finished while waiting
+        if (__builtin_amdgcn_readfirstlane(got)) break;   // pick < 0: everything finished while waiting
+        continue;                                          // the entry went to another wave: poll again
       }
       if (have_f) {
         if (lane == 0) {
@@ -2714,22 +2732,27 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
             const unsigned long long m8 = ml & (0x0101010101010101ull << r);
             if (m8) { src = (int)__builtin_ctzll(m8) >> 3; sb = 7 - r; }
           }
+          int got = 0;
           if (lane == 0) {
             uint32_t* sbq = q.ctr + src * GM_CQ_NB * 32;
             uint64_t* rb = q.ring + (size_t)src * GM_CQ_NB * q.cap + (size_t)sb * q.cap;
-            const uint32_t i = add_agent(sbq + sb * 32, 1u) % (uint32_t)q.cap;
-            uint64_t v;
-            while ((v = __hip_atomic_load(rb + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0ull &&
-                   ld_agent(n_done) < n)
-              __builtin_amdgcn_s_sleep(2);
-            if (v != 0ull) {
-              st_agent(rb + i, 0ull);
-              add_agent(q.ctr + GM_CQ_DONE + 2, 1u);
-              add_agent(q.ctr + GM_CQ_DONE + 4, 1u);   // steals
-              pick = (int)(uint32_t)v - 1;
+            const int64_t c = claim_bucket(sbq + sb * 32);
+            if (c >= 0) {
+              got = 1;
+              const uint32_t i = (uint32_t)c % (uint32_t)q.cap;
+              uint64_t v;
+              while ((v = __hip_atomic_load(rb + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0ull &&
+                     ld_agent(n_done) < n)
+                __builtin_amdgcn_s_sleep(2);
+              if (v != 0ull) {
+                st_agent(rb + i, 0ull);
+                add_agent(q.ctr + GM_CQ_DONE + 2, 1u);
+                add_agent(q.ctr + GM_CQ_DONE + 4, 1u);   // steals
+                pick = (int)(uint32_t)v - 1;
+              }
             }
           }
-          break;                           // pick < 0: everything finished while waiting
+          if (__builtin_amdgcn_readfirstlane(got)) break;   // pick < 0: everything finished while waiting
         }
       }
       if (__builtin_amdgcn_readfirstlane(ld_agent(n_done)) >= n) break;

@@ -16,11 +16,14 @@ Workload = BASELINE.json configs[2] ("C3"): 4096 envs per GPU, 20-object synthet
 set6-like mixed set, randomised spawn (MjEnv._spawn_object: object drawn per episode,
 spawn_into_scene grid search), at STEADY STATE: before the timed region
 (and independent of --warmup) the batch is pre-rolled untimed so that the envs are spread
-uniformly over episode steps 1..250, driven by the scripted grasp mix (close, squeeze,
-palm press, lift, with jitter), so grasp contacts, done flags and resets all fall inside
-the timed window.  N GPUs run N x 4096 envs sharded by env id (weak scaling); the only
-collective is an RCCL all-gather of the per-env episode-end records (return, length,
-success) each step.
+uniformly over episode steps 1..250, driven by the benchmark mix (gm_program_actions mode
+4): in 1 episode of 4 per env the closed-loop grasp-lift-hold program (close, squeeze, lift,
+palm onto the object, hold -- it reaches the reference's successful_grasp on spheres), the
+scripted grasp mix (close, squeeze, palm press, lift, with jitter) in the others, so grasp
+contacts, lifts, successes, done flags and resets all fall inside the timed window.  N GPUs
+run N x 4096 envs sharded by env id (weak scaling); the only collective is an RCCL
+all-gather of the per-env episode-end records (return, length, success) of every env-step
+(SURVEY.md 8e): a launch of R env-steps is followed by its R per-env-step gathers.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -47,6 +50,7 @@ METRIC = "env-steps/sec (batched rollout) at 4096 envs; obs max-rel-err vs C++ r
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM")
 NCON_NOMINAL = 12              # SURVEY.md 8d nominal contacts per env-substep
 MAX_EP = 250                   # baseline yaml env.max_episode_steps
+DRIVER_MODE = 4                # gm_program_actions: grasp program in 1 episode of 4, scripted mix otherwise
 
 
 def algorithmic_bytes_per_substep(model, ncon: int = NCON_NOMINAL) -> dict:
@@ -94,17 +98,50 @@ def load_traffic(n_envs: int, steps_per_launch: int):
     return None, None
 
 
+FP64_VECTOR_PEAK_TFS = 78.6    # half the FP32 vector peak (157.3 TF, MI355X_MICROARCH.md); not in the guide
+
+
+def load_compute(n_envs: int, substeps: int, steps_per_launch: int, launch_s: float):
+    """The bound that applies to the step kernel (VALU issue / dependent latency, not HBM):
+    fp64 VALU work per env-substep and lane utilisation from the committed rocprofv3 SQ
+    counter pass of the same workload (profiles/pmc_sq_c3.json), and the fp64 rate they give
+    at this run's launch time."""
+    path = os.path.join(REPO, "profiles", "pmc_sq_c3.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        pe = d["per_env_substep"]
+        util = float(d["valu_lane_utilisation"])
+    except (OSError, ValueError, KeyError):
+        return None
+    fma, add, mul = pe["SQ_INSTS_VALU_FMA_F64"], pe["SQ_INSTS_VALU_ADD_F64"], pe["SQ_INSTS_VALU_MUL_F64"]
+    flop_substep = (2 * fma + add + mul) * 64 * util          # active lanes per wave instruction
+    flop_launch = flop_substep * n_envs * substeps * steps_per_launch
+    rate = flop_launch / launch_s / 1e12
+    return {"bound": "fp64 VALU issue / dependent latency (2 waves per SIMD, LDS-resident working set)",
+            "valu_insts_per_env_substep": pe["SQ_INSTS_VALU"],
+            "fp64_fma_add_mul_per_env_substep": [fma, add, mul],
+            "salu_insts_per_env_substep": pe.get("SQ_INSTS_SALU"),
+            "lds_insts_per_env_substep": pe.get("SQ_INSTS_LDS"),
+            "valu_lane_utilisation": util,
+            "wave_cycle_fractions": d.get("wave_cycle_fractions"),
+            "lds_bank_conflict_cycles_per_launch": d.get("per_launch", {}).get("SQ_LDS_BANK_CONFLICT"),
+            "fp64_flop_per_launch": flop_launch, "achieved_fp64_tflops": round(rate, 3),
+            "fp64_vector_peak_tflops": FP64_VECTOR_PEAK_TFS, "frac": round(rate / FP64_VECTOR_PEAK_TFS, 4),
+            "source": d.get("source", path)}
+
+
 def obs_parity(gmx, env, seed: int):
     """obs max-rel-err of the GPU path vs the fp64 oracle ON THE BENCHMARK'S OWN STATES
     (rel over |ref| >= 1e-3, abs elsewhere): the whole batch's fp64 state
     after the timed window is handed to the oracle (gm_get_env_states -> or_import_state),
-    and both run the next env-step of the scripted mix.  Done flags and event rows are
-    compared bit for bit."""
+    and both run the next env-step of the benchmark mix (the device's driver actions).  Done
+    flags and event rows are compared bit for bit."""
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib
     rec = env.env_states()
-    a = env.scripted_actions(seed)
+    a = env.program_actions(seed, 0.2, 4)
     env.set_action(a)
     env.action_step()
     obs = env.observation()
@@ -299,8 +336,8 @@ def host_cpu_model() -> str:
 def cpu_baseline(gmx, n_envs: int, n_steps: int, n_threads: int):
     """The fp64 CPU oracle on the host cores: envs are independent (one env
     per thread, as the reference runs one env per process), spread over n_threads; the
-    same workload as the GPU line (scripted grasp mix, device-identical spawn draws,
-    resets at done / 250 steps)."""
+    same workload as the GPU line (the benchmark mix, device-identical spawn draws and
+    driver decisions, resets at done / 250 steps)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib
     s = gmx.canonical_settings(seed=1234)
@@ -317,7 +354,8 @@ def cpu_baseline(gmx, n_envs: int, n_steps: int, n_threads: int):
                           "16 there and worker pools must stay within it); the other visible CPUs belong to "
                           "other jobs, so 16 threads is every core this job may use",
             "sample": f"fp64 C oracle (oracle/oracle.c, gcc -O2 -mavx), {n_threads} thread(s), {n_envs} envs x "
-                      f"{n_steps} env-steps of the C3 workload (set6_synthetic, scripted grasp mix, resets at "
+                      f"{n_steps} env-steps of the C3 workload (set6_synthetic, the benchmark mix: grasp program / "
+                      f"scripted grasp mix, resets at "
                       f"done / 250 steps), {time.time() - t:.1f} s wall"}
 
 
@@ -382,22 +420,26 @@ def measure(drive, episodes, K: int, W: int, world: int, dev, sync):
     """The contract's timed region, independent of what steps the envs (the device here,
     the oracle in tests/test_distributed.py): W untimed warmup drives, then EXACTLY K
     drives bracketed by sync + barrier + sync on both sides; the wall time is the MAX over
-    ranks.  Every drive's episode-end records (return, length, success per env:
-    gm_episode_end) are all-gathered -- the one collective, SURVEY.md 8e -- and the finished
-    episodes, their successes and their lengths summed over the whole job.  drive(k) takes
-    the timed index k (None when untimed); `episodes` is the [n, 3] int32 record buffer the
+    ranks.  Every env-step's episode-end records (return, length, success per env:
+    gm_episode_end) are all-gathered -- the one collective, SURVEY.md 8e, once per env-step
+    also when a drive runs R env-steps in one launch -- and the finished episodes, their
+    successes and their lengths summed over the whole job.  drive(k) takes the timed index k
+    (None when untimed); `episodes` is the [R, n, 3] (or [n, 3]) int32 record buffer the
     drive's auto-reset writes (length 0 where an env's episode did not end)."""
     import torch
     import torch.distributed as dist
     from gmx.shard import gather_episodes, max_over_ranks, unpack_episodes
     tally = torch.zeros(3, device=dev, dtype=torch.int64)   # episodes, successes, length sum
 
+    recs = episodes if episodes.dim() == 3 else episodes.unsqueeze(0)
+
     def step(k=None):
         drive(k)
-        _, length, success = unpack_episodes(gather_episodes(episodes, world))
-        tally[0] += (length > 0).sum()
-        tally[1] += success.sum()
-        tally[2] += length.sum()
+        for r in range(recs.shape[0]):          # one gather per env-step of the drive
+            _, length, success = unpack_episodes(gather_episodes(recs[r], world))
+            tally[0] += (length > 0).sum()
+            tally[1] += success.sum()
+            tally[2] += length.sum()
 
     # warmup counts episodes too, so every kernel the timed loop launches (incl. torch's
     # reductions for the tally) is loaded before the clock starts
@@ -498,7 +540,7 @@ def main():
     def drive_ps(timed=None, rec=None):
         """one MjEnv.step-equivalent for the whole batch through the per-step API, all on the
         device (driver actions, set_action, step, auto-reset: five launches)"""
-        env.lib.gm_scripted_actions(env.ctx, args.seed, 0.2, d_act, 1)
+        env.lib.gm_program_actions(env.ctx, args.seed, 0.2, DRIVER_MODE, d_act, 1)
         env.lib.gm_set_action(env.ctx, d_act, 1)
         if timed is not None:
             ev[timed][0].record(stream)
@@ -514,7 +556,7 @@ def main():
             return
         if timed is not None:
             ev[timed][0].record(stream)
-        env.rollout(R, 0, args.seed, 0.2, MAX_EP, episodes.data_ptr())
+        env.rollout(R, DRIVER_MODE, args.seed, 0.2, MAX_EP, episodes.data_ptr())
         if timed is not None:
             ev[timed][1].record(stream)
 
@@ -529,7 +571,7 @@ def main():
             env.lib.gm_reset(env.ctx, np.ascontiguousarray(m.astype(np.uint8)).ctypes.data_as(
                 __import__("ctypes").POINTER(__import__("ctypes").c_uint8)), None)
         drive_ps()
-    elapsed, ep_stats = measure(drive, episodes.view(-1, 3), n_drives, w_drives, world, dev, torch.cuda.synchronize)
+    elapsed, ep_stats = measure(drive, episodes, n_drives, w_drives, world, dev, torch.cuda.synchronize)
     steps_view = gmx.env_state_view(env.env_states())["num_action_steps"]
 
     kern_ms = [a.elapsed_time(b) for a, b in ev[:n_drives]]
@@ -547,7 +589,7 @@ def main():
         ps_k = sum(a.elapsed_time(b) for a, b in ev[:K]) / K
         per_step_api = {"ms_per_step": round(ps_s * 1e3, 3), "value": round(n / ps_s, 1), "unit": "env-steps/s",
                         "step_kernel_ms": round(ps_k, 4),
-                        "path": "gm_scripted_actions + gm_set_action + gm_step + gm_autoreset_episodes per env-step"}
+                        "path": "gm_program_actions + gm_set_action + gm_step + gm_autoreset_episodes per env-step"}
     finite = bool(torch.isfinite(torch.as_tensor(env.observation())).all())
     overflow = int(env.overflow().sum())
     parity = None if (args.no_parity or rank != 0) else obs_parity(gmx, env, args.seed)
@@ -570,15 +612,22 @@ def main():
     if rank == 0:
         B = algorithmic_bytes_per_substep(env.model)
         Bm = algorithmic_bytes_per_substep(env.model, ncon=int(round(float(ncon_m.mean()))))
-        bytes_per_launch = n * S * B["bytes"]
-        achieved = bytes_per_launch / kern_avg_s / 1e9
+        # bytes and traffic both per LAUNCH (R env-steps of every env); per env-step = / R
+        bytes_per_env_step = n * S * B["bytes"]
+        bytes_per_launch = bytes_per_env_step * R
+        achieved = bytes_per_launch / kern_launch_s / 1e9
         traffic, traffic_src = load_traffic(n, R)
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "per": "launch (R env-steps of the whole batch): achieved = algorithmic_bytes_per_launch / "
+                       "kernel_launch_ms; traffic = PMC HBM bytes per launch",
                 "kernel": "gm_step_kernel", "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
                 # one launch runs R env-steps of every env (gm_rollout); per-step = launch / R
                 "kernel_launch_ms": round(kern_launch_s * 1e3, 4), "env_steps_per_launch": R,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
+                "algorithmic_bytes_per_env_step": bytes_per_env_step,
+                "traffic_per_env_step": None if traffic is None else traffic / R,
+                "compute": load_compute(n, S, R, kern_launch_s),
                 "traffic_source": traffic_src,
                 "traffic_measured_in_this_run": False,   # PMC counters need their own rocprofv3 pass
                 # the same roofline with the per-substep bytes at the batch's measured mean
@@ -600,8 +649,10 @@ def main():
         out["warmup_steps_run"] = max(w_drives, 1) * R
         out["config"].update({"workload": "C3: set6_synthetic 20 mixed objects, randomised spawn (object drawn per "
                                    "episode, spawn_into_scene grid search on the device), steady state: envs "
-                                   "staggered over episode steps 1..250 by an untimed pre-roll, scripted grasp "
-                                   "mix (close / squeeze / palm / lift + jitter), canonical sensor/reward "
+                                   "staggered over episode steps 1..250 by an untimed pre-roll, benchmark mix "
+                                   "(1 episode in 4: the closed-loop grasp-lift-hold program; otherwise the "
+                                   "scripted grasp mix: close / squeeze / palm / lift + jitter), canonical "
+                                   "sensor/reward "
                                    "config, device auto-reset at done / 250 steps; driven as gm_rollout launches "
                                    f"of {R} env-steps (driver actions, env-step, episode-end record and reset "
                                    "fused per env; bit-identical to the per-step API, tests/test_rollout.py)"

@@ -39,6 +39,7 @@ struct gm_ctx {
   hipStream_t own_stream = nullptr;    // the one gm_create made (destroyed with the ctx)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
+  int last_launch_steps = 1;           // env-steps per env of the last timed launch
   gm_model model;
   gm_config cfg;
   GmTopo topo;
@@ -60,6 +61,10 @@ struct gm_ctx {
   hipEvent_t stage_ev = nullptr;
   int32_t* d_dact = nullptr;
   uint8_t* d_mask = nullptr;
+  // scratch of the force-measurement calls (gm_set_motor_target's targets and flags,
+  // gm_get_sensor_si's readings): allocated once with the context, no per-call hipMalloc /
+  // hipFree (a hipFree synchronises the whole device)
+  void* d_scratch = nullptr;
   gm_spawn* d_spawn = nullptr;
   int32_t* d_order = nullptr;          // workgroup -> env dispatch order (cost-sorted)
   uint32_t* d_cost = nullptr;          // per-env cost of the last env-step (clocks / 64)
@@ -392,6 +397,8 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   c->stage_bytes = std::max(sizeof(float) * (size_t)n_envs * GM_ACTION_CODE_COUNT, sizeof(int32_t) * (size_t)n_envs);
   HIPCHK(c, hipHostMalloc(&c->h_stage, c->stage_bytes, hipHostMallocDefault));
   HIPCHK(c, hipMalloc(&c->d_state, sizeof(GmEnvState) * (size_t)n_envs));
+  HIPCHK(c, hipMalloc(&c->d_scratch, std::max(sizeof(double) * 3 * (size_t)n_envs + (size_t)n_envs + 16,
+                                              sizeof(float) * 5 * (size_t)n_envs)));
   HIPCHK(c, hipMalloc(&c->d_model, sizeof(gm_model)));
   HIPCHK(c, hipMalloc(&c->d_cfg, sizeof(gm_config)));
   HIPCHK(c, hipMalloc(&c->d_topo, sizeof(GmTopo)));
@@ -508,7 +515,7 @@ void gm_destroy(gm_ctx* c) {
   if (c->h_stage) (void)hipHostFree(c->h_stage);
   if (c->stage_ev) (void)hipEventDestroy(c->stage_ev);
   (void)hipFree(c->d_eq); (void)hipFree(c->d_obs); (void)hipFree(c->d_rew); (void)hipFree(c->d_done); (void)hipFree(c->d_act);
-  (void)hipFree(c->d_dact); (void)hipFree(c->d_mask); (void)hipFree(c->d_spawn);
+  (void)hipFree(c->d_dact); (void)hipFree(c->d_mask); (void)hipFree(c->d_spawn); (void)hipFree(c->d_scratch);
   (void)hipFree(c->d_order); (void)hipFree(c->d_cost); (void)hipFree(c->d_scene);
   (void)hipFree(c->d_chunk_ctr); (void)hipFree(c->d_chunk_ring); (void)hipFree(c->d_chunk_carry);
   (void)hipFree(c->d_chunk_st);
@@ -571,10 +578,8 @@ int gm_set_motor_target(gm_ctx* c, const uint8_t* mask, const double* xyz, int n
   const size_t n = (size_t)c->n_envs;
   const uint8_t* dm = nullptr;
   if (mask) { HIPCHK(c, hipMemcpyAsync(c->d_mask, mask, n, hipMemcpyHostToDevice, c->stream)); dm = c->d_mask; }
-  double* d_xyz = nullptr;
-  uint8_t* d_ok = nullptr;
-  HIPCHK(c, hipMalloc(&d_xyz, sizeof(double) * 3 * (size_t)n_xyz));
-  HIPCHK(c, hipMalloc(&d_ok, n));
+  double* d_xyz = static_cast<double*>(c->d_scratch);
+  uint8_t* d_ok = reinterpret_cast<uint8_t*>(d_xyz + 3 * n);
   HIPCHK(c, hipMemcpyAsync(d_xyz, xyz, sizeof(double) * 3 * (size_t)n_xyz, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(d_ok, 1, n, c->stream));
   int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
@@ -582,9 +587,7 @@ int gm_set_motor_target(gm_ctx* c, const uint8_t* mask, const double* xyz, int n
                      n_xyz == c->n_envs ? 1 : 0, d_ok, c->n_envs);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess && in_limits) e = hipMemcpyAsync(in_limits, d_ok, n, hipMemcpyDeviceToHost, c->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  (void)hipFree(d_xyz);
-  (void)hipFree(d_ok);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);   // xyz / in_limits: host arrays
   HIPCHK(c, e);
   return GM_OK;
 }
@@ -593,14 +596,12 @@ int gm_get_sensor_si(gm_ctx* c, float* out) {
   if (!c || !out) return GM_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   const size_t n = (size_t)c->n_envs;
-  float* d_out = nullptr;
-  HIPCHK(c, hipMalloc(&d_out, sizeof(float) * 5 * n));
+  float* d_out = static_cast<float*>(c->d_scratch);
   int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
   hipLaunchKernelGGL(gm_sensor_si_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, d_out, c->n_envs);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, sizeof(float) * 5 * n, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  (void)hipFree(d_out);
   HIPCHK(c, e);
   return GM_OK;
 }
@@ -702,6 +703,22 @@ int gm_scripted_actions(gm_ctx* c, uint64_t seed, float jitter, float* out, int 
   return GM_OK;
 }
 
+int gm_program_actions(gm_ctx* c, uint64_t seed, float jitter, int mode, float* out, int on_device) {
+  if (!c || !out || (mode != 3 && mode != 4)) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  float* d = on_device ? out : c->d_act;
+  int threads = 64, blocks = (c->n_envs + threads - 1) / threads;
+  hipLaunchKernelGGL(gm_program_action_kernel, dim3(blocks), dim3(threads), 0, c->stream, c->d_state, c->d_model,
+                     c->d_cfg, d, c->n_envs, seed, (long long)c->env_offset, jitter, mode);
+  HIPCHK(c, hipGetLastError());
+  if (!on_device) {
+    HIPCHK(c, hipMemcpyAsync(out, d, sizeof(float) * (size_t)c->n_envs * c->cfg.n_actions, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return GM_OK;
+}
+
 int gm_random_actions(gm_ctx* c, uint64_t seed, float* out, int on_device) {
   if (!c || !out) return GM_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
@@ -728,11 +745,14 @@ static int rollout_launch(gm_ctx* c, const RolloutArgs& ra) {
                      c->d_chunk_ctr, c->d_chunk_st);
   HIPCHK(c, hipGetLastError());
   c->timed = true;
+  c->last_launch_steps = ra.steps;
   return GM_OK;
 }
 
 int gm_rollout(gm_ctx* c, int n_steps, const gm_rollout_params* p, gm_episode_end* records) {
-  if (!c || !p || n_steps < 1 || (p->action_mode != 0 && p->action_mode != 1)) return GM_E_ARG;
+  if (!c || !p || n_steps < 1 ||
+      (p->action_mode != 0 && p->action_mode != 1 && p->action_mode != 3 && p->action_mode != 4))
+    return GM_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   if (c->chunk > 0 && c->chunk_grid > 0) {
     // one persistent launch: every env runs its n_steps env-steps back to back
@@ -742,7 +762,8 @@ int gm_rollout(gm_ctx* c, int n_steps, const gm_rollout_params* p, gm_episode_en
   // the one-shot kernel (GM_CHUNK_SUBSTEPS=0): the same sequence as per-step launches
   for (int k = 0; k < n_steps; k++) {
     int rc = p->action_mode == 0 ? gm_scripted_actions(c, p->seed, p->jitter, c->d_act, 1)
-                                 : gm_random_actions(c, p->seed, c->d_act, 1);
+             : p->action_mode == 1 ? gm_random_actions(c, p->seed, c->d_act, 1)
+                                   : gm_program_actions(c, p->seed, p->jitter, p->action_mode, c->d_act, 1);
     if (rc == GM_OK) rc = gm_set_action(c, c->d_act, 1);
     if (rc == GM_OK) rc = gm_step(c);
     if (rc == GM_OK) rc = gm_autoreset_episodes(c, p->max_episode_steps, nullptr, 1, nullptr,
@@ -974,6 +995,17 @@ int gm_step(gm_ctx* c) {
                      c->d_chunk_ctr, c->d_chunk_st);
   HIPCHK(c, hipGetLastError());
   c->timed = true;
+  c->last_launch_steps = 1;
+  return GM_OK;
+}
+
+int gm_chunk_claim_waits(gm_ctx* c, uint32_t* out2) {
+  if (!c || !out2) return GM_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  uint32_t w[2];
+  HIPCHK(c, hipMemcpyAsync(w, c->d_chunk_ctr + GM_CQ_LAST + 37, sizeof(w), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  out2[0] = w[0]; out2[1] = w[1];
   return GM_OK;
 }
 
@@ -1002,7 +1034,7 @@ int gm_chunk_timeline(gm_ctx* c, uint64_t* out, int max_out) {
 
 int gm_dispatch_info(const gm_ctx* c, int32_t* out) {
   if (!c || !out) return GM_E_ARG;
-  out[0] = c->chunk; out[1] = c->chunk_grid; out[2] = c->duo ? 2 : 1; out[3] = 0;
+  out[0] = c->chunk; out[1] = c->chunk_grid; out[2] = c->duo ? 2 : 1; out[3] = c->last_launch_steps;
   return GM_OK;
 }
 
@@ -1357,8 +1389,19 @@ int gm_policy_rollout(gm_policy* p, int n_steps, const float* eps, uint64_t seed
       HIPCHK(c, hipMalloc(&p->d_eps, sizeof(float) * (size_t)n_steps));
       p->eps_cap = n_steps;
     }
-    // (a pageable source: the copy is staged before the call returns, the caller may reuse eps)
-    HIPCHK(c, hipMemcpyAsync(p->d_eps, eps, sizeof(float) * (size_t)n_steps, hipMemcpyHostToDevice, c->stream));
+    // eps is the caller's (pageable) array: stage it through the ctx's pinned buffer so the
+    // copy owns its bytes before the call returns (stage_ev: the previous staging copy has
+    // left the buffer), or copy and wait when it does not fit
+    const size_t eb = sizeof(float) * (size_t)n_steps;
+    if (eb <= c->stage_bytes) {
+      HIPCHK(c, hipEventSynchronize(c->stage_ev));
+      std::memcpy(c->h_stage, eps, eb);
+      HIPCHK(c, hipMemcpyAsync(p->d_eps, c->h_stage, eb, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipEventRecord(c->stage_ev, c->stream));
+    } else {
+      HIPCHK(c, hipMemcpyAsync(p->d_eps, eps, eb, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
     RolloutArgs ra{n_steps, 2, seed, 0.0f, max_episode_steps, records};
     ra.pparams = p->d_params;
     ra.pnet = p->net;

@@ -527,14 +527,23 @@ int gm_build_model(const gm_model_params* p, gm_model* m) {
 
   // ---- palm: slide "palm_prismatic_joint" along -z; palm z=0 is 165 mm above the
   //      finger end (fingerend_to_palm_Z, myfunctions.cpp:3636) ----
+  //      palm body frame: x along the gripper axis pointing up (away from the palm face),
+  //      y = world y, z = x cross y, so palm_local[0] is the axial force ("+ve for
+  //      compression", mjclass.cpp:1010; the palm sensor reads it, mjclass.cpp:826) --
+  //      not a horizontal component.  MuJoCo orders a pair by geom type, so a sphere or
+  //      cylinder object is geom1 of the palm pair and the pair's force is the one on the
+  //      palm (up: +ve); a box object (same type, higher index) is geom2 and reads -ve.
   {
     double in[3];
-    box_inertia(0.1, 0.03, 0.03, 0.004, in);
-    m->body_palm = B.add_body(m->body_base, GM_GRP_PALM, zero3, id4, 0.1, zero3, in);
-    double ax[3] = {0, 0, -1};
+    box_inertia(0.1, 0.004, 0.03, 0.03, in);
+    const double Rp[9] = {0, 0, -1, 0, 1, 0, 1, 0, 0};
+    double qp[4];
+    quat_from_mat(Rp, qp);
+    m->body_palm = B.add_body(m->body_base, GM_GRP_PALM, zero3, qp, 0.1, zero3, in);
+    double ax[3] = {-1, 0, 0};   // world -z
     m->dof_palm = B.add_joint(m->body_palm, GM_JNT_SLIDE, ax, 0, 10.0, p->actuator_armature[2], m->dof_base);
-    double gpos[3] = {0, 0, -(p->finger_length - 165e-3)};
-    double gsz[3] = {0.03, 0.03, 0.004};
+    double gpos[3] = {-(p->finger_length - 165e-3), 0, 0};
+    double gsz[3] = {0.004, 0.03, 0.03};
     B.add_geom(m->body_palm, GM_GEOM_BOX, GM_CLS_PALM, gpos, id4, gsz, 1.0);
   }
   int palm_geom = m->ngeom - 1;

@@ -2550,7 +2550,9 @@ struct GmChunkCarry {        // what a chunk hands the next besides the hot stat
 // counters (zeroed by gm_dispatch_order_kernel before every launch), one 128-B line each:
 // ring r = x * GM_CQ_NB + bucket: [r * 32] its head, [r * 32 + 1] its tail; GM_CQ_FRESH the
 // next unstarted env, GM_CQ_DONE envs finished, + 1 yields, + 2 resumes, + 4 resumes on another
-// XCD; GM_CQ_LAST the previous launch's [GM_CQ_FRESH ..] (37 words, diagnostics)
+// XCD, + 5 claims whose ring slot was still empty (the producer between its tail increment and
+// its entry store), + 6 polls those claims made; GM_CQ_LAST the previous launch's
+// [GM_CQ_FRESH ..] (39 words, diagnostics)
 #define GM_CQ_FRESH (8 * GM_CQ_NB * 32)
 #define GM_CQ_DONE (GM_CQ_FRESH + 32)
 #define GM_CQ_CMAX (GM_CQ_DONE + 3)   // this launch's bucket scale (written by the order kernel)
@@ -2617,19 +2619,57 @@ __device__ __noinline__ void reset_env(GmEnvHot& s, GmEnvState& rec, GmResetKeep
                                        uint16_t* sh_pxy, uint16_t* sh_prot, int lane);
 __device__ void set_action_one(GmEnvHot& s, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
                                int action, float frac);
+// the grasp program's inputs (gm_state.h gm_program_fraction) from an env's state and its
+// SI sensor windows
+__device__ __forceinline__ gm_program_in program_input(const GmEnvHot& s, RingRef R, const gm_model* __restrict__ m) {
+  gm_program_in in;
+  in.x = s.end.x; in.y = s.end.y; in.z = s.end.z;
+  in.base_z = s.base[2];
+  in.q_base = s.qpos[m->jnt_qposadr[m->body_jnt[m->body_base]]];
+  in.q_palm = s.qpos[m->jnt_qposadr[m->body_jnt[m->body_palm]]];
+  in.obj_z = s.qpos[m->jnt_qposadr[m->body_jnt[m->body_obj]] + 2];
+  in.obj_top = gm_program_obj_top(s.obj_type, s.obj_size);
+  in.z_root = m->body_pos[m->body_base][2];
+  in.palm_drop = (m->finger_length - 165e-3) + 0.004;
+  const float g0 = ring_latest(s, R, ST_SI_GAUGE), g1 = ring_latest(s, R, ST_SI_GAUGE + 1),
+              g2 = ring_latest(s, R, ST_SI_GAUGE + 2);
+  in.g_max = fmaxf(g0, fmaxf(g1, g2));
+  in.palm = ring_latest(s, R, ST_SI_PALM);
+  return in;
+}
+// the driver's fraction for action i of kind `kind` (modes: 0 scripted grasp mix, 1 uniform
+// random, 3 grasp program, 4 the program in 1 episode of 4 and the scripted mix otherwise)
+__device__ __forceinline__ float driver_fraction(const GmEnvHot& s, RingRef R, const gm_model* __restrict__ m,
+                                                 const gm_config* __restrict__ C, int mode, uint64_t seed, float jitter,
+                                                 int64_t gid, int i, int kind) {
+  if (mode == 3 || (mode == 4 && gm_program_episode(seed, gid, s.episode))) {
+    if (kind < 0) return 0.0f;
+    const gm_action* acts[GM_N_ACTION_KINDS] = {
+#define GM_AA(n, u, vv, sg) &C->s.n,
+#include "gm_settings.def"
+    };
+    const gm_program_in in = program_input(s, R, m);
+    return gm_program_fraction(&in, kind, acts[kind]->value, acts[kind]->sign);
+  }
+  if (mode == 0 || mode == 4) return gm_script_fraction(seed, gid, s.episode, s.num_action_steps, i, kind, jitter);
+  return gm_random_fraction(seed, gid, s.episode, s.num_action_steps, i);
+}
 // the rollout driver's actions for the env's next env-step (lane 0): the same fractions
-// gm_scripted_actions / gm_random_actions produce, applied as gm_set_action applies them
-__device__ __noinline__ void driver_actions(GmEnvHot& s, const gm_model* __restrict__ m, const gm_config* __restrict__ C,
-                                            int mode, uint64_t seed, float jitter, int64_t gid) {
+// gm_scripted_actions / gm_random_actions / gm_program_actions produce, applied as
+// gm_set_action applies them
+__device__ __noinline__ void driver_actions(GmEnvHot& s, RingRef R, const gm_model* __restrict__ m,
+                                            const gm_config* __restrict__ C, int mode, uint64_t seed, float jitter,
+                                            int64_t gid) {
   const int na = C->n_actions;
+  float f[GM_ACTION_CODE_COUNT];
+  // every fraction from the state before any action moves a target (the program reads them)
   for (int i = 0; i < na; i++) {
     const int code = C->action_options[i];
     const int kind = (code >= 0 && code < GM_ACTION_TERMINATION) ? code / 3 : -1;
-    float f = mode == 0 ? gm_script_fraction(seed, gid, s.episode, s.num_action_steps, i, kind, jitter)
-                        : gm_random_fraction(seed, gid, s.episode, s.num_action_steps, i);
-    if (f < -1.0f) f = -1.0f; else if (f > 1.0f) f = 1.0f;
-    set_action_one(s, m, C, i, f);
+    float v = driver_fraction(s, R, m, C, mode, seed, jitter, gid, i, kind);
+    f[i] = v < -1.0f ? -1.0f : (v > 1.0f ? 1.0f : v);
   }
+  for (int i = 0; i < na; i++) set_action_one(s, m, C, i, f[i]);
 }
 
 // the persistent loop of gm_step_kernel's chunked mode (a mode of the one kernel, not a
@@ -2689,10 +2729,14 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
             got = 1;
             const uint32_t i = (uint32_t)c % (uint32_t)q.cap;
             uint64_t v;
+            uint32_t polls = 0;
             // acquire: pairs with the producer's release store of this entry
             while ((v = __hip_atomic_load(rb + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0ull &&
-                   ld_agent(n_done) < n)
+                   ld_agent(n_done) < n) {
               __builtin_amdgcn_s_sleep(2);
+              polls++;
+            }
+            if (polls) { add_agent(q.ctr + GM_CQ_DONE + 5, 1u); add_agent(q.ctr + GM_CQ_DONE + 6, polls); }
             if (v != 0ull) {
               st_agent(rb + i, 0ull);
               add_agent(q.ctr + GM_CQ_DONE + 2, 1u);
@@ -2741,9 +2785,13 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
               got = 1;
               const uint32_t i = (uint32_t)c % (uint32_t)q.cap;
               uint64_t v;
+              uint32_t polls = 0;
               while ((v = __hip_atomic_load(rb + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0ull &&
-                     ld_agent(n_done) < n)
+                     ld_agent(n_done) < n) {
                 __builtin_amdgcn_s_sleep(2);
+                polls++;
+              }
+              if (polls) { add_agent(q.ctr + GM_CQ_DONE + 5, 1u); add_agent(q.ctr + GM_CQ_DONE + 6, polls); }
               if (v != 0ull) {
                 st_agent(rb + i, 0ull);
                 add_agent(q.ctr + GM_CQ_DONE + 2, 1u);
@@ -2818,7 +2866,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
             S.stp_fixed = 0;
           }
         } else if (lane == 0) {
-          driver_actions(S.s, m, C, q.act_mode, q.act_seed, q.jitter, q.sr.env_offset + env);
+          driver_actions(S.s, g->ring, m, C, q.act_mode, q.act_seed, q.jitter, q.sr.env_offset + env);
           S.stp_fixed = 0;
         }
         GM_ENV_SYNC();
@@ -3098,7 +3146,7 @@ extern "C" __global__ __launch_bounds__(1024) void gm_dispatch_order_kernel(uint
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t cmax;
   const int t = threadIdx.x;
-  if (chunk_ctr && t < 37) chunk_ctr[GM_CQ_LAST + t] = chunk_ctr[GM_CQ_FRESH + t];   // last launch's, for diagnostics
+  if (chunk_ctr && t < 39) chunk_ctr[GM_CQ_LAST + t] = chunk_ctr[GM_CQ_FRESH + t];   // last launch's, for diagnostics
   __syncthreads();
   if (chunk_ctr)
     for (int w = t; w < GM_CQ_WORDS; w += 1024) chunk_ctr[w] = 0;   // the chunked launch's queue counters
@@ -3269,6 +3317,25 @@ extern "C" __global__ void gm_scripted_action_kernel(const GmEnvState* __restric
     const int code = C->action_options[i];
     const int kind = (code >= 0 && code < GM_ACTION_TERMINATION) ? code / 3 : -1;
     out[(size_t)env * na + i] = gm_script_fraction(seed, env_offset + env, s.episode, s.num_action_steps, i, kind, jitter);
+  }
+}
+#endif
+
+// the driver's actions for the current state of every env (gm_program_actions): modes 3
+// (grasp program) and 4 (program / scripted mix), thread per env
+#ifndef GM_CAL_TU   // env-step translation unit only
+extern "C" __global__ void gm_program_action_kernel(const GmEnvState* __restrict__ states, const gm_model* __restrict__ m,
+                                                    const gm_config* __restrict__ C, float* __restrict__ out, int n_envs,
+                                                    uint64_t seed, long long env_offset, float jitter, int mode) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n_envs) return;
+  const GmEnvState& s = states[env];
+  const int na = C->n_actions;
+  for (int i = 0; i < na; i++) {
+    const int code = C->action_options[i];
+    const int kind = (code >= 0 && code < GM_ACTION_TERMINATION) ? code / 3 : -1;
+    const float v = driver_fraction(s, const_cast<RingRef>(s.ring), m, C, mode, seed, jitter, env_offset + env, i, kind);
+    out[(size_t)env * na + i] = v < -1.0f ? -1.0f : (v > 1.0f ? 1.0f : v);
   }
 }
 #endif

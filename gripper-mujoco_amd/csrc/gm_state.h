@@ -206,6 +206,95 @@ float gm_random_fraction(uint64_t seed, int64_t gid, int32_t ep, int32_t k, int 
   return (float)(h >> 40) * (2.0f / 16777216.0f) - 1.0f;
 }
 
+// Grasp-lift-hold program (rollout action modes 3 / 4, gm_program_actions; the CPU oracle's
+// or_program_actions; tests/grasp_program.py drives the oracle with it): a closed-loop
+// driver that takes an episode through the reference's whole success chain
+// (mjclass.cpp:1148-1210, 1295-1322: lifted -> lifted_to_height -> target_height ->
+// object_stable -> stable_height -> successful_grasp).  Stateless: the phase is read off
+// the env's targets and its latest SI readings each env-step, so it resumes anywhere:
+//   close   prismatic X until a gauge reads GM_PROG_G_TOUCH or x reaches GM_PROG_X_CLOSE;
+//   squeeze tilt the tips inward (y below x) until a gauge reads GM_PROG_G_SQUEEZE or y hits
+//           its limit -- the fixed hooks meet the object under its widest section;
+//   lift    the base up to GM_PROG_BASE_LIFT (gripper_z_height > gripper_target_height);
+//   palm    lower the palm onto the object (full speed until 1 mm from its top, then in
+//           proportion to the gap), then hold the palm reading near GM_PROG_PALM_HOLD
+//           (stable_palm_force band [1, 4] N) -- object_stable and stable_height fire.
+// The palm's approach uses the object's pose and size (a scripted test driver may, a
+// policy could not).  Fractions are for the canonical action signs (close = -x, inward =
+// -th, palm down = +z, lift = -base z), mapped through each action's sign; arithmetic is
+// adds, subtracts and divides only (no contractible multiply-add), so the device and the
+// oracle decide on the same bits.
+#define GM_PROG_X_CLOSE 58.5e-3
+#define GM_PROG_Y_MIN 49.5e-3
+#define GM_PROG_Z_HOME 4.8768e-3        /* luke::Gripper::z_home (gripper.h:50) */
+#define GM_PROG_BASE_LIFT (-24e-3)
+#define GM_PROG_G_TOUCH 0.2f
+#define GM_PROG_G_SQUEEZE 1.5f
+#define GM_PROG_PALM_ON 1.0f
+#define GM_PROG_PALM_HOLD 2.5f
+typedef struct gm_program_in {
+  double x, y, z;              // gripper target (luke::Gripper end: x, y, palm z)
+  double base_z;               // base target z (+ve down)
+  double q_base, q_palm;       // base and palm joint positions
+  double obj_z, obj_top;       // object centre height and its centre-to-top extent
+  double z_root, palm_drop;    // base origin height at q = 0; palm face below it at q = 0
+  float g_max, palm;           // largest finger gauge and palm sensor: latest SI readings, N
+} gm_program_in;
+static inline
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+float gm_program_fraction(const gm_program_in* in, int kind, double value, int sign) {
+  const float p = in->palm < 0.0f ? -in->palm : in->palm;
+  const int inward = (in->y - in->x) < -1e-9;
+  int want;
+  float c;
+  if (in->z > GM_PROG_Z_HOME + 0.5e-3 || in->base_z <= GM_PROG_BASE_LIFT + 1e-6) {
+    want = GM_ACT_gripper_Z;
+    if (p >= GM_PROG_PALM_ON) {
+      c = (GM_PROG_PALM_HOLD - p) / 5.0f;
+      c = c > 0.25f ? 0.25f : (c < -0.25f ? -0.25f : c);
+    } else {
+      const double face = ((in->z_root - in->q_base) - in->palm_drop) - in->q_palm;
+      const double gap = face - (in->obj_z + in->obj_top);
+      double f = (gap + 1e-3) / value;
+      f = f > 1.0 ? 1.0 : (f < 0.05 ? 0.05 : f);
+      c = (float)f;
+    }
+  } else if (in->base_z < -1e-6 || (inward && (in->g_max >= GM_PROG_G_SQUEEZE || in->y <= GM_PROG_Y_MIN))) {
+    want = GM_ACT_base_Z;
+    c = 1.0f;
+  } else if (inward || in->g_max >= GM_PROG_G_TOUCH || in->x <= GM_PROG_X_CLOSE) {
+    want = GM_ACT_gripper_revolute_Y;
+    c = 1.0f;
+  } else {
+    want = GM_ACT_gripper_prismatic_X;
+    c = 1.0f;
+  }
+  if (kind != want) return 0.0f;
+  // canonical direction -> fraction: an action moves its target by sign * value * fraction
+  const float s = sign < 0 ? -1.0f : 1.0f;
+  return kind == GM_ACT_gripper_Z ? c * s : -c * s;
+}
+// the live object's centre-to-top extent (MuJoCo sizes: sphere r; cylinder r, half height;
+// box half sizes)
+static inline
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+double gm_program_obj_top(int type, const double* size) {
+  return type == GM_GEOM_SPHERE ? size[0] : (type == GM_GEOM_CYLINDER ? size[1] : size[2]);
+}
+// rollout action mode 4 (the benchmark mix): the program drives 1 episode in 4 of each env
+// (draw 21 of the episode's counter-based hash), the scripted grasp mix the rest
+static inline
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+int gm_program_episode(uint64_t seed, int64_t gid, int32_t ep) {
+  return gm_spawn_int(seed, gid, ep, 21, 0, 3) == 0;
+}
+
 // Topology derived from gm_model on the host (the canonical gripper tree):
 // dof/body of chain position p in finger chain f is first + p - 1 (p >= 1),
 // position 0 of every finger / palm chain is the base dof.

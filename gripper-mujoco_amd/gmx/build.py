@@ -32,13 +32,20 @@ def build(verbose: bool = False, force: bool = False, out: str | None = None, ex
     os.makedirs(objdir, exist_ok=True)
     inc = ["-I" + os.path.join(REPO_DIR, "include"), "-I" + os.path.join(PKG_DIR, "csrc")]
     procs, objs = [], []
+    headers = [os.path.join(PKG_DIR, "csrc", "gm_state.h")] + \
+        [os.path.join(REPO_DIR, "include", f) for f in ("gripper_mi355x.h", "gm_settings.def")]
     for src in srcs:
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        # host-only translation units (.cpp) depend on their source and the shared headers;
+        # the device ones on every kernel source
+        tu_deps = [src] + headers if src.endswith(".cpp") else deps
+        if not force and os.path.exists(obj) and all(os.path.getmtime(d) <= os.path.getmtime(obj) for d in tu_deps):
+            continue
         cmd = [HIPCC, *FLAGS, *extra_flags, *inc, "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append((subprocess.Popen(cmd), cmd))
-        objs.append(obj)
     for p, cmd in procs:
         if p.wait() != 0:
             raise subprocess.CalledProcessError(p.returncode, cmd)

@@ -192,6 +192,13 @@ class BatchedGripperEnv:
         self._check(self.lib.gm_scripted_actions(self._ctx, int(seed), float(jitter), out.ctypes.data, 0))
         return out
 
+    def program_actions(self, seed: int = 0, jitter: float = 0.2, mode: int = 3) -> np.ndarray:
+        """The device grasp-lift-hold program (mode 3) or the benchmark's program / scripted
+        mix (mode 4) for every env's current state (gm_program_actions)."""
+        out = np.zeros((self.n_envs, self.n_actions), dtype=np.float32)
+        self._check(self.lib.gm_program_actions(self._ctx, int(seed), float(jitter), int(mode), out.ctypes.data, 0))
+        return out
+
     def set_action(self, actions):
         a = np.ascontiguousarray(np.asarray(actions, dtype=np.float32).reshape(self.n_envs, self.n_actions))
         self._check(self.lib.gm_set_action(self._ctx, a.ctypes.data, 0))
@@ -206,7 +213,8 @@ class BatchedGripperEnv:
     def rollout(self, n_steps: int, action_mode: int = 0, seed: int = 1234, jitter: float = 0.2,
                 max_episode_steps: int | None = None, records_dev_ptr: int | None = None):
         """gm_rollout: n_steps env-steps of every env in one launch with the device driver
-        (0: scripted grasp mix, 1: uniform random actions) and the device auto-reset; equal bit
+        (0: scripted grasp mix, 1: uniform random actions, 3: the grasp program, 4: the
+        benchmark's program / scripted mix) and the device auto-reset; equal bit
         for bit to n_steps rounds of driver actions -> set_action -> step -> autoreset.
         records_dev_ptr: device [n_steps x n_envs] gm_episode_end records (or None)."""
         mx = self.max_episode_steps if max_episode_steps is None else max_episode_steps
@@ -307,6 +315,13 @@ class BatchedGripperEnv:
                     busy=(t[3] / (v[5] * (t[2] - t[0]))) if span and v[5] else 0.0,
                     poll=(t[4] / (v[5] * (t[2] - t[0]))) if span and v[5] else 0.0)
 
+    def claim_waits(self) -> dict:
+        """The last chunked launch's claims that found their ring slot still empty, and the
+        polls they made (gm_chunk_claim_waits)."""
+        v = (C.c_uint32 * 2)()
+        self._check(self.lib.gm_chunk_claim_waits(self._ctx, v))
+        return dict(waiting_claims=int(v[0]), polls=int(v[1]))
+
     def chunk_timeline(self):
         """When each workgroup of the last chunked launch finished its last work, ms after the
         launch's first pick, its XCD, and per env [start, finish] ms (gm_chunk_timeline)."""
@@ -330,7 +345,7 @@ class BatchedGripperEnv:
         """How gm_step / gm_rollout dispatch this context (include/gripper_mi355x.h gm_dispatch_info)."""
         v = (C.c_int32 * 4)()
         self._check(self.lib.gm_dispatch_info(self._ctx, v))
-        return dict(chunk=v[0], grid=v[1], waves_per_env=v[2])
+        return dict(chunk=v[0], grid=v[1], waves_per_env=v[2], last_launch_env_steps=v[3])
 
     # ------------------------------------------------------------ inspection
     def state(self):

@@ -136,6 +136,7 @@ class MjClass:
         self._params = None          # gm_model_params overrides (finger dimensions)
         self._env = None
         self._pending = None         # continuous action vector buffered between calls
+        self._rd = None              # (reward, done) of the current transition, read with the obs
         self._rng = np.random.default_rng(0)
         self._base_limits = _BASE_LIMITS_DEFAULT     # j_.baseLims (reset by hard_reset)
         self._base_yaw = _BASE_YAW_DEFAULT
@@ -151,6 +152,7 @@ class MjClass:
         self.load(file_path)
 
     def _drop(self):
+        self._rd = None              # the cached transition belongs to the env being dropped
         if self._env is not None:
             self._env.close()
             self._env = None
@@ -264,7 +266,7 @@ class MjClass:
     def _reward_done(self):
         """(reward, done) of the current transition, one device read per transition:
         MjEnv.step asks is_done() then reward() (MjEnv.py:616-637) with nothing in between."""
-        rd = getattr(self, "_rd", None)
+        rd = self._rd
         if rd is None:
             env = self._ensure()
             r, d = env.reward_done()

@@ -493,6 +493,14 @@ int  gm_scripted_actions(gm_ctx* ctx, uint64_t seed, float jitter, float* out, i
  * step, action index) -- the north star's "synthetic random-action rollouts" -- written like
  * gm_scripted_actions. */
 int  gm_random_actions(gm_ctx* ctx, uint64_t seed, float* out, int on_device);
+/* Synthetic driver (not a reference interface): the grasp-lift-hold program (mode 3) or the
+ * benchmark mix (mode 4: the program in 1 episode of 4 per env -- draw 21 of the episode's
+ * counter-based hash -- the scripted grasp mix with `jitter` otherwise) for the current
+ * state of every env, written like gm_scripted_actions.  The program is closed-loop and
+ * stateless (gm_state.h gm_program_fraction): close, squeeze, lift the base, lower the palm
+ * onto the object and hold the palm reading in the stable band -- the reference's success
+ * chain (mjclass.cpp:1148-1210, 1295-1322).  GM_E_ARG for another mode. */
+int  gm_program_actions(gm_ctx* ctx, uint64_t seed, float jitter, int mode, float* out, int on_device);
 
 /* MjClass::set_continous_action for every action index i in order
  * (mjclass.cpp:1517-1630; called per index by MjEnv._set_action, MjEnv.py:591-594).
@@ -573,7 +581,8 @@ int  gm_autoreset_episodes(gm_ctx* ctx, int max_episode_steps, const gm_spawn* s
 
 /* A fused batched rollout (the env-step hot path with its synthetic driver on the device):
  * n_steps repetitions, for every env, of exactly the per-step API's sequence
- *   gm_scripted_actions (action_mode 0, seed, jitter) or gm_random_actions (1, seed)
+ *   gm_scripted_actions (action_mode 0, seed, jitter), gm_random_actions (1, seed) or
+ *   gm_program_actions (3: the grasp program, 4: the benchmark's program / scripted mix)
  *   -> gm_set_action -> gm_step -> gm_autoreset_episodes(max_episode_steps, spawn = NULL,
  *      records + k * n_envs)
  * -- the same code on the same state, so the results are bit for bit those of the n_steps
@@ -584,7 +593,8 @@ int  gm_autoreset_episodes(gm_ctx* ctx, int max_episode_steps, const gm_spawn* s
  * records: device array [n_steps x n_envs] (or NULL); obs / reward / done buffers hold the last
  * env-step's (the reset observation for envs reset at its end), as after the per-step calls. */
 typedef struct gm_rollout_params {
-  int32_t  action_mode;        /* 0: scripted grasp mix, 1: uniform random */
+  int32_t  action_mode;        /* 0: scripted grasp mix, 1: uniform random, 3: grasp program,
+                                  4: program in 1 episode of 4, scripted mix otherwise */
   int32_t  max_episode_steps;  /* MjEnv truncation; <= 0 disables it */
   uint64_t seed;
   float    jitter;             /* scripted mode only */
@@ -592,7 +602,10 @@ typedef struct gm_rollout_params {
 } gm_rollout_params;
 int  gm_rollout(gm_ctx* ctx, int n_steps, const gm_rollout_params* params, gm_episode_end* records);
 
-/* Timing of the fused env-step kernel (HIP events on the context's stream). */
+/* Timing of the last env-step kernel launch (HIP events on the context's stream): a gm_step
+ * (one env-step per env) or a gm_rollout / gm_policy_rollout launch of n_steps env-steps per
+ * env -- gm_dispatch_info out[3] says which; divide by it for a per-env-step figure.
+ * gm_chunk_stats and gm_chunk_timeline likewise describe that last launch. */
 int  gm_last_step_ms(gm_ctx* ctx, float* ms);
 /* The last gm_step's work queue (chunked dispatch): out[0] envs started,
  * out[1] envs finished, out[2] yields (an env handed back to its XCD's queue because an
@@ -603,11 +616,18 @@ int  gm_last_step_ms(gm_ctx* ctx, float* ms);
  * unstarted env, [2] last env finished, [3] sum of wave-busy time, [4] sum of wave polling.
  * Synchronises the context's stream. */
 int  gm_chunk_stats(gm_ctx* ctx, uint32_t* out7, uint64_t* times5);
+/* The last chunked launch's claim waits: out[0] claims of a yielded env's ring slot that found
+ * the slot still empty (its producer between the tail increment and the entry store), out[1]
+ * the polls those claims made.  A claimed slot always has a producer in flight
+ * (claim_bucket's invariant), so the polls per waiting claim stay small; a claim parked on a
+ * slot only a future yield would fill shows as a run of polls.  Synchronises the stream. */
+int  gm_chunk_claim_waits(gm_ctx* ctx, uint32_t* out2);
 /* How gm_step / gm_rollout dispatch this context (fixed at gm_create): out[0] substeps
  * between preemption tests (0: the one-shot kernel), out[1] workgroups of the chunked
  * grid, out[2] waves per env (1; 2 = DUO workgroups, whose second wave runs the collider
  * concurrently -- chosen when every env's two waves fit resident, GM_DUO=0/1 forces it),
- * out[3] reserved (0). */
+ * out[3] env-steps per env of the last launch (1 after gm_step, n_steps after a rollout:
+ * the unit of gm_last_step_ms / gm_chunk_stats / gm_chunk_timeline). */
 int  gm_dispatch_info(const gm_ctx* ctx, int32_t* out4);
 /* The last chunked launch's per-workgroup end of work: when workgroup w finished the last
  * env (or env chunk) it ran, before it polled out the rest of the launch (100 MHz constant

@@ -1095,6 +1095,43 @@ void or_set_action(or_env* e, const float* a) {
 }
 void or_set_discrete_action(or_env* e, int32_t a) { set_action(e, a, 0); }
 
+/* the rollout drivers' fractions for the env's current state (the device's driver_fraction,
+ * gm_kernels.hip; test infrastructure): 0 scripted grasp mix, 1 uniform random (the counter
+ * hash), 3 grasp-lift-hold program (gm_state.h gm_program_fraction), 4 the program in 1
+ * episode of 4 and the scripted mix otherwise; gid = the env's global id */
+void or_driver_actions(const or_env* e, int mode, uint64_t seed, float jitter, int64_t gid, float* out) {
+  const gm_model* m = &e->m;
+  const gm_settings* st = &e->c.s;
+  const gm_action* acts[GM_N_ACTION_KINDS] = {
+#define GM_AA(n, u, vv, sg) &st->n,
+#include "gm_settings.def"
+  };
+  gm_program_in in;
+  in.x = e->end.x; in.y = e->end.y; in.z = e->end.z;
+  in.base_z = e->base[2];
+  in.q_base = e->qpos[m->jnt_qposadr[m->body_jnt[m->body_base]]];
+  in.q_palm = e->qpos[m->jnt_qposadr[m->body_jnt[m->body_palm]]];
+  in.obj_z = e->qpos[m->jnt_qposadr[m->body_jnt[m->body_obj]] + 2];
+  in.obj_top = gm_program_obj_top(m->geom_type[m->geom_obj], m->geom_size[m->geom_obj]);
+  in.z_root = m->body_pos[m->body_base][2];
+  in.palm_drop = (m->finger_length - 165e-3) + 0.004;
+  {
+    const float g0 = ring_latest(&e->si_gauge[0]), g1 = ring_latest(&e->si_gauge[1]), g2 = ring_latest(&e->si_gauge[2]);
+    in.g_max = fmaxf(g0, fmaxf(g1, g2));
+  }
+  in.palm = ring_latest(&e->si_palm);
+  const int prog = mode == 3 || (mode == 4 && gm_program_episode(seed, gid, e->episode));
+  for (int i = 0; i < e->c.n_actions; i++) {
+    const int code = e->c.action_options[i];
+    const int kind = (code >= 0 && code < GM_ACTION_TERMINATION) ? code / 3 : -1;
+    float v;
+    if (prog) v = kind < 0 ? 0.0f : gm_program_fraction(&in, kind, acts[kind]->value, acts[kind]->sign);
+    else if (mode == 0 || mode == 4) v = gm_script_fraction(seed, gid, e->episode, e->num_action_steps, i, kind, jitter);
+    else v = gm_random_fraction(seed, gid, e->episode, e->num_action_steps, i);
+    out[i] = v < -1.0f ? -1.0f : (v > 1.0f ? 1.0f : v);
+  }
+}
+
 /* MjClass::step (mjclass.cpp:504-530): physics + update_all + monitor_sensors */
 static void full_substep(or_env* e) {
   physics_substep(e);
@@ -1993,8 +2030,9 @@ int or_batch_substep(const gm_model* m, const gm_config* c, const gm_object* obj
  * n_threads POSIX threads (envs share nothing, like the reference's one-env-per-process
  * model).  The workload is the benchmark's: MjEnv.reset -> _spawn_object with the same
  * counter-based object / pose draws as the device (gm_spawn_int; spawn_into_scene with
- * +-10 mm / +-pi/2, 3 tries, then the fallback pose), actions from the scripted grasp mix
- * (mode 1, gm_script_fraction) or uniform random (mode 0), a reset at done or at
+ * +-10 mm / +-pi/2, 3 tries, then the fallback pose), actions from the benchmark mix
+ * (mode 1: or_driver_actions mode 4, the grasp program in 1 episode of 4 and the scripted
+ * grasp mix otherwise) or uniform random (mode 0), a reset at done or at
  * max_episode_steps (MjEnv.py:616-637).  Returns env-steps per wall second. */
 typedef struct {
   const or_env* proto;
@@ -2033,13 +2071,11 @@ static void* bench_worker(void* arg) {
     bench_reset(e, j->seed, k, j->n_objects);
     uint64_t x = j->seed + (uint64_t)k * 0x9E3779B97F4A7C15ull;
     for (int t = 0; t < j->n_steps; t++) {
-      float a[16];
-      for (int i = 0; i < e->c.n_actions && i < 16; i++) {
-        if (j->mode == 1) {
-          const int code = e->c.action_options[i];
-          const int kind = (code >= 0 && code < GM_ACTION_TERMINATION) ? code / 3 : -1;
-          a[i] = gm_script_fraction(j->seed, k, e->episode, e->num_action_steps, i, kind, 0.2f);
-        } else {
+      float a[GM_ACTION_CODE_COUNT];
+      if (j->mode == 1) {
+        or_driver_actions(e, 4, j->seed, 0.2f, k, a);   /* the benchmark mix (device mode 4) */
+      } else {
+        for (int i = 0; i < e->c.n_actions && i < GM_ACTION_CODE_COUNT; i++) {
           x = x * 6364136223846793005ull + 1442695040888963407ull;
           a[i] = (float)((double)(x >> 11) / 9007199254740992.0 * 2 - 1);
         }

@@ -42,6 +42,8 @@ void  or_spawn(or_env* e, const gm_spawn* spawn);                  /* MjClass::s
 int   or_spawn_into_scene(or_env* e, const gm_spawn_params* p);    /* MjClass::spawn_into_scene */
 void  or_set_action(or_env* e, const float* actions);              /* set_continous_action x n_actions */
 void  or_set_discrete_action(or_env* e, int32_t action);           /* set_discrete_action */
+void  or_driver_actions(const or_env* e, int mode, uint64_t seed, float jitter, int64_t gid,
+                        float* out);   /* the rollout drivers (scripted / random / grasp program) */
 void  or_step(or_env* e);                                          /* action_step */
 int   or_get_obs(or_env* e, float* out);                           /* get_observation */
 int   or_is_done(or_env* e);                                       /* is_done */

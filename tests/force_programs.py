@@ -58,12 +58,17 @@ def sphere(gm, diameter_mm: float):
     return objs
 
 
-def scene(gm, ol, variant: str, diameter_mm: float, revolute_kp=None, stepper=None, timestep=None):
+def scene(gm, ol, variant: str, diameter_mm: float, revolute_kp=None, stepper=None, timestep=None, hook_length=None,
+          clearance=None):
     """(model, cfg, objects) of one program run.  revolute_kp overrides the revolute PD gain
     (the tilt CSV's "Kp=..." columns); stepper = (num_steps, time_per_step) overrides
     j_.ctrl (the tilt program's own instruction: num_steps = 1, pulses_per_s = 5000)."""
     import indep_physics as ip
     p = model_params(gm, variant, diameter_mm)
+    if hook_length is not None:
+        p.hook_length = hook_length
+    if clearance is not None:
+        p.fingertip_clearance = clearance
     p.timestep = auto_timestep(gm, ol, p) if timestep is None else timestep
     model = gm.ModelBlob(p)
     if revolute_kp is not None or stepper is not None:
@@ -114,6 +119,40 @@ def tilt(env, start_mm=100.0, span_mm=6.0, inc_mm=0.25, settle=100, per=5):
         g = env.sensor_si()
         out.append((y * 1e3, float(g[0]), float(g[1]), float(g[2])))
     return np.array(out)
+
+
+def palm(env, start_mm=60.0, span_mm=25.0, inc_mm=0.25, settle=100, per=5, xy=130e-3):
+    """"measure palm" (mysimulate.cpp:2813-2853): fingers fully open (x = y = 130 mm), the palm
+    z target stepped 60 .. 84.75 mm in 0.25 mm steps onto the centred sphere; 100 action steps
+    at the start, then 5 per point; the SI palm sensor after each point (its stepper at 1 step
+    / 0.2 ms, as the program instructs).  Returns [n_points, 2]: z mm, palm N."""
+    pos = []
+    i = start_mm
+    while i < start_mm + span_mm:
+        pos.append(i * 1e-3)
+        i += inc_mm
+    env.set_motor_target(xy, xy, pos[0])
+    for _ in range(settle):
+        env.action_step()
+    out = []
+    for z in pos:
+        env.set_motor_target(xy, xy, z)
+        for _ in range(per):
+            env.action_step()
+        out.append((z * 1e3, float(env.sensor_si()[3])))
+    return np.array(out)
+
+
+def level_crossing(x, F, level):
+    """First x where the curve reaches `level` (linear between the bracketing points)."""
+    F = np.asarray(F, dtype=np.float64)
+    x = np.asarray(x, dtype=np.float64)
+    i = int(np.argmax(F >= level))
+    if F[i] < level:
+        return float("nan")
+    if i == 0:
+        return float(x[0])
+    return float(x[i - 1] + (level - F[i - 1]) * (x[i] - x[i - 1]) / (F[i] - F[i - 1]))
 
 
 def features(x, F, contact_above=0.1, base_from=110.0):

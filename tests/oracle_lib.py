@@ -66,6 +66,7 @@ def load(path):
             "or_sizeof": (C.c_size_t, []),
             "or_reset": (None, [vp, vp]),
             "or_set_action": (None, [vp, f32p]),
+            "or_driver_actions": (None, [vp, i32, C.c_uint64, C.c_float, C.c_int64, f32p]),
             "or_set_discrete_action": (None, [vp, C.c_int32]),
             "or_step": (None, [vp]),
             "or_get_obs": (i32, [vp, f32p]),
@@ -128,6 +129,7 @@ class OracleEnv:
         self.model = model
         self.cfg = cfg
         self.objects = objects
+        self.env_id = int(env_id)
         self.h = L.or_create(model.ptr, cfg.ptr, C.cast(objects, C.c_void_p), len(objects), env_id)
         if not self.h:
             raise RuntimeError("or_create failed")
@@ -151,6 +153,14 @@ class OracleEnv:
     def set_action(self, a):
         a = _f32(a)
         self.L.or_set_action(self.h, a.ctypes.data_as(C.POINTER(C.c_float)))
+
+    def driver_actions(self, mode: int = 3, seed: int = 0, jitter: float = 0.2, gid: int | None = None):
+        """The rollout drivers' fractions for this env's current state (or_driver_actions:
+        0 scripted mix, 1 random, 3 grasp program, 4 program / scripted mix)."""
+        out = np.zeros(max(self.n_actions, 1), dtype=np.float32)
+        self.L.or_driver_actions(self.h, int(mode), int(seed), float(jitter), int(self.env_id if gid is None else gid),
+                                 out.ctypes.data_as(C.POINTER(C.c_float)))
+        return out[:self.n_actions]
 
     def set_discrete_action(self, a: int):
         self.L.or_set_discrete_action(self.h, int(a))

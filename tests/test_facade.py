@@ -122,3 +122,27 @@ def test_facade_episode_matches_oracle(gm):
         assert r == pytest.approx(rr, rel=1e-4, abs=1e-6)
     ev = mj.get_event_state()
     assert isinstance(ev.lifted.row, int)
+
+
+@pytest.mark.gpu
+def test_facade_hard_reset_drops_the_cached_transition(gm):
+    """get_observation_numpy caches the transition's (reward, done) for MjEnv's next
+    is_done() / reward(); a hard_reset (a fresh context) must not answer with the old env's
+    done flag."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    from mjpy.bind import MjClass
+    mj = MjClass()
+    mj.set = gm.canonical_settings(noise=False, seed=4)
+    mj.set.step_num.done = 1          # every env-step ends the episode
+    mj.set.step_num.trigger = 1
+    mj.object_set_name = "set1_synthetic"
+    mj.reset()
+    for i in range(mj.get_n_actions()):
+        mj.set_continous_action(i, 0.0)
+    mj.action_step()
+    mj.get_observation_numpy()
+    assert mj.is_done()
+    mj.hard_reset()
+    assert not mj.is_done()
+    mj._drop()

@@ -14,12 +14,21 @@ Bands (measured values in DESIGN.md section 4):
 - constrict, spheres 80 / 100 / 120 mm x finger variants EI1..3, both CSVs: contact onset
   within 1.0 mm, force-vs-travel slope within -6 % / +8 %, every reading within 0.10 N,
   the pre-contact reading within 0.04 N;
+- constrict, the CSV's other Sim columns (spheres 70 / 90 / 110 mm x EI1..3, which the
+  notebook does not plot): their onsets sit 7 mm past 35 + sqrt(r^2 - 6^2) (76.4-76.8 /
+  86.0-86.5 / 96.6-96.9 mm against 69.5 / 79.6 / 89.7), i.e. they were made with a longer
+  fingertip reach -- all nine fit one hook length, 42 mm: onset within 1.0 mm, slope
+  within -6 % / +15 %, every reading within 0.20 N (DESIGN.md section 4);
 - tilt, 14 (Kp, EI) columns: force rises as y is stepped below x (the fingertips tilt
   inward, gripper.h:88-93), slope per mm of y within +-12 %, slope increasing with Kp as
-  in the reference.  The tilt CSV does not say which sphere the run used (its force starts
-  at the first point); the 120 mm sphere of the constrict scene is used and the onset is
-  not asserted (the thesis notebook aligns the curves' onsets by hand, offsets [-1, -0.3,
-  -0.3]).
+  in the reference, and the y where the force reaches 0.5 N and 1 N within 0.75 mm of the
+  reference's (the CSV does not say which sphere the run used; the 120 mm sphere of the
+  constrict scene is used.  The notebook's offsets [-1, -0.3, -0.3] mm align these sim
+  curves with the real ones, design_modelling_chapters.ipynb "tilt", not with each other);
+- palm ("measure palm", mysimulate.cpp:2813-2853): no reference output exists (parity
+  unpinned): property test on the oracle -- the palm reading is zero until the palm face
+  meets the sphere's top, within 0.5 mm of the geometric onset, then rises monotonically --
+  and the device reading for reading against the oracle.
 """
 import json
 import os
@@ -35,6 +44,8 @@ from conftest import gpu_available
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "force_curves.json")
 ONSET_MM, SLOPE_BAND, MAX_ERR_N, BASE_N = 1.0, (0.94, 1.08), 0.10, 0.04
 TILT_SLOPE_BAND = (0.88, 1.12)
+TILT_CROSS_MM = 0.75
+LONG_HOOK, LONG_SLOPE_BAND, LONG_MAX_ERR_N = 42e-3, (0.94, 1.15), 0.20
 
 
 def golden():
@@ -100,6 +111,39 @@ def test_constrict_onset_tracks_sphere_radius(constrict_runs):
         assert abs(o - geo) <= 1.0, (d, v, o, geo)
 
 
+def test_constrict_70_90_110_columns_fit_one_longer_hook(gm):
+    """The constrict CSV's Sim 70 / 90 / 110 x EI1..3 columns (not plotted by the notebook):
+    with the 35 mm hook their onsets would be 69.5 / 79.6 / 89.7 mm, the reference's are 7 mm
+    later; one hook length, 42 mm, puts every onset within 1 mm (35 -> 42 mm is the only
+    change), the nine curves then within the stated bands."""
+    g = golden()["constrict_A"]
+    dts = {v: fp.auto_timestep(gm, ol, fp.model_params(gm, v, 120)) for v in fp.VARIANTS}
+    cases = [(d, v) for d in (70, 90, 110) for v in fp.VARIANTS]
+
+    def one(c):
+        d, v = c
+        model, cfg, objs = fp.scene(gm, ol, v, d, timestep=dts[v], hook_length=LONG_HOOK)
+        return fp.constrict(fp.oracle_env(gm, ol, model, cfg, objs))
+    with ThreadPoolExecutor(max_workers=min(9, os.cpu_count() or 1)) as ex:
+        res = list(ex.map(one, cases))
+    xr = ref_col(g, "XY pos")
+    report = []
+    for (d, v), r in zip(cases, res):
+        x, F = r[:, 0], r[:, 1]
+        Fr = ref_col(g, f"Sim {d} {v}")
+        o, s, b = fp.features(x, F)
+        o2, s2, b2 = fp.features(xr, Fr)
+        err = float(np.nanmax(np.abs(F[:len(Fr)] - Fr)))
+        report.append((d, v, o - o2, s / s2, err))
+        # the 35 mm hook's geometric onset misses the reference by ~7 mm; the 42 mm one fits
+        assert abs(35.0 + np.sqrt((0.5 * d) ** 2 - 36.0) - o2) > 6.0, (d, v, o2)
+        assert abs(o - o2) <= ONSET_MM, (d, v, o, o2)
+        assert LONG_SLOPE_BAND[0] <= s / s2 <= LONG_SLOPE_BAND[1], (d, v, s, s2)
+        assert err <= LONG_MAX_ERR_N, (d, v, err)
+        assert abs(b - b2) <= BASE_N, (d, v, b, b2)
+    print("\n".join(f"D{d} {v}: onset {do:+.2f} mm, slope x{sr:.3f}, max err {e:.3f} N" for d, v, do, sr, e in report))
+
+
 @pytest.fixture(scope="module")
 def tilt_runs(gm):
     g = golden()["tilt"]
@@ -132,6 +176,11 @@ def test_tilt_matches_reference_mujoco_slopes(tilt_runs):
         _, s2, _ = fp.features(xr[:nr], Fr[:nr], base_from=100.0)
         slopes[h] = (s, s2)
         assert TILT_SLOPE_BAND[0] <= s / s2 <= TILT_SLOPE_BAND[1], (h, s, s2)
+        # where the press reaches 0.5 N and 1 N: the onset of the tilt curve
+        for lvl in (0.5, 1.0):
+            c = fp.level_crossing(-y, F, lvl)
+            c2 = fp.level_crossing(-xr[:nr], Fr[:nr], lvl)
+            assert abs(c - c2) <= TILT_CROSS_MM, (h, lvl, -c, -c2)
     # a stiffer revolute PD gives a stiffer tilt, as in the reference
     for v in fp.VARIANTS:
         ks = sorted((float(h.split()[0][3:]), slopes[h]) for h in slopes if h.endswith(v))
@@ -139,6 +188,49 @@ def test_tilt_matches_reference_mujoco_slopes(tilt_runs):
         theirs = [s for _, (_, s) in ks]
         assert ours == sorted(ours) and theirs == sorted(theirs), (v, ks)
     print("\n".join(f"{h}: slope {s:.4f} N/mm vs reference {s2:.4f} (x{s / s2:.3f})" for h, (s, s2) in slopes.items()))
+
+
+def palm_scene(gm, d=100):
+    """The "measure palm" scene: the sphere centred, the fingers open; fingertip clearance
+    10 mm (MjEnv's default -- with the constrict scene's r + 6 mm the sphere's top would sit
+    below the program's 60-85 mm palm range), the palm stepper at 1 step / 0.2 ms."""
+    return fp.scene(gm, ol, "EI3", d, stepper=(1, 1.0 / 5000.0), clearance=10e-3, timestep=3.0e-3)
+
+
+def palm_onset_mm(gm, model, cfg, objs, d, z0=60e-3):
+    """Where the palm face meets the sphere's top: settle at the program's first point, then
+    face - top from the settled joint positions (the base and the palm sag under gravity on
+    their PD springs, 4.6 / 0.9 mm), the target z at which that gap closes."""
+    import indep_physics as ip
+    mv = ip.GmModel.from_buffer(model.buf)
+    o = fp.oracle_env(gm, ol, model, cfg, objs)
+    o.set_motor_target(130e-3, 130e-3, z0)
+    for _ in range(100):
+        o.action_step()
+    q, _, _ = o.state()
+    face = mv.body_pos[mv.body_base][2] - q[mv.dof_base] - ((mv.finger_length - 165e-3) + 0.004) - q[mv.dof_palm]
+    top = q[mv.jnt_qposadr[mv.body_jnt[mv.body_obj]] + 2] + 0.5e-3 * d
+    return (z0 + face - top) * 1e3
+
+
+@pytest.mark.parametrize("d", [90, 100])
+def test_palm_program_reads_the_press(gm, d):
+    """Parity unpinned (no reference output): the palm reading stays at zero while the palm
+    face is above the sphere, starts within 0.5 mm of where the face meets its top, and rises
+    monotonically (the palm's axial force, +ve for compression -- the sphere is geom1 of the
+    palm pair)."""
+    model, cfg, objs = palm_scene(gm, d)
+    r = fp.palm(fp.oracle_env(gm, ol, model, cfg, objs))
+    z, P = r[:, 0], r[:, 1]
+    on = palm_onset_mm(gm, model, cfg, objs, d)
+    assert 60.0 < on < 84.0, on
+    assert np.abs(P[z < on - 0.5]).max() < 0.02, P[z < on - 0.5]
+    c = fp.level_crossing(z, P, 0.05)
+    assert abs(c - on) <= 0.5, (c, on)
+    after = P[z > on + 0.5]
+    assert (np.diff(after) > -0.02).all() and after[-1] > 2.0, after
+    print(f"D{d}: onset {c:.2f} mm (geometric {on:.2f}), {after[-1]:.2f} N at {z[-1]:.2f} mm, "
+          f"slope {np.polyfit(z[z > on + 1.0], P[z > on + 1.0], 1)[0]:.2f} N/mm")
 
 
 # ---------------------------------------------------------------- device vs oracle
@@ -188,3 +280,21 @@ def test_set_motor_target_reports_limits(gm):
     assert not o.set_motor_target(0.2, 0.1, 5e-3)
     e, _, _, _ = o.target()
     assert e[0] == pytest.approx(0.134)
+
+
+@pytest.mark.gpu
+def test_gpu_palm_matches_oracle(gm):
+    """The "measure palm" program on one device env equals the oracle reading for reading
+    (parity unpinned against the reference: it kept no output of this program)."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    model, cfg, objs = palm_scene(gm, 100)
+    dev = fp.DeviceEnv1(gm, model, gm.canonical_settings(noise=False, seed=1), objs)
+    try:
+        rd = fp.palm(dev)
+    finally:
+        dev.close()
+    ro = fp.palm(fp.oracle_env(gm, ol, model, cfg, objs))
+    np.testing.assert_array_equal(rd[:, 0], ro[:, 0])
+    np.testing.assert_allclose(rd[:, 1], ro[:, 1], rtol=1e-4, atol=1e-5)
+    assert rd[-1, 1] > 5.0

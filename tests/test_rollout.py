@@ -49,8 +49,10 @@ def per_step(gm, env, mode, records, steps=K, max_ep=MAX_EP):
     for k in range(steps):
         if mode == 0:
             env.lib.gm_scripted_actions(env.ctx, SEED, 0.2, d_act, 1)
-        else:
+        elif mode == 1:
             env.lib.gm_random_actions(env.ctx, SEED, d_act, 1)
+        else:
+            env.lib.gm_program_actions(env.ctx, SEED, 0.2, mode, d_act, 1)
         env.lib.gm_set_action(env.ctx, d_act, 1)
         env.lib.gm_step(env.ctx)
         env.autoreset_device(0, None, max_episode_steps=max_ep, episodes_dev_ptr=records[k].data_ptr())
@@ -67,7 +69,8 @@ def snapshot(env, records):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode,dispatch", [(0, "default"), (1, "default"), (0, "handoff-heavy")])
+@pytest.mark.parametrize("mode,dispatch", [(0, "default"), (1, "default"), (0, "handoff-heavy"), (3, "default"),
+                                           (4, "handoff-heavy")])
 def test_rollout_equals_per_step_api(gm, mode, dispatch):
     if not gpu_available():
         pytest.skip("no GPU")
@@ -147,6 +150,76 @@ def test_rollout_equals_per_step_api_full_size(gm):
         assert int((sa[5][..., 1] > 0).sum()) >= n
         st = b.chunk_stats()
         assert st["finished"] == n and st["yields"] > 0, st
+    finally:
+        a.close()
+        b.close()
+
+
+@pytest.mark.gpu
+def test_program_rollout_equals_per_step_api_through_the_lift(gm):
+    """The grasp program (mode 3) is closed-loop: its fractions read each env's targets,
+    joint positions and SI sensor windows.  Over 110 env-steps (close, squeeze, lift, palm,
+    hold, successes and their resets) the fused launch equals the per-step calls bit for bit,
+    under the hand-off heavy dispatch (envs move between waves mid env-step)."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import torch
+    n, k, mx = 256, 110, 250
+    ra = torch.zeros((k, n, 3), dtype=torch.int32, device="cuda")
+    rb = torch.zeros((k, n, 3), dtype=torch.int32, device="cuda")
+    a, b = make_env(gm, n=n), make_env(gm, HANDOFF, n=n)
+    try:
+        per_step(gm, a, 3, ra, steps=k, max_ep=mx)
+        per_step(gm, b, 3, rb, steps=1, max_ep=mx)
+        b.rollout(k - 1, action_mode=3, seed=SEED, jitter=0.2, max_episode_steps=mx, records_dev_ptr=rb[1:].data_ptr())
+        sa, sb = snapshot(a, ra), snapshot(b, rb)
+        assert sa[0] == sb[0]
+        for i in range(2, 6):
+            np.testing.assert_array_equal(sa[i], sb[i])
+        # the program got through the chain in this window: successes in the records
+        assert int((sa[5][..., 2] & 0xFF).sum()) > 0
+    finally:
+        a.close()
+        b.close()
+
+
+@pytest.mark.gpu
+def test_work_queue_claims_never_park_tiny_grid_4096(gm):
+    """Regression test of the work queue's claim protocol (claim_bucket, gm_kernels.hip): a
+    4096-env rollout on a deliberately tiny persistent grid (16 workgroups) with the hand-off
+    heavy knobs -- thousands of yields and resumptions, every wave contending for the same
+    bucket slots -- equals the per-step calls bit for bit, and no claim parks: a claimed slot
+    always has its producer in flight, so the claims that find their slot empty poll only
+    briefly (the r05 race parked a wave on a slot only a future yield would fill: one rank
+    took 50 s instead of 0.6 s)."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import time
+    import torch
+    n, k, mx = 4096, 3, 250
+    tiny = dict(HANDOFF, GM_CHUNK_GRID="16")
+    ra = torch.zeros((k, n, 3), dtype=torch.int32, device="cuda")
+    rb = torch.zeros((k, n, 3), dtype=torch.int32, device="cuda")
+    a, b = make_env(gm, n=n), make_env(gm, tiny, n=n)
+    try:
+        assert b.dispatch_info()["grid"] == 16
+        per_step(gm, a, 0, ra, steps=k, max_ep=mx)
+        per_step(gm, b, 0, rb, steps=1, max_ep=mx)
+        t0 = time.time()
+        b.rollout(k - 1, action_mode=0, seed=SEED, jitter=0.2, max_episode_steps=mx, records_dev_ptr=rb[1:].data_ptr())
+        torch.cuda.synchronize()
+        wall = time.time() - t0
+        st, cw = b.chunk_stats(), b.claim_waits()
+        print(f"tiny grid: {wall:.2f} s, {st}, {cw}")
+        sa, sb = snapshot(a, ra), snapshot(b, rb)
+        assert sa[0] == sb[0]
+        for i in range(2, 6):
+            np.testing.assert_array_equal(sa[i], sb[i])
+        assert st["finished"] == n and st["yields"] > n and st["resumes"] == st["yields"], st
+        assert b.dispatch_info()["last_launch_env_steps"] == k - 1
+        # no parked claim: the waits are the producer's two-instruction window
+        assert cw["polls"] <= 64 * cw["waiting_claims"] + 64, cw
+        assert wall < 60.0, wall
     finally:
         a.close()
         b.close()

@@ -230,3 +230,81 @@ def test_bench_timed_loop_two_ranks(gm):
     assert line["episodes_finished"] == ended
     assert line["episode_successes"] == ep["successes"]
     assert line["mean_episode_length"] == round(ep["length_sum"] / ended, 2)
+
+
+# ---------------------------------------------------------------- successes through the collective
+SUCC_STEPS = 110
+
+
+def program_records(env_ids):
+    """Each env's first episode under the grasp-lift-hold program (oracle or_driver_actions,
+    mode 3), centred set6 objects: spheres for even global ids (carried on the hooks to
+    successful_grasp), boxes for odd ones (squeezed, not carried); the gm_episode_end
+    record of each, packed [n, 3] int32."""
+    import gmx
+    import oracle_lib
+    from gmx.shard import pack_episodes
+    s = gmx.canonical_settings(noise=False, seed=5)
+    model = gmx.ModelBlob()
+    cfg = gmx.ConfigBlob(s, model)
+    objs = gmx.make_object_set("set6_synthetic", 1234)
+    spheres = [i for i in range(len(objs)) if objs[i].type == 2 and objs[i].size[0] > 0.02]
+    boxes = [i for i in range(len(objs)) if objs[i].type == 6]
+    i_succ = list(gmx.BINARY_EVENTS).index("successful_grasp")
+    recs = []
+    for g in env_ids:
+        e = oracle_lib.OracleEnv(model, cfg, objs, int(g))
+        sp = gmx.Spawn()
+        sp.object_index = spheres[int(g) // 2 % len(spheres)] if int(g) % 2 == 0 else boxes[0]
+        sp.x, sp.y, sp.zrot = 0.0, 0.0, 0.0
+        e.reset(sp)
+        tot, rec = np.float32(0.0), None
+        for k in range(SUCC_STEPS):
+            e.set_action(e.driver_actions(mode=3, seed=5, gid=int(g)))
+            e.action_step()
+            d, r = e.is_done(), e.reward()
+            tot = np.float32(tot + np.float32(r))
+            if d or k + 1 == SUCC_STEPS:
+                rec = (tot, k + 1, int(e.event_rows()[0][i_succ] > 0))
+                break
+        recs.append(rec)
+    r = np.array(recs, dtype=np.float64)
+    return pack_episodes(torch.tensor(r[:, 0], dtype=torch.float32), torch.tensor(r[:, 1]),
+                         torch.tensor(r[:, 2])).numpy()
+
+
+def succ_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gmx.shard import shard_range, gather_episodes
+        lo, hi = shard_range(rank, world, N_PER_RANK)
+        allrec = gather_episodes(torch.from_numpy(program_records(range(lo, hi))), world)
+        if rank == 0:
+            q.put(allrec.numpy().tolist())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gather_carries_program_successes(gm):
+    """The episode-end collective with real successes in it: 2 gloo ranks x 2 envs under the
+    grasp program; the gathered records equal a single-process run, the sphere envs' success
+    bytes are 1 with their +1 return, the box envs' 0."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=succ_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = program_records(range(world * N_PER_RANK))
+    np.testing.assert_array_equal(np.array(got, dtype=np.int32), ref)
+    from gmx.shard import unpack_episodes
+    r, length, success = unpack_episodes(torch.from_numpy(ref))
+    assert success.tolist() == [1, 0, 1, 0], success
+    assert (r[success.bool()] > 0.5).all() and (length[success.bool()] < SUCC_STEPS).all()

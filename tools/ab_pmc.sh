@@ -4,8 +4,9 @@
 # one SQ counter pass per build over the C3 grasp workload (tools/pmc_grasp.py), each pass its
 # own rocprofv3 run.  usage (GPU box): [AB_C2=1] [AB_ROUNDS=3] bash tools/ab_pmc.sh <tag> <libA> <libB>
 set -e -o pipefail
-TAG=$1; A=$2; B=$3
+TAG=$1
 R=${GRAFT_REPO_ROOT:-$(pwd)}
+A=$(realpath $2); B=$(realpath $3)
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 bash $R/tools/ab_bench.sh $TAG $A $B

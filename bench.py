@@ -256,6 +256,20 @@ def c3_random_line(gmx, torch, dev, stream, steps: int, seed: int, env_offset: i
                         "scene spawn, auto-reset, steady state after a staggered pre-roll"}
 
 
+def c3_scripted_line(gmx, torch, dev, stream, steps: int, seed: int, env_offset: int, n: int, R: int):
+    """C3 driven by the scripted grasp mix alone (mode 0: close / squeeze / palm / lift with
+    jitter in every episode) -- the r05 headline's workload, reported beside the headline so
+    the two rounds compare like with like: the r06 headline's mix (mode 4) adds the grasp
+    program's lifted, multi-contact holds (more constraint rows per substep)."""
+    env, drive = steady_env(gmx, torch, dev, stream, n, "set6_synthetic", seed, env_offset, mode=0)
+    t = time_both(env, drive, torch, steps, R, seed, 0)
+    env.close()
+    ms = t.get("rollout_ms", t["per_step_api_ms"])
+    return {"value": round(n / ms * 1e3, 1), "unit": "env-steps/s", "envs": n, "steps": steps, "ms_per_step": ms,
+            **t, "workload": "C3 with the scripted grasp mix only (the r05 headline's workload), set6_synthetic, "
+                             "scene spawn, auto-reset, steady state after a staggered pre-roll"}
+
+
 def c1_line(gmx, seed: int, n_steps: int = 200):
     """C1 (BASELINE.json configs[0]): 1 env, one 200-step random-action episode, actions
     U[-1,1]^4 from np.random.default_rng(1234) (TrainDQN.py:2520).  Device: the mjpy.bind
@@ -492,6 +506,8 @@ def main():
     ap.add_argument("--no-policy", action="store_true", help="skip the C5 on-device DQN rollout line item")
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 (256 envs, one cylinder) line item")
     ap.add_argument("--no-random", action="store_true", help="skip the C3 random-action line item")
+    ap.add_argument("--no-scripted", action="store_true",
+                    help="skip the C3 scripted-mix-only line item (the r05 headline's workload)")
     ap.add_argument("--no-c1", action="store_true", help="skip the C1 (1 env, 200 random steps) line item")
     ap.add_argument("--no-preroll", dest="preroll", action="store_false",
                     help="skip the steady-state pre-roll (profiling runs only; the headline needs it)")
@@ -642,6 +658,8 @@ def main():
         c2 = None if (args.no_c2 or world > 1) else c2_line(gmx, torch, dev, stream, K, args.seed, first_env, R if rollout else 0)
         c3r = None if (args.no_random or world > 1) else c3_random_line(gmx, torch, dev, stream, K, args.seed, first_env, n,
                                                                         R if rollout else 0)
+        c3s = None if (args.no_scripted or world > 1) else c3_scripted_line(gmx, torch, dev, stream, K, args.seed,
+                                                                             first_env, n, R if rollout else 0)
         c1 = None if (args.no_c1 or world > 1) else c1_line(gmx, args.seed)
         c5 = None if (args.no_policy or world > 1) else policy_rollout(gmx, torch, dev, stream, n, max(3, K // 2), args.seed,
                                                         first_env, R if rollout else 0)
@@ -676,6 +694,7 @@ def main():
             "per_step_api": per_step_api,
             "c2_single_cylinder_256": c2,
             "c3_random_actions": c3r,
+            "c3_scripted_mix_only": c3s,
             "c1_single_env_200_steps": c1,
             "c5_device_policy_rollout": c5,
             "overflow_envs": overflow, "finite": finite,

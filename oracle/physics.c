@@ -1691,6 +1691,14 @@ static int row_active(const or_env* e, int r, double jar) { return r < e->nl ? 1
  * H~ + J_a^T D_a J_a), accept it when the active set at x is the same (then x is the
  * exact optimum), otherwise an exact line search along x - q (bracketed Newton on the
  * piecewise-quadratic cost, stopping on the piece it lands in). */
+#ifdef OR_NEWTON_STATS
+/* developer probe (tools/newton_active_set_probe.py): per extra Newton point, how many
+ * constraint rows entered / left the active set since the previous point -- the work an
+ * incremental (rank-1 update) factorisation would do instead of a refactor */
+long long or_nstat[40];
+void or_newton_stats(long long* out) { for (int i = 0; i < 40; i++) out[i] = or_nstat[i]; }
+#define OR_NSTAT(k, v) __atomic_fetch_add(&or_nstat[k], (v), __ATOMIC_RELAXED)
+#endif
 static void newton_solve(or_env* e) {
   const gm_model* m = &e->m;
   const int nv = m->nv, nefc = e->nefc;
@@ -1705,6 +1713,18 @@ static void newton_solve(or_env* e) {
   const int maxit = (m->newton_maxit > 0 && m->newton_maxit < GM_NEWTON_MAXIT) ? m->newton_maxit : GM_NEWTON_MAXIT;
   for (it = 0; it < maxit; it++) {
     for (int r = 0; r < nefc; r++) act[r] = row_active(e, r, jq[r]);
+#ifdef OR_NEWTON_STATS
+    {
+      static __thread int pact[NE];
+      if (it > 0) {
+        int ent = 0, lv = 0;
+        for (int r = 0; r < nefc; r++) if (act[r] != pact[r]) { if (act[r]) ent++; else lv++; }
+        OR_NSTAT(ent + lv < 30 ? ent + lv : 30, 1); OR_NSTAT(31, ent); OR_NSTAT(32, lv);
+      }
+      OR_NSTAT(33, 1);
+      for (int r = 0; r < nefc; r++) pact[r] = act[r];
+    }
+#endif
     nsys_t S;
     newton_assemble(e, act, &S);
     newton_factor_solve(e, &S, xv);
@@ -1762,6 +1782,9 @@ static void newton_solve(or_env* e) {
     for (int r = 0; r < nefc; r++) jq[r] = jq[r] + alpha * dj[r];
   }
   e->stat_it = it;
+#ifdef OR_NEWTON_STATS
+  OR_NSTAT(34, 1); OR_NSTAT(35, nefc);
+#endif
   /* a solve that ran out of iterations, or a line search out of evaluations, is counted
    * (GmEnvState::newton_caps; the device counts the same) */
   if (capped || ls_cap) e->newton_caps += 1;

@@ -76,6 +76,7 @@ struct gm_ctx {
   unsigned long long* d_chunk_st = nullptr;
   int chunk = 0, chunk_grid = 0, chunk_cap = 0, chunk_margin = 50, chunk_yields = 20, chunk_cmargin = 50;
   int chunk_steal = 1;                 // idle waves resume yielded envs of other XCDs (GM_CHUNK_STEAL=0: off)
+  int chunk_prio = 1;                  // issue priority by predicted work left (GM_CHUNK_PRIO=0: off)
   // DUO workgroups (gm_step_kernel<CL, false, true>): two waves per env, the second running
   // the collider concurrently -- for batches small enough that wave slots are spare
   bool duo = false;
@@ -129,6 +130,7 @@ hipError_t launch_step(gm_ctx* c, int grid, int n_envs, int mode, DebugOut dbg, 
   GmChunkQ q{c->d_chunk_ctr, c->d_chunk_ring, c->d_chunk_carry, c->chunk_cap, chunked ? c->chunk : 0,
              c->chunk_margin, c->chunk_yields, c->chunk_cmargin, c->d_chunk_st};
   q.steal = c->chunk_steal;
+  q.prio = c->chunk_prio;
   q.steps = 1;
   q.act_mode = -1;   // gm_step: one plain env-step per env (gm_rollout sets the rollout fields)
   if (roll && chunked) {
@@ -428,6 +430,7 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
     if (const char* e3 = std::getenv("GM_CHUNK_YIELDS")) c->chunk_yields = std::atoi(e3);
     if (const char* e4 = std::getenv("GM_CHUNK_CMARGIN")) c->chunk_cmargin = std::atoi(e4);
     if (const char* e6 = std::getenv("GM_CHUNK_STEAL")) c->chunk_steal = std::atoi(e6) != 0;
+    if (const char* e7 = std::getenv("GM_CHUNK_PRIO")) c->chunk_prio = std::atoi(e7);
     int per_cu = 0, per_cu_duo = 0, n_cu = 0;
     switch (c->model.n_seg) {
 #define X(N)                                                                                              \
@@ -1006,6 +1009,20 @@ int gm_chunk_claim_waits(gm_ctx* c, uint32_t* out2) {
   HIPCHK(c, hipMemcpyAsync(w, c->d_chunk_ctr + GM_CQ_LAST + 37, sizeof(w), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   out2[0] = w[0]; out2[1] = w[1];
+  return GM_OK;
+}
+
+int gm_chunk_job_stats(gm_ctx* c, uint32_t* clk, int32_t* yields) {
+  if (!c || (!clk && !yields)) return GM_E_ARG;
+  if (!c->d_chunk_carry) return GM_E_STATE;
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<GmChunkCarry> h((size_t)c->n_envs);
+  HIPCHK(c, hipMemcpyAsync(h.data(), c->d_chunk_carry, sizeof(GmChunkCarry) * h.size(), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (int e = 0; e < c->n_envs; e++) {
+    if (clk) clk[e] = h[(size_t)e].clk;
+    if (yields) yields[e] = h[(size_t)e].job_yields;
+  }
   return GM_OK;
 }
 

@@ -2042,9 +2042,24 @@ struct GmPreempt {
   const uint32_t* bq;
   uint32_t cmax;
   int cmargin;
+  int prio;                     // > 0: the wave's issue priority follows the work left (job_prio)
+  int steps;                    // env-steps per job: the cost array holds per-env-step costs
 };
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The wave's VALU issue priority from its job's predicted work left (rem, in the cost array's
+// units) against the launch's heaviest job (cmax): 0..3 in quarters.  Two waves share a SIMD's
+// issue and it goes by priority, then age (MI355X_MICROARCH.md, two waves per SIMD) -- the
+// persistent grid's waves never change age, so without this the job with the most work left
+// runs at the younger wave's pace on half the SIMDs.  Longest-remaining-work-first, at issue.
+__device__ __forceinline__ void job_prio(uint64_t rem, uint32_t cmax, int mode) {
+  if (mode <= 0) return;
+  const uint32_t p = __builtin_amdgcn_readfirstlane((uint32_t)(rem * 4u / (uint64_t)(cmax ? cmax : 1u)));
+  if (p >= 3) __builtin_amdgcn_s_setprio(3);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
 }
 // Claim the next entry of a yielded-env bucket (head at b[0], tail at b[1]; lane 0): the head
 // advances only while it is below the tail, so every claimed slot was reserved by a producer
@@ -2086,12 +2101,15 @@ __device__ __noinline__ int substep_loop(GM_AS_LDS SharedT<CL>* S_, const GM_AS_
       const uint64_t left = (uint64_t)__builtin_amdgcn_readfirstlane(pre.own) *
                             (uint64_t)(__builtin_amdgcn_readfirstlane(pre.left) - i);
       const uint64_t total = (uint64_t)__builtin_amdgcn_readfirstlane(pre.total);
+      const int pm = __builtin_amdgcn_readfirstlane(pre.prio);
+      if (pm > 0) job_prio(left / (total ? total : 1u), __builtin_amdgcn_readfirstlane(pre.cmax), pm);
       const uint32_t fh = __builtin_amdgcn_readfirstlane(ld_agent(pre.fresh_head));
       const uint32_t n = __builtin_amdgcn_readfirstlane(pre.n);
       if (fh < n) {
-        const uint32_t next = __builtin_amdgcn_readfirstlane(pre.cost[pre.order[fh]]);
+        const uint64_t next = (uint64_t)__builtin_amdgcn_readfirstlane(pre.cost[pre.order[fh]]) *
+                              (uint64_t)__builtin_amdgcn_readfirstlane(pre.steps);
         // (with a margin: a yield costs a state hand-off)
-        if (left * (uint64_t)(100 + __builtin_amdgcn_readfirstlane(pre.margin)) < (uint64_t)next * total * 100u) break;
+        if (left * (uint64_t)(100 + __builtin_amdgcn_readfirstlane(pre.margin)) < next * total * 100u) break;
       }
       const int cm = __builtin_amdgcn_readfirstlane(pre.cmargin);
       if (cm >= 0) {
@@ -2546,6 +2564,7 @@ struct GmChunkCarry {        // what a chunk hands the next besides the hot stat
   int32_t yielded;           // yields so far this env-step (at most GmChunkQ::max_yields)
   int32_t steps_left;        // env-steps of this launch's job still to run, the current one included
   int32_t step_idx;          // index of the current env-step in the launch (rollout records)
+  int32_t job_yields;        // yields over the whole job (gm_chunk_job_stats)
 };
 // counters (zeroed by gm_dispatch_order_kernel before every launch), one 128-B line each:
 // ring r = x * GM_CQ_NB + bucket: [r * 32] its head, [r * 32 + 1] its tail; GM_CQ_FRESH the
@@ -2589,6 +2608,7 @@ struct GmChunkQ {
   const gm_spawn_params* scene;
   GmSpawnRand sr;
   int steal;                 // an idle wave may resume a yielded env of another XCD
+  int prio;                  // > 0: issue priority by predicted work left (job_prio)
   // act_mode 2: the DQN policy picks each env-step's discrete action on the env's own wave
   // (gm_policy_rollout; gp_select_one = gm_policy_kernel's select_action for one env)
   const float* pparams;      // packed network (gm_policy_pack layout)
@@ -2691,10 +2711,12 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
   const uint32_t n = (uint32_t)n_envs;
   // bucket scale: the heaviest env's last cost + 1, snapshot by gm_dispatch_order_kernel, so
   // every wave of the launch buckets alike (costs of this launch go to the second half)
-  const uint32_t cmax = q.ctr[GM_CQ_CMAX];
+  // (costs are per env-step: a job of q.steps env-steps is predicted at q.steps times its env's)
+  const uint32_t cmax = q.ctr[GM_CQ_CMAX] * (uint32_t)(q.steps > 1 ? q.steps : 1);
   unsigned long long busy = 0, poll = 0, last_end = 0;
   bool first = true, saw_empty = false;
   for (;;) {
+    if (q.prio > 0) __builtin_amdgcn_s_setprio(0);   // looking for work: the partner wave first
     const unsigned long long tw = __builtin_amdgcn_s_memrealtime();
     // take work (lane 0): a continuation queued on this XCD first, else a fresh env in
     // cost order; -1 once every env has finished its env-step
@@ -2718,7 +2740,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       if (take_c && have_f) {
         const uint32_t h = __builtin_amdgcn_readlane(hb, bsel);
         const uint64_t e = ld_agent64(ring + (size_t)bsel * q.cap + h % (uint32_t)q.cap);
-        take_c = e == 0ull || (uint32_t)(e >> 32) >= cost[order[fh]];
+        take_c = e == 0ull || (uint64_t)(uint32_t)(e >> 32) >= (uint64_t)cost[order[fh]] * (uint64_t)(q.steps > 1 ? q.steps : 1);
       }
       if (take_c) {
         int got = 0;
@@ -2834,6 +2856,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       cr.yielded = 0;
       cr.steps_left = q.steps;
       cr.step_idx = 0;
+      cr.job_yields = 0;
     } else {
       // agent-scope loads: never served by a scalar cache that the acquire does not reach
       const uint32_t* src = reinterpret_cast<const uint32_t*>(q.carry + env);
@@ -2846,7 +2869,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       S.stp_fixed = cr.stp_fixed;
     }
     GM_ENV_SYNC();
-    const uint32_t own = cost[env];
+    const uint64_t own = (uint64_t)cost[env] * (uint64_t)(q.steps > 1 ? q.steps : 1);   // the job's predicted cost
     const int s_nom = C->sim_steps_per_action;
     bool finished = false;
     for (;;) {   // the env-steps of this pick
@@ -2877,8 +2900,11 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
       const int left = cr.nsub - cr.sub_done;
       const int job_left = (cr.steps_left - 1) * s_nom + left;
       const int job_total = q.steps > 1 ? q.steps * s_nom : cr.nsub;
-      const GmPreempt pre{fresh_head, order, cost, n, own, job_left, job_total,
-                          cr.yielded < q.max_yields ? q.chunk : 0, q.margin, bq, cmax, q.cmargin};
+      const uint32_t est = (uint32_t)(own > 0xFFFFFFFFull ? 0xFFFFFFFFull : own);
+      const GmPreempt pre{fresh_head, order, cost, n, est, job_left, job_total,
+                          cr.yielded < q.max_yields ? q.chunk : 0, q.margin, bq, cmax, q.cmargin, q.prio,
+                          q.steps > 1 ? q.steps : 1};
+      job_prio((uint64_t)est * (uint64_t)job_left / (uint64_t)(job_total > 0 ? job_total : 1), cmax, q.prio);
       const int k = substep_loop<CL, false, false, DUO>((GM_AS_LDS SharedT<CL>*)&S, (const GM_AS_GLOBAL gm_model*)m,
                                             (const GM_AS_GLOBAL GmTopo*)T, (const GM_AS_GLOBAL gm_config*)C, lane,
                                             false, left, false, pre);
@@ -2924,7 +2950,11 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
         const uint32_t now = cr.clk + (uint32_t)((__builtin_amdgcn_s_memtime() - t_start) >> 6);
         const uint32_t model = 14000u * (uint32_t)q.steps + 19u * (uint32_t)S.work_nefc + 188u * (uint32_t)S.work_mpr +
                                940u * (uint32_t)S.work_newton;
-        cost[n + env] = (now >> 1) + (model >> 1);   // recorded for the next launch's order
+        // recorded for the next launch's order, per env-step (whatever the next launch's job length)
+        cost[n + env] = ((now >> 1) + (model >> 1)) / (uint32_t)(q.steps > 1 ? q.steps : 1);
+        // diagnostics (gm_chunk_job_stats): the job's busy clocks / 64 and its yields
+        __hip_atomic_store(&q.carry[env].clk, now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&q.carry[env].job_yields, cr.job_yields, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       store_state(S, g, lane);
       if (lane == 0) {
@@ -2939,6 +2969,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
         cr.work_nefc = S.work_nefc; cr.work_mpr = S.work_mpr; cr.work_newton = S.work_newton;
         cr.stp_fixed = S.stp_fixed;
         cr.yielded += 1;
+        cr.job_yields += 1;
         cr.clk += (uint32_t)((__builtin_amdgcn_s_memtime() - t_start) >> 6);
         q.carry[env] = cr;
       }
@@ -2953,7 +2984,7 @@ __device__ __forceinline__ void chunked_env_steps(SharedT<CL>& S, GmEnvState* __
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int job_total = q.steps > 1 ? q.steps * s_nom : cr.nsub;
         const int job_left = (cr.steps_left - 1) * s_nom + (cr.nsub - cr.sub_done);
-        const uint64_t rem = (uint64_t)own * (uint64_t)job_left / (uint64_t)job_total;
+        const uint64_t rem = own * (uint64_t)job_left / (uint64_t)job_total;
         add_agent(q.ctr + GM_CQ_DONE + 1, 1u);
         const uint32_t b = rem * GM_CQ_NB / cmax < GM_CQ_NB - 1 ? (uint32_t)(rem * GM_CQ_NB / cmax) : GM_CQ_NB - 1;
         const uint32_t t = add_agent(bq + b * 32 + 1, 1u) % (uint32_t)q.cap;

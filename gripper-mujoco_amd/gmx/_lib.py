@@ -274,6 +274,7 @@ def _declare(lib):
         "gm_scripted_actions": (i32, [vp, C.c_uint64, C.c_float, vp, i32]),
         "gm_program_actions": (i32, [vp, C.c_uint64, C.c_float, i32, vp, i32]),
         "gm_chunk_claim_waits": (i32, [vp, vp]),
+        "gm_chunk_job_stats": (i32, [vp, vp, vp]),
         "gm_device_reset_mask": (vp, [vp]),
         "gm_policy_create": (i32, [vp, i32p, i32, f32p, C.POINTER(vp)]),
         "gm_policy_destroy": (None, [vp]),

@@ -322,6 +322,16 @@ class BatchedGripperEnv:
         self._check(self.lib.gm_chunk_claim_waits(self._ctx, v))
         return dict(waiting_claims=int(v[0]), polls=int(v[1]))
 
+    def job_stats(self):
+        """The last chunked launch's jobs (gm_chunk_job_stats): per env the shader clocks / 64
+        its job ran for and the job's yields, as two numpy arrays."""
+        import numpy as np
+        clk = np.zeros(self.n_envs, dtype=np.uint32)
+        yl = np.zeros(self.n_envs, dtype=np.int32)
+        self._check(self.lib.gm_chunk_job_stats(self._ctx, clk.ctypes.data_as(C.c_void_p),
+                                                 yl.ctypes.data_as(C.c_void_p)))
+        return clk, yl
+
     def chunk_timeline(self):
         """When each workgroup of the last chunked launch finished its last work, ms after the
         launch's first pick, its XCD, and per env [start, finish] ms (gm_chunk_timeline)."""

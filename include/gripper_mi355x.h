@@ -622,6 +622,12 @@ int  gm_chunk_stats(gm_ctx* ctx, uint32_t* out7, uint64_t* times5);
  * (claim_bucket's invariant), so the polls per waiting claim stay small; a claim parked on a
  * slot only a future yield would fill shows as a run of polls.  Synchronises the stream. */
 int  gm_chunk_claim_waits(gm_ctx* ctx, uint32_t* out2);
+/* The last chunked launch's jobs, per env (arrays of n_envs, either may be NULL): clk[e] the
+ * shader clocks / 64 (s_memtime) env e's job ran for, summed over its chunks; yields[e] how
+ * often the job was handed back to the queue.  Set when a job finishes (an env the launch
+ * did not reach keeps the previous value).  Synchronises the context's stream.  Diagnostics:
+ * a job's work against its life (gm_chunk_timeline). */
+int  gm_chunk_job_stats(gm_ctx* ctx, uint32_t* clk, int32_t* yields);
 /* How gm_step / gm_rollout dispatch this context (fixed at gm_create): out[0] substeps
  * between preemption tests (0: the one-shot kernel), out[1] workgroups of the chunked
  * grid, out[2] waves per env (1; 2 = DUO workgroups, whose second wave runs the collider

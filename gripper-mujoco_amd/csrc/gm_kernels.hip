@@ -1254,7 +1254,7 @@ __device__ __forceinline__ void write_contact(SharedT<CL>& S, int slot, int g1, 
 // hit: the box-box hit slots (S.cl.hit, in the union; a DUO workgroup's helper wave passes
 // its own array, the union being live with crb_rne's composites while it runs)
 template <int CL>
-__device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
+__device__ __forceinline__ bool collision(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                           bool prof, real (*hit)[8][4]) {
   unsigned long long t0 = prof ? clock64() : 0;
   (void)t0;
@@ -1430,12 +1430,10 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
     }
     written += total;
   }
-  {
-    const bool any_mpr = __ballot(ran_mpr) != 0;
-    if (lane == 0 && any_mpr) {
-      S.work_mpr += 1;
-      if (prof) S.tph[29] += 1;
-    }
+  const bool any_mpr = __ballot(ran_mpr) != 0;
+  if (lane == 0 && any_mpr) {
+    S.work_mpr += 1;
+    if (prof) S.tph[29] += 1;
   }
   // contact frames, one contact per lane (GM_MAX_CON <= 64): the normal and a tangent, as
   // make_frame builds them; the rest of the frame is implied by the two
@@ -1455,6 +1453,7 @@ __device__ __forceinline__ void collision(SharedT<CL>& S, const gm_model* __rest
     S.overflow = written > GM_MAX_CON;
   }
   GM_WAVE_SYNC();
+  return any_mpr;
 }
 
 // DUO workgroups: the helper wave's euler_factor results, lane-major ([j][64]: L[1..CL], lb,
@@ -1530,6 +1529,9 @@ using gmf::newton_solve;
 using gmf::integrate;
 using gmf::euler_factor;
 using gmf::duo_ef;
+using gmf::contact_rows;
+using gmf::duo_rows;
+using gmf::DuoRows;
 
 // ============================================================ reference scalar logic (lane 0)
 // luke::Gripper in fp64 (gripper.cpp), bit-for-bit the same operations as the reference
@@ -1982,7 +1984,7 @@ __device__ __forceinline__ void physics_substep_body(SharedT<CL>& S, const gm_mo
     collision(S, m, T, fresh_lane(), prof, S.cl.hit);
   }
   PH(5);
-  newton_solve<CL, CAL>(S, m, T, fresh_lane(), prof);
+  newton_solve<CL, CAL, DUO>(S, m, T, fresh_lane(), prof);
   PH(6);
   integrate<CL, CAL, DUO>(S, m, T, fresh_lane());
   PH(8);
@@ -3021,6 +3023,25 @@ __device__ __forceinline__ void duo_helper(SharedT<CL>& S, const gm_model* __res
     __syncthreads();
     if (S.duo_cmd == 0) return;
     collision<CL>(S, m, T, fresh_lane(), false, hit);
+    {
+      // the constraint setup's contact rows for the owner (contact_rows), the body
+      // velocities in the hit slots (dead once the contacts are written).  (Measured: only
+      // on the substeps whose collider ran no MPR, the owner forming them on the rest, was
+      // no better: tools/duo_rows_ab.sh, profiles/r06_ab_duo_rows.txt)
+      static_assert(sizeof(hit) >= sizeof(real) * 12 * SharedT<CL>::NB, "two velocity sets fit the hit slots");
+      const int ln = fresh_lane();
+      real (*V)[6] = reinterpret_cast<real (*)[6]>(&hit[0][0][0]);
+      real cD, caref[4], jq[4];
+      bool oo;
+      contact_rows<CL, false>(S, m, T, ln, V, V + SharedT<CL>::NB, cD, caref, jq, oo);
+      DuoRows<CL>* dr = duo_rows<CL>();
+      if (ln < GM_MAX_CON) {
+        dr->cD[ln] = cD;
+#pragma unroll
+        for (int e = 0; e < 4; e++) { dr->caref[e][ln] = caref[e]; dr->jq[e][ln] = jq[e]; }
+      }
+      if (ln == 0) dr->obj_only = oo ? 1 : 0;
+    }
     __syncthreads();
     // M is formed (the owner wave's mass_and_forces ran before the barrier): the Euler
     // damping factor for integrate, while the owner runs the constraint solve

@@ -534,34 +534,27 @@ __device__ __forceinline__ void lock_rows(SharedT<CL>& S, const gm_model* __rest
   S.nl = nl;   // (wave-uniform: every lane stores the same value)
 }
 
-// constraint setup (mj_makeConstraint / mj_makeImpedance): impedance, the regulariser
-// R = (1 - d) / d diagApprox (lock rows: dof_invweight0; pyramid edges:
-// tran + mu^2 tran, tran = the two bodies' invweight0), reference accelerations
+// The contact rows of the constraint setup (mj_makeConstraint / mj_makeImpedance for the
+// pyramid edges): body velocities at qvel (reference accelerations) and at the warm start
+// (the first iterate's J q - aref) into V / V2, one fused pass; then per contact lane the
+// edges' D = 1 / R (R = (1 - d) / d diagApprox, diagApprox = tran + mu^2 tran, tran = the two
+// bodies' invweight0), their aref and the warm start's J q - aref.  The owner wave runs it
+// inside constraint_setup; in a DUO workgroup the helper runs it right after its collider
+// (duo_helper: it needs only the contacts, the motion subspaces and qvel / qacc_warm) and
+// hands the rows over in LDS (duo_rows) -- the same code on the same operands.
 template <int CL, bool CAL>
-__device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
-                                 int lane, RowsT& R, real* jq, real& jql, bool& obj_only, bool prof = false) {
-  unsigned long long t0 = prof ? clock64() : 0;
-  (void)t0;
+__device__ __forceinline__ void contact_rows(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
+                                             int lane, real (*V)[6], real (*V2)[6], real& cD, real* caref, real* jq,
+                                             bool& obj_only) {
   const real h = CAL ? S.s.dt : m->timestep;
   real tc = m->solref[0];
   if (tc < 2 * h) tc = 2 * h;
   const real dr = m->solref[1], dmax = m->solimp[1];
   const real K = rcp_n(dmax * dmax * tc * tc * dr * dr);
   const real Bd = div_n(2.0, dmax * tc);
-  // lock rows: formed in crb_rne's first block (lock_rows below) and read back here
-  const int nl = S.nl;
-  R.lD = 0; R.laref = 0; R.ldof = 0;
-  if (lane < GM_MAX_LOCK) { R.lD = S.lrow_D[lane]; R.laref = S.lrow_aref[lane]; R.ldof = S.lrow_dof[lane]; }
-  if (lane >= nl) { R.lD = 0; R.laref = 0; R.ldof = 0; }
-  if (lane == 0) S.nefc = nl + 4 * S.ncon;
-#ifdef GM_PHASE_SPLIT_SETUP
-  PH(15);   // developer split: lock rows
-#endif
-  // body velocities at qvel (reference accelerations) and at the warm start (the first
-  // iterate's J q - aref), one fused pass
   {
     const real* vv[2] = {S.s.qvel, S.s.qacc_warm};
-    real (*VV[2])[6] = {S.nw2.V, S.nw2.V2};
+    real (*VV[2])[6] = {V, V2};
     bool og = true;
     if (lane < S.ncon) {
       const int b1 = S.cbody[lane][0], b2 = S.cbody[lane][1];
@@ -570,18 +563,11 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
     obj_only = __ballot(!og) == 0ull;
     body_vel<CL, 2>(S, vv, VV, m, T, lane, obj_only);
   }
-#ifdef GM_PHASE_SPLIT_SETUP
-  PH(16);   // developer split: the two velocity scans
-#endif
-  {
-    const real qw = S.s.qacc_warm[R.ldof];   // (ldof = 0 off the lock lanes)
-    jql = (lane < nl) ? qw - R.laref : 0.0;
-  }
 #pragma unroll
   for (int e = 0; e < 4; e++) jq[e] = 0.0;
-  R.cD = 0;
+  cD = 0;
 #pragma unroll
-  for (int e = 0; e < 4; e++) R.caref[e] = 0;
+  for (int e = 0; e < 4; e++) caref[e] = 0;
   if (lane < S.ncon) {
     const real* C = S.con[lane];
     const int b1 = S.cbody[lane][0], b2 = S.cbody[lane][1];
@@ -594,15 +580,65 @@ __device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m,
     const real imp = impedance(m, C[0]);
     real Rr = div_n(1 - imp, imp) * diag;
     if (Rr < 1e-15) Rr = 1e-15;
-    R.cD = rcp_n(Rr);
+    cD = rcp_n(Rr);
     real vel[4], jv[4];
-    contact_jv<CL>(S, S.nw2.V, m, lane, vel);
-    contact_jv<CL>(S, S.nw2.V2, m, lane, jv);
+    contact_jv<CL>(S, V, m, lane, vel);
+    contact_jv<CL>(S, V2, m, lane, jv);
 #pragma unroll
     for (int e = 0; e < 4; e++) {
-      R.caref[e] = -Bd * vel[e] - K * imp * C[0];
-      jq[e] = jv[e] - R.caref[e];
+      caref[e] = -Bd * vel[e] - K * imp * C[0];
+      jq[e] = jv[e] - caref[e];
     }
+  }
+}
+
+// DUO workgroups: the contact rows the helper formed (contact_rows), contact-lane-major
+template <int CL>
+struct DuoRows {
+  real cD[GM_MAX_CON], caref[4][GM_MAX_CON], jq[4][GM_MAX_CON];
+  int32_t obj_only;
+};
+template <int CL>
+__device__ __forceinline__ DuoRows<CL>* duo_rows() {
+  __shared__ DuoRows<CL> r;
+  return &r;
+}
+
+// constraint setup (mj_makeConstraint / mj_makeImpedance): impedance, the regulariser
+// R = (1 - d) / d diagApprox (lock rows: dof_invweight0; pyramid edges:
+// tran + mu^2 tran, tran = the two bodies' invweight0), reference accelerations
+template <int CL, bool CAL, bool DUO = false>
+__device__ void constraint_setup(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T,
+                                 int lane, RowsT& R, real* jq, real& jql, bool& obj_only, bool prof = false) {
+  unsigned long long t0 = prof ? clock64() : 0;
+  (void)t0;
+  // lock rows: formed in crb_rne's first block (lock_rows below) and read back here
+  const int nl = S.nl;
+  R.lD = 0; R.laref = 0; R.ldof = 0;
+  if (lane < GM_MAX_LOCK) { R.lD = S.lrow_D[lane]; R.laref = S.lrow_aref[lane]; R.ldof = S.lrow_dof[lane]; }
+  if (lane >= nl) { R.lD = 0; R.laref = 0; R.ldof = 0; }
+  if (lane == 0) S.nefc = nl + 4 * S.ncon;
+#ifdef GM_PHASE_SPLIT_SETUP
+  PH(15);   // developer split: lock rows
+#endif
+  if constexpr (DUO) {
+    // formed by the helper wave after its collider (duo_helper), read after the barrier
+    const DuoRows<CL>* dr = duo_rows<CL>();
+    obj_only = dr->obj_only != 0;
+    R.cD = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) { R.caref[e] = 0; jq[e] = 0.0; }
+    if (lane < S.ncon) {
+      R.cD = dr->cD[lane];
+#pragma unroll
+      for (int e = 0; e < 4; e++) { R.caref[e] = dr->caref[e][lane]; jq[e] = dr->jq[e][lane]; }
+    }
+  } else {
+    contact_rows<CL, CAL>(S, m, T, lane, S.nw2.V, S.nw2.V2, R.cD, R.caref, jq, obj_only);
+  }
+  {
+    const real qw = S.s.qacc_warm[R.ldof];   // (ldof = 0 off the lock lanes)
+    jql = (lane < nl) ? qw - R.laref : 0.0;
   }
   GM_WAVE_SYNC();
 #ifdef GM_PHASE_SPLIT_SETUP
@@ -1218,14 +1254,14 @@ __device__ void newton_point(SharedT<CL>& S, const gm_model* __restrict__ m, con
 // mj_solNewton restated (oracle newton_solve): warm start, Newton point on the active
 // pattern, accept when the pattern at x is unchanged (x is then the exact optimum), else
 // an exact line search along x - q; contact forces and the warm start at the end.
-template <int CL, bool CAL>
+template <int CL, bool CAL, bool DUO = false>
 __device__ __forceinline__ void newton_solve(SharedT<CL>& S, const gm_model* __restrict__ m, const GmTopo* __restrict__ T, int lane,
                              bool prof) {
   unsigned long long t0 = prof ? clock64() : 0;
   RowsT R;
   real jq[4], jql;
   bool obj_only;
-  constraint_setup<CL, CAL>(S, m, T, lane, R, jq, jql, obj_only, prof);
+  constraint_setup<CL, CAL, DUO>(S, m, T, lane, R, jq, jql, obj_only, prof);
 #ifdef GM_PHASE_SPLIT_SETUP
   if (prof) t0 = clock64();   // the split phases above were charged inside; the rest: contact rows
 #endif

@@ -1,3 +1,6 @@
+#!/bin/bash
+# The -m gpu suite on the tree's libgm.so, then tools/ab_bench.sh's C3 A/B of lib/ab_A.so and
+# lib/ab_B.so (tools/build_ab.sh makes them).  usage: bash tools/c3_ab_with_tests.sh
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out/r06i

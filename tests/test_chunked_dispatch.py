@@ -70,3 +70,22 @@ def test_chunked_equals_one_shot(gm, n, setting):
         yields += st["yields"]
     if setting == "handoff-heavy" and n > chk.chunk_stats()["workgroups"]:
         assert yields > n   # the hand-off path really ran (yields need more envs than waves)
+
+
+def test_job_stats_account_for_the_launch(gm):
+    """gm_chunk_job_stats (the per-job diagnostics of the last chunked launch): every job
+    that ran has busy clocks, the jobs' yields add up to the queue's yield counter, and no
+    job was busy for longer than the launch lasted (shader clocks / 64 at <= 2.6 GHz)."""
+    n = 2500
+    env = make(gm, n, CHUNKED["handoff-heavy"])
+    rng = np.random.default_rng(5)
+    for _ in range(2):
+        env.step(rng.uniform(-1, 1, size=(n, env.n_actions)).astype(np.float32))
+    st = env.chunk_stats()
+    clk, yl = env.job_stats()
+    assert clk.shape == (n,) and yl.shape == (n,)
+    assert (clk > 0).all()
+    assert (yl >= 0).all() and int(yl.sum()) == st["yields"]
+    assert st["yields"] > 0
+    busy_ms = clk.astype(np.float64) * 64 / 2.6e6
+    assert busy_ms.max() <= st["span_ms"] * 1.05 + 0.05, (busy_ms.max(), st["span_ms"])

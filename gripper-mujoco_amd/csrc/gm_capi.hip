@@ -50,9 +50,12 @@ struct gm_ctx {
   GmTopo* d_topo = nullptr;
   gm_object* d_objs = nullptr;
   double* d_eq = nullptr;
-  float* d_obs = nullptr;
-  float* d_rew = nullptr;
+  float* d_obs = nullptr;              // d_obs, d_rew, d_done: one allocation (d_out), read back
+  float* d_rew = nullptr;              // by gm_get_outputs in one copy through h_out (pinned)
   uint8_t* d_done = nullptr;
+  void* d_out = nullptr;
+  void* h_out = nullptr;
+  size_t out_bytes = 0;
   float* d_act = nullptr;
   // host actions are staged through a pinned buffer so gm_set_action / gm_set_discrete_action
   // return without a stream synchronisation (stage_ev: the previous staging copy is done)
@@ -406,9 +409,16 @@ int gm_create(const gm_model* model, const gm_config* cfg, const gm_object* obje
   HIPCHK(c, hipMalloc(&c->d_topo, sizeof(GmTopo)));
   HIPCHK(c, hipMalloc(&c->d_objs, sizeof(gm_object) * (size_t)n_objects));
   HIPCHK(c, hipMalloc(&c->d_eq, sizeof(double) * GM_MAX_QPOS));
-  HIPCHK(c, hipMalloc(&c->d_obs, sizeof(float) * (size_t)n_envs * (cfg->n_obs > 0 ? cfg->n_obs : 1)));
-  HIPCHK(c, hipMalloc(&c->d_rew, sizeof(float) * (size_t)n_envs));
-  HIPCHK(c, hipMalloc(&c->d_done, (size_t)n_envs));
+  {
+    const size_t obs_b = sizeof(float) * (size_t)n_envs * (cfg->n_obs > 0 ? cfg->n_obs : 1);
+    const size_t rew_b = sizeof(float) * (size_t)n_envs;
+    c->out_bytes = obs_b + rew_b + (size_t)n_envs;
+    HIPCHK(c, hipMalloc(&c->d_out, c->out_bytes));
+    HIPCHK(c, hipHostMalloc(&c->h_out, c->out_bytes, hipHostMallocDefault));
+    c->d_obs = static_cast<float*>(c->d_out);
+    c->d_rew = reinterpret_cast<float*>(static_cast<char*>(c->d_out) + obs_b);
+    c->d_done = reinterpret_cast<uint8_t*>(static_cast<char*>(c->d_out) + obs_b + rew_b);
+  }
   HIPCHK(c, hipMalloc(&c->d_act, sizeof(float) * (size_t)n_envs * GM_ACTION_CODE_COUNT));
   HIPCHK(c, hipMalloc(&c->d_dact, sizeof(int32_t) * (size_t)n_envs));
   HIPCHK(c, hipMalloc(&c->d_mask, (size_t)n_envs));
@@ -516,8 +526,9 @@ void gm_destroy(gm_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   (void)hipFree(c->d_state); (void)hipFree(c->d_model); (void)hipFree(c->d_cfg); (void)hipFree(c->d_topo); (void)hipFree(c->d_objs);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
+  if (c->h_out) (void)hipHostFree(c->h_out);
   if (c->stage_ev) (void)hipEventDestroy(c->stage_ev);
-  (void)hipFree(c->d_eq); (void)hipFree(c->d_obs); (void)hipFree(c->d_rew); (void)hipFree(c->d_done); (void)hipFree(c->d_act);
+  (void)hipFree(c->d_eq); (void)hipFree(c->d_out); (void)hipFree(c->d_act);
   (void)hipFree(c->d_dact); (void)hipFree(c->d_mask); (void)hipFree(c->d_spawn); (void)hipFree(c->d_scratch);
   (void)hipFree(c->d_order); (void)hipFree(c->d_cost); (void)hipFree(c->d_scene);
   (void)hipFree(c->d_chunk_ctr); (void)hipFree(c->d_chunk_ring); (void)hipFree(c->d_chunk_carry);
@@ -1074,10 +1085,17 @@ int gm_get_obs(gm_ctx* c, float* out, int on_device) {
 int gm_get_outputs(gm_ctx* c, float* obs, float* reward, uint8_t* done) {
   if (!c || !obs || !reward || !done) return GM_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, hipMemcpyAsync(obs, c->d_obs, sizeof(float) * (size_t)c->n_envs * c->cfg.n_obs, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(reward, c->d_rew, sizeof(float) * (size_t)c->n_envs, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(done, c->d_done, (size_t)c->n_envs, hipMemcpyDeviceToHost, c->stream));
+  // one copy of the contiguous obs / reward / done block into pinned memory (one DMA, no
+  // pageable staging), then the three host copies
+  HIPCHK(c, hipMemcpyAsync(c->h_out, c->d_out, c->out_bytes, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  const char* h = static_cast<const char*>(c->h_out);
+  const size_t obs_b = sizeof(float) * (size_t)c->n_envs * c->cfg.n_obs;
+  const size_t off_rew = reinterpret_cast<const char*>(c->d_rew) - static_cast<const char*>(c->d_out);
+  const size_t off_done = reinterpret_cast<const char*>(c->d_done) - static_cast<const char*>(c->d_out);
+  std::memcpy(obs, h, obs_b);
+  std::memcpy(reward, h + off_rew, sizeof(float) * (size_t)c->n_envs);
+  std::memcpy(done, h + off_done, (size_t)c->n_envs);
   return GM_OK;
 }
 

@@ -9,7 +9,7 @@ OUT=$R/gpurun_out/$1
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 for ctr in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 180 rocprofv3 --pmc $ctr --output-format csv -d $OUT/$ctr -o run -- python3 $R/bench.py --steps 10 --warmup 10 --no-cpu --no-parity --no-policy --no-c2 --no-random --no-c1 > $OUT/$ctr.log 2>&1 || { echo "pass $ctr failed"; tail -5 $OUT/$ctr.log; exit 1; }
+  timeout -s KILL 180 rocprofv3 --pmc $ctr --output-format csv -d $OUT/$ctr -o run -- python3 $R/bench.py --steps 10 --warmup 10 --no-cpu --no-parity --no-policy --no-c2 --no-random --no-scripted --no-c1 > $OUT/$ctr.log 2>&1 || { echo "pass $ctr failed"; tail -5 $OUT/$ctr.log; exit 1; }
   echo "pass $ctr ok"
 done
 echo done > $OUT/DONE

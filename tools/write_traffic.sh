@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$1
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-B="python3 $R/bench.py --steps 3 --warmup 1 --no-cpu --no-parity --no-policy --no-c2 --no-random --no-c1"
+B="python3 $R/bench.py --steps 3 --warmup 1 --no-cpu --no-parity --no-policy --no-c2 --no-random --no-scripted --no-c1"
 for mode in chunked oneshot; do
   for ctr in WRITE_SIZE FETCH_SIZE; do
     if [ $mode = oneshot ]; then export GM_CHUNK_SUBSTEPS=0; else unset GM_CHUNK_SUBSTEPS; fi

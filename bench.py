@@ -25,7 +25,7 @@ run N x 4096 envs sharded by env id (weak scaling); the only collective is an RC
 all-gather of the per-env episode-end records (return, length, success) of every env-step
 (SURVEY.md 8e): a launch of R env-steps is followed by its R per-env-step gathers.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]       (defaults: N 1, K 30, W 2)
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
 Rank 0 prints one JSON line.  `roofline.achieved` = algorithmic bytes per launch of
@@ -493,7 +493,7 @@ def headline(world: int, n: int, K: int, W: int, elapsed: float, ep: dict) -> di
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--seed", type=int, default=1234)

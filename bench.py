@@ -513,6 +513,10 @@ def main():
                     help="skip the steady-state pre-roll (profiling runs only; the headline needs it)")
     ap.add_argument("--rollout", type=int, default=10,
                     help="env-steps per gm_rollout launch for the headline (0: the per-step API's launches)")
+    ap.add_argument("--c2-rollout", type=int, default=30,
+                    help="env-steps per gm_rollout launch for the C2 line (its 256 envs: a launch lasts as long as "
+                         "its slowest env's job, so longer jobs average each env's heavy and light env-steps; "
+                         "profiles/r06_bench_window.txt)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -655,7 +659,8 @@ def main():
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(gmx, args.cpu_envs * args.cpu_threads // 4, args.cpu_steps, args.cpu_threads)
             cpu["single_thread"] = cpu_baseline(gmx, args.cpu_envs, args.cpu_steps, 1)["value"]
-        c2 = None if (args.no_c2 or world > 1) else c2_line(gmx, torch, dev, stream, K, args.seed, first_env, R if rollout else 0)
+        c2 = None if (args.no_c2 or world > 1) else c2_line(gmx, torch, dev, stream, K, args.seed, first_env,
+                                                            math.gcd(K, args.c2_rollout) if rollout and args.c2_rollout > 0 else 0)
         c3r = None if (args.no_random or world > 1) else c3_random_line(gmx, torch, dev, stream, K, args.seed, first_env, n,
                                                                         R if rollout else 0)
         c3s = None if (args.no_scripted or world > 1) else c3_scripted_line(gmx, torch, dev, stream, K, args.seed,

@@ -308,3 +308,19 @@ def test_two_rank_gather_carries_program_successes(gm):
     r, length, success = unpack_episodes(torch.from_numpy(ref))
     assert success.tolist() == [1, 0, 1, 0], success
     assert (r[success.bool()] > 0.5).all() and (length[success.bool()] < SUCC_STEPS).all()
+
+
+def test_bench_cli_contract():
+    """bench.py's command line (the driver's contract): --gpus / --steps / --warmup, the
+    headline's and the C2 line's rollout lengths, and the side-line switches; --help needs
+    no GPU."""
+    import subprocess
+    import sys
+    import os
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--help"], capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    for opt in ("--gpus", "--steps", "--warmup", "--rollout", "--c2-rollout", "--no-scripted", "--no-random",
+                "--no-c2", "--no-c1", "--no-policy", "--no-cpu", "--no-parity"):
+        assert opt in out.stdout, opt
